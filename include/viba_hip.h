@@ -1,0 +1,277 @@
+/*
+ * viba_hip.h -- C-ABI drop-in boundary for the MI355X-native Levenberg-Marquardt inner loop
+ * of visual-inertial bundle adjustment (VI-BA).
+ *
+ * The boundary sits where the reference's `viba::problem` builder hands factors to the generic
+ * NLLS engine `small_thing::Optimizer`:
+ *
+ *   reference call                                             replaced by
+ *   ---------------------------------------------------------  ---------------------------------
+ *   SingleSessionProblem::inertialPose_set / *_addNew          vb_set_vars
+ *     (viba/problem/SingleSessionProblem.h:199-364)
+ *   Optimizer::addFactor (lib/small_thing/Optimizer.h:115-175)  vb_add_factors
+ *     as called from SingleSessionProblem::add{VisualFactor,
+ *     InertialFactor, OmegaPriorFactor, *RWFactor, *Prior}
+ *     (viba/problem/SingleSessionProblem.h:64-129)
+ *   RollingShutterData::compute results                        vb_set_rs_tables
+ *     (lib/motion/preintegration/RollingShutterData.cpp:16-65)
+ *   registerPointVariables + registeredVariablesToElimination  vb_set_elim_points (implicit: the
+ *     Range (SingleSessionProblem.cpp:41-45, Optimizer.cpp:31)   point kind is always eliminated)
+ *   Optimizer::initSolver (Optimizer.cpp:166-207)              vb_finalize
+ *   Optimizer::computeGradHess (Optimizer.cpp:57-71)           vb_linearize
+ *   Optimizer::computeCost (Optimizer.cpp:88-97)               vb_cost
+ *   addDamping + factor + solve (Optimizer.cpp:826-833)        vb_damp_factor_solve
+ *   solveFunc(gradNewX) (Optimizer.cpp:970)                    vb_solve_with_new_gradient
+ *   Optimizer::applyStep (Optimizer.cpp:121-134)               vb_apply_step
+ *   backupVariables / restoreVariables (Optimizer.cpp:99-119)  vb_backup / vb_restore
+ *   Optimizer::optimize (Optimizer.cpp:768-1106)               vb_optimize
+ *
+ * Conventions
+ *   - All values are IEEE fp64 (the reference path is fp64 end to end).
+ *   - SE3 data layout = Sophus::SE3d::data(): [qx, qy, qz, qw, tx, ty, tz]; tangent [upsilon, omega].
+ *   - Variables are addressed per kind by a 0-based handle (the order of vb_set_vars rows).
+ *   - Every function returns 0 on success, a negative VB_E_* code on error, and never throws;
+ *     vb_last_error() returns the message of the last error on the calling thread.
+ *   - Host buffers are copied; the handle owns device memory. One handle = one HIP stream.
+ */
+#ifndef VIBA_HIP_H
+#define VIBA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- error codes */
+#define VB_OK 0
+#define VB_E_ARG (-1)        /* invalid argument / shape mismatch */
+#define VB_E_STATE (-2)      /* call out of order (e.g. add after finalize) */
+#define VB_E_HIP (-3)        /* HIP runtime error (incl. missing device) */
+#define VB_E_NUMERIC (-4)    /* Cholesky breakdown / non-finite values */
+#define VB_E_RANGE (-5)      /* rolling-shutter lookup out of range (RollingShutterData.cpp:82-91) */
+#define VB_E_UNSUPPORTED (-6)
+
+/* ---------------------------------------------------------------- variable kinds */
+enum vb_var_kind {
+  VB_VAR_POINT = 0,     /* Variable<Vec3> world point; data 3, tangent 3 (SingleSessionProblem.h:42) */
+  VB_VAR_POSE = 1,      /* T_bodyImu_world SE3; data 7, tangent 6 (SingleSessionProblem.h:27) */
+  VB_VAR_VEL = 2,       /* vel_world; data 3 (SingleSessionProblem.h:28) */
+  VB_VAR_OMEGA = 3,     /* omega in body-imu frame; data 3 (SingleSessionProblem.h:29) */
+  VB_VAR_CAM_INTR = 4,  /* CameraModelParam; data VB_CAM_DATA, tangent nParams+estRO+estOff */
+  VB_VAR_CAM_EXTR = 5,  /* T_Cam_BodyImu SE3 */
+  VB_VAR_IMU_CALIB = 6, /* ImuCalibParam; data 32 (ImuCalibParam.cpp:214-228), tangent = error state */
+  VB_VAR_IMU_EXTR = 7,  /* T_Imu_BodyImu SE3 */
+  VB_VAR_GRAVITY = 8,   /* S2 gravity: data [x, y, z, radius]; only constant gravity is supported */
+  VB_NUM_VAR_KINDS = 9
+};
+
+/* camera data record (VB_VAR_CAM_INTR rows and camera priors), VB_CAM_DATA doubles:
+ *  [0] model (VB_CAM_LINEAR | VB_CAM_FISHEYE624)  [1] number of projection params
+ *  [2] image width   [3] image height   [4] has readout time (0/1)  [5] readout time [s]
+ *  [6] time offset Dev->Camera [s]      [7] estimate readout (0/1)   [8] estimate time offset (0/1)
+ *  [9 ..] projection params (Linear: fx fy cx cy; Fisheye624: f cx cy k0..k5 p0 p1 s0..s3) */
+#define VB_CAM_DATA 24
+#define VB_CAM_LINEAR 0
+#define VB_CAM_FISHEYE624 1
+#define VB_CAM_MAX_TANGENT 17 /* kMaxCamParams, CameraModelParam.h:17 */
+
+#define VB_IMU_CALIB_DATA 32
+#define VB_IMU_CALIB_MAX_TANGENT 23 /* kMaxCalibrationStateSize, ImuCalibrationJacobianIndices.h:21 */
+
+/* IMU calibration estimation options (ImuCalibrationOptions; default all on, ImuCalibParam.cpp:15-24) */
+#define VB_IMU_OPT_GYRO_BIAS (1 << 0)
+#define VB_IMU_OPT_ACCEL_BIAS (1 << 1)
+#define VB_IMU_OPT_GYRO_SCALE (1 << 2)
+#define VB_IMU_OPT_ACCEL_SCALE (1 << 3)
+#define VB_IMU_OPT_GYRO_NONORTH (1 << 4)
+#define VB_IMU_OPT_ACCEL_NONORTH (1 << 5)
+#define VB_IMU_OPT_REF_TIME_OFFSET (1 << 6)
+#define VB_IMU_OPT_GYRO_ACCEL_TIME_OFFSET (1 << 7)
+#define VB_IMU_OPT_ALL 0xff
+
+/* ---------------------------------------------------------------- factor kinds
+ * var handle order per factor row, and constants per row (doubles):              */
+enum vb_factor_kind {
+  /* VisualFactor / RollingShutterVisualFactor (VisualFactor.cpp:36-214, added at :216-264)
+   * vars  [point, pose, cam_extr, cam_intr, vel]  (vel = -1 and rs = -1 for global shutter)
+   * ivals [rs_table]  consts [u, v, sqrtH00, sqrtH01, sqrtH10, sqrtH11]; loss = reprojection loss */
+  VB_F_VISUAL = 0,
+  /* InertialFactor (InertialFactor.cpp:19-127, added at :322-332)
+   * vars [imu_calib, prev_pose, prev_vel, next_pose, next_vel, gravity]
+   * consts VB_PREINT_CONSTS: [R qx qy qz qw, dV 3, dP 3, dtSec, J 9x23 col-major (207),
+   *                           rvpCov 9x9 col-major (81), calibEvalPoint 32]; loss = imu loss */
+  VB_F_IMU = 1,
+  /* SecondaryImuInertialFactor, common extrinsics (InertialFactor.cpp:256-301, added :339-351)
+   * vars [imu_calib, prev_pose, prev_vel, prev_omega, next_pose, next_vel, next_omega,
+   *       imu_extr, gravity]; consts VB_PREINT_CONSTS */
+  VB_F_IMU_SEC_COMMON = 2,
+  /* SecondaryImuInertialFactor, split extrinsics (InertialFactor.cpp:190-254, added :356-369)
+   * vars [imu_calib, prev_pose, prev_vel, prev_omega, prev_imu_extr, next_pose, next_vel,
+   *       next_omega, next_imu_extr, gravity]; consts VB_PREINT_CONSTS */
+  VB_F_IMU_SEC_SPLIT = 3,
+  /* addOmegaPriorFactor (OmegaPriorFactor.cpp:16-62): vars [omega, imu_extr or -1]
+   * consts [omega_imu 3, sigma] (sigma = kMultiImuOmegaPriorStdRadSec, Constants.h:19) */
+  VB_F_OMEGA_PRIOR = 4,
+  /* RW factors (RandomWalkFactor.cpp): vars [prev, next]; consts diagSqrtH (tangent dim) */
+  VB_F_RW_IMU_CALIB = 5, /* :16-55 (residual zero-padded to 23) */
+  VB_F_RW_CAM_INTR = 6,  /* :57-94 (residual zero-padded to 17) */
+  VB_F_RW_IMU_EXTR = 7,  /* :96-130 */
+  VB_F_RW_CAM_EXTR = 8,  /* :132-166 */
+  /* priors (PriorFactor.cpp) */
+  VB_F_POSE_PRIOR = 9,      /* :37-55  vars [pose]; consts [prior T_bodyImu_world 7, H 6x6 (36)] */
+  VB_F_IMU_PRIOR = 10,      /* :82-109 vars [imu_calib]; consts [prior data 32, diagH (tangent)] */
+  VB_F_CAM_INTR_PRIOR = 11, /* :111-136 vars [cam_intr]; consts [prior cam data 24, diagH] */
+  VB_F_CAM_EXTR_PRIOR = 12, /* :138-156 vars [cam_extr]; consts [prior SE3 7, diagH 6] */
+  VB_F_IMU_EXTR_PRIOR = 13, /* :158-176 vars [imu_extr]; consts [prior SE3 7, diagH 6] */
+  VB_NUM_FACTOR_KINDS = 14
+};
+
+#define VB_PREINT_CONSTS (4 + 3 + 3 + 1 + 9 * 23 + 81 + 32)
+
+/* number of variable handles per factor row and constants per row for each kind; constants of the
+ * RW / prior kinds are padded to their maximum size (diagonals beyond the tangent dim ignored) */
+int vb_factor_num_vars(int kind);
+int vb_factor_num_consts(int kind);
+
+/* ---------------------------------------------------------------- settings / summary */
+typedef struct vb_config {
+  double reproj_loss_radius;  /* HuberLossWithCutoff a (kReprojectionErrorHuberLossWidth = 1) */
+  double reproj_loss_cutoff;  /* k (kReprojectionErrorHuberLossCutoff = 3) */
+  double imu_loss_radius;     /* +inf by default (Constants.h:24) */
+  double imu_loss_cutoff;     /* +inf */
+  int32_t imu_calib_options;  /* VB_IMU_OPT_* mask */
+  int32_t device;             /* HIP device ordinal */
+  int32_t tile;               /* reduced-system tile size (0 = default) */
+  int32_t reserved;
+} vb_config;
+
+/* Optimizer::Settings (lib/small_thing/Optimizer.h:40-91), direct-solver subset */
+typedef struct vb_settings {
+  int32_t max_num_iterations;          /* 50 */
+  int32_t stop_if_no_improvement_for;  /* 3 */
+  int32_t distance_from_troubled_iteration; /* 3 */
+  int32_t max_step_factor_attempts;    /* 2 */
+  int32_t try_sub_step;                /* 1 */
+  int32_t verbose;                     /* log through callback */
+  double absolute_cost_tolerance;      /* 1e-8 */
+  double relative_cost_tolerance;      /* 1e-10 */
+  double variables_tolerance;          /* 1e-5 */
+  double damping;                      /* 1e-5 */
+  double damping_adjust_on_fail;       /* 2.5 */
+  double damping_adjust_on_good_step;  /* 0.7 */
+  double damping_adjust_on_average_step; /* 1.5 */
+  double damping_max;                  /* 1e8 */
+  double damping_min;                  /* 1e-9 */
+  double min_relative_cost_reduction;  /* 0.3 */
+  double step_factor_decrease;         /* 0.3 */
+  double min_step_factor_for_good;     /* 0.7 */
+} vb_settings;
+
+typedef struct vb_summary { /* Optimizer::Summary (Optimizer.h:93-99) */
+  double initial_cost;
+  double final_cost;
+  int32_t num_troubled_seqs;
+  int32_t largest_troubled_seq;
+  int32_t num_iterations;
+  int32_t reserved;
+} vb_summary;
+
+typedef struct vb_cost_stats { /* CostStats (Factor.h:20-30) */
+  int64_t num_total;
+  int64_t num_invalid;
+  int64_t num_prev_invalid;
+} vb_cost_stats;
+
+typedef struct vb_phase_times { /* per-phase device time of the last LM iteration [ms] */
+  double linearize_ms, schur_ms, factor_ms, solve_ms, step_ms, cost_ms, total_ms;
+} vb_phase_times;
+
+typedef void (*vb_log_cb)(const char* msg, void* user);
+typedef void (*vb_prestep_cb)(int iteration, void* user);
+
+typedef struct vb_handle_s* vb_handle;
+
+/* ---------------------------------------------------------------- lifecycle */
+void vb_default_config(vb_config* cfg);
+void vb_default_settings(vb_settings* s);
+int vb_create(const vb_config* cfg, vb_handle* out);
+int vb_destroy(vb_handle h);
+const char* vb_last_error(void);
+
+/* set (or replace before finalize) all variables of one kind: n rows of data (row size per kind:
+ * 3/7/3/3/VB_CAM_DATA/7/32/7/4), constant[n] = 1 marks a constant variable (setConstant) */
+int vb_set_vars(vb_handle h, int kind, int64_t n, const double* data, const uint8_t* constant);
+/* append n factors of one kind: var_idx[n * vb_factor_num_vars(kind)],
+ * ivals[n] (VB_F_VISUAL: rs table index or -1; ignored/NULL for other kinds),
+ * consts[n * vb_factor_num_consts(kind)] */
+int vb_add_factors(vb_handle h, int kind, int64_t n, const int32_t* var_idx, const int32_t* ivals,
+                   const double* consts);
+/* rolling-shutter tables (RollingShutterData::sampledRvp_ / interp_ / gravityWorld_):
+ * table t owns samples [offsets[t], offsets[t+1]) with 11 doubles each
+ * [R qx qy qz qw, dV 3, dP 3, dtSec] and (count-1) interpolants of 9 doubles each
+ * [gyroRadSec 3, accelMSec2 3, deltaVelMSec 3] stored at interp[(offsets[t] - t) * 9 ...];
+ * gravity[3 * t] = gravityWorld */
+int vb_set_rs_tables(vb_handle h, int32_t n_tables, const int64_t* offsets, const double* samples,
+                     const double* interp, const double* gravity);
+/* build the symbolic structure (≙ Optimizer::initSolver) and upload everything to HBM */
+int vb_finalize(vb_handle h);
+int64_t vb_reduced_order(vb_handle h);   /* order of the Schur-reduced (non-point) system */
+int64_t vb_total_order(vb_handle h);     /* all registered tangent dims (points included) */
+
+/* ---------------------------------------------------------------- LM building blocks */
+/* Optimizer::computeGradHess (updateCachedResults, dontRetryFailed semantics of Factor.h:543-661);
+ * linearizes at the current variables and keeps J/e on device; returns the cost */
+int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* cost);
+/* addDamping(lambda) + factor + solve(step = grad) (Optimizer.cpp:826-833): returns
+ * model_cost_reduction = 0.5 * step . grad; the step is kept on device (negated, as :857) */
+int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reduction);
+/* gradient at the current variables (computeGradHess with hess = nullptr, :910-917) and
+ * back_red = -0.5 * grad_new . step */
+int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red);
+/* sub-step: solve with the gradient computed by vb_gradient_dot_step using the existing factor,
+ * negate, and store as the sub-step (Optimizer.cpp:958-972) */
+int vb_solve_with_new_gradient(vb_handle h);
+/* step *= factor (in place) */
+int vb_scale_step(vb_handle h, double factor);
+/* applyStep(step) or applyStep(substep) (which = 0 / 1); ratios = {Linf, L2, L1} */
+int vb_apply_step(vb_handle h, int which, double ratios[3]);
+/* Optimizer::computeCost(makeComparableWithStored, &stats) (Factor.h:390-417, 664-701) */
+int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats);
+int vb_backup(vb_handle h);
+int vb_restore(vb_handle h);
+/* download variables of one kind (row layout as vb_set_vars) */
+int vb_get_vars(vb_handle h, int kind, double* out);
+/* download the last step (negated solution, per variable kind, rows of the kind's tangent size;
+ * constant / unregistered variables get zeros); which = 0 step, 1 sub-step */
+int vb_get_step(vb_handle h, int which, int kind, double* out);
+/* download gradient (as computed by the last vb_linearize) per kind, like vb_get_step */
+int vb_get_gradient(vb_handle h, int kind, double* out);
+
+/* ---------------------------------------------------------------- full loop */
+/* Optimizer::optimize (Optimizer.cpp:768-1106, direct solver) */
+int vb_optimize(vb_handle h, const vb_settings* s, vb_log_cb log, vb_prestep_cb prestep, void* user,
+                vb_summary* out);
+int vb_last_phase_times(vb_handle h, vb_phase_times* out);
+
+/* ---------------------------------------------------------------- multi-device (landmark shards)
+ * Restrict the visual factors this handle linearizes to landmarks [lm_begin, lm_end) and mark the
+ * handle as a non-root shard (is_root = 0: small factors are skipped). The partial reduced system
+ * is exchanged by the caller through the device pointers below (RCCL reduce in bench/driver). */
+int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_root);
+/* device pointers + sizes (in doubles) of the reduced matrix storage and the reduced RHS */
+int vb_reduced_buffers(vb_handle h, double** matrix, int64_t* matrix_len, double** rhs,
+                       int64_t* rhs_len);
+/* split of vb_damp_factor_solve for sharded use: (1) assemble/eliminate into the reduced buffers,
+ * (2) factor + solve the reduced system (root), (3) back-substitute points from a given reduced
+ * solution already placed in the rhs buffer */
+int vb_assemble_reduced(vb_handle h, double lambda);
+int vb_factor_solve_reduced(vb_handle h);
+int vb_back_substitute(vb_handle h, double* model_cost_reduction_partial);
+/* the HIP stream of the handle (hipStream_t), for interop with torch / RCCL */
+void* vb_stream(vb_handle h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VIBA_HIP_H */

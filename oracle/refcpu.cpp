@@ -1,0 +1,1172 @@
+// ORACLE / TEST INFRASTRUCTURE ONLY.
+//
+// refcpu: single-threaded CPU restatement of the reference LM inner loop, used (a) as the parity
+// checker of the HIP path in tests/ and __graft_entry__.smoke(), and (b) as the timed CPU
+// baseline ("port") in bench.py.  It is never linked into, loaded by, or called from the product
+// library (visual_inertial_bundle_adjustment_amd/csrc).
+//
+// What it restates (file:line in /root/reference):
+//   FactorStore::computeSingleGradHess / computeGradHess     lib/small_thing/Factor.h:543-661,704-734
+//   FactorStore::computeSingleCost / computeCost             lib/small_thing/Factor.h:390-417,664-701
+//   HuberLossWithCutoff::{val, jet2}                        lib/small_thing/SoftLoss.h:115-176
+//   Optimizer::addDamping / applyStep / backup / restore    lib/small_thing/Optimizer.cpp:99-146
+//   Optimizer::optimize (direct solver branch)              lib/small_thing/Optimizer.cpp:768-1106
+//   VarSpec box-plus of Vec/SE3 (Variable.h:25-127), camera (CameraModelParam.cpp:54-67),
+//   IMU calib (ImuCalibParam.cpp:55-116)
+//   factor functors                                          viba/problem/*Factor.cpp (ref_factors.hpp)
+// The sparse direct solve of BaSpaCho (absent, un-vendored) is restated as: exact Schur
+// elimination of the point range (3x3 Cholesky per point, as BaSpaCho's "sparse elimination"
+// of elimRanges {0, nPts}) followed by an envelope (skyline) Cholesky of the reduced system.
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include "ref_factors.hpp"
+
+using namespace refcpu;
+
+namespace {
+
+thread_local std::string g_err;
+
+constexpr int kVarData[9] = {3, 7, 3, 3, 24, 7, 32, 7, 4};
+constexpr int kNumVars[14] = {5, 6, 9, 10, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1};
+constexpr int kNumConsts[14] = {6, 331, 331, 331, 4, 23, 17, 6, 6, 43, 55, 41, 13, 13};
+
+struct Loss {  // HuberLossWithCutoff (SoftLoss.h:115-176)
+  double a, b, k2, h;
+  bool trivial;
+  Loss(double a_ = 1, double k_ = 3) { set(a_, k_); }
+  void set(double a_, double k_) {
+    trivial = !std::isfinite(a_);
+    a = a_, b = a_ * a_, k2 = k_ * k_, h = 2.0 * a_ * k_ - b;
+  }
+  double val(double s) const {
+    if (trivial) return s;  // a = +inf: s > k2 and s > b are never true
+    if (s > k2) return h;
+    if (s > b) return 2.0 * a * std::sqrt(s) - b;
+    return s;
+  }
+  void jet2(double s, double& v, double& d) const {
+    if (trivial || s <= b) {
+      v = s, d = 1.0;
+    } else if (s > k2) {
+      v = h, d = 0.0;
+    } else {
+      const double r = std::sqrt(s);
+      d = a / r;
+      v = 2.0 * a * r - b;
+    }
+  }
+};
+
+struct VarRef {
+  int kind, handle;
+};
+
+struct Problem {
+  Loss reprojLoss{1, 3}, imuLoss{INFINITY, INFINITY};
+  ImuJacInd jac{0xff};
+  std::vector<double> data[9];
+  std::vector<uint8_t> cst[9];
+  std::vector<int32_t> fvars[14];
+  std::vector<int32_t> fint[14];
+  std::vector<double> fconst[14];
+  std::vector<RSTable> rs;
+  bool finalized = false;
+
+  // registration
+  std::vector<int64_t> pidx[9];   // param index per var, -1 if unregistered
+  std::vector<VarRef> params;     // param -> var
+  std::vector<int> pdim;          // tangent dim per param
+  std::vector<int64_t> pstart;    // offset in full vector
+  int64_t nPts = 0;               // elimination range [0, nPts)
+  int64_t order = 0;              // total dims
+
+  // reduced (non-point) system
+  std::vector<int64_t> redPos;    // param -> position in reduced order (params >= nPts)
+  std::vector<int64_t> redStart;  // reduced param -> row offset (in reduced order)
+  std::vector<int64_t> rowFirst;  // envelope first column per reduced row
+  std::vector<int64_t> rowOff;    // offset of row i's first stored element
+  int64_t nRed = 0;               // reduced dims
+  std::vector<double> Hred;       // skyline storage (lower, by rows)
+  std::vector<double> Vpt;        // point diag blocks 3x3 (nPts*9)
+  // point -> coupled reduced params (sorted) and W block offsets
+  std::vector<int64_t> ptCoupStart;
+  std::vector<int64_t> ptCoupParam;
+  std::vector<int64_t> ptCoupOff;
+  std::vector<double> W;          // blocks 3 x d (col-major) per (point, reduced param)
+  std::vector<double> grad;       // full gradient (param order)
+  std::vector<double> cache;      // ResultCache per visual factor
+  // factorization state
+  std::vector<double> L;          // skyline factor
+  std::vector<double> Vchol;      // per point lower Cholesky (9 doubles)
+  std::vector<double> step, substep, gradNew;
+  std::vector<double> backup[9];
+};
+
+inline int varTdim(const Problem& P, int kind, int h) {
+  switch (kind) {
+    case 0: return 3;
+    case 1: return 6;
+    case 2: return 3;
+    case 3: return 3;
+    case 4: return CamModel::fromData(&P.data[4][(size_t)h * 24]).tdim();
+    case 5: return 6;
+    case 6: return P.jac.size;
+    case 7: return 6;
+    case 8: return 2;
+  }
+  return 0;
+}
+
+// kinds of variables for each factor kind (argument order as in the reference functor)
+const int kFK[14][10] = {
+    {0, 1, 5, 4, 2},                          // visual: point pose extr cam vel
+    {6, 1, 2, 1, 2, 8},                       // imu
+    {6, 1, 2, 3, 1, 2, 3, 7, 8},              // sec common
+    {6, 1, 2, 3, 7, 1, 2, 3, 7, 8},           // sec split
+    {3, 7},                                   // omega prior
+    {6, 6}, {4, 4}, {7, 7}, {5, 5},           // RW
+    {1}, {6}, {4}, {5}, {7}};                 // priors
+
+inline SE3 poseOf(const Problem& P, int kind, int h) { return SE3::fromData(&P.data[kind][(size_t)h * 7]); }
+inline V3 vecOf(const Problem& P, int kind, int h) {
+  const double* d = &P.data[kind][(size_t)h * 3];
+  return v3(d[0], d[1], d[2]);
+}
+inline ImuModel imuOf(const Problem& P, int h) {
+  ImuModel m;
+  std::memcpy(m.d, &P.data[6][(size_t)h * 32], sizeof(m.d));
+  return m;
+}
+
+// evaluate factor k of kind fk; wants[] per var slot; info: precision (for IMU and pose prior)
+struct EvalOut {
+  FactorEval fe;
+  const Loss* loss = nullptr;  // nullptr -> trivial
+  Mat P;                       // precision (empty = identity)
+  bool optionalErr = false;
+};
+
+EvalOut evalFactor(const Problem& P, int fk, int64_t k, const bool* wants) {
+  const int nv = kNumVars[fk];
+  const int32_t* vi = &P.fvars[fk][(size_t)k * nv];
+  const double* c = &P.fconst[fk][(size_t)k * kNumConsts[fk]];
+  EvalOut o;
+  switch (fk) {
+    case 0: {
+      o.loss = &P.reprojLoss;
+      o.optionalErr = true;
+      const double* pd = &P.data[0][(size_t)vi[0] * 3];
+      V3 X = v3(pd[0], pd[1], pd[2]);
+      SE3 T = poseOf(P, 1, vi[1]), E = poseOf(P, 5, vi[2]);
+      CamModel cam = CamModel::fromData(&P.data[4][(size_t)vi[3] * 24]);
+      const int rs = P.fint[0][k];
+      if (rs < 0) {
+        o.fe = visualFactor(c, c + 2, X, T, E, cam, wants);
+        o.fe.J.resize(5);
+      } else {
+        V3 vel = vecOf(P, 2, vi[4]);
+        o.fe = rsVisualFactor(c, c + 2, P.rs[rs], X, T, E, cam, vel, wants);
+      }
+      break;
+    }
+    case 1: case 2: case 3: {
+      o.loss = &P.imuLoss;
+      Preint pi = Preint::fromConsts(c, P.jac.size);
+      o.P = spd_inverse(pi.cov);  // InertialFactor.cpp:313
+      ImuModel cal = imuOf(P, vi[0]);
+      const int gi = vi[nv - 1];
+      const double* gd = &P.data[8][(size_t)gi * 4];
+      V3 g = v3(gd[0], gd[1], gd[2]);
+      if (fk == 1) {
+        o.fe = inertialFactor(pi, P.jac, cal, poseOf(P, 1, vi[1]), vecOf(P, 2, vi[2]), poseOf(P, 1, vi[3]),
+                              vecOf(P, 2, vi[4]), g, wants);
+        o.fe.J.resize(6);
+      } else if (fk == 3) {
+        o.fe = secImuFactor(pi, P.jac, cal, poseOf(P, 1, vi[1]), vecOf(P, 2, vi[2]), vecOf(P, 3, vi[3]),
+                            poseOf(P, 7, vi[4]), poseOf(P, 1, vi[5]), vecOf(P, 2, vi[6]), vecOf(P, 3, vi[7]),
+                            poseOf(P, 7, vi[8]), g, wants);
+        o.fe.J.resize(10);
+      } else {
+        // common extrinsics: the split form with both extrinsics = common, J_common = J_prev + J_next
+        bool w9[9] = {wants[0], wants[1], wants[2], wants[3], wants[7],
+                      wants[4], wants[5], wants[6], wants[7]};
+        SE3 E = poseOf(P, 7, vi[7]);
+        FactorEval f = secImuFactor(pi, P.jac, cal, poseOf(P, 1, vi[1]), vecOf(P, 2, vi[2]),
+                                    vecOf(P, 3, vi[3]), E, poseOf(P, 1, vi[4]), vecOf(P, 2, vi[5]),
+                                    vecOf(P, 3, vi[6]), E, g, w9);
+        o.fe.e = f.e;
+        o.fe.J.resize(9);
+        o.fe.J[0] = f.J[0], o.fe.J[1] = f.J[1], o.fe.J[2] = f.J[2], o.fe.J[3] = f.J[3];
+        o.fe.J[4] = f.J[5], o.fe.J[5] = f.J[6], o.fe.J[6] = f.J[7];
+        if (wants[7]) o.fe.J[7] = add(f.J[4], f.J[8]);
+      }
+      break;
+    }
+    case 4: {
+      V3 om = vecOf(P, 3, vi[0]);
+      if (vi[1] < 0) {
+        o.fe = omegaPrior(om, c, nullptr, wants);
+      } else {
+        SE3 E = poseOf(P, 7, vi[1]);
+        o.fe = omegaPrior(om, c, &E, wants);
+      }
+      break;
+    }
+    case 5: {  // imu calib RW, residual padded to 23
+      const int n = P.jac.size;
+      ImuModel a = imuOf(P, vi[0]), b = imuOf(P, vi[1]);
+      double d[23] = {0};
+      imu_boxMinus(b, a, P.jac, d);
+      o.fe.e.assign(23, 0.0);
+      for (int i = 0; i < n; i++) o.fe.e[i] = d[i] * c[i];
+      o.fe.J.resize(2);
+      if (wants[0]) {
+        o.fe.J[0] = Mat(23, n);
+        for (int i = 0; i < n; i++) o.fe.J[0](i, i) = -c[i];
+      }
+      if (wants[1]) {
+        o.fe.J[1] = Mat(23, n);
+        for (int i = 0; i < n; i++) o.fe.J[1](i, i) = c[i];
+      }
+      break;
+    }
+    case 6: {  // cam intr RW, residual padded to 17
+      CamModel a = CamModel::fromData(&P.data[4][(size_t)vi[0] * 24]);
+      CamModel b = CamModel::fromData(&P.data[4][(size_t)vi[1] * 24]);
+      const int n = a.tdim();
+      double d[17] = {0};
+      cam_boxMinus(b, a, d);
+      o.fe.e.assign(17, 0.0);
+      for (int i = 0; i < n; i++) o.fe.e[i] = d[i] * c[i];
+      o.fe.J.resize(2);
+      if (wants[0]) {
+        o.fe.J[0] = Mat(17, n);
+        for (int i = 0; i < n; i++) o.fe.J[0](i, i) = -c[i];
+      }
+      if (wants[1]) {
+        o.fe.J[1] = Mat(17, n);
+        for (int i = 0; i < n; i++) o.fe.J[1](i, i) = c[i];
+      }
+      break;
+    }
+    case 7: case 8: {
+      const int kk = fk == 7 ? 7 : 5;
+      o.fe = se3RW(poseOf(P, kk, vi[0]), poseOf(P, kk, vi[1]), c, wants);
+      break;
+    }
+    case 9: {
+      SE3 prior = SE3::fromData(c);
+      o.fe = posePrior(poseOf(P, 1, vi[0]), prior.inverse(), wants[0]);
+      o.P = Mat(6, 6);
+      for (int i = 0; i < 36; i++) o.P.a[i] = c[7 + i];
+      break;
+    }
+    case 10: {
+      const int n = P.jac.size;
+      ImuModel a = imuOf(P, vi[0]), pr;
+      std::memcpy(pr.d, c, sizeof(pr.d));
+      double d[23] = {0};
+      imu_boxMinus(a, pr, P.jac, d);
+      o.fe.e.assign(23, 0.0);
+      for (int i = 0; i < n; i++) o.fe.e[i] = d[i] * std::sqrt(c[32 + i]);
+      o.fe.J.resize(1);
+      if (wants[0]) {
+        o.fe.J[0] = Mat(23, n);
+        for (int i = 0; i < n; i++) o.fe.J[0](i, i) = std::sqrt(c[32 + i]);
+      }
+      break;
+    }
+    case 11: {
+      CamModel a = CamModel::fromData(&P.data[4][(size_t)vi[0] * 24]);
+      CamModel pr = CamModel::fromData(c);
+      const int n = a.tdim();
+      double d[17] = {0};
+      cam_boxMinus(a, pr, d);
+      o.fe.e.assign(17, 0.0);
+      for (int i = 0; i < n; i++) o.fe.e[i] = d[i] * std::sqrt(c[24 + i]);
+      o.fe.J.resize(1);
+      if (wants[0]) {
+        o.fe.J[0] = Mat(17, n);
+        for (int i = 0; i < n; i++) o.fe.J[0](i, i) = std::sqrt(c[24 + i]);
+      }
+      break;
+    }
+    case 12: case 13: {
+      const int kk = fk == 12 ? 5 : 7;
+      double sq[6];
+      for (int i = 0; i < 6; i++) sq[i] = std::sqrt(c[7 + i]);
+      o.fe = se3Prior(poseOf(P, kk, vi[0]), SE3::fromData(c).inverse(), sq, wants[0]);
+      break;
+    }
+  }
+  return o;
+}
+
+double squaredError(const EvalOut& o) {
+  const auto& e = o.fe.e;
+  if (o.P.r == 0) {
+    double s = 0;
+    for (double v : e) s += v * v;
+    return s;
+  }
+  double s = 0;
+  for (int i = 0; i < o.P.r; i++)
+    for (int j = 0; j < o.P.c; j++) s += e[i] * o.P(i, j) * e[j];
+  return s;
+}
+
+// ------------------------------------------------------------------ registration / structure
+int64_t redElem(const Problem& P, int64_t i, int64_t j) {  // reduced (row, col), row >= col
+  return P.rowOff[i] + (j - P.rowFirst[i]);
+}
+
+void finalize(Problem& P) {
+  for (int k = 0; k < 9; k++) P.pidx[k].assign(P.cst[k].size(), -1);
+  P.params.clear(), P.pdim.clear();
+  auto reg = [&](int kind, int h) {
+    if (h < 0) return;
+    if (P.cst[kind][h]) return;
+    if (P.pidx[kind][h] >= 0) return;
+    P.pidx[kind][h] = (int64_t)P.params.size();
+    P.params.push_back({kind, h});
+    P.pdim.push_back(varTdim(P, kind, h));
+  };
+  // points first (registerPointVariables + registeredVariablesToEliminationRange)
+  for (size_t f = 0; f < P.fvars[0].size() / 5; f++) reg(0, P.fvars[0][f * 5]);
+  P.nPts = (int64_t)P.params.size();
+  for (int fk = 0; fk < 14; fk++) {
+    const int nv = kNumVars[fk];
+    for (size_t f = 0; f < P.fvars[fk].size() / nv; f++)
+      for (int s = 0; s < nv; s++) {
+        if (kFK[fk][s] == 8) {
+          int g = P.fvars[fk][f * nv + s];
+          if (g >= 0 && !P.cst[8][g]) throw std::invalid_argument("non-constant gravity unsupported");
+          continue;
+        }
+        reg(kFK[fk][s], P.fvars[fk][f * nv + s]);
+      }
+  }
+  const int64_t nParams = (int64_t)P.params.size();
+  P.pstart.resize(nParams);
+  int64_t off = 0;
+  for (int64_t i = 0; i < nParams; i++) P.pstart[i] = off, off += P.pdim[i];
+  P.order = off;
+
+  // reduced ordering: key = mean pose ordinal of co-occurring poses (own ordinal for poses)
+  std::vector<double> keySum(nParams, 0.0), keyCnt(nParams, 0.0);
+  for (int fk = 0; fk < 14; fk++) {
+    const int nv = kNumVars[fk];
+    for (size_t f = 0; f < P.fvars[fk].size() / nv; f++) {
+      std::vector<int64_t> ps;
+      std::vector<double> poses;
+      for (int s = 0; s < nv; s++) {
+        int kind = kFK[fk][s], h = P.fvars[fk][f * nv + s];
+        if (kind == 8 || h < 0) continue;
+        if (kind == 1) poses.push_back(h);
+        if (P.pidx[kind][h] >= 0) ps.push_back(P.pidx[kind][h]);
+      }
+      for (int64_t p : ps)
+        for (double h : poses) keySum[p] += h, keyCnt[p] += 1;
+    }
+  }
+  std::vector<int64_t> red;
+  for (int64_t p = P.nPts; p < nParams; p++) red.push_back(p);
+  auto key = [&](int64_t p) {
+    if (P.params[p].kind == 1) return (double)P.params[p].handle;
+    return keyCnt[p] > 0 ? keySum[p] / keyCnt[p] : 1e30;
+  };
+  std::stable_sort(red.begin(), red.end(), [&](int64_t a, int64_t b) {
+    double ka = key(a), kb = key(b);
+    if (ka != kb) return ka < kb;
+    if (P.params[a].kind != P.params[b].kind) return P.params[a].kind < P.params[b].kind;
+    return P.params[a].handle < P.params[b].handle;
+  });
+  P.redPos.assign(nParams, -1);
+  P.redStart.assign(red.size() + 1, 0);
+  for (size_t i = 0; i < red.size(); i++) {
+    P.redPos[red[i]] = (int64_t)i;
+    P.redStart[i + 1] = P.redStart[i] + P.pdim[red[i]];
+  }
+  P.nRed = P.redStart[red.size()];
+
+  // envelope: first column per reduced row, from direct couplings and shared points
+  std::vector<int64_t> firstBlk(red.size());
+  for (size_t i = 0; i < red.size(); i++) firstBlk[i] = (int64_t)i;
+  auto couple = [&](int64_t ra, int64_t rb) {  // reduced positions
+    if (ra < rb) std::swap(ra, rb);
+    firstBlk[ra] = std::min(firstBlk[ra], rb);
+  };
+  // point couplings
+  std::vector<std::vector<int64_t>> ptRed(P.nPts);
+  for (int fk = 0; fk < 14; fk++) {
+    const int nv = kNumVars[fk];
+    for (size_t f = 0; f < P.fvars[fk].size() / nv; f++) {
+      std::vector<int64_t> rs;
+      int64_t pt = -1;
+      for (int s = 0; s < nv; s++) {
+        int kind = kFK[fk][s], h = P.fvars[fk][f * nv + s];
+        if (kind == 8 || h < 0) continue;
+        int64_t p = P.pidx[kind][h];
+        if (p < 0) continue;
+        if (p < P.nPts) pt = p;
+        else rs.push_back(P.redPos[p]);
+      }
+      for (size_t a = 0; a < rs.size(); a++)
+        for (size_t b = 0; b <= a; b++) couple(rs[a], rs[b]);
+      if (pt >= 0)
+        for (int64_t r : rs) ptRed[pt].push_back(r);
+    }
+  }
+  P.ptCoupStart.assign(P.nPts + 1, 0);
+  P.ptCoupParam.clear(), P.ptCoupOff.clear();
+  int64_t woff = 0;
+  for (int64_t pt = 0; pt < P.nPts; pt++) {
+    auto& v = ptRed[pt];
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
+    for (size_t a = 0; a < v.size(); a++)
+      for (size_t b = 0; b <= a; b++) couple(v[a], v[b]);
+    for (int64_t r : v) {
+      P.ptCoupParam.push_back(r);
+      P.ptCoupOff.push_back(woff);
+      woff += 3 * P.pdim[red[r]];
+    }
+    P.ptCoupStart[pt + 1] = (int64_t)P.ptCoupParam.size();
+  }
+  P.W.assign(woff, 0.0);
+  // rows
+  P.rowFirst.assign(P.nRed, 0);
+  P.rowOff.assign(P.nRed + 1, 0);
+  for (size_t i = 0; i < red.size(); i++) {
+    int64_t fc = P.redStart[firstBlk[i]];
+    for (int64_t r = P.redStart[i]; r < P.redStart[i + 1]; r++) P.rowFirst[r] = fc;
+  }
+  for (int64_t r = 0; r < P.nRed; r++) P.rowOff[r + 1] = P.rowOff[r] + (r - P.rowFirst[r] + 1);
+  P.Hred.assign(P.rowOff[P.nRed], 0.0);
+  P.Vpt.assign(P.nPts * 9, 0.0);
+  P.grad.assign(P.order, 0.0);
+  P.cache.assign(P.fvars[0].size() / 5, 0.0);
+  P.step.assign(P.order, 0.0);
+  P.substep.assign(P.order, 0.0);
+  P.gradNew.assign(P.order, 0.0);
+  P.finalized = true;
+}
+
+// add block B (dA x dB) = contribution H_{a,b} for params a, b (b may equal a)
+void addHessBlock(Problem& P, int64_t pa, int64_t pb, const Mat& B) {
+  const bool aPt = pa < P.nPts, bPt = pb < P.nPts;
+  if (aPt && bPt) {  // point diagonal (only a == b possible)
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) P.Vpt[pa * 9 + j * 3 + i] += B(i, j);
+    return;
+  }
+  if (aPt || bPt) {  // point-reduced coupling: store W = H_{pt, red} (3 x d)
+    const int64_t pt = aPt ? pa : pb;
+    const int64_t rp = P.redPos[aPt ? pb : pa];
+    const int64_t s = P.ptCoupStart[pt], e = P.ptCoupStart[pt + 1];
+    int64_t q = std::lower_bound(P.ptCoupParam.begin() + s, P.ptCoupParam.begin() + e, rp) -
+                P.ptCoupParam.begin();
+    double* w = &P.W[P.ptCoupOff[q]];
+    const int d = aPt ? B.c : B.r;
+    for (int j = 0; j < d; j++)
+      for (int i = 0; i < 3; i++) w[j * 3 + i] += aPt ? B(i, j) : B(j, i);
+    return;
+  }
+  const int64_t ra = P.redStart[P.redPos[pa]], rb = P.redStart[P.redPos[pb]];
+  for (int j = 0; j < B.c; j++)
+    for (int i = 0; i < B.r; i++) {
+      int64_t r = ra + i, c = rb + j;
+      if (r < c) {
+        if (pa == pb) continue;  // diagonal block: upper half implied
+        std::swap(r, c);
+      }
+      P.Hred[redElem(P, r, c)] += B(i, j);
+    }
+}
+
+// one factor's grad/hess contribution (Factor.h:543-661, PlainOps)
+double singleGradHess(Problem& P, int fk, int64_t k, double* g, bool hess, bool updateCache,
+                      bool dontRetry) {
+  const int nv = kNumVars[fk];
+  const int32_t* vi = &P.fvars[fk][(size_t)k * nv];
+  bool wants[10] = {false};
+  int64_t pi[10];
+  for (int s = 0; s < nv; s++) {
+    pi[s] = -1;
+    if (kFK[fk][s] == 8 || vi[s] < 0) continue;
+    pi[s] = P.pidx[kFK[fk][s]][vi[s]];
+    wants[s] = pi[s] >= 0;
+  }
+  if (fk == 0 && dontRetry && P.cache[k] < 0.0) return 0.0;
+  EvalOut o = evalFactor(P, fk, k, wants);
+  if (!o.fe.ok) {
+    if (updateCache || dontRetry) P.cache[k] = -1.0;
+    return 0.0;
+  }
+  double rho, drho;
+  const double s2 = squaredError(o);
+  if (o.loss) o.loss->jet2(s2, rho, drho);
+  else rho = s2, drho = 1.0;
+  const int m = (int)o.fe.e.size();
+  Mat e(m, 1);
+  for (int i = 0; i < m; i++) e(i, 0) = o.fe.e[i];
+  std::vector<Mat> A(nv);
+  for (int s = 0; s < nv; s++) {
+    if (!wants[s]) continue;
+    A[s] = o.P.r ? mul(o.P, o.fe.J[s]) : o.fe.J[s];
+    A[s] = scale(A[s], drho);
+    Mat gs = tmul(A[s], e);  // iAdjJac^T e
+    for (int i = 0; i < gs.r; i++) g[P.pstart[pi[s]] + i] += gs(i, 0);
+    if (hess) {
+      for (int t = 0; t < s; t++) {
+        if (!wants[t]) continue;
+        addHessBlock(P, pi[s], pi[t], tmul(A[s], o.fe.J[t]));
+      }
+      addHessBlock(P, pi[s], pi[s], tmul(A[s], o.fe.J[s]));
+    }
+  }
+  double ret = rho * 0.5;
+  if (fk == 0 && updateCache) P.cache[k] = ret;
+  return ret;
+}
+
+double computeGradHess(Problem& P, double* g, bool hess, bool updateCache, bool dontRetry) {
+  if (hess) {
+    std::fill(P.Hred.begin(), P.Hred.end(), 0.0);
+    std::fill(P.Vpt.begin(), P.Vpt.end(), 0.0);
+    std::fill(P.W.begin(), P.W.end(), 0.0);
+  }
+  double cost = 0;
+  for (int fk = 0; fk < 14; fk++) {
+    const int64_t n = (int64_t)P.fvars[fk].size() / kNumVars[fk];
+    for (int64_t k = 0; k < n; k++) cost += singleGradHess(P, fk, k, g, hess, updateCache, dontRetry);
+  }
+  return cost;
+}
+
+// computeSingleCost (Factor.h:390-417) summed as computeCost (Factor.h:664-701)
+double computeCost(Problem& P, bool comparable, int64_t* stats) {
+  double cost = 0;
+  int64_t nTot = 0, nInv = 0, nPrevInv = 0;
+  for (int fk = 0; fk < 14; fk++) {
+    const int nv = kNumVars[fk];
+    const int64_t n = (int64_t)P.fvars[fk].size() / nv;
+    bool wants[10] = {false};
+    for (int64_t k = 0; k < n; k++) {
+      nTot++;
+      EvalOut o = evalFactor(P, fk, k, wants);
+      if (fk == 0) {
+        const double prev = P.cache[k];
+        const bool prevInvalid = prev < 0.0;
+        nInv += o.fe.ok ? 0 : 1;
+        nPrevInv += prevInvalid ? 1 : 0;
+        if (comparable) {
+          if (prevInvalid) continue;
+          if (!o.fe.ok) {
+            cost += prev;
+            continue;
+          }
+        }
+        if (!o.fe.ok) continue;
+      }
+      const double s2 = squaredError(o);
+      cost += (o.loss ? o.loss->val(s2) : s2) * 0.5;
+    }
+  }
+  if (stats) stats[0] = nTot, stats[1] = nInv, stats[2] = nPrevInv;
+  return cost;
+}
+
+// ------------------------------------------------------------------ direct solve
+// addDamping (Optimizer.cpp:136-146) + Schur elimination of points + skyline Cholesky + solve.
+// Returns false on numeric breakdown.
+bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<double>& rhs,
+                    std::vector<double>& x) {
+  const int64_t nPts = P.nPts;
+  if (doFactor) {
+    P.L = P.Hred;
+    // damping on the reduced diagonal
+    for (int64_t r = 0; r < P.nRed; r++) {
+      double& d = P.L[redElem(P, r, r)];
+      d = d * (1.0 + lambda) + lambda;
+    }
+    P.Vchol.assign(nPts * 9, 0.0);
+    for (int64_t pt = 0; pt < nPts; pt++) {
+      Mat V(3, 3);
+      for (int i = 0; i < 9; i++) V.a[i] = P.Vpt[pt * 9 + i];
+      for (int i = 0; i < 3; i++) V(i, i) = V(i, i) * (1.0 + lambda) + lambda;
+      if (!cholesky(V)) return false;
+      for (int i = 0; i < 9; i++) P.Vchol[pt * 9 + i] = V.a[i];
+      // Y = L^-1 W for each coupled block, then S -= Y_a^T Y_b
+      const int64_t s = P.ptCoupStart[pt], e = P.ptCoupStart[pt + 1];
+      std::vector<Mat> Y;
+      for (int64_t q = s; q < e; q++) {
+        const int64_t rp = P.ptCoupParam[q];
+        const int d = (int)(P.redStart[rp + 1] - P.redStart[rp]);
+        Mat Wb(3, d);
+        for (int i = 0; i < 3 * d; i++) Wb.a[i] = P.W[P.ptCoupOff[q] + i];
+        for (int j = 0; j < d; j++) {  // forward solve L y = w
+          double y0 = Wb(0, j) / V(0, 0);
+          double y1 = (Wb(1, j) - V(1, 0) * y0) / V(1, 1);
+          double y2 = (Wb(2, j) - V(2, 0) * y0 - V(2, 1) * y1) / V(2, 2);
+          Wb(0, j) = y0, Wb(1, j) = y1, Wb(2, j) = y2;
+        }
+        Y.push_back(Wb);
+      }
+      for (int64_t a = s; a < e; a++)
+        for (int64_t b = s; b <= a; b++) {
+          const Mat& Ya = Y[a - s];
+          const Mat& Yb = Y[b - s];
+          const int64_t ra = P.redStart[P.ptCoupParam[a]], rb = P.redStart[P.ptCoupParam[b]];
+          for (int i = 0; i < Ya.c; i++)
+            for (int j = 0; j < Yb.c; j++) {
+              if (a == b && j > i) continue;
+              const double v = Ya(0, i) * Yb(0, j) + Ya(1, i) * Yb(1, j) + Ya(2, i) * Yb(2, j);
+              P.L[redElem(P, ra + i, rb + j)] -= v;
+            }
+        }
+    }
+    // skyline Cholesky (row-oriented)
+    for (int64_t i = 0; i < P.nRed; i++) {
+      const int64_t fi = P.rowFirst[i];
+      double* Li = &P.L[P.rowOff[i]];
+      for (int64_t j = fi; j < i; j++) {
+        const int64_t fj = P.rowFirst[j];
+        const double* Lj = &P.L[P.rowOff[j]];
+        const int64_t k0 = std::max(fi, fj);
+        double s = Li[j - fi];
+        for (int64_t k = k0; k < j; k++) s -= Li[k - fi] * Lj[k - fj];
+        Li[j - fi] = s / Lj[j - fj];
+      }
+      double d = Li[i - fi];
+      for (int64_t k = fi; k < i; k++) d -= Li[k - fi] * Li[k - fi];
+      if (!(d > 0)) return false;
+      Li[i - fi] = std::sqrt(d);
+    }
+  }
+  // ---- solve: reduced rhs
+  std::vector<double> r(P.nRed, 0.0);
+  for (int64_t p = nPts; p < (int64_t)P.params.size(); p++) {
+    const int64_t ro = P.redStart[P.redPos[p]];
+    for (int i = 0; i < P.pdim[p]; i++) r[ro + i] = rhs[P.pstart[p] + i];
+  }
+  std::vector<double> z(nPts * 3);
+  for (int64_t pt = 0; pt < nPts; pt++) {
+    const double* V = &P.Vchol[pt * 9];
+    const double* g = &rhs[P.pstart[pt]];
+    double z0 = g[0] / V[0];
+    double z1 = (g[1] - V[1] * z0) / V[4];
+    double z2 = (g[2] - V[2] * z0 - V[5] * z1) / V[8];
+    z[pt * 3] = z0, z[pt * 3 + 1] = z1, z[pt * 3 + 2] = z2;
+    for (int64_t q = P.ptCoupStart[pt]; q < P.ptCoupStart[pt + 1]; q++) {
+      const int64_t rp = P.ptCoupParam[q];
+      const int d = (int)(P.redStart[rp + 1] - P.redStart[rp]);
+      const double* w = &P.W[P.ptCoupOff[q]];
+      for (int j = 0; j < d; j++) {  // Y_j = L^-1 w_j
+        double y0 = w[j * 3] / V[0];
+        double y1 = (w[j * 3 + 1] - V[1] * y0) / V[4];
+        double y2 = (w[j * 3 + 2] - V[2] * y0 - V[5] * y1) / V[8];
+        r[P.redStart[rp] + j] -= y0 * z0 + y1 * z1 + y2 * z2;
+      }
+    }
+  }
+  // forward / backward with the skyline factor
+  for (int64_t i = 0; i < P.nRed; i++) {
+    const int64_t fi = P.rowFirst[i];
+    const double* Li = &P.L[P.rowOff[i]];
+    double s = r[i];
+    for (int64_t k = fi; k < i; k++) s -= Li[k - fi] * r[k];
+    r[i] = s / Li[i - fi];
+  }
+  for (int64_t i = P.nRed - 1; i >= 0; i--) {
+    const int64_t fi = P.rowFirst[i];
+    const double* Li = &P.L[P.rowOff[i]];
+    r[i] /= Li[i - fi];
+    for (int64_t k = fi; k < i; k++) r[k] -= Li[k - fi] * r[i];
+  }
+  x.assign(P.order, 0.0);
+  for (int64_t p = nPts; p < (int64_t)P.params.size(); p++) {
+    const int64_t ro = P.redStart[P.redPos[p]];
+    for (int i = 0; i < P.pdim[p]; i++) x[P.pstart[p] + i] = r[ro + i];
+  }
+  // back-substitute points: x_p = L^-T (z - Y xc)
+  for (int64_t pt = 0; pt < nPts; pt++) {
+    const double* V = &P.Vchol[pt * 9];
+    double t0 = z[pt * 3], t1 = z[pt * 3 + 1], t2 = z[pt * 3 + 2];
+    for (int64_t q = P.ptCoupStart[pt]; q < P.ptCoupStart[pt + 1]; q++) {
+      const int64_t rp = P.ptCoupParam[q];
+      const int d = (int)(P.redStart[rp + 1] - P.redStart[rp]);
+      const double* w = &P.W[P.ptCoupOff[q]];
+      for (int j = 0; j < d; j++) {
+        double y0 = w[j * 3] / V[0];
+        double y1 = (w[j * 3 + 1] - V[1] * y0) / V[4];
+        double y2 = (w[j * 3 + 2] - V[2] * y0 - V[5] * y1) / V[8];
+        const double xv = r[P.redStart[rp] + j];
+        t0 -= y0 * xv, t1 -= y1 * xv, t2 -= y2 * xv;
+      }
+    }
+    const double x2 = t2 / V[8];
+    const double x1 = (t1 - V[5] * x2) / V[4];
+    const double x0 = (t0 - V[1] * x1 - V[2] * x2) / V[0];
+    x[P.pstart[pt]] = x0, x[P.pstart[pt] + 1] = x1, x[P.pstart[pt] + 2] = x2;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ applyStep (Variable.h:352-370)
+void applyStep(Problem& P, const std::vector<double>& st, double ratios[3]) {
+  double maxR = 0, sq = 0, sum = 0;
+  const int64_t nParams = (int64_t)P.params.size();
+  for (int64_t p = 0; p < nParams; p++) {
+    const int kind = P.params[p].kind, h = P.params[p].handle;
+    const double* s = &st[P.pstart[p]];
+    double r = 0;
+    if (kind == 0 || kind == 2 || kind == 3) {  // Vec3: value += step; |s|inf / (1 + |v|inf)
+      double* v = &P.data[kind][(size_t)h * 3];
+      double sn = 0, vn = 0;
+      for (int i = 0; i < 3; i++) v[i] += s[i];
+      for (int i = 0; i < 3; i++) sn = std::max(sn, std::abs(s[i])), vn = std::max(vn, std::abs(v[i]));
+      r = sn / (1.0 + vn);
+    } else if (kind == 1 || kind == 5 || kind == 7) {  // SE3: exp(step) * value
+      double* d = &P.data[kind][(size_t)h * 7];
+      SE3 T = se3_exp(s) * SE3::fromData(d);
+      T.toData(d);
+      double tn = 0, un = 0, rn = 0;
+      for (int i = 0; i < 3; i++)
+        un = std::max(un, std::abs(s[i])), rn = std::max(rn, std::abs(s[3 + i])),
+        tn = std::max(tn, std::abs(T.t[i]));
+      r = std::max(rn, un / (1.0 + tn));
+    } else if (kind == 4) {  // CameraModelParam.cpp:54-67
+      double* d = &P.data[4][(size_t)h * 24];
+      CamModel c = CamModel::fromData(d);
+      int n = c.n;
+      for (int i = 0; i < c.n; i++) c.p[i] += s[i];
+      if (c.estRO) {
+        c.ro = c.readoutTimeSec() + s[n++];
+        c.hasRO = true;
+      }
+      if (c.estOff) c.off += s[n++];
+      c.toData(d);
+      for (int i = 0; i < c.tdim(); i++) r = std::max(r, std::abs(s[i]));
+    } else if (kind == 6) {
+      ImuModel m = imuOf(P, h);
+      imu_boxPlus(m, P.jac, s);
+      std::memcpy(&P.data[6][(size_t)h * 32], m.d, sizeof(m.d));
+      for (int i = 0; i < P.jac.size; i++) r = std::max(r, std::abs(s[i]));
+    }
+    maxR = std::max(maxR, r);
+    sq += r * r;
+    sum += r;
+  }
+  ratios[0] = maxR;
+  ratios[1] = std::sqrt(sq / nParams);
+  ratios[2] = sum / nParams;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI (oracle)
+extern "C" {
+
+typedef void (*ref_log_cb)(const char*, void*);
+typedef void (*ref_prestep_cb)(int, void*);
+
+const char* ref_last_error(void) { return g_err.c_str(); }
+int ref_factor_num_vars(int k) { return (k >= 0 && k < 14) ? kNumVars[k] : -1; }
+int ref_factor_num_consts(int k) { return (k >= 0 && k < 14) ? kNumConsts[k] : -1; }
+
+void* ref_create(double reprojA, double reprojK, double imuA, double imuK, int imuMask) {
+  Problem* P = new Problem();
+  P->reprojLoss.set(reprojA, reprojK);
+  P->imuLoss.set(imuA, imuK);
+  P->jac = ImuJacInd(imuMask);
+  return P;
+}
+void ref_destroy(void* h) { delete (Problem*)h; }
+
+int ref_set_vars(void* h, int kind, int64_t n, const double* data, const uint8_t* cst) {
+  Problem& P = *(Problem*)h;
+  if (kind < 0 || kind >= 9 || P.finalized) return -1;
+  P.data[kind].assign(data, data + n * kVarData[kind]);
+  P.cst[kind].assign(n, 0);
+  if (cst) std::copy(cst, cst + n, P.cst[kind].begin());
+  return 0;
+}
+
+int ref_add_factors(void* h, int kind, int64_t n, const int32_t* vars, const int32_t* ivals,
+                    const double* consts) {
+  Problem& P = *(Problem*)h;
+  if (kind < 0 || kind >= 14 || P.finalized) return -1;
+  P.fvars[kind].insert(P.fvars[kind].end(), vars, vars + n * kNumVars[kind]);
+  for (int64_t i = 0; i < n; i++) P.fint[kind].push_back(ivals ? ivals[i] : -1);
+  P.fconst[kind].insert(P.fconst[kind].end(), consts, consts + n * kNumConsts[kind]);
+  return 0;
+}
+
+int ref_set_rs_tables(void* h, int32_t nt, const int64_t* offsets, const double* samples,
+                      const double* interp, const double* gravity) {
+  Problem& P = *(Problem*)h;
+  P.rs.assign(nt, RSTable());
+  for (int t = 0; t < nt; t++) {
+    RSTable& T = P.rs[t];
+    for (int64_t i = offsets[t]; i < offsets[t + 1]; i++) {
+      const double* s = samples + i * 11;
+      RVP r;
+      r.R = SO3::fromQ(s[0], s[1], s[2], s[3]);
+      r.dV = v3(s[4], s[5], s[6]);
+      r.dP = v3(s[7], s[8], s[9]);
+      r.dt = s[10];
+      T.samples.push_back(r);
+    }
+    for (int64_t i = offsets[t] - t; i < offsets[t + 1] - t - 1; i++) {
+      const double* s = interp + i * 9;
+      RVPInterp ip;
+      ip.gyro = v3(s[0], s[1], s[2]);
+      ip.accel = v3(s[3], s[4], s[5]);
+      ip.dvel = v3(s[6], s[7], s[8]);
+      T.interp.push_back(ip);
+    }
+    T.gravity = v3(gravity[3 * t], gravity[3 * t + 1], gravity[3 * t + 2]);
+  }
+  return 0;
+}
+
+int ref_finalize(void* h) {
+  try {
+    finalize(*(Problem*)h);
+  } catch (std::exception& e) {
+    g_err = e.what();
+    return -6;
+  }
+  return 0;
+}
+int64_t ref_reduced_order(void* h) { return ((Problem*)h)->nRed; }
+int64_t ref_total_order(void* h) { return ((Problem*)h)->order; }
+int64_t ref_num_params(void* h) { return (int64_t)((Problem*)h)->params.size(); }
+
+int ref_linearize(void* h, int updateCache, int dontRetry, double* cost) {
+  Problem& P = *(Problem*)h;
+  try {
+    std::fill(P.grad.begin(), P.grad.end(), 0.0);
+    *cost = computeGradHess(P, P.grad.data(), true, updateCache, dontRetry);
+  } catch (std::range_error& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+
+int ref_damp_factor_solve(void* h, double lambda, double* modelRed) {
+  Problem& P = *(Problem*)h;
+  std::vector<double> x;
+  if (!factorAndSolve(P, lambda, true, P.grad, x)) {
+    g_err = "cholesky breakdown";
+    return -4;
+  }
+  double d = 0;
+  for (int64_t i = 0; i < P.order; i++) d += x[i] * P.grad[i];
+  *modelRed = 0.5 * d;
+  for (int64_t i = 0; i < P.order; i++) P.step[i] = -x[i];
+  return 0;
+}
+
+int ref_gradient_dot_step(void* h, int dontRetry, double* backRed) {
+  Problem& P = *(Problem*)h;
+  try {
+    std::fill(P.gradNew.begin(), P.gradNew.end(), 0.0);
+    computeGradHess(P, P.gradNew.data(), false, false, dontRetry);
+  } catch (std::range_error& e) {
+    g_err = e.what();
+    return -5;
+  }
+  double d = 0;
+  for (int64_t i = 0; i < P.order; i++) d += P.gradNew[i] * P.step[i];
+  *backRed = -0.5 * d;
+  return 0;
+}
+
+int ref_solve_with_new_gradient(void* h) {
+  Problem& P = *(Problem*)h;
+  std::vector<double> x;
+  factorAndSolve(P, 0.0, false, P.gradNew, x);
+  for (int64_t i = 0; i < P.order; i++) P.substep[i] = -x[i];
+  return 0;
+}
+
+int ref_scale_step(void* h, double f) {
+  Problem& P = *(Problem*)h;
+  for (auto& v : P.step) v *= f;
+  return 0;
+}
+
+int ref_apply_step(void* h, int which, double ratios[3]) {
+  Problem& P = *(Problem*)h;
+  applyStep(P, which ? P.substep : P.step, ratios);
+  return 0;
+}
+
+int ref_cost(void* h, int comparable, double* cost, int64_t* stats) {
+  Problem& P = *(Problem*)h;
+  try {
+    *cost = computeCost(P, comparable, stats);
+  } catch (std::range_error& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+
+int ref_backup(void* h) {
+  Problem& P = *(Problem*)h;
+  for (int k = 0; k < 9; k++) P.backup[k] = P.data[k];
+  return 0;
+}
+int ref_restore(void* h) {
+  Problem& P = *(Problem*)h;
+  for (int k = 0; k < 9; k++) P.data[k] = P.backup[k];
+  return 0;
+}
+
+int ref_get_vars(void* h, int kind, double* out) {
+  Problem& P = *(Problem*)h;
+  std::copy(P.data[kind].begin(), P.data[kind].end(), out);
+  return 0;
+}
+
+static int getPerKind(Problem& P, const std::vector<double>& v, int kind, double* out) {
+  const int64_t n = (int64_t)P.cst[kind].size();
+  int maxd = kind == 4 ? 17 : kind == 6 ? 23 : kind == 1 || kind == 5 || kind == 7 ? 6 : kind == 8 ? 2 : 3;
+  std::fill(out, out + n * maxd, 0.0);
+  for (int64_t hh = 0; hh < n; hh++) {
+    const int64_t p = P.pidx[kind][hh];
+    if (p < 0) continue;
+    for (int i = 0; i < P.pdim[p]; i++) out[hh * maxd + i] = v[P.pstart[p] + i];
+  }
+  return 0;
+}
+int ref_get_step(void* h, int which, int kind, double* out) {
+  Problem& P = *(Problem*)h;
+  return getPerKind(P, which ? P.substep : P.step, kind, out);
+}
+int ref_get_gradient(void* h, int kind, double* out) {
+  Problem& P = *(Problem*)h;
+  return getPerKind(P, P.grad, kind, out);
+}
+
+// Optimizer::optimize (Optimizer.cpp:768-1106), direct solver; settings as vb_settings layout
+struct RefSettings {
+  int32_t maxIt, stopNoImpr, distTroubled, maxStepAttempts, trySubStep, verbose;
+  double absTol, relTol, varTol, damping, dFail, dGood, dAvg, dMax, dMin, minRelRed, stepDec,
+      minStepGood;
+};
+struct RefSummary {
+  double initialCost, finalCost;
+  int32_t numTroubledSeqs, largestTroubledSeq, numIterations, reserved;
+};
+
+int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb pre, void* user,
+                 RefSummary* out) {
+  Problem& P = *(Problem*)h;
+  double damping = s->damping;
+  int it = 0, lastImpr = 0, lastTroubled = -10;
+  double initialCost = 0, finalCost = 0, troubledStartDamping = damping;
+  int troubledStart = 0, nTroubled = 0, largestTroubled = 0;
+  bool dontRetry = false;
+  char buf[512];
+  auto acceptable = [](const int64_t* st) {
+    const double rate = st[1] / (st[0] + 1.0);
+    return rate < 0.03 && (st[1] < st[2] * 2.0 + 50);
+  };
+  int rc;
+  while (true) {
+    if (pre) pre(it, user);
+    double prevCost;
+    if ((rc = ref_linearize(h, 1, dontRetry, &prevCost))) return rc;
+    finalCost = prevCost;
+    if (it == 0) initialCost = prevCost;
+    double modelRed;
+    if ((rc = ref_damp_factor_solve(h, damping, &modelRed))) return rc;
+    if (modelRed < 0) {  // :835-854 (the `continue` leaves the do-while: old step is kept)
+      double c2;
+      if ((rc = ref_linearize(h, 1, dontRetry, &c2))) return rc;
+      damping *= s->dFail;
+    }
+    ref_backup(h);
+    double ratios[3];
+    ref_apply_step(h, 0, ratios);
+    int64_t st[3];
+    double newCost;
+    if ((rc = ref_cost(h, 1, &newCost, st))) return rc;
+    double costRed = prevCost - newCost;
+    const double ratioRedToCost = costRed / newCost;
+    double ratioRedToExp = costRed / modelRed;
+    double applied = 1.0;
+    bool okRate = acceptable(st);
+    if (s->maxStepAttempts > 0 && (ratioRedToExp < s->minRelRed || !okRate)) {
+      double backRed;
+      if ((rc = ref_gradient_dot_step(h, dontRetry, &backRed))) return rc;
+      double sf = backRed > 0 ? modelRed / (modelRed + backRed) : s->stepDec;
+      for (int i = 0; i < s->maxStepAttempts; i++) {
+        applied *= sf;
+        ref_scale_step(h, sf);
+        ref_restore(h);
+        ref_apply_step(h, 0, ratios + 0);  // ratios of scaled steps are not used later
+        int64_t stF[3];
+        double costF;
+        if ((rc = ref_cost(h, 1, &costF, stF))) return rc;
+        const double redF = prevCost - newCost;  // :935 reference quirk (uses full-step cost)
+        const double rF = redF / (modelRed * applied);
+        if (rF >= s->minRelRed && acceptable(stF)) {
+          newCost = costF;
+          std::copy(stF, stF + 3, st);
+          costRed = redF;
+          ratioRedToExp = rF;
+          okRate = true;
+          break;
+        }
+        if (s->trySubStep) {
+          double br;
+          if ((rc = ref_gradient_dot_step(h, dontRetry, &br))) return rc;
+          ref_solve_with_new_gradient(h);
+          double rr[3];
+          ref_apply_step(h, 1, rr);
+          int64_t stS[3];
+          double costS;
+          if ((rc = ref_cost(h, 1, &costS, stS))) return rc;
+          const double redS = prevCost - costS;
+          const double rS = redS / (modelRed * applied);
+          if (rS >= s->minRelRed && acceptable(stS)) {
+            newCost = costS;
+            std::copy(stS, stS + 3, st);
+            costRed = redS;
+            ratioRedToExp = rS;
+            okRate = true;
+            break;
+          }
+        }
+        dontRetry = true;
+        sf = s->stepDec;
+      }
+    }
+    const char* tol = ratioRedToCost < s->relTol ? "relative cost"
+                      : costRed < s->absTol      ? "absolute cost"
+                      : ratios[1] < s->varTol    ? "variable"
+                                                 : nullptr;
+    if (newCost > prevCost || !okRate) {
+      if (lastTroubled != it - 1) troubledStartDamping = damping, troubledStart = it;
+      damping *= s->dFail;
+      ref_restore(h);
+      if (damping > s->dMax) break;
+      lastTroubled = it;
+    } else {
+      if (lastTroubled == it - 1) {
+        if (troubledStartDamping < 1e1 && damping > 1e-3) {
+          nTroubled++;
+          largestTroubled = std::max(largestTroubled, it - troubledStart);
+        }
+      }
+      if (ratioRedToExp >= s->minRelRed && applied > s->minStepGood) {
+        damping = std::max(damping * s->dGood, s->dMin);
+      } else {
+        damping *= s->dAvg;
+      }
+      finalCost = newCost;
+    }
+    it++;
+    if (log && s->verbose) {
+      snprintf(buf, sizeof(buf), "it %d cost %.12g -> %.12g lambda %.3g", it, prevCost, newCost,
+               damping);
+      log(buf, user);
+    }
+    if (!tol) lastImpr = it;
+    if (it >= lastImpr + s->stopNoImpr && it >= lastTroubled + s->distTroubled) break;
+    if (it >= s->maxIt) break;
+  }
+  out->initialCost = initialCost;
+  out->finalCost = finalCost;
+  out->numTroubledSeqs = nTroubled;
+  out->largestTroubledSeq = largestTroubled;
+  out->numIterations = it;
+  return 0;
+}
+
+// raw evaluation of one factor (residual + Jacobians) for finite-difference Jacobian tests:
+// e_out[m], J_out[m * sum(tdims)] (blocks in var order, col-major per block); returns m or <0
+int ref_eval_factor(void* h, int fk, int64_t k, double* e_out, double* J_out) {
+  Problem& P = *(Problem*)h;
+  const int nv = kNumVars[fk];
+  bool wants[10] = {false};
+  const int32_t* vi = &P.fvars[fk][(size_t)k * nv];
+  for (int s = 0; s < nv; s++) wants[s] = kFK[fk][s] != 8 && vi[s] >= 0;
+  EvalOut o;
+  try {
+    o = evalFactor(P, fk, k, wants);
+  } catch (std::range_error& e) {
+    g_err = e.what();
+    return -5;
+  }
+  if (!o.fe.ok) return 0;
+  const int m = (int)o.fe.e.size();
+  std::copy(o.fe.e.begin(), o.fe.e.end(), e_out);
+  if (J_out) {
+    size_t off = 0;
+    for (int s = 0; s < nv; s++) {
+      if (!wants[s]) continue;
+      const Mat& J = o.fe.J[s];
+      std::copy(J.a.begin(), J.a.end(), J_out + off);
+      off += J.a.size();
+    }
+  }
+  return m;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- test helpers (FD Jacobians)
+extern "C" {
+int ref_get_var(void* h, int kind, int64_t handle, double* out) {
+  Problem& P = *(Problem*)h;
+  const int d = kVarData[kind];
+  std::copy(&P.data[kind][handle * d], &P.data[kind][handle * d] + d, out);
+  return 0;
+}
+int ref_set_var(void* h, int kind, int64_t handle, const double* in) {
+  Problem& P = *(Problem*)h;
+  const int d = kVarData[kind];
+  std::copy(in, in + d, &P.data[kind][handle * d]);
+  return 0;
+}
+// box-plus one variable by a tangent vector with the VarSpec semantics (used for FD checks)
+int ref_boxplus_var(void* h, int kind, int64_t handle, const double* delta) {
+  Problem& P = *(Problem*)h;
+  if (kind == 0 || kind == 2 || kind == 3) {
+    for (int i = 0; i < 3; i++) P.data[kind][handle * 3 + i] += delta[i];
+  } else if (kind == 1 || kind == 5 || kind == 7) {
+    double* d = &P.data[kind][handle * 7];
+    SE3 T = se3_exp(delta) * SE3::fromData(d);
+    T.toData(d);
+  } else if (kind == 4) {
+    double* d = &P.data[4][handle * 24];
+    CamModel c = CamModel::fromData(d);
+    int n = c.n;
+    for (int i = 0; i < c.n; i++) c.p[i] += delta[i];
+    if (c.estRO) c.ro = c.readoutTimeSec() + delta[n++], c.hasRO = true;
+    if (c.estOff) c.off += delta[n++];
+    c.toData(d);
+  } else if (kind == 6) {
+    ImuModel m = imuOf(P, (int)handle);
+    imu_boxPlus(m, P.jac, delta);
+    std::memcpy(&P.data[6][handle * 32], m.d, sizeof(m.d));
+  } else {
+    return -6;
+  }
+  return 0;
+}
+int ref_var_tdim(void* h, int kind, int64_t handle) { return varTdim(*(Problem*)h, kind, (int)handle); }
+}

@@ -1,0 +1,108 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/_ref/librefcpu.so (the single-threaded CPU restatement of the reference
+LM inner loop, oracle/refcpu.cpp).  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module; the product package never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import subprocess
+
+import numpy as np
+
+from visual_inertial_bundle_adjustment_amd.engine import CEngineBase, Settings, Summary, _dp
+from visual_inertial_bundle_adjustment_amd.kinds import VAR_DATA
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_ref", "librefcpu.so")
+P = C.c_void_p
+
+
+def build_oracle(force: bool = False) -> str:
+    """Compile the oracle (g++, no external deps) into oracle/_ref/."""
+    src = [os.path.join(HERE, f) for f in ("refcpu.cpp", "ref_factors.hpp", "ref_math.hpp")]
+    if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s)
+                                                   for s in src):
+        return LIB
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", LIB, src[0]])
+    return LIB
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build_oracle()
+        _lib = C.CDLL(LIB)
+    return _lib
+
+
+class RefEngine(CEngineBase):
+    prefix = "ref_"
+
+    def __init__(self, reproj_loss=(1.0, 3.0), imu_loss=(math.inf, math.inf), imu_calib_options=0xFF):
+        lib = load()
+        lib.ref_create.restype = P
+        lib.ref_create.argtypes = [C.c_double] * 4 + [C.c_int]
+        super().__init__(lib, lib.ref_create(reproj_loss[0], reproj_loss[1], imu_loss[0],
+                                             imu_loss[1], imu_calib_options))
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.ref_destroy.argtypes = [P]
+                self.lib.ref_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    def cost(self, comparable=False):
+        c = C.c_double()
+        st = (C.c_int64 * 3)()
+        self._check(self._fn("cost", [C.c_int, _dp, C.c_int64 * 3])(self.h, int(comparable),
+                                                                    C.byref(c), st))
+        return c.value, tuple(st)
+
+    def optimize(self, settings: Settings | None = None) -> Summary:
+        s = settings or Settings.default()
+        out = Summary()
+        cb_log = C.CFUNCTYPE(None, C.c_char_p, P)
+        cb_pre = C.CFUNCTYPE(None, C.c_int, P)
+        self._check(self._fn("optimize", [C.POINTER(Settings), cb_log, cb_pre, P,
+                                          C.POINTER(Summary)])(
+            self.h, C.byref(s), cb_log(), cb_pre(), None, C.byref(out)))
+        return out
+
+    # ---------------------------------------------------------------- test helpers
+    def eval_factor(self, kind: int, k: int, with_jac=True, max_m=23, max_cols=128):
+        e = np.zeros(max_m)
+        J = np.zeros(max_m * max_cols * 2) if with_jac else None
+        m = self._fn("eval_factor", [C.c_int, C.c_int64, _dp, _dp])(
+            self.h, kind, k, e.ctypes.data_as(_dp), None if J is None else J.ctypes.data_as(_dp))
+        if m < 0:
+            self._check(m)
+        return m, e[:m], J
+
+    def get_var(self, kind, handle):
+        out = np.zeros(VAR_DATA[kind])
+        self._fn("get_var", [C.c_int, C.c_int64, _dp])(self.h, kind, handle, out.ctypes.data_as(_dp))
+        return out
+
+    def set_var(self, kind, handle, data):
+        d = np.ascontiguousarray(data, dtype=np.float64)
+        self._fn("set_var", [C.c_int, C.c_int64, _dp])(self.h, kind, handle, d.ctypes.data_as(_dp))
+
+    def boxplus_var(self, kind, handle, delta):
+        d = np.ascontiguousarray(delta, dtype=np.float64)
+        self._check(self._fn("boxplus_var", [C.c_int, C.c_int64, _dp])(self.h, kind, handle,
+                                                                       d.ctypes.data_as(_dp)))
+
+    def var_tdim(self, kind, handle):
+        return self._fn("var_tdim", [C.c_int, C.c_int64])(self.h, kind, handle)

@@ -1,0 +1,60 @@
+"""Locating and loading the in-tree native libraries (built by build.py into ./lib)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+HIP_LIB = os.path.join(LIB_DIR, "libviba_hip.so")
+SYNTH_LIB = os.path.join(LIB_DIR, "libviba_synth.so")
+
+_synth = None
+_hip = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def _load(path: str) -> C.CDLL:
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            f"{path} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(no CPU fallback exists for the HIP path)")
+    return C.CDLL(path)
+
+
+def load_synth_lib() -> C.CDLL:
+    global _synth
+    if _synth is None:
+        lib = _load(SYNTH_LIB)
+        P = C.c_void_p
+        lib.vbs_generate.restype = P
+        lib.vbs_generate.argtypes = [P]
+        lib.vbs_default_config.argtypes = [P, C.c_int]
+        lib.vbs_free.argtypes = [P]
+        for name, rt in [("vbs_vars", P), ("vbs_gt_vars", P), ("vbs_var_const", P),
+                         ("vbs_factor_vars", P), ("vbs_factor_ivals", P), ("vbs_factor_consts", P)]:
+            f = getattr(lib, name)
+            f.restype = rt
+            f.argtypes = [P, C.c_int]
+        for name in ("vbs_num_vars", "vbs_num_factors"):
+            f = getattr(lib, name)
+            f.restype = C.c_int64
+            f.argtypes = [P, C.c_int]
+        lib.vbs_num_rs_tables.restype = C.c_int32
+        lib.vbs_num_rs_tables.argtypes = [P]
+        for name in ("vbs_rs_offsets", "vbs_rs_samples", "vbs_rs_interp", "vbs_rs_gravity"):
+            f = getattr(lib, name)
+            f.restype = P
+            f.argtypes = [P]
+        _synth = lib
+    return _synth
+
+
+def load_hip_lib() -> C.CDLL:
+    """Load the HIP product library. Raises NativeLibraryMissing when it was not built."""
+    global _hip
+    if _hip is None:
+        _hip = _load(HIP_LIB)
+    return _hip

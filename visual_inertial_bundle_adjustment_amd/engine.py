@@ -1,0 +1,255 @@
+"""ctypes binding of the C-ABI (include/viba_hip.h): the HIP LM engine.
+
+:class:`HipEngine` mirrors the part of ``small_thing::Optimizer`` the VI-BA path uses
+(lib/small_thing/Optimizer.h): computeGradHess -> ``linearize``, addDamping+factor+solve ->
+``damp_factor_solve``, applyStep, computeCost, backup/restore and ``optimize``.
+The engine runs entirely on the GPU; there is no CPU fallback: constructing it without the
+built library or without a HIP device raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+
+from .kinds import NUM_VAR_KINDS, VAR_DATA, VAR_MAX_TANGENT, factor_num_consts, factor_num_vars
+
+P = C.c_void_p
+_dp = C.POINTER(C.c_double)
+
+
+class VbError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"error {code}: {msg}")
+        self.code = code
+
+
+class Settings(C.Structure):
+    """Optimizer::Settings, direct-solver subset (lib/small_thing/Optimizer.h:40-91)."""
+    _fields_ = [
+        ("max_num_iterations", C.c_int32),
+        ("stop_if_no_improvement_for", C.c_int32),
+        ("distance_from_troubled_iteration", C.c_int32),
+        ("max_step_factor_attempts", C.c_int32),
+        ("try_sub_step", C.c_int32),
+        ("verbose", C.c_int32),
+        ("absolute_cost_tolerance", C.c_double),
+        ("relative_cost_tolerance", C.c_double),
+        ("variables_tolerance", C.c_double),
+        ("damping", C.c_double),
+        ("damping_adjust_on_fail", C.c_double),
+        ("damping_adjust_on_good_step", C.c_double),
+        ("damping_adjust_on_average_step", C.c_double),
+        ("damping_max", C.c_double),
+        ("damping_min", C.c_double),
+        ("min_relative_cost_reduction", C.c_double),
+        ("step_factor_decrease", C.c_double),
+        ("min_step_factor_for_good", C.c_double),
+    ]
+
+    @staticmethod
+    def default(**kw) -> "Settings":
+        s = Settings(50, 3, 3, 2, 1, 0, 1e-8, 1e-10, 1e-5, 1e-5, 2.5, 0.7, 1.5, 1e8, 1e-9, 0.3, 0.3,
+                     0.7)
+        for k, v in kw.items():
+            setattr(s, k, v)
+        return s
+
+
+class Summary(C.Structure):
+    """Optimizer::Summary (lib/small_thing/Optimizer.h:93-99)."""
+    _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("num_troubled_seqs", C.c_int32), ("largest_troubled_seq", C.c_int32),
+                ("num_iterations", C.c_int32), ("reserved", C.c_int32)]
+
+
+class PhaseTimes(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("linearize_ms", "schur_ms", "factor_ms", "solve_ms",
+                                          "step_ms", "cost_ms", "total_ms")]
+
+
+LOG_CB = C.CFUNCTYPE(None, C.c_char_p, P)
+PRESTEP_CB = C.CFUNCTYPE(None, C.c_int, P)
+
+
+def _arr(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class CEngineBase:
+    """Shared ctypes plumbing for engines exposing the vb_* function family under a prefix."""
+
+    prefix = "vb_"
+
+    def __init__(self, lib: C.CDLL, handle):
+        self.lib = lib
+        self.h = handle
+        self.nvars = [0] * NUM_VAR_KINDS
+        self._keep = []
+
+    # ---------------------------------------------------------------- plumbing
+    def _fn(self, name, argtypes, restype=C.c_int):
+        f = getattr(self.lib, self.prefix + name)
+        f.argtypes = [P] + argtypes
+        f.restype = restype
+        return f
+
+    def _check(self, rc: int):
+        if rc != 0:
+            err = getattr(self.lib, self.prefix + "last_error")
+            err.restype = C.c_char_p
+            raise VbError(rc, err().decode())
+
+    # ---------------------------------------------------------------- problem
+    def set_vars(self, kind: int, data, const=None):
+        data = _arr(data, np.float64).reshape(-1, VAR_DATA[kind])
+        n = data.shape[0]
+        c = None if const is None else _arr(const, np.uint8)
+        f = self._fn("set_vars", [C.c_int, C.c_int64, _dp, C.POINTER(C.c_uint8)])
+        self._check(f(self.h, kind, n, data.ctypes.data_as(_dp),
+                      None if c is None else c.ctypes.data_as(C.POINTER(C.c_uint8))))
+        self.nvars[kind] = n
+
+    def add_factors(self, kind: int, var_idx, ivals, consts):
+        v = _arr(var_idx, np.int32).reshape(-1, factor_num_vars(kind))
+        n = v.shape[0]
+        iv = _arr(ivals if ivals is not None else np.full(n, -1), np.int32)
+        cs = _arr(consts, np.float64).reshape(n, factor_num_consts(kind))
+        f = self._fn("add_factors", [C.c_int, C.c_int64, C.POINTER(C.c_int32),
+                                     C.POINTER(C.c_int32), _dp])
+        self._check(f(self.h, kind, n, v.ctypes.data_as(C.POINTER(C.c_int32)),
+                      iv.ctypes.data_as(C.POINTER(C.c_int32)), cs.ctypes.data_as(_dp)))
+
+    def set_rs_tables(self, offsets, samples, interp, gravity):
+        off = _arr(offsets, np.int64)
+        s, ip, g = (_arr(x, np.float64) for x in (samples, interp, gravity))
+        f = self._fn("set_rs_tables", [C.c_int32, C.POINTER(C.c_int64), _dp, _dp, _dp])
+        self._check(f(self.h, len(off) - 1, off.ctypes.data_as(C.POINTER(C.c_int64)),
+                      s.ctypes.data_as(_dp), ip.ctypes.data_as(_dp), g.ctypes.data_as(_dp)))
+
+    def finalize(self):
+        self._check(self._fn("finalize", [])(self.h))
+
+    def reduced_order(self) -> int:
+        return self._fn("reduced_order", [], C.c_int64)(self.h)
+
+    def total_order(self) -> int:
+        return self._fn("total_order", [], C.c_int64)(self.h)
+
+    # ---------------------------------------------------------------- LM building blocks
+    def linearize(self, update_cache=True, dont_retry=False) -> float:
+        c = C.c_double()
+        self._check(self._fn("linearize", [C.c_int, C.c_int, _dp])(
+            self.h, int(update_cache), int(dont_retry), C.byref(c)))
+        return c.value
+
+    def damp_factor_solve(self, lam: float) -> float:
+        m = C.c_double()
+        self._check(self._fn("damp_factor_solve", [C.c_double, _dp])(self.h, lam, C.byref(m)))
+        return m.value
+
+    def gradient_dot_step(self, dont_retry=False) -> float:
+        b = C.c_double()
+        self._check(self._fn("gradient_dot_step", [C.c_int, _dp])(self.h, int(dont_retry),
+                                                                   C.byref(b)))
+        return b.value
+
+    def solve_with_new_gradient(self):
+        self._check(self._fn("solve_with_new_gradient", [])(self.h))
+
+    def scale_step(self, f: float):
+        self._check(self._fn("scale_step", [C.c_double])(self.h, f))
+
+    def apply_step(self, which=0):
+        r = (C.c_double * 3)()
+        self._check(self._fn("apply_step", [C.c_int, C.c_double * 3])(self.h, which, r))
+        return tuple(r)
+
+    def backup(self):
+        self._check(self._fn("backup", [])(self.h))
+
+    def restore(self):
+        self._check(self._fn("restore", [])(self.h))
+
+    def get_vars(self, kind: int) -> np.ndarray:
+        out = np.zeros((self.nvars[kind], VAR_DATA[kind]))
+        self._check(self._fn("get_vars", [C.c_int, _dp])(self.h, kind, out.ctypes.data_as(_dp)))
+        return out
+
+    def get_step(self, kind: int, which=0) -> np.ndarray:
+        out = np.zeros((self.nvars[kind], VAR_MAX_TANGENT[kind]))
+        self._check(self._fn("get_step", [C.c_int, C.c_int, _dp])(
+            self.h, which, kind, out.ctypes.data_as(_dp)))
+        return out
+
+    def get_gradient(self, kind: int) -> np.ndarray:
+        out = np.zeros((self.nvars[kind], VAR_MAX_TANGENT[kind]))
+        self._check(self._fn("get_gradient", [C.c_int, _dp])(self.h, kind,
+                                                              out.ctypes.data_as(_dp)))
+        return out
+
+
+class HipEngine(CEngineBase):
+    """The MI355X LM engine. One instance = one vb_handle = one HIP stream on `device`."""
+
+    prefix = "vb_"
+
+    class Config(C.Structure):
+        _fields_ = [("reproj_loss_radius", C.c_double), ("reproj_loss_cutoff", C.c_double),
+                    ("imu_loss_radius", C.c_double), ("imu_loss_cutoff", C.c_double),
+                    ("imu_calib_options", C.c_int32), ("device", C.c_int32),
+                    ("tile", C.c_int32), ("reserved", C.c_int32)]
+
+    def __init__(self, reproj_loss=(1.0, 3.0), imu_loss=(math.inf, math.inf), imu_calib_options=0xFF,
+                 device=0, tile=0):
+        from ._lib import load_hip_lib
+        lib = load_hip_lib()
+        cfg = HipEngine.Config()
+        lib.vb_default_config.argtypes = [P]
+        lib.vb_default_config(C.byref(cfg))
+        cfg.reproj_loss_radius, cfg.reproj_loss_cutoff = reproj_loss
+        cfg.imu_loss_radius, cfg.imu_loss_cutoff = imu_loss
+        cfg.imu_calib_options = imu_calib_options
+        cfg.device = device
+        cfg.tile = tile
+        h = P()
+        lib.vb_create.argtypes = [P, C.POINTER(P)]
+        lib.vb_create.restype = C.c_int
+        super().__init__(lib, None)
+        self._check(lib.vb_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.vb_destroy.argtypes = [P]
+            self.lib.vb_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def cost(self, comparable=False):
+        c = C.c_double()
+        st = (C.c_int64 * 3)()
+        self._check(self._fn("cost", [C.c_int, _dp, C.c_int64 * 3])(self.h, int(comparable),
+                                                                    C.byref(c), st))
+        return c.value, tuple(st)
+
+    def optimize(self, settings: Settings | None = None, log=None, prestep=None) -> Summary:
+        s = settings or Settings.default()
+        out = Summary()
+        lcb = LOG_CB(lambda m, u: log(m.decode())) if log else LOG_CB()
+        pcb = PRESTEP_CB(lambda i, u: prestep(i)) if prestep else PRESTEP_CB()
+        self._check(self._fn("optimize", [C.POINTER(Settings), LOG_CB, PRESTEP_CB, P,
+                                          C.POINTER(Summary)])(
+            self.h, C.byref(s), lcb, pcb, None, C.byref(out)))
+        return out
+
+    def phase_times(self) -> PhaseTimes:
+        t = PhaseTimes()
+        self._check(self._fn("last_phase_times", [C.POINTER(PhaseTimes)])(self.h, C.byref(t)))
+        return t
