@@ -992,10 +992,8 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
     if (it == 0) initialCost = prevCost;
     double modelRed;
     if ((rc = ref_damp_factor_solve(h, damping, &modelRed))) return rc;
-    if (modelRed < 0) {  // :835-854 (the `continue` leaves the do-while: old step is kept)
-      double c2;
-      if ((rc = ref_linearize(h, 1, dontRetry, &c2))) return rc;
-      damping *= s->dFail;
+    if (modelRed < 0) {  // :835-854 (the `continue` leaves the do-while: old step is kept; the
+      damping *= s->dFail;  // re-linearization at the same point only refreshes identical caches)
     }
     ref_backup(h);
     double ratios[3];

@@ -1,0 +1,67 @@
+"""In-tree build of the native libraries (no JIT, no cmake):
+
+    lib/libviba_hip.so    HIP kernels + C-ABI, gfx950 code objects (hipcc --offload-arch=gfx950)
+    lib/libviba_synth.so  synthetic problem generator (g++)
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib")
+HIP_SOURCES = ["factors.hip", "solver.hip", "api.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("VIBA_OFFLOAD_ARCH", "gfx950")
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+             "-Wno-unused-variable", "-Wno-unused-but-set-variable", "-Wno-unused-value"]
+
+
+def _newer(target: str, deps: list[str]) -> bool:
+    return os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(d) for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build(force: bool = False, verbose: bool = False) -> list[str]:
+    os.makedirs(LIB, exist_ok=True)
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    headers.append(os.path.join(HERE, "..", "include", "viba_hip.h"))
+    out = []
+    # synthetic generator
+    synth = os.path.join(LIB, "libviba_synth.so")
+    src = os.path.join(CSRC, "synth.cpp")
+    if force or not _newer(synth, [src] + headers):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", synth, src])
+    out.append(synth)
+    # HIP library: compile objects in parallel, then link
+    objs = []
+    jobs = []
+    with cf.ThreadPoolExecutor(max_workers=3) as ex:
+        for s in HIP_SOURCES:
+            sp = os.path.join(CSRC, s)
+            o = os.path.join(LIB, s.replace(".hip", ".o"))
+            objs.append(o)
+            if force or not _newer(o, [sp] + headers):
+                jobs.append(ex.submit(_run, [HIPCC, *HIP_FLAGS, "-c", sp, "-o", o]))
+        for j in jobs:
+            r = j.result()
+            if verbose and r.stderr:
+                print(r.stderr)
+    hip = os.path.join(LIB, "libviba_hip.so")
+    if force or not _newer(hip, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", hip, *objs])
+    out.append(hip)
+    return out
+
+
+if __name__ == "__main__":
+    import sys
+    print("\n".join(build(force="--force" in sys.argv, verbose=True)))

@@ -1,0 +1,1103 @@
+// Host side of the HIP LM engine: C-ABI (include/viba_hip.h), symbolic analysis (≙
+// Optimizer::initSolver, Optimizer.cpp:166-207) and the Levenberg-Marquardt controller
+// (≙ Optimizer::optimize, Optimizer.cpp:768-1106).  All numeric work runs in HIP kernels on the
+// handle's stream; the host only orders launches, reads back scalars and takes LM decisions.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/viba_hip.h"
+#include "engine.hpp"
+
+namespace viba {
+// kernels (factors.hip / solver.hip)
+void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st);
+void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
+void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
+void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
+void launch_schur(const Dev& d, double lambda, hipStream_t st);
+void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
+void launch_potrf_trsm(const Dev& d, const int32_t* colTiles, int n, double* diagScratch, hipStream_t st);
+void launch_gemm_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets,
+                        int npairs, const double* diagScratch, hipStream_t st);
+void launch_pad_diag(const Dev& d, hipStream_t st);
+void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, double* b, double* x,
+                hipStream_t st);
+void launch_bwd(const Dev& d, int J, int32_t diagTile, const int32_t* rowTiles, const int32_t* rowCol, int n,
+                double* t, double* x, hipStream_t st);
+void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st);
+void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t st);
+void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hipStream_t st);
+void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, hipStream_t st);
+}  // namespace viba
+
+using namespace viba;
+
+namespace {
+
+thread_local std::string g_err = "";
+constexpr int TS = 64;
+constexpr int kVarData[9] = {3, 7, 3, 3, 24, 7, 32, 7, 4};
+constexpr int kMaxTan[9] = {3, 6, 3, 3, 17, 6, 23, 6, 2};
+constexpr int kNumVars[14] = {5, 6, 9, 10, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1};
+constexpr int kNumConsts[14] = {6, 331, 331, 331, 4, 23, 17, 6, 6, 43, 55, 41, 13, 13};
+const int kFK[14][10] = {{0, 1, 5, 4, 2}, {6, 1, 2, 1, 2, 8}, {6, 1, 2, 3, 1, 2, 3, 7, 8},
+                         {6, 1, 2, 3, 7, 1, 2, 3, 7, 8}, {3, 7}, {6, 6}, {4, 4}, {7, 7}, {5, 5}, {1}, {6}, {4},
+                         {5}, {7}};
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) return fail(VB_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+ImuIdx makeJac(int mask) {
+  ImuIdx J;
+  int i = 0;
+  J.gB = (mask & 1) ? (i += 3) - 3 : -1;
+  J.aB = (mask & 2) ? (i += 3) - 3 : -1;
+  J.gS = (mask & 4) ? (i += 3) - 3 : -1;
+  J.aS = (mask & 8) ? (i += 3) - 3 : -1;
+  J.gN = (mask & 16) ? (i += 6) - 6 : -1;
+  J.aN = (mask & 32) ? (i += 3) - 3 : -1;
+  J.rT = (mask & 64) ? (i += 1) - 1 : -1;
+  J.gaT = (mask & 128) ? (i += 1) - 1 : -1;
+  J.size = i;
+  return J;
+}
+LossParams makeLoss(double a, double k) {
+  LossParams L;
+  L.a = a, L.b = a * a, L.k2 = k * k, L.h = 2.0 * a * k - a * a;
+  return L;
+}
+
+// symmetric square root U (P = U^T U) of a PSD m x m matrix via cyclic Jacobi eigen-decomposition
+void psdSqrt(const double* Pm, int m, double* U) {
+  std::vector<double> A(Pm, Pm + m * m), V(m * m, 0.0);
+  for (int i = 0; i < m; i++) V[i * m + i] = 1.0;
+  for (int sweep = 0; sweep < 60; sweep++) {
+    double off = 0;
+    for (int p = 0; p < m; p++)
+      for (int q = p + 1; q < m; q++) off += A[p * m + q] * A[p * m + q];
+    if (off < 1e-30) break;
+    for (int p = 0; p < m; p++)
+      for (int q = p + 1; q < m; q++) {
+        const double apq = A[p * m + q];
+        if (std::abs(apq) < 1e-300) continue;
+        const double th = 0.5 * (A[q * m + q] - A[p * m + p]) / apq;
+        const double t = (th >= 0 ? 1.0 : -1.0) / (std::abs(th) + std::sqrt(th * th + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < m; k++) {
+          const double akp = A[k * m + p], akq = A[k * m + q];
+          A[k * m + p] = c * akp - s * akq, A[k * m + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < m; k++) {
+          const double apk = A[p * m + k], aqk = A[q * m + k];
+          A[p * m + k] = c * apk - s * aqk, A[q * m + k] = s * apk + c * aqk;
+        }
+        for (int k = 0; k < m; k++) {
+          const double vkp = V[k * m + p], vkq = V[k * m + q];
+          V[k * m + p] = c * vkp - s * vkq, V[k * m + q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  // U = diag(sqrt(lambda)) V^T  (rows = eigenvectors scaled)
+  for (int i = 0; i < m; i++) {
+    const double l = std::sqrt(std::max(0.0, A[i * m + i]));
+    for (int j = 0; j < m; j++) U[i * m + j] = l * V[j * m + i];
+  }
+}
+// upper Cholesky U of P = inverse(cov) (cov SPD, col-major m x m): P = U^T U
+bool precisionChol(const double* cov, int m, double* U) {
+  std::vector<double> A(cov, cov + m * m), Pi(m * m, 0.0);
+  // invert via Gauss-Jordan with partial pivoting
+  std::vector<double> I(m * m, 0.0);
+  for (int i = 0; i < m; i++) I[i * m + i] = 1.0;
+  std::vector<double> M(m * m);
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < m; j++) M[i * m + j] = A[j * m + i];  // row-major
+  for (int c = 0; c < m; c++) {
+    int piv = c;
+    for (int r = c + 1; r < m; r++)
+      if (std::abs(M[r * m + c]) > std::abs(M[piv * m + c])) piv = r;
+    if (std::abs(M[piv * m + c]) < 1e-300) return false;
+    for (int k = 0; k < m; k++) std::swap(M[c * m + k], M[piv * m + k]), std::swap(I[c * m + k], I[piv * m + k]);
+    const double inv = 1.0 / M[c * m + c];
+    for (int k = 0; k < m; k++) M[c * m + k] *= inv, I[c * m + k] *= inv;
+    for (int r = 0; r < m; r++) {
+      if (r == c) continue;
+      const double f = M[r * m + c];
+      if (f == 0.0) continue;
+      for (int k = 0; k < m; k++) M[r * m + k] -= f * M[c * m + k], I[r * m + k] -= f * I[c * m + k];
+    }
+  }
+  // symmetrize P and Cholesky (lower L, row-major), U = L^T
+  std::vector<double> L(m * m, 0.0);
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < m; j++) Pi[i * m + j] = 0.5 * (I[i * m + j] + I[j * m + i]);
+  for (int j = 0; j < m; j++) {
+    double dd = Pi[j * m + j];
+    for (int k = 0; k < j; k++) dd -= L[j * m + k] * L[j * m + k];
+    if (!(dd > 0)) return false;
+    dd = std::sqrt(dd);
+    L[j * m + j] = dd;
+    for (int i = j + 1; i < m; i++) {
+      double s = Pi[i * m + j];
+      for (int k = 0; k < j; k++) s -= L[i * m + k] * L[j * m + k];
+      L[i * m + j] = s / dd;
+    }
+  }
+  for (int i = 0; i < m; i++)
+    for (int j = 0; j < m; j++) U[i * m + j] = L[j * m + i];
+  return true;
+}
+
+template <typename T>
+int upload(T** dptr, const std::vector<T>& v) {
+  const size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
+  HIPCHK(hipMalloc((void**)dptr, bytes));
+  if (!v.empty()) HIPCHK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return 0;
+}
+template <typename T>
+int alloc0(T** dptr, size_t n) {
+  HIPCHK(hipMalloc((void**)dptr, std::max<size_t>(1, n) * sizeof(T)));
+  HIPCHK(hipMemset(*dptr, 0, std::max<size_t>(1, n) * sizeof(T)));
+  return 0;
+}
+
+struct Timer {
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct vb_handle_s {
+  vb_config cfg;
+  hipStream_t st = nullptr;
+  std::vector<double> data[9];
+  std::vector<uint8_t> cst[9];
+  std::vector<int32_t> fvars[14], fint[14];
+  std::vector<double> fconst[14];
+  int32_t nRS = 0;
+  std::vector<int64_t> rsOff;
+  std::vector<double> rsS, rsI, rsG;
+  bool finalized = false;
+  Dev d;
+  std::vector<void*> allocs;
+  // symbolic (host)
+  std::vector<int32_t> rvKind, rvHandle, rvDim;
+  std::vector<int64_t> rvOff;
+  std::vector<int32_t> lmOfPoint;
+  int64_t nParams = 0, order = 0, nLmObs = 0;
+  std::vector<int64_t> colStart;   // per tile column into colTilesH / colRowsH
+  std::vector<int32_t> colTilesH, colRowsH;
+  std::vector<int64_t> pairStart;  // per tile column into pairs / targets
+  std::vector<int64_t> rowStart;   // per tile row into rowTilesH / rowColH
+  std::vector<int32_t> rowTilesH, rowColH;
+  int32_t *colTilesD = nullptr, *colRowsD = nullptr, *pairsD = nullptr, *targetsD = nullptr, *rowTilesD = nullptr,
+          *rowColD = nullptr;
+  double *diagScratch = nullptr, *yvec = nullptr, *rhsWork = nullptr;
+  // shard
+  int64_t lmBegin = 0, lmEnd = -1;
+  bool isRoot = true;
+  // state
+  bool linearized = false, factored = false;
+  vb_phase_times times{};
+  hipEvent_t ev[8];
+};
+
+namespace {
+
+int checkErr(vb_handle h) {
+  int32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, h->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  if (e & 1) return fail(VB_E_RANGE, "RollingShutterData::getEstimate: out of range");
+  if (e & 2) return fail(VB_E_NUMERIC, "landmark 3x3 Cholesky breakdown");
+  if (e & 8) return fail(VB_E_NUMERIC, "reduced system Cholesky breakdown (not positive definite)");
+  if (e & 4) return fail(VB_E_STATE, "internal: Schur contribution outside the symbolic structure");
+  return 0;
+}
+
+int readRed(vb_handle h, double* out, int i0, int n) {
+  HIPCHK(hipMemcpyAsync(out, h->d.red + i0, n * sizeof(double), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+int doFinalize(vb_handle h) {
+  Dev& d = h->d;
+  d.jac = makeJac(h->cfg.imu_calib_options);
+  d.reproj = makeLoss(h->cfg.reproj_loss_radius, h->cfg.reproj_loss_cutoff);
+  d.imu = makeLoss(h->cfg.imu_loss_radius, h->cfg.imu_loss_cutoff);
+  d.T = TS;
+  for (int k = 0; k < 9; k++) {
+    d.nvar[k] = (int64_t)h->cst[k].size();
+    if ((int64_t)h->data[k].size() != d.nvar[k] * kVarData[k]) return fail(VB_E_ARG, "variable data size mismatch");
+  }
+  // ---------------- registration (registerAllVariables; points = elimination range)
+  auto tdimOf = [&](int kind, int hh) -> int {
+    switch (kind) {
+      case 0: case 2: case 3: return 3;
+      case 1: case 5: case 7: return 6;
+      case 4: {
+        const double* c = &h->data[4][(size_t)hh * 24];
+        return (int)c[1] + (c[7] != 0 ? 1 : 0) + (c[8] != 0 ? 1 : 0);
+      }
+      case 6: return d.jac.size;
+      default: return 2;
+    }
+  };
+  std::vector<int32_t> redOf[9];
+  for (int k = 0; k < 9; k++) redOf[k].assign(d.nvar[k], -1);
+  std::vector<int32_t>& lmOf = h->lmOfPoint;
+  lmOf.assign(d.nvar[0], -1);
+  int64_t nPts = 0;
+  std::vector<std::pair<int, int>> red;  // (kind, handle)
+  for (int fk = 0; fk < 14; fk++) {
+    const int nv = kNumVars[fk];
+    const int64_t n = (int64_t)h->fint[fk].size();
+    for (int64_t f = 0; f < n; f++)
+      for (int s = 0; s < nv; s++) {
+        const int kind = kFK[fk][s], hh = h->fvars[fk][f * nv + s];
+        if (hh < 0) continue;
+        if (hh >= d.nvar[kind]) return fail(VB_E_ARG, "factor references an unknown variable handle");
+        if (h->cst[kind][hh]) continue;
+        if (kind == 8) return fail(VB_E_UNSUPPORTED, "non-constant gravity is not supported");
+        if (kind == 0) {
+          if (lmOf[hh] < 0) lmOf[hh] = -2;  // mark; numbered below in handle order
+          continue;
+        }
+        if (redOf[kind][hh] < 0) {
+          redOf[kind][hh] = (int32_t)red.size();
+          red.push_back({kind, hh});
+        }
+      }
+  }
+  for (int64_t p = 0; p < d.nvar[0]; p++)
+    if (lmOf[p] == -2) lmOf[p] = (int32_t)nPts++;
+  // ---------------- reduced ordering: mean pose ordinal of co-occurring poses
+  const int nRV = (int)red.size();
+  std::vector<double> ks(nRV, 0.0), kc(nRV, 0.0);
+  for (int fk = 0; fk < 14; fk++) {
+    const int nv = kNumVars[fk];
+    const int64_t n = (int64_t)h->fint[fk].size();
+    for (int64_t f = 0; f < n; f++) {
+      double ps = 0;
+      int pc = 0;
+      for (int s = 0; s < nv; s++)
+        if (kFK[fk][s] == 1 && h->fvars[fk][f * nv + s] >= 0) ps += h->fvars[fk][f * nv + s], pc++;
+      if (!pc) continue;
+      for (int s = 0; s < nv; s++) {
+        const int kind = kFK[fk][s], hh = h->fvars[fk][f * nv + s];
+        if (hh < 0 || kind == 0 || kind == 8 || redOf[kind][hh] < 0) continue;
+        ks[redOf[kind][hh]] += ps, kc[redOf[kind][hh]] += pc;
+      }
+    }
+  }
+  std::vector<int> ord(nRV);
+  std::iota(ord.begin(), ord.end(), 0);
+  auto key = [&](int r) { return red[r].first == 1 ? (double)red[r].second : (kc[r] > 0 ? ks[r] / kc[r] : 1e30); };
+  std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+    const double ka = key(a), kb = key(b);
+    if (ka != kb) return ka < kb;
+    if (red[a].first != red[b].first) return red[a].first < red[b].first;
+    return red[a].second < red[b].second;
+  });
+  std::vector<int> pos(nRV);
+  for (int i = 0; i < nRV; i++) pos[ord[i]] = i;
+  h->rvKind.resize(nRV), h->rvHandle.resize(nRV), h->rvDim.resize(nRV), h->rvOff.resize(nRV + 1);
+  int64_t off = 0;
+  for (int i = 0; i < nRV; i++) {
+    const auto [kind, hh] = red[ord[i]];
+    h->rvKind[i] = kind, h->rvHandle[i] = hh, h->rvDim[i] = tdimOf(kind, hh), h->rvOff[i] = off;
+    off += h->rvDim[i];
+    redOf[kind][hh] = i;
+  }
+  h->rvOff[nRV] = off;
+  const int64_t nRed = off;
+  d.nRV = nRV, d.nRed = nRed, d.nPts = nPts;
+  h->nParams = nPts + nRV;
+  h->order = nPts * 3 + nRed;
+
+  // ---------------- visual observations, sorted by landmark (constant-point obs at the end)
+  const int64_t nObs = (int64_t)h->fint[0].size();
+  std::vector<int64_t> perm(nObs);
+  std::iota(perm.begin(), perm.end(), 0);
+  auto lmKey = [&](int64_t f) -> int64_t {
+    const int l = lmOf[h->fvars[0][f * 5]];
+    return l < 0 ? INT64_MAX : l;
+  };
+  std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return lmKey(a) < lmKey(b); });
+  d.nObs = nObs;
+  d.nObsPad = ((nObs + 255) / 256) * 256;
+  std::vector<int32_t> obPose(nObs), obExtr(nObs), obIntr(nObs), obVel(nObs), obRS(nObs), obPt(nObs);
+  std::vector<int32_t> obRed(nObs * 4, -1), obCol(nObs * 4, -1);
+  std::vector<double> obC(nObs * 6);
+  std::vector<int64_t> lmObs(nPts + 1, 0);
+  for (int64_t i = 0; i < nObs; i++) {
+    const int64_t f = perm[i];
+    const int32_t* v = &h->fvars[0][f * 5];
+    obPt[i] = v[0], obPose[i] = v[1], obExtr[i] = v[2], obIntr[i] = v[3];
+    obRS[i] = h->fint[0][f];
+    obVel[i] = obRS[i] >= 0 ? v[4] : 0;
+    if (obRS[i] >= h->nRS) return fail(VB_E_ARG, "visual factor references an unknown RS table");
+    if (obRS[i] >= 0 && (v[4] < 0 || v[4] >= d.nvar[2])) return fail(VB_E_ARG, "RS visual factor needs a velocity");
+    obRed[i * 4 + 0] = redOf[1][v[1]];
+    obRed[i * 4 + 1] = redOf[5][v[2]];
+    obRed[i * 4 + 2] = redOf[4][v[3]];
+    obRed[i * 4 + 3] = obRS[i] >= 0 ? redOf[2][v[4]] : -1;
+    std::copy(&h->fconst[0][f * 6], &h->fconst[0][f * 6] + 6, &obC[i * 6]);
+    const int l = lmOf[v[0]];
+    if (l >= 0) lmObs[l + 1]++;
+  }
+  for (int64_t l = 0; l < nPts; l++) lmObs[l + 1] += lmObs[l];
+  h->nLmObs = lmObs[nPts];
+  // landmark blocks D(l)
+  std::vector<int64_t> lmBlk(nPts + 1, 0), lmY(nPts + 1, 0);
+  std::vector<int32_t> blkRed, blkCol;
+  std::vector<int32_t> tmp;
+  for (int64_t l = 0; l < nPts; l++) {
+    tmp.clear();
+    for (int64_t o = lmObs[l]; o < lmObs[l + 1]; o++)
+      for (int s = 0; s < 4; s++)
+        if (obRed[o * 4 + s] >= 0) tmp.push_back(obRed[o * 4 + s]);
+    std::sort(tmp.begin(), tmp.end());
+    tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+    int32_t col = 0;
+    for (int32_t r : tmp) {
+      blkRed.push_back(r);
+      blkCol.push_back(col);
+      col += h->rvDim[r];
+    }
+    lmBlk[l + 1] = (int64_t)blkRed.size();
+    lmY[l + 1] = lmY[l] + 3 * (int64_t)col;
+    for (int64_t o = lmObs[l]; o < lmObs[l + 1]; o++)
+      for (int s = 0; s < 4; s++) {
+        const int32_t r = obRed[o * 4 + s];
+        if (r < 0) continue;
+        const int64_t q = std::lower_bound(blkRed.begin() + lmBlk[l], blkRed.begin() + lmBlk[l + 1], r) - blkRed.begin();
+        obCol[o * 4 + s] = blkCol[q];
+      }
+  }
+  // incidence lists O(X), L(X)
+  std::vector<int64_t> oxStart(nRV + 1, 0), lxStart(nRV + 1, 0);
+  for (int64_t o = 0; o < nObs; o++)
+    for (int s = 0; s < 4; s++)
+      if (obRed[o * 4 + s] >= 0) oxStart[obRed[o * 4 + s] + 1]++;
+  for (int64_t b = 0; b < (int64_t)blkRed.size(); b++) lxStart[blkRed[b] + 1]++;
+  for (int i = 0; i < nRV; i++) oxStart[i + 1] += oxStart[i], lxStart[i + 1] += lxStart[i];
+  std::vector<int32_t> oxObs(oxStart[nRV]), oxSlot(oxStart[nRV]), lxLm(lxStart[nRV]), lxCol(lxStart[nRV]);
+  {
+    std::vector<int64_t> fo(oxStart.begin(), oxStart.end() - 1), fl(lxStart.begin(), lxStart.end() - 1);
+    for (int64_t o = 0; o < nObs; o++)
+      for (int s = 0; s < 4; s++) {
+        const int32_t r = obRed[o * 4 + s];
+        if (r < 0) continue;
+        oxObs[fo[r]] = (int32_t)o, oxSlot[fo[r]] = s, fo[r]++;
+      }
+    for (int64_t l = 0; l < nPts; l++)
+      for (int64_t b = lmBlk[l]; b < lmBlk[l + 1]; b++) {
+        const int32_t r = blkRed[b];
+        lxLm[fl[r]] = (int32_t)l, lxCol[fl[r]] = blkCol[b], fl[r]++;
+      }
+  }
+  // ---------------- couplings: row ends and the tile pattern
+  const int32_t nT = (int32_t)((nRed + TS - 1) / TS);
+  d.nT = nT;
+  std::vector<int64_t> rowEnd(nRV);
+  for (int i = 0; i < nRV; i++) rowEnd[i] = h->rvOff[i] + h->rvDim[i];
+  std::vector<uint8_t> pat((size_t)nT * nT, 0);
+  auto coupleBlocks = [&](int a, int b) {  // reduced ids; a, b any order
+    if (h->rvOff[a] < h->rvOff[b]) std::swap(a, b);
+    rowEnd[b] = std::max(rowEnd[b], h->rvOff[a] + h->rvDim[a]);
+    const int64_t r0 = h->rvOff[a] / TS, r1 = (h->rvOff[a] + h->rvDim[a] - 1) / TS;
+    const int64_t c0 = h->rvOff[b] / TS, c1 = (h->rvOff[b] + h->rvDim[b] - 1) / TS;
+    for (int64_t I = r0; I <= r1; I++)
+      for (int64_t J = c0; J <= c1; J++)
+        if (I >= J) pat[I * nT + J] = 1;
+  };
+  for (int i = 0; i < nRV; i++) coupleBlocks(i, i);
+  for (int64_t o = 0; o < nObs; o++)
+    for (int s = 0; s < 4; s++)
+      for (int t = 0; t <= s; t++)
+        if (obRed[o * 4 + s] >= 0 && obRed[o * 4 + t] >= 0) coupleBlocks(obRed[o * 4 + s], obRed[o * 4 + t]);
+  for (int64_t l = 0; l < nPts; l++) {
+    const int64_t b0 = lmBlk[l], b1 = lmBlk[l + 1];
+    if (b1 == b0) continue;
+    // row end: the suffix partner with the largest offset is the last block
+    const int last = blkRed[b1 - 1];
+    for (int64_t b = b0; b < b1; b++)
+      rowEnd[blkRed[b]] = std::max(rowEnd[blkRed[b]], h->rvOff[last] + h->rvDim[last]);
+    // tile pattern over the distinct tiles touched
+    std::vector<int64_t> tl;
+    for (int64_t b = b0; b < b1; b++) {
+      const int r = blkRed[b];
+      for (int64_t t = h->rvOff[r] / TS; t <= (h->rvOff[r] + h->rvDim[r] - 1) / TS; t++) tl.push_back(t);
+    }
+    std::sort(tl.begin(), tl.end());
+    tl.erase(std::unique(tl.begin(), tl.end()), tl.end());
+    for (size_t a = 0; a < tl.size(); a++)
+      for (size_t b = 0; b <= a; b++) pat[tl[a] * nT + tl[b]] = 1;
+  }
+  for (int fk = 1; fk < 14; fk++) {
+    const int nv = kNumVars[fk];
+    const int64_t n = (int64_t)h->fint[fk].size();
+    for (int64_t f = 0; f < n; f++)
+      for (int s = 0; s < nv; s++)
+        for (int t = 0; t <= s; t++) {
+          const int ks_ = kFK[fk][s], kt = kFK[fk][t];
+          const int hs = h->fvars[fk][f * nv + s], ht = h->fvars[fk][f * nv + t];
+          if (hs < 0 || ht < 0 || ks_ == 8 || kt == 8 || ks_ == 0 || kt == 0) continue;
+          if (redOf[ks_][hs] < 0 || redOf[kt][ht] < 0) continue;
+          coupleBlocks(redOf[ks_][hs], redOf[kt][ht]);
+        }
+  }
+  // symbolic tile Cholesky (fill)
+  for (int32_t J = 0; J < nT; J++) {
+    std::vector<int32_t> rows;
+    for (int32_t I = J + 1; I < nT; I++)
+      if (pat[(size_t)I * nT + J]) rows.push_back(I);
+    for (size_t a = 0; a < rows.size(); a++)
+      for (size_t b = 0; b <= a; b++) pat[(size_t)rows[a] * nT + rows[b]] = 1;
+  }
+  std::vector<int32_t> tileIdx((size_t)nT * nT, -1);
+  h->colStart.assign(nT + 1, 0);
+  h->colTilesH.clear(), h->colRowsH.clear();
+  int64_t nTiles = 0;
+  for (int32_t J = 0; J < nT; J++) {
+    for (int32_t I = J; I < nT; I++)
+      if (I == J || pat[(size_t)I * nT + J]) {
+        tileIdx[(size_t)I * nT + J] = (int32_t)nTiles;
+        h->colTilesH.push_back((int32_t)nTiles++);
+        h->colRowsH.push_back(I);
+      }
+    h->colStart[J + 1] = (int64_t)h->colTilesH.size();
+  }
+  d.nTiles = nTiles;
+  std::vector<int32_t> pairs, targets;
+  h->pairStart.assign(nT + 1, 0);
+  for (int32_t J = 0; J < nT; J++) {
+    const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+    for (int64_t qi = 1; qi < n; qi++)
+      for (int64_t qk = 1; qk <= qi; qk++) {
+        pairs.push_back((int32_t)qi), pairs.push_back((int32_t)qk);
+        const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
+        if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
+        targets.push_back(t);
+      }
+    h->pairStart[J + 1] = (int64_t)targets.size();
+  }
+  h->rowStart.assign(nT + 1, 0);
+  h->rowTilesH.clear(), h->rowColH.clear();
+  for (int32_t J = 0; J < nT; J++) {
+    for (int32_t K = 0; K < J; K++)
+      if (tileIdx[(size_t)J * nT + K] >= 0) h->rowTilesH.push_back(tileIdx[(size_t)J * nT + K]), h->rowColH.push_back(K);
+    h->rowStart[J + 1] = (int64_t)h->rowTilesH.size();
+  }
+  // ---------------- small factors (+ whitening square roots)
+  for (int fk = 1; fk < 14; fk++) {
+    SmallFactors& sf = d.sf[fk];
+    sf.nv = kNumVars[fk];
+    sf.n = (int64_t)h->fint[fk].size();
+    const int extra = (fk >= 1 && fk <= 3) ? 81 : fk == 9 ? 36 : 0;
+    sf.nc = kNumConsts[fk] + extra;
+    std::vector<double> cs((size_t)sf.n * sf.nc);
+    for (int64_t f = 0; f < sf.n; f++) {
+      const double* src = &h->fconst[fk][f * kNumConsts[fk]];
+      double* dst = &cs[f * sf.nc];
+      std::copy(src, src + kNumConsts[fk], dst);
+      if (fk >= 1 && fk <= 3) {
+        if (!precisionChol(src + 11 + 207, 9, dst + 331)) return fail(VB_E_NUMERIC, "preintegration covariance not SPD");
+      } else if (fk == 9) {
+        psdSqrt(src + 7, 6, dst + 43);
+      }
+    }
+    if (upload(&sf.vars, h->fvars[fk])) return VB_E_HIP;
+    if (upload(&sf.consts, cs)) return VB_E_HIP;
+  }
+  // ---------------- uploads
+  for (int k = 0; k < 9; k++) {
+    if (upload(&d.var[k], h->data[k])) return VB_E_HIP;
+    if (alloc0(&d.varBak[k], h->data[k].size())) return VB_E_HIP;
+    if (upload(&d.redOf[k], redOf[k])) return VB_E_HIP;
+  }
+  if (upload(&d.rvKind, h->rvKind) || upload(&d.rvHandle, h->rvHandle) || upload(&d.rvDim, h->rvDim) ||
+      upload(&d.rvOff, h->rvOff) || upload(&d.rvRowEnd, rowEnd))
+    return VB_E_HIP;
+  if (upload(&d.obPose, obPose) || upload(&d.obExtr, obExtr) || upload(&d.obIntr, obIntr) ||
+      upload(&d.obVel, obVel) || upload(&d.obRS, obRS) || upload(&d.obPt, obPt) || upload(&d.obRed, obRed) ||
+      upload(&d.obCol, obCol) || upload(&d.obC, obC))
+    return VB_E_HIP;
+  if (alloc0(&d.cache, nObs) || alloc0(&d.Jt, (size_t)kJPlanes * d.nObsPad)) return VB_E_HIP;
+  if (upload(&d.lmObs, lmObs) || upload(&d.lmY, lmY) || upload(&d.lmBlk, lmBlk) || upload(&d.blkRed, blkRed) ||
+      upload(&d.blkCol, blkCol) || upload(&d.ptLm, lmOf))
+    return VB_E_HIP;
+  if (alloc0(&d.Vchol, nPts * 6) || alloc0(&d.gp, nPts * 3) || alloc0(&d.z, nPts * 3) || alloc0(&d.xp, nPts * 3) ||
+      alloc0(&d.Y, lmY[nPts]) || alloc0(&d.gpNew, nPts * 3) || alloc0(&d.zNew, nPts * 3))
+    return VB_E_HIP;
+  if (upload(&d.oxStart, oxStart) || upload(&d.oxObs, oxObs) || upload(&d.oxSlot, oxSlot) ||
+      upload(&d.lxStart, lxStart) || upload(&d.lxLm, lxLm) || upload(&d.lxCol, lxCol))
+    return VB_E_HIP;
+  if (upload(&d.tileIdx, tileIdx) || alloc0(&d.tiles, (size_t)nTiles * TS * TS)) return VB_E_HIP;
+  const size_t nPad = (size_t)nT * TS;
+  if (alloc0(&d.gRed, nPad) || alloc0(&d.rhs, nPad) || alloc0(&d.xRed, nPad) || alloc0(&d.gRedNew, nPad) ||
+      alloc0(&d.stepRed, nPad) || alloc0(&d.stepPt, nPts * 3) || alloc0(&d.subRed, nPad) ||
+      alloc0(&d.subPt, nPts * 3) || alloc0(&h->yvec, nPad) || alloc0(&h->rhsWork, nPad))
+    return VB_E_HIP;
+  if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) || upload(&h->pairsD, pairs) ||
+      upload(&h->targetsD, targets) || upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
+    return VB_E_HIP;
+  if (alloc0(&h->diagScratch, TS * TS)) return VB_E_HIP;
+  d.nRS = h->nRS;
+  if (upload(&d.rsOff, h->rsOff) || upload(&d.rsS, h->rsS) || upload(&d.rsI, h->rsI) || upload(&d.rsG, h->rsG))
+    return VB_E_HIP;
+  if (alloc0(&d.red, 64) || alloc0(&d.err, 4)) return VB_E_HIP;
+  h->finalized = true;
+  if (h->lmEnd < 0) h->lmEnd = nPts;
+  return 0;
+}
+
+// ------------------------------------------------------------------ numeric phases
+void factorReduced(vb_handle h) {
+  Dev& d = h->d;
+  for (int32_t J = 0; J < d.nT; J++) {
+    const int64_t c0 = h->colStart[J];
+    const int n = (int)(h->colStart[J + 1] - c0);
+    launch_potrf_trsm(d, h->colTilesD + c0, n, h->diagScratch, h->st);
+    const int64_t p0 = h->pairStart[J];
+    const int np = (int)(h->pairStart[J + 1] - p0);
+    launch_gemm_update(d, h->colTilesD + c0, h->pairsD + 2 * p0, h->targetsD + p0, np, h->diagScratch, h->st);
+  }
+}
+
+// solve L L^T x = b (b is clobbered), result into x
+void solveReduced(vb_handle h, double* b, double* x) {
+  Dev& d = h->d;
+  for (int32_t J = 0; J < d.nT; J++) {
+    const int64_t c0 = h->colStart[J];
+    launch_fwd(d, h->colTilesD + c0, h->colRowsD + c0, (int)(h->colStart[J + 1] - c0), b, h->yvec, h->st);
+  }
+  for (int32_t J = d.nT - 1; J >= 0; J--) {
+    const int64_t r0 = h->rowStart[J];
+    launch_bwd(d, J, h->colTilesH[h->colStart[J]], h->rowTilesD + r0, h->rowColD + r0,
+               (int)(h->rowStart[J + 1] - r0), h->yvec, x, h->st);
+  }
+}
+
+double elapsed(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  return ms;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char* vb_last_error(void) { return g_err.c_str(); }
+int vb_factor_num_vars(int k) { return (k >= 0 && k < 14) ? kNumVars[k] : -1; }
+int vb_factor_num_consts(int k) { return (k >= 0 && k < 14) ? kNumConsts[k] : -1; }
+
+void vb_default_config(vb_config* c) {
+  c->reproj_loss_radius = 1.0, c->reproj_loss_cutoff = 3.0;
+  c->imu_loss_radius = INFINITY, c->imu_loss_cutoff = INFINITY;
+  c->imu_calib_options = VB_IMU_OPT_ALL, c->device = 0, c->tile = 0, c->reserved = 0;
+}
+void vb_default_settings(vb_settings* s) {
+  s->max_num_iterations = 50, s->stop_if_no_improvement_for = 3, s->distance_from_troubled_iteration = 3;
+  s->max_step_factor_attempts = 2, s->try_sub_step = 1, s->verbose = 0;
+  s->absolute_cost_tolerance = 1e-8, s->relative_cost_tolerance = 1e-10, s->variables_tolerance = 1e-5;
+  s->damping = 1e-5, s->damping_adjust_on_fail = 2.5, s->damping_adjust_on_good_step = 0.7;
+  s->damping_adjust_on_average_step = 1.5, s->damping_max = 1e8, s->damping_min = 1e-9;
+  s->min_relative_cost_reduction = 0.3, s->step_factor_decrease = 0.3, s->min_step_factor_for_good = 0.7;
+}
+
+int vb_create(const vb_config* cfg, vb_handle* out) {
+  if (!out) return fail(VB_E_ARG, "null output handle");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(VB_E_HIP, "no HIP device available");
+  vb_config c;
+  if (cfg) c = *cfg;
+  else vb_default_config(&c);
+  if (c.tile != 0 && c.tile != TS) return fail(VB_E_UNSUPPORTED, "only tile size 64 is built");
+  if (c.device < 0 || c.device >= ndev) return fail(VB_E_ARG, "bad device ordinal");
+  HIPCHK(hipSetDevice(c.device));
+  vb_handle h = new vb_handle_s();
+  h->cfg = c;
+  HIPCHK(hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking));
+  for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
+  *out = h;
+  return 0;
+}
+
+int vb_destroy(vb_handle h) {
+  if (!h) return 0;
+  hipSetDevice(h->cfg.device);
+  hipStreamSynchronize(h->st);
+  Dev& d = h->d;
+  void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obPose, d.obExtr, d.obIntr, d.obVel,
+                  d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
+                  d.blkCol, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
+                  d.lxStart, d.lxLm, d.lxCol, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
+                  d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
+                  h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->diagScratch, h->yvec,
+                  h->rhsWork};
+  for (void* p : ptrs)
+    if (p) hipFree(p);
+  for (int k = 0; k < 9; k++) {
+    if (d.var[k]) hipFree(d.var[k]);
+    if (d.varBak[k]) hipFree(d.varBak[k]);
+    if (d.redOf[k]) hipFree(d.redOf[k]);
+  }
+  for (int k = 0; k < 14; k++) {
+    if (d.sf[k].vars) hipFree(d.sf[k].vars);
+    if (d.sf[k].consts) hipFree(d.sf[k].consts);
+  }
+  for (auto& e : h->ev) hipEventDestroy(e);
+  hipStreamDestroy(h->st);
+  delete h;
+  return 0;
+}
+
+int vb_set_vars(vb_handle h, int kind, int64_t n, const double* data, const uint8_t* constant) {
+  if (!h || kind < 0 || kind >= 9 || n < 0 || (n > 0 && !data)) return fail(VB_E_ARG, "bad vb_set_vars arguments");
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_vars after vb_finalize");
+  h->data[kind].assign(data, data + n * kVarData[kind]);
+  h->cst[kind].assign(n, 0);
+  if (constant) std::copy(constant, constant + n, h->cst[kind].begin());
+  return 0;
+}
+
+int vb_add_factors(vb_handle h, int kind, int64_t n, const int32_t* var_idx, const int32_t* ivals,
+                   const double* consts) {
+  if (!h || kind < 0 || kind >= 14 || n < 0 || (n > 0 && (!var_idx || !consts)))
+    return fail(VB_E_ARG, "bad vb_add_factors arguments");
+  if (h->finalized) return fail(VB_E_STATE, "vb_add_factors after vb_finalize");
+  h->fvars[kind].insert(h->fvars[kind].end(), var_idx, var_idx + n * kNumVars[kind]);
+  for (int64_t i = 0; i < n; i++) h->fint[kind].push_back(ivals ? ivals[i] : -1);
+  h->fconst[kind].insert(h->fconst[kind].end(), consts, consts + n * kNumConsts[kind]);
+  return 0;
+}
+
+int vb_set_rs_tables(vb_handle h, int32_t nt, const int64_t* offsets, const double* samples, const double* interp,
+                     const double* gravity) {
+  if (!h || nt < 0) return fail(VB_E_ARG, "bad vb_set_rs_tables arguments");
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_rs_tables after vb_finalize");
+  h->nRS = nt;
+  h->rsOff.assign(offsets, offsets + nt + 1);
+  const int64_t ns = offsets[nt];
+  h->rsS.assign(samples, samples + ns * 11);
+  h->rsI.assign(interp, interp + (ns - nt) * 9);
+  h->rsG.assign(gravity, gravity + nt * 3);
+  for (int t = 0; t < nt; t++)
+    if (offsets[t + 1] - offsets[t] < 2) return fail(VB_E_ARG, "RS table needs >= 2 samples");
+  return 0;
+}
+
+int vb_finalize(vb_handle h) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  if (h->finalized) return fail(VB_E_STATE, "already finalized");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  return doFinalize(h);
+}
+
+int64_t vb_reduced_order(vb_handle h) { return h ? h->d.nRed : -1; }
+int64_t vb_total_order(vb_handle h) { return h ? h->order : -1; }
+
+int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_root) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_set_landmark_shard needs a finalized handle");
+  if (lm_begin < 0 || lm_end > h->d.nPts || lm_begin > lm_end) return fail(VB_E_ARG, "bad landmark range");
+  h->lmBegin = lm_begin, h->lmEnd = lm_end, h->isRoot = is_root != 0;
+  return 0;
+}
+
+int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* cost) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_linearize before vb_finalize");
+  Dev& d = h->d;
+  HIPCHK(hipEventRecord(h->ev[0], h->st));
+  HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  launch_pad_diag(d, h->st);
+  const int64_t o0 = 0, o1 = d.nObs;  // (shard restriction applies to landmark-side work)
+  launch_visual_lin(d, update_cache, dont_retry_failed, o0, o1, h->st);
+  if (h->isRoot) launch_small(d, 0, d.gRed, h->st);
+  HIPCHK(hipEventRecord(h->ev[1], h->st));
+  double c = 0;
+  if (int rc = readRed(h, &c, 0, 1)) return rc;
+  if (int rc = checkErr(h)) return rc;
+  h->times.linearize_ms = elapsed(h->ev[0], h->ev[1]);
+  if (cost) *cost = c;
+  h->linearized = true, h->factored = false;
+  return 0;
+}
+
+int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reduction) {
+  if (!h || !h->linearized) return fail(VB_E_STATE, "vb_damp_factor_solve needs a fresh vb_linearize");
+  Dev& d = h->d;
+  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  HIPCHK(hipEventRecord(h->ev[2], h->st));
+  launch_landmark(d, lambda, 0, 0, d.nPts, h->st);
+  launch_schur(d, lambda, h->st);
+  HIPCHK(hipEventRecord(h->ev[3], h->st));
+  factorReduced(h);
+  HIPCHK(hipEventRecord(h->ev[4], h->st));
+  HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  solveReduced(h, h->rhsWork, d.xRed);
+  launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
+  HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
+  launch_dot(d.xRed, d.gRed, d.nRed, d.red + 16, h->st);
+  launch_dot(d.xp, d.gp, d.nPts * 3, d.red + 16, h->st);
+  launch_axpby(d.stepRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
+  launch_axpby(d.stepPt, d.xp, -1.0, 0.0, d.nPts * 3, h->st);
+  HIPCHK(hipEventRecord(h->ev[5], h->st));
+  double dotv = 0;
+  if (int rc = readRed(h, &dotv, 16, 1)) return rc;
+  if (int rc = checkErr(h)) return rc;
+  h->times.schur_ms = elapsed(h->ev[2], h->ev[3]);
+  h->times.factor_ms = elapsed(h->ev[3], h->ev[4]);
+  h->times.solve_ms = elapsed(h->ev[4], h->ev[5]);
+  if (model_cost_reduction) *model_cost_reduction = 0.5 * dotv;
+  h->linearized = false, h->factored = true;
+  return 0;
+}
+
+int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red) {
+  if (!h || !h->factored) return fail(VB_E_STATE, "vb_gradient_dot_step needs a factorization");
+  Dev& d = h->d;
+  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.red, 0, 1 * sizeof(double), h->st));
+  launch_visual_lin(d, 0, dont_retry_failed, 0, d.nObs, h->st);
+  if (h->isRoot) launch_small(d, 1, d.gRedNew, h->st);
+  launch_landmark(d, 0.0, 1, 0, d.nPts, h->st);
+  launch_reduced_grad(d, 0, h->st);
+  HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
+  launch_dot(d.gRedNew, d.stepRed, d.nRed, d.red + 16, h->st);
+  launch_dot(d.gpNew, d.stepPt, d.nPts * 3, d.red + 16, h->st);
+  double dotv = 0;
+  if (int rc = readRed(h, &dotv, 16, 1)) return rc;
+  if (int rc = checkErr(h)) return rc;
+  if (back_red) *back_red = -0.5 * dotv;
+  return 0;
+}
+
+int vb_solve_with_new_gradient(vb_handle h) {
+  if (!h || !h->factored) return fail(VB_E_STATE, "vb_solve_with_new_gradient needs a factorization");
+  Dev& d = h->d;
+  launch_landmark(d, 0.0, 2, 0, d.nPts, h->st);
+  launch_reduced_grad(d, 1, h->st);
+  HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  solveReduced(h, h->rhsWork, d.xRed);
+  launch_backsub(d, 1, 0, d.nPts, d.xRed, d.xp, h->st);
+  launch_axpby(d.subRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
+  launch_axpby(d.subPt, d.xp, -1.0, 0.0, d.nPts * 3, h->st);
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+int vb_scale_step(vb_handle h, double f) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  launch_axpby(h->d.stepRed, h->d.stepRed, 0.0, f, h->d.nRed, h->st);
+  launch_axpby(h->d.stepPt, h->d.stepPt, 0.0, f, h->d.nPts * 3, h->st);
+  return 0;
+}
+
+int vb_apply_step(vb_handle h, int which, double ratios[3]) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  Dev& d = h->d;
+  HIPCHK(hipEventRecord(h->ev[6], h->st));
+  HIPCHK(hipMemsetAsync(d.red + 8, 0, 3 * sizeof(double), h->st));
+  launch_boxplus(d, which ? d.subRed : d.stepRed, which ? d.subPt : d.stepPt, h->st);
+  HIPCHK(hipEventRecord(h->ev[7], h->st));
+  double r[3];
+  if (int rc = readRed(h, r, 8, 3)) return rc;
+  h->times.step_ms = elapsed(h->ev[6], h->ev[7]);
+  const double n = (double)std::max<int64_t>(1, h->nParams);
+  if (ratios) ratios[0] = r[0], ratios[1] = std::sqrt(r[1] / n), ratios[2] = r[2] / n;
+  return 0;
+}
+
+int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  Dev& d = h->d;
+  HIPCHK(hipEventRecord(h->ev[6], h->st));
+  HIPCHK(hipMemsetAsync(d.red + 1, 0, 4 * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  launch_visual_cost(d, comparable, 0, d.nObs, h->st);
+  if (h->isRoot) launch_small(d, 2, nullptr, h->st);
+  HIPCHK(hipEventRecord(h->ev[7], h->st));
+  double r[4];
+  if (int rc = readRed(h, r, 1, 4)) return rc;
+  if (int rc = checkErr(h)) return rc;
+  h->times.cost_ms = elapsed(h->ev[6], h->ev[7]);
+  int64_t nSmall = 0;
+  if (h->isRoot)
+    for (int k = 1; k < 14; k++) nSmall += d.sf[k].n;
+  if (cost) *cost = r[0];
+  if (stats) stats->num_total = (int64_t)std::llround(r[1]) + nSmall, stats->num_invalid = std::llround(r[2]),
+             stats->num_prev_invalid = std::llround(r[3]);
+  return 0;
+}
+
+int vb_backup(vb_handle h) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  for (int k = 0; k < 9; k++)
+    if (!h->data[k].empty())
+      HIPCHK(hipMemcpyAsync(h->d.varBak[k], h->d.var[k], h->data[k].size() * sizeof(double), hipMemcpyDeviceToDevice,
+                            h->st));
+  return 0;
+}
+int vb_restore(vb_handle h) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  for (int k = 0; k < 9; k++)
+    if (!h->data[k].empty())
+      HIPCHK(hipMemcpyAsync(h->d.var[k], h->d.varBak[k], h->data[k].size() * sizeof(double), hipMemcpyDeviceToDevice,
+                            h->st));
+  return 0;
+}
+
+int vb_get_vars(vb_handle h, int kind, double* out) {
+  if (!h || kind < 0 || kind >= 9 || !out) return fail(VB_E_ARG, "bad vb_get_vars arguments");
+  if (!h->finalized) {
+    std::copy(h->data[kind].begin(), h->data[kind].end(), out);
+    return 0;
+  }
+  HIPCHK(hipMemcpyAsync(out, h->d.var[kind], h->data[kind].size() * sizeof(double), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+static int getPerKind(vb_handle h, const double* red, const double* pt, int kind, double* out) {
+  Dev& d = h->d;
+  const int64_t n = d.nvar[kind];
+  const int md = kMaxTan[kind];
+  std::fill(out, out + n * md, 0.0);
+  if (kind == 0) {
+    std::vector<double> v(d.nPts * 3);
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(v.data(), pt, v.size() * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    for (int64_t p = 0; p < n; p++) {
+      const int l = h->lmOfPoint[p];
+      if (l >= 0) std::copy(&v[l * 3], &v[l * 3] + 3, out + p * 3);
+    }
+    return 0;
+  }
+  std::vector<double> v(d.nRed);
+  if (!v.empty()) HIPCHK(hipMemcpyAsync(v.data(), red, v.size() * sizeof(double), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  for (int i = 0; i < d.nRV; i++)
+    if (h->rvKind[i] == kind) std::copy(&v[h->rvOff[i]], &v[h->rvOff[i]] + h->rvDim[i], out + (int64_t)h->rvHandle[i] * md);
+  return 0;
+}
+
+int vb_get_step(vb_handle h, int which, int kind, double* out) {
+  if (!h || !h->finalized || kind < 0 || kind >= 9 || !out) return fail(VB_E_ARG, "bad vb_get_step arguments");
+  return getPerKind(h, which ? h->d.subRed : h->d.stepRed, which ? h->d.subPt : h->d.stepPt, kind, out);
+}
+// The visual part of the gradient is assembled inside the Schur pass (vb_damp_factor_solve); before
+// that, assemble it on demand into the gradient-only buffers (same kernels as gradient_dot_step).
+int vb_get_gradient(vb_handle h, int kind, double* out) {
+  if (!h || !h->finalized || kind < 0 || kind >= 9 || !out) return fail(VB_E_ARG, "bad vb_get_gradient arguments");
+  if (h->linearized) {
+    Dev& d = h->d;
+    HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
+    if (h->isRoot) launch_small(d, 1, d.gRedNew, h->st);
+    launch_landmark(d, 0.0, 1, 0, d.nPts, h->st);
+    launch_reduced_grad(d, 0, h->st);
+    return getPerKind(h, d.gRedNew, d.gpNew, kind, out);
+  }
+  return getPerKind(h, h->d.gRed, h->d.gp, kind, out);
+}
+
+int vb_last_phase_times(vb_handle h, vb_phase_times* out) {
+  if (!h || !out) return fail(VB_E_ARG, "null argument");
+  *out = h->times;
+  return 0;
+}
+
+void* vb_stream(vb_handle h) { return h ? (void*)h->st : nullptr; }
+
+int vb_reduced_buffers(vb_handle h, double** matrix, int64_t* matrix_len, double** rhs, int64_t* rhs_len) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  if (matrix) *matrix = h->d.tiles;
+  if (matrix_len) *matrix_len = h->d.nTiles * TS * TS;
+  if (rhs) *rhs = h->d.rhs;
+  if (rhs_len) *rhs_len = (int64_t)h->d.nT * TS;
+  return 0;
+}
+
+// Optimizer::optimize (Optimizer.cpp:768-1106), direct solver
+int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb pre, void* user, vb_summary* out) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_optimize before vb_finalize");
+  vb_settings s;
+  if (sp) s = *sp;
+  else vb_default_settings(&s);
+  double damping = s.damping;
+  int it = 0, lastImpr = 0, lastTroubled = -10;
+  double initialCost = 0, finalCost = 0, troubledStartDamping = damping;
+  int troubledStart = 0, nTroubled = 0, largestTroubled = 0;
+  int dontRetry = 0;
+  auto acceptable = [](const vb_cost_stats& st) {
+    const double rate = st.num_invalid / (st.num_total + 1.0);
+    return rate < 0.03 && (st.num_invalid < st.num_prev_invalid * 2.0 + 50);
+  };
+  int rc;
+  char buf[512];
+  while (true) {
+    auto t0 = std::chrono::steady_clock::now();
+    if (pre) pre(it, user);
+    double prevCost;
+    if ((rc = vb_linearize(h, 1, dontRetry, &prevCost))) return rc;
+    finalCost = prevCost;
+    if (it == 0) initialCost = prevCost;
+    double modelRed;
+    if ((rc = vb_damp_factor_solve(h, damping, &modelRed))) return rc;
+    if (modelRed < 0) {
+      // Optimizer.cpp:835-854: the reference re-linearizes into `hess` (same point, same cached
+      // costs) and raises the damping, keeping the old step; re-linearizing would only discard the
+      // factor a later sub-step solve reuses, so only the damping update is mirrored.
+      damping *= s.damping_adjust_on_fail;
+    }
+    if ((rc = vb_backup(h))) return rc;
+    double ratios[3];
+    if ((rc = vb_apply_step(h, 0, ratios))) return rc;
+    vb_cost_stats st;
+    double newCost;
+    if ((rc = vb_cost(h, 1, &newCost, &st))) return rc;
+    double costRed = prevCost - newCost;
+    const double ratioRedToCost = costRed / newCost;
+    double ratioRedToExp = costRed / modelRed;
+    double applied = 1.0;
+    bool okRate = acceptable(st);
+    if (s.max_step_factor_attempts > 0 && (ratioRedToExp < s.min_relative_cost_reduction || !okRate)) {
+      double backRed;
+      if ((rc = vb_gradient_dot_step(h, dontRetry, &backRed))) return rc;
+      double sf = backRed > 0 ? modelRed / (modelRed + backRed) : s.step_factor_decrease;
+      for (int i = 0; i < s.max_step_factor_attempts; i++) {
+        applied *= sf;
+        vb_scale_step(h, sf);
+        vb_restore(h);
+        double rr[3];
+        if ((rc = vb_apply_step(h, 0, rr))) return rc;
+        vb_cost_stats stF;
+        double costF;
+        if ((rc = vb_cost(h, 1, &costF, &stF))) return rc;
+        const double redF = prevCost - newCost;  // Optimizer.cpp:935 (reference uses the full-step cost)
+        const double rF = redF / (modelRed * applied);
+        if (rF >= s.min_relative_cost_reduction && acceptable(stF)) {
+          newCost = costF, st = stF, costRed = redF, ratioRedToExp = rF, okRate = true;
+          break;
+        }
+        if (s.try_sub_step) {
+          double br;
+          if ((rc = vb_gradient_dot_step(h, dontRetry, &br))) return rc;
+          if ((rc = vb_solve_with_new_gradient(h))) return rc;
+          double r2[3];
+          if ((rc = vb_apply_step(h, 1, r2))) return rc;
+          vb_cost_stats stS;
+          double costS;
+          if ((rc = vb_cost(h, 1, &costS, &stS))) return rc;
+          const double redS = prevCost - costS;
+          const double rS = redS / (modelRed * applied);
+          if (rS >= s.min_relative_cost_reduction && acceptable(stS)) {
+            newCost = costS, st = stS, costRed = redS, ratioRedToExp = rS, okRate = true;
+            break;
+          }
+        }
+        dontRetry = 1;
+        sf = s.step_factor_decrease;
+      }
+    }
+    const char* tol = ratioRedToCost < s.relative_cost_tolerance     ? "relative cost"
+                      : costRed < s.absolute_cost_tolerance          ? "absolute cost"
+                      : ratios[1] < s.variables_tolerance            ? "variable"
+                                                                     : nullptr;
+    if (newCost > prevCost || !okRate) {
+      if (lastTroubled != it - 1) troubledStartDamping = damping, troubledStart = it;
+      damping *= s.damping_adjust_on_fail;
+      vb_restore(h);
+      if (damping > s.damping_max) break;
+      lastTroubled = it;
+    } else {
+      if (lastTroubled == it - 1)
+        if (troubledStartDamping < 1e1 && damping > 1e-3) {
+          nTroubled++;
+          largestTroubled = std::max(largestTroubled, it - troubledStart);
+        }
+      if (ratioRedToExp >= s.min_relative_cost_reduction && applied > s.min_step_factor_for_good)
+        damping = std::max(damping * s.damping_adjust_on_good_step, s.damping_min);
+      else
+        damping *= s.damping_adjust_on_average_step;
+      finalCost = newCost;
+    }
+    HIPCHK(hipStreamSynchronize(h->st));
+    h->times.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    it++;
+    if (log && s.verbose) {
+      snprintf(buf, sizeof(buf),
+               "it %d cost %.12g -> %.12g lambda %.3g (t %.2f ms: lin %.2f schur %.2f factor %.2f solve %.2f)", it,
+               prevCost, newCost, damping, h->times.total_ms, h->times.linearize_ms, h->times.schur_ms,
+               h->times.factor_ms, h->times.solve_ms);
+      log(buf, user);
+    }
+    if (!tol) lastImpr = it;
+    if (it >= lastImpr + s.stop_if_no_improvement_for && it >= lastTroubled + s.distance_from_troubled_iteration) break;
+    if (it >= s.max_num_iterations) break;
+  }
+  if (out) {
+    out->initial_cost = initialCost, out->final_cost = finalCost;
+    out->num_troubled_seqs = nTroubled, out->largest_troubled_seq = largestTroubled, out->num_iterations = it;
+    out->reserved = 0;
+  }
+  return 0;
+}
+
+// sharded building blocks (landmark shards)
+int vb_assemble_reduced(vb_handle h, double lambda) {
+  if (!h || !h->linearized) return fail(VB_E_STATE, "vb_assemble_reduced needs vb_linearize");
+  launch_landmark(h->d, lambda, 0, 0, h->d.nPts, h->st);
+  launch_schur(h->d, lambda, h->st);
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkErr(h);
+}
+int vb_factor_solve_reduced(vb_handle h) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  factorReduced(h);
+  HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  solveReduced(h, h->rhsWork, h->d.xRed);
+  HIPCHK(hipMemcpyAsync(h->d.rhs, h->d.xRed, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkErr(h);
+}
+int vb_back_substitute(vb_handle h, double* mcr) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  Dev& d = h->d;
+  HIPCHK(hipMemcpyAsync(d.xRed, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
+  HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
+  if (h->isRoot) launch_dot(d.xRed, d.gRed, d.nRed, d.red + 16, h->st);
+  launch_dot(d.xp, d.gp, d.nPts * 3, d.red + 16, h->st);
+  launch_axpby(d.stepRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
+  launch_axpby(d.stepPt, d.xp, -1.0, 0.0, d.nPts * 3, h->st);
+  double v = 0;
+  if (int rc = readRed(h, &v, 16, 1)) return rc;
+  if (mcr) *mcr = 0.5 * v;
+  h->factored = true;
+  return 0;
+}
+
+}  // extern "C"

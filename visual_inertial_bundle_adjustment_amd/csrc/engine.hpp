@@ -1,0 +1,109 @@
+// Device-resident problem state of one vb_handle and the kernel launch wrappers.
+// HBM layout (fp64 throughout, SoA where a kernel streams it):
+//   variables      var[kind]      rows of VB data size (3/7/3/3/24/7/32/7/4 doubles)
+//   visual obs     sorted by landmark; ob_* int32 index arrays + obC[6] (u, v, sqrtH 2x2)
+//   whitened J     Jt[plane * nObsPad + o], 72 planes (see kJ* below), written once per linearize
+//   landmarks      per point: Vchol[6], gp[3], z[3], xp[3]; Y panel 3 x d_l at Y + lmY[l]
+//   reduced system dense T x T column-major tiles (envelope / tile-sparse), tileIdx[I*nT+J]
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace viba {
+
+// planes of the whitened visual Jacobian record
+constexpr int kJe = 0;      // e0, e1
+constexpr int kJpt = 2;     // 2x3 point, row-major
+constexpr int kJpose = 8;   // 2x6
+constexpr int kJextr = 20;  // 2x6
+constexpr int kJintr = 32;  // 2x17
+constexpr int kJvel = 66;   // 2x3
+constexpr int kJPlanes = 72;
+// slot order of an observation's reduced blocks
+constexpr int kSlotPose = 0, kSlotExtr = 1, kSlotIntr = 2, kSlotVel = 3;
+__host__ __device__ inline int slotPlane(int s) {
+  return s == 0 ? kJpose : s == 1 ? kJextr : s == 2 ? kJintr : kJvel;
+}
+__host__ __device__ inline int slotStride(int s) { return s == 0 || s == 1 ? 6 : s == 2 ? 17 : 3; }
+
+struct ImuIdx {
+  int gB, aB, gS, aS, gN, aN, rT, gaT, size;
+};
+
+struct LossParams {
+  double a, b, k2, h;
+};
+
+struct SmallFactors {  // one kind
+  int64_t n = 0;
+  int32_t* vars = nullptr;   // n * nv
+  double* consts = nullptr;  // n * nc (+ whitening appended for IMU / pose prior)
+  int nv = 0, nc = 0;
+};
+
+struct Dev {
+  // variables
+  double* var[9] = {};
+  double* varBak[9] = {};
+  int64_t nvar[9] = {};
+  int32_t* redOf[9] = {};  // reduced id per variable (-1: point / constant / unregistered)
+  // reduced variables
+  int32_t nRV = 0;
+  int64_t nRed = 0;
+  int32_t* rvKind = nullptr;
+  int32_t* rvHandle = nullptr;
+  int32_t* rvDim = nullptr;
+  int64_t* rvOff = nullptr;
+  int64_t* rvRowEnd = nullptr;
+  // visual observations (sorted by landmark)
+  int64_t nObs = 0, nObsPad = 0;
+  int32_t *obPose = nullptr, *obExtr = nullptr, *obIntr = nullptr, *obVel = nullptr,
+          *obRS = nullptr, *obPt = nullptr;
+  int32_t* obRed = nullptr;  // 4 per obs
+  int32_t* obCol = nullptr;  // 4 per obs (column offset in the landmark's Y panel, -1)
+  double* obC = nullptr;     // 6 per obs
+  double* cache = nullptr;   // ResultCache per obs
+  double* Jt = nullptr;
+  // landmarks
+  int64_t nPts = 0;
+  int64_t* lmObs = nullptr;   // nPts + 1
+  int64_t* lmY = nullptr;     // nPts + 1 (doubles)
+  int64_t* lmBlk = nullptr;   // nPts + 1 into blkRed/blkCol
+  int32_t* blkRed = nullptr;  // reduced ids of D(l), sorted by reduced offset
+  int32_t* blkCol = nullptr;  // column offset in Y panel
+  double *Vchol = nullptr, *gp = nullptr, *z = nullptr, *xp = nullptr, *Y = nullptr;
+  double *gpNew = nullptr, *zNew = nullptr;
+  int32_t* ptRed = nullptr;  // point param registered? (1/0) per point var handle
+  int32_t* ptLm = nullptr;   // point var handle -> landmark index (-1)
+  // per reduced variable incidence lists
+  int64_t* oxStart = nullptr;
+  int32_t* oxObs = nullptr;
+  int32_t* oxSlot = nullptr;
+  int64_t* lxStart = nullptr;
+  int32_t* lxLm = nullptr;
+  int32_t* lxCol = nullptr;
+  // tiles
+  int T = 64;
+  int32_t nT = 0;
+  int64_t nTiles = 0;
+  int32_t* tileIdx = nullptr;  // nT * nT
+  double* tiles = nullptr;
+  int64_t* colStart = nullptr;  // host-side copy used for launches
+  // reduced vectors
+  double *gRed = nullptr, *rhs = nullptr, *xRed = nullptr, *gRedNew = nullptr;
+  double *stepRed = nullptr, *stepPt = nullptr, *subRed = nullptr, *subPt = nullptr;
+  // small factors
+  SmallFactors sf[14];
+  // rolling shutter
+  int32_t nRS = 0;
+  int64_t* rsOff = nullptr;
+  double *rsS = nullptr, *rsI = nullptr, *rsG = nullptr;
+  // scratch for reductions
+  double* red = nullptr;  // 64 doubles
+  int32_t* err = nullptr;  // error flags
+  // config
+  LossParams reproj, imu;
+  ImuIdx jac;
+};
+
+}  // namespace viba

@@ -1,0 +1,740 @@
+// Factor linearization kernels (gfx950).
+//
+//   visual_kernel<WantJ>  one thread per observation: VisualFactor / RollingShutterVisualFactor
+//                         (viba/problem/VisualFactor.cpp:40-82, 131-210) + HuberLossWithCutoff
+//                         (SoftLoss.h:115-176).  WantJ: writes the loss-whitened residual and
+//                         Jacobian planes (sqrt(rho') * [e | J]) with coalesced SoA stores and
+//                         applies the ResultCache rules of Factor.h:555-583; !WantJ: cost pass
+//                         with the makeComparableWithStored rules of Factor.h:390-417.
+//   small_kernel<FK>      one thread per non-visual factor: inertial (InertialFactor.cpp:23-305),
+//                         omega priors (OmegaPriorFactor.cpp), random walks (RandomWalkFactor.cpp)
+//                         and priors (PriorFactor.cpp); whitened by the precision's Cholesky
+//                         factor, scattered into the reduced tiles / gradient with fp64 atomics.
+#include "device_math.hpp"
+#include "engine.hpp"
+
+namespace viba {
+using namespace dev;
+
+__device__ __forceinline__ v3 mk3(const double* base, int h) {
+  const double* p = base + (int64_t)h * 3;
+  return mk(p[0], p[1], p[2]);
+}
+
+// ------------------------------------------------------------------ block reduction helpers
+template <int N>
+__device__ void block_sum_atomic(double (&v)[N], double* out) {
+  __shared__ double sh[N][4];
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    double x = v[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    if ((threadIdx.x & 63) == 0) sh[k][threadIdx.x >> 6] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      double s = 0;
+      for (int w = 0; w < nw; w++) s += sh[k][w];
+      if (s != 0.0) atomicAdd(out + k, s);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ visual factor evaluation
+struct VisOut {
+  double e[2];
+  double Jpt[6], Jpose[12], Jextr[12], Jintr[34], Jvel[6];
+};
+
+// VisualFactor::operator() (VisualFactor.cpp:40-82) for T_bw given; Jacobians wrt point, the
+// pose argument (2x6), extrinsics (2x6) and intrinsics (2x nparams)
+template <bool WantJ>
+__device__ bool vis_eval(const double* obsC, v3 X, const se3& Tbw, const se3& Tcb, const double* cam,
+                         VisOut& o) {
+  v3 pRig = se3_act(Tbw, X);
+  v3 pCam = se3_act(Tcb, pRig);
+  double uv[2], Jc[6], Jp[30];
+  if (!project<WantJ>(cam, pCam, uv, Jc, Jp)) return false;
+  const double s00 = obsC[2], s01 = obsC[3], s10 = obsC[4], s11 = obsC[5];
+  const double r0 = uv[0] - obsC[0], r1 = uv[1] - obsC[1];
+  o.e[0] = s00 * r0 + s01 * r1;
+  o.e[1] = s10 * r0 + s11 * r1;
+  if (WantJ) {
+    double dW[6];  // sqrtH * dProj (2x3)
+#pragma unroll
+    for (int j = 0; j < 3; j++) dW[j] = s00 * Jc[j] + s01 * Jc[3 + j], dW[3 + j] = s10 * Jc[j] + s11 * Jc[3 + j];
+    m3 Rcb = qmat(Tcb.R);
+    m3 Rcw = qmat(qmul(Tcb.R, Tbw.R));
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        o.Jpt[r * 3 + j] = dW[r * 3] * Rcw.a[0][j] + dW[r * 3 + 1] * Rcw.a[1][j] + dW[r * 3 + 2] * Rcw.a[2][j];
+      double A[3];
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        A[j] = dW[r * 3] * Rcb.a[0][j] + dW[r * 3 + 1] * Rcb.a[1][j] + dW[r * 3 + 2] * Rcb.a[2][j];
+      // [A, A hat(-p)] ; A hat(-p) = p x A (row vector form): (A hat(-p))_j = sum_i A_i hat(-p)_ij
+      const v3 mp = neg(pRig);
+      o.Jpose[r * 6 + 0] = A[0], o.Jpose[r * 6 + 1] = A[1], o.Jpose[r * 6 + 2] = A[2];
+      o.Jpose[r * 6 + 3] = A[1] * mp.z - A[2] * mp.y;
+      o.Jpose[r * 6 + 4] = -A[0] * mp.z + A[2] * mp.x;
+      o.Jpose[r * 6 + 5] = A[0] * mp.y - A[1] * mp.x;
+      const v3 mc = neg(pCam);
+      const double* B = dW + r * 3;
+      o.Jextr[r * 6 + 0] = B[0], o.Jextr[r * 6 + 1] = B[1], o.Jextr[r * 6 + 2] = B[2];
+      o.Jextr[r * 6 + 3] = B[1] * mc.z - B[2] * mc.y;
+      o.Jextr[r * 6 + 4] = -B[0] * mc.z + B[2] * mc.x;
+      o.Jextr[r * 6 + 5] = B[0] * mc.y - B[1] * mc.x;
+    }
+    const int n = (int)cam[1];
+#pragma unroll
+    for (int j = 0; j < 17; j++) {
+      const double a0 = j < n ? Jp[j] : 0.0, a1 = j < n ? Jp[15 + j] : 0.0;
+      o.Jintr[j] = s00 * a0 + s01 * a1;
+      o.Jintr[17 + j] = s10 * a0 + s11 * a1;
+    }
+  }
+  return true;
+}
+
+// RollingShutterVisualFactor::operator() (VisualFactor.cpp:131-210)
+template <bool WantJ>
+__device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se3& Tbw, const se3& Tcb,
+                        const double* cam, v3 vel, bool wantTime, bool wantVel, VisOut& o, bool* oor) {
+  const double tpf = obsC[1] / cam[3] - 0.5;
+  const double ro = cam[4] != 0.0 ? cam[5] : 0.0;
+  const double dt = ro * tpf - cam[6];
+  const int64_t s0 = d.rsOff[rs], ns = d.rsOff[rs + 1] - s0;
+  const double* S = d.rsS + s0 * 11;
+  const double* I = d.rsI + (s0 - rs) * 9;
+  const double* G = d.rsG + rs * 3;
+  se3 Twb = se3_inv(Tbw);
+  q4 Rbw = qinv(Twb.R);
+  se3 TmidAtT = rs_estimate(S, I, (int)ns, G, dt, vel, Rbw, oor);
+  if (*oor) return false;
+  se3 TAtTMid = se3_inv(TmidAtT);
+  se3 TAtTw = se3_mul(TAtTMid, Tbw);
+  if (!vis_eval<WantJ>(obsC, X, TAtTw, Tcb, cam, o)) return false;
+  if (WantJ) {
+    double Jt[12];  // wrt T_AtT_w
+#pragma unroll
+    for (int i = 0; i < 12; i++) Jt[i] = o.Jpose[i];
+    const int n = (int)cam[1];
+    const bool estRO = cam[7] != 0.0, estOff = cam[8] != 0.0;
+    if (wantTime && (estRO || estOff)) {
+      const double kEps = 1e-6;
+      se3 TP = rs_estimate(S, I, (int)ns, G, dt + kEps, vel, Rbw, oor);
+      if (*oor) return false;
+      se3 dd = se3_mul(se3_inv(TP), TmidAtT);
+      double lg[6];
+      se3_log(dd, lg);
+      double dE[2];
+#pragma unroll
+      for (int r = 0; r < 2; r++) {
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) s += Jt[r * 6 + k] * (lg[k] / kEps);
+        dE[r] = s;
+      }
+      int idx = n + (estRO ? 1 : 0) + (estOff ? 1 : 0);
+      if (estOff) {
+        --idx;
+        o.Jintr[idx] = -dE[0], o.Jintr[17 + idx] = -dE[1];
+      }
+      if (estRO) {
+        --idx;
+        o.Jintr[idx] = dE[0] * tpf, o.Jintr[17 + idx] = dE[1] * tpf;
+      }
+    }
+    // pose Jacobian: Jt * (Adj(T_AtT_Mid) + [0, hat(R_AtT_w (v dt + 0.5 dt^2 g))])
+    double M[36];
+    se3_Adj(TAtTMid, M);
+    v3 vv = add(scl(dt, vel), scl(0.5 * dt * dt, mk(G[0], G[1], G[2])));
+    m3 H = hat(qrot(TAtTw.R, vv));
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+      for (int j = 0; j < 3; j++) M[i * 6 + 3 + j] += H.a[i][j];
+#pragma unroll
+    for (int r = 0; r < 2; r++)
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) s += Jt[r * 6 + k] * M[k * 6 + j];
+        o.Jpose[r * 6 + j] = s;
+      }
+    if (wantVel) {
+      m3 R = qmat(TAtTw.R);
+#pragma unroll
+      for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+          o.Jvel[r * 3 + j] = -dt * (Jt[r * 6] * R.a[0][j] + Jt[r * 6 + 1] * R.a[1][j] + Jt[r * 6 + 2] * R.a[2][j]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 6; i++) o.Jvel[i] = 0.0;
+    }
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ visual kernels
+// mode bits: 1 = update cache, 2 = dont retry failed
+__global__ void __launch_bounds__(256) visual_lin_kernel(Dev d, int updateCache, int dontRetry,
+                                                         int64_t lo, int64_t hi) {
+  const int64_t o = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double acc[1] = {0.0};
+  if (o < hi) {
+    double* Jt = d.Jt;
+    const int64_t P = d.nObsPad;
+    VisOut v;
+    bool ok = true, oor = false;
+    const double c0 = d.cache[o];
+    if (dontRetry && c0 < 0.0) {
+      ok = false;
+    } else {
+      const double* obsC = d.obC + o * 6;
+      const int pt = d.obPt[o];
+      const double* Xp = d.var[0] + (int64_t)pt * 3;
+      v3 X = mk(Xp[0], Xp[1], Xp[2]);
+      se3 Tbw = se3_load(d.var[1] + (int64_t)d.obPose[o] * 7);
+      se3 Tcb = se3_load(d.var[5] + (int64_t)d.obExtr[o] * 7);
+      const double* cam = d.var[4] + (int64_t)d.obIntr[o] * 24;
+      const int rs = d.obRS[o];
+      if (rs < 0) {
+        ok = vis_eval<true>(obsC, X, Tbw, Tcb, cam, v);
+#pragma unroll
+        for (int i = 0; i < 6; i++) v.Jvel[i] = 0.0;
+      } else {
+        const double* vp = d.var[2] + (int64_t)d.obVel[o] * 3;
+        const int32_t* red = d.obRed + o * 4;
+        ok = rs_eval<true>(d, obsC, rs, X, Tbw, Tcb, cam, mk(vp[0], vp[1], vp[2]), red[kSlotIntr] >= 0,
+                           red[kSlotVel] >= 0, v, &oor);
+        if (oor) atomicOr(d.err, 1);
+      }
+      if (!ok && (updateCache || dontRetry)) d.cache[o] = -1.0;
+    }
+    if (ok) {
+      const double s = v.e[0] * v.e[0] + v.e[1] * v.e[1];
+      double rho, drho;
+      huber_jet2(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s, rho, drho);
+      const double w = sqrt(drho);
+      Jt[(kJe + 0) * P + o] = w * v.e[0];
+      Jt[(kJe + 1) * P + o] = w * v.e[1];
+#pragma unroll
+      for (int i = 0; i < 6; i++) Jt[(kJpt + i) * P + o] = w * v.Jpt[i];
+#pragma unroll
+      for (int i = 0; i < 12; i++) Jt[(kJpose + i) * P + o] = w * v.Jpose[i];
+#pragma unroll
+      for (int i = 0; i < 12; i++) Jt[(kJextr + i) * P + o] = w * v.Jextr[i];
+#pragma unroll
+      for (int i = 0; i < 34; i++) Jt[(kJintr + i) * P + o] = w * v.Jintr[i];
+#pragma unroll
+      for (int i = 0; i < 6; i++) Jt[(kJvel + i) * P + o] = w * v.Jvel[i];
+      acc[0] = 0.5 * rho;
+      if (updateCache) d.cache[o] = 0.5 * rho;
+    } else {
+#pragma unroll 8
+      for (int i = 0; i < kJPlanes; i++) Jt[i * P + o] = 0.0;
+    }
+  }
+  block_sum_atomic<1>(acc, d.red + 0);
+}
+
+// cost pass: red[1] += cost, red[2..4] += stats (numTotal, numInvalid, numPrevInvalid)
+__global__ void __launch_bounds__(256) visual_cost_kernel(Dev d, int comparable, int64_t lo, int64_t hi) {
+  const int64_t o = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  if (o < hi) {
+    VisOut v;
+    bool oor = false, ok;
+    const double* obsC = d.obC + o * 6;
+    const int pt = d.obPt[o];
+    const double* Xp = d.var[0] + (int64_t)pt * 3;
+    v3 X = mk(Xp[0], Xp[1], Xp[2]);
+    se3 Tbw = se3_load(d.var[1] + (int64_t)d.obPose[o] * 7);
+    se3 Tcb = se3_load(d.var[5] + (int64_t)d.obExtr[o] * 7);
+    const double* cam = d.var[4] + (int64_t)d.obIntr[o] * 24;
+    const int rs = d.obRS[o];
+    if (rs < 0) {
+      ok = vis_eval<false>(obsC, X, Tbw, Tcb, cam, v);
+    } else {
+      const double* vp = d.var[2] + (int64_t)d.obVel[o] * 3;
+      ok = rs_eval<false>(d, obsC, rs, X, Tbw, Tcb, cam, mk(vp[0], vp[1], vp[2]), false, false, v, &oor);
+      if (oor) atomicOr(d.err, 1);
+    }
+    const double prev = d.cache[o];
+    const bool prevInvalid = prev < 0.0;
+    acc[1] = 1.0;
+    acc[2] = ok ? 0.0 : 1.0;
+    acc[3] = prevInvalid ? 1.0 : 0.0;
+    if (comparable && prevInvalid) {
+      // forced comparable: contributes nothing
+    } else if (comparable && !ok) {
+      acc[0] = prev;
+    } else if (ok) {
+      const double s = v.e[0] * v.e[0] + v.e[1] * v.e[1];
+      acc[0] = 0.5 * huber_val(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s);
+    }
+  }
+  block_sum_atomic<4>(acc, d.red + 1);
+}
+
+// ------------------------------------------------------------------ small factors
+constexpr int kMaxM = 23;
+constexpr int kMaxCols = 80;
+
+struct SmallEval {
+  int m = 0;
+  int nslot = 0;
+  int col[10], dim[10], red[10];
+  double e[kMaxM];
+  double J[kMaxM][kMaxCols];
+};
+
+__device__ inline void imu_boxminus(const double* v, const double* r, const ImuIdx& J, double* res) {
+  if (J.gB >= 0) for (int i = 0; i < 3; i++) res[J.gB + i] = v[6 + i] - r[6 + i];
+  if (J.aB >= 0) for (int i = 0; i < 3; i++) res[J.aB + i] = v[9 + i] - r[9 + i];
+  if (J.gS >= 0) for (int i = 0; i < 3; i++) res[J.gS + i] = 1.0 / v[i] - 1.0 / r[i];
+  if (J.aS >= 0) for (int i = 0; i < 3; i++) res[J.aS + i] = 1.0 / v[3 + i] - 1.0 / r[3 + i];
+  if (J.gN >= 0) {
+    // col-major nonorth at 12: (i, j) -> 12 + 3 j + i
+    res[J.gN + 0] = v[12 + 3] - r[12 + 3];   // (0,1)
+    res[J.gN + 1] = v[12 + 6] - r[12 + 6];   // (0,2)
+    res[J.gN + 2] = v[12 + 1] - r[12 + 1];   // (1,0)
+    res[J.gN + 3] = v[12 + 7] - r[12 + 7];   // (1,2)
+    res[J.gN + 4] = v[12 + 2] - r[12 + 2];   // (2,0)
+    res[J.gN + 5] = v[12 + 5] - r[12 + 5];   // (2,1)
+  }
+  if (J.aN >= 0) {
+    res[J.aN + 0] = v[21 + 3] - r[21 + 3];   // (0,1)
+    res[J.aN + 1] = v[21 + 6] - r[21 + 6];   // (0,2)
+    res[J.aN + 2] = v[21 + 7] - r[21 + 7];   // (1,2)
+  }
+  if (J.rT >= 0) res[J.rT] = v[31] - r[31];
+  if (J.gaT >= 0) res[J.gaT] = (v[30] - v[31]) - (r[30] - r[31]);
+}
+
+// InertialFactor::operator() (InertialFactor.cpp:23-123). Jacobian blocks written into E.J at
+// columns c[0..4] (calib, Tp, vp, Tn, vn); a column offset < 0 skips that block.
+__device__ void inertial_eval(const double* c, const double* calib, const ImuIdx& jac, const se3& Tp, v3 vp,
+                              const se3& Tn, v3 vn, v3 g, SmallEval& E, const int cols[5]) {
+  const int n = jac.size;
+  const double dt = c[10];
+  double dc[23];
+  imu_boxminus(calib, c + 11 + 207 + 81, jac, dc);
+  double corr[9];
+  for (int i = 0; i < 9; i++) {
+    double s = 0;
+    for (int j = 0; j < n; j++) s += c[11 + j * 9 + i] * dc[j];
+    corr[i] = s;
+  }
+  q4 Rc = qexp(mk(-corr[0], -corr[1], -corr[2]));
+  q4 cR = qmul(Rc, qinv(q4{c[0], c[1], c[2], c[3]}));
+  q4 Rerr = qmul(qmul(cR, Tp.R), qinv(Tn.R));
+  v3 lre = neg(qlog(Rerr));
+  v3 dVp = qrot(Tp.R, sub(sub(vn, vp), scl(dt, g)));
+  v3 velErr = add(sub(mk(c[4], c[5], c[6]), dVp), mk(corr[3], corr[4], corr[5]));
+  q4 Rpn = qmul(Tp.R, qinv(Tn.R));
+  v3 dPp = sub(sub(Tp.t, qrot(Rpn, Tn.t)), qrot(Tp.R, add(scl(dt, vp), scl(0.5 * dt * dt, g))));
+  v3 posErr = add(sub(mk(c[7], c[8], c[9]), dPp), mk(corr[6], corr[7], corr[8]));
+  E.e[0] = lre.x, E.e[1] = lre.y, E.e[2] = lre.z;
+  E.e[3] = velErr.x, E.e[4] = velErr.y, E.e[5] = velErr.z;
+  E.e[6] = posErr.x, E.e[7] = posErr.y, E.e[8] = posErr.z;
+  m3 dL = so3_leftJacInv(neg(lre));
+  m3 Rp = qmat(Tp.R);
+  if (cols[1] >= 0) {
+    const int c0 = cols[1];
+    m3 A = mmul(dL, qmat(cR));
+    m3 hv = hat(dVp), hp = hat(dPp);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        E.J[i][c0 + j] = 0.0, E.J[i][c0 + 3 + j] = -A.a[i][j];
+        E.J[3 + i][c0 + j] = 0.0, E.J[3 + i][c0 + 3 + j] = hv.a[i][j];
+        E.J[6 + i][c0 + j] = (i == j) ? -1.0 : 0.0, E.J[6 + i][c0 + 3 + j] = hp.a[i][j];
+      }
+  }
+  if (cols[2] >= 0) {
+    const int c0 = cols[2];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        E.J[i][c0 + j] = 0.0;
+        E.J[3 + i][c0 + j] = Rp.a[i][j];
+        E.J[6 + i][c0 + j] = Rp.a[i][j] * dt;
+      }
+  }
+  if (cols[3] >= 0) {
+    const int c0 = cols[3];
+    m3 A = mmul(dL, qmat(Rerr));
+    m3 Rm = qmat(Rpn);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        E.J[i][c0 + j] = 0.0, E.J[i][c0 + 3 + j] = A.a[i][j];
+        E.J[3 + i][c0 + j] = 0.0, E.J[3 + i][c0 + 3 + j] = 0.0;
+        E.J[6 + i][c0 + j] = Rm.a[i][j], E.J[6 + i][c0 + 3 + j] = 0.0;
+      }
+  }
+  if (cols[4] >= 0) {
+    const int c0 = cols[4];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        E.J[i][c0 + j] = 0.0;
+        E.J[3 + i][c0 + j] = -Rp.a[i][j];
+        E.J[6 + i][c0 + j] = 0.0;
+      }
+  }
+  if (cols[0] >= 0) {
+    const int c0 = cols[0];
+    m3 dR = mmul(dL, so3_leftJac(mk(-corr[0], -corr[1], -corr[2])));
+    for (int j = 0; j < n; j++) {
+      const double j0 = c[11 + j * 9], j1 = c[11 + j * 9 + 1], j2 = c[11 + j * 9 + 2];
+      for (int i = 0; i < 3; i++) E.J[i][c0 + j] = dR.a[i][0] * j0 + dR.a[i][1] * j1 + dR.a[i][2] * j2;
+      for (int i = 3; i < 9; i++) E.J[i][c0 + j] = c[11 + j * 9 + i];
+    }
+  }
+}
+
+// SecondaryImuInertialFactor::SecondaryState (InertialFactor.cpp:136-181)
+struct SecState {
+  v3 t_b_i, v_b, vw;
+  q4 R_w_b;
+  se3 T_iw;
+};
+__device__ SecState sec_state(const se3& Tbw, v3 vel, v3 om, const se3& Tib) {
+  SecState s;
+  s.t_b_i = se3_inv(Tib).t;
+  s.v_b = cross(om, s.t_b_i);
+  s.R_w_b = qinv(Tbw.R);
+  s.T_iw = se3_mul(Tib, Tbw);
+  s.vw = add(vel, qrot(s.R_w_b, s.v_b));
+  return s;
+}
+// compose the 9x6 / 9x3 Jacobians at columns (cT, cV) of `J` (wrt imu pose/vel) into the body
+// state blocks at columns oT, oV, oO, oE (each < 0 to skip; oE accumulates when addE)
+__device__ void sec_compose(const SecState& s, v3 om, const se3& Tib, double (*J)[kMaxCols], int cT, int cV,
+                            int oT, int oV, int oO, int oE, bool addE) {
+  m3 RA = qmat(s.R_w_b);
+  double JT[9][6], Jv[9][3];
+  for (int i = 0; i < 9; i++) {
+    for (int j = 0; j < 6; j++) JT[i][j] = J[i][cT + j];
+    for (int j = 0; j < 3; j++) Jv[i][j] = J[i][cV + j];
+  }
+  if (oT >= 0) {
+    double A[36];
+    se3_Adj(Tib, A);
+    m3 dv = mmul(RA, hat(s.v_b));  // RA * (-hat(-v_b))
+    for (int i = 0; i < 9; i++)
+      for (int j = 0; j < 6; j++) {
+        double x = 0;
+        for (int k = 0; k < 6; k++) x += JT[i][k] * A[k * 6 + j];
+        if (j >= 3) x += Jv[i][0] * dv.a[0][j - 3] + Jv[i][1] * dv.a[1][j - 3] + Jv[i][2] * dv.a[2][j - 3];
+        J[i][oT + j] = x;
+      }
+  }
+  if (oO >= 0) {
+    m3 B = mmul(RA, hat(neg(s.t_b_i)));
+    for (int i = 0; i < 9; i++)
+      for (int j = 0; j < 3; j++)
+        J[i][oO + j] = Jv[i][0] * B.a[0][j] + Jv[i][1] * B.a[1][j] + Jv[i][2] * B.a[2][j];
+  }
+  if (oE >= 0) {
+    m3 B = mmul(mmul(RA, hat(om)), mT(qmat(Tib.R)));  // times -1 below
+    for (int i = 0; i < 9; i++)
+      for (int j = 0; j < 6; j++) {
+        double x = JT[i][j];
+        if (j < 3) x -= Jv[i][0] * B.a[0][j] + Jv[i][1] * B.a[1][j] + Jv[i][2] * B.a[2][j];
+        J[i][oE + j] = addE ? J[i][oE + j] + x : x;
+      }
+  }
+  if (oV >= 0)
+    for (int i = 0; i < 9; i++)
+      for (int j = 0; j < 3; j++) J[i][oV + j] = Jv[i][j];
+}
+
+struct SmallArgs {
+  int64_t n;
+  const int32_t* vars;
+  const double* consts;
+  int nc;
+  int mode;  // 0: grad+hess, 1: grad only (into gOut), 2: cost
+  double* gOut;
+};
+
+__device__ inline int tdim_of(const Dev& d, int kind, int h) {
+  switch (kind) {
+    case 0: case 2: case 3: return 3;
+    case 1: case 5: case 7: return 6;
+    case 4: {
+      const double* c = d.var[4] + (int64_t)h * 24;
+      return (int)c[1] + (c[7] != 0.0 ? 1 : 0) + (c[8] != 0.0 ? 1 : 0);
+    }
+    case 6: return d.jac.size;
+  }
+  return 0;
+}
+
+__device__ inline double* tile_addr(const Dev& d, int64_t r, int64_t c) {
+  const int T = d.T;
+  const int32_t ti = d.tileIdx[(r / T) * d.nT + (c / T)];
+  return d.tiles + (int64_t)ti * T * T + (c % T) * T + (r % T);
+}
+
+// kinds of the factor arguments (reference functor order)
+__constant__ int kFK[14][10] = {
+    {0, 1, 5, 4, 2}, {6, 1, 2, 1, 2, 8}, {6, 1, 2, 3, 1, 2, 3, 7, 8}, {6, 1, 2, 3, 7, 1, 2, 3, 7, 8},
+    {3, 7}, {6, 6}, {4, 4}, {7, 7}, {5, 5}, {1}, {6}, {4}, {5}, {7}};
+__constant__ int kNV[14] = {5, 6, 9, 10, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1};
+
+template <int FK>
+__global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double acc[1] = {0.0};
+  if (k < a.n) {
+    SmallEval E;
+    const int nv = kNV[FK];
+    const int32_t* vi = a.vars + k * nv;
+    const double* c = a.consts + k * a.nc;
+    // column layout: every non-gravity slot gets columns (also constant ones: simpler eval)
+    int colc = 0;
+    E.nslot = nv;
+    for (int s = 0; s < nv; s++) {
+      const int kind = kFK[FK][s], h = vi[s];
+      if (kind == 8 || h < 0) {
+        E.col[s] = -1, E.dim[s] = 0, E.red[s] = -1;
+        continue;
+      }
+      E.dim[s] = tdim_of(d, kind, h);
+      E.col[s] = colc;
+      colc += E.dim[s];
+      E.red[s] = d.redOf[kind][h];
+    }
+    for (int i = 0; i < kMaxM; i++)
+      for (int j = 0; j < colc; j++) E.J[i][j] = 0.0;
+    bool whiten = false;
+    const double* U = nullptr;
+    bool useImuLoss = false;
+    if (FK == 1 || FK == 2 || FK == 3) {
+      E.m = 9;
+      whiten = true;
+      U = c + 331;
+      useImuLoss = true;
+      const double* gd = d.var[8] + (int64_t)vi[nv - 1] * 4;
+      v3 g = mk(gd[0], gd[1], gd[2]);
+      const double* calib = d.var[6] + (int64_t)vi[0] * 32;
+      if (FK == 1) {
+        int cols[5] = {E.col[0], E.col[1], E.col[2], E.col[3], E.col[4]};
+        inertial_eval(c, calib, d.jac, se3_load(d.var[1] + (int64_t)vi[1] * 7), mk3(d.var[2], vi[2]),
+                      se3_load(d.var[1] + (int64_t)vi[3] * 7), mk3(d.var[2], vi[4]), g, E, cols);
+      } else {
+        // slots: split  [c, pT, pV, pO, pE, nT, nV, nO, nE, g]
+        //        common [c, pT, pV, pO, nT, nV, nO, E, g]
+        const bool split = FK == 3;
+        const int spT = 1, spV = 2, spO = 3, spE = split ? 4 : 7;
+        const int snT = split ? 5 : 4, snV = split ? 6 : 5, snO = split ? 7 : 6, snE = split ? 8 : 7;
+        se3 pT = se3_load(d.var[1] + (int64_t)vi[spT] * 7), nT = se3_load(d.var[1] + (int64_t)vi[snT] * 7);
+        se3 pE = se3_load(d.var[7] + (int64_t)vi[spE] * 7), nE = se3_load(d.var[7] + (int64_t)vi[snE] * 7);
+        v3 pV = mk3(d.var[2], vi[spV]), nV = mk3(d.var[2], vi[snV]);
+        v3 pO = mk3(d.var[3], vi[spO]), nO = mk3(d.var[3], vi[snO]);
+        SecState ps = sec_state(pT, pV, pO, pE), ns = sec_state(nT, nV, nO, nE);
+        // primary-factor blocks in scratch columns after the slot columns
+        const int sc = colc;  // pT 6, pV 3, nT 6, nV 3 => 18 scratch columns
+        int cols[5] = {E.col[0], sc, sc + 6, sc + 9, sc + 15};
+        inertial_eval(c, calib, d.jac, ps.T_iw, ps.vw, ns.T_iw, ns.vw, g, E, cols);
+        sec_compose(ps, pO, pE, E.J, sc, sc + 6, E.col[spT], E.col[spV], E.col[spO], E.col[spE], false);
+        sec_compose(ns, nO, nE, E.J, sc + 9, sc + 15, E.col[snT], E.col[snV], E.col[snO], E.col[snE], !split);
+      }
+    } else if (FK == 4) {  // omega prior
+      E.m = 3;
+      const double sig = c[3];
+      v3 om = mk3(d.var[3], vi[0]);
+      v3 wI = mk(c[0], c[1], c[2]);
+      v3 r;
+      if (vi[1] < 0) {
+        r = scl(1.0 / sig, sub(om, wI));
+      } else {
+        se3 Tib = se3_load(d.var[7] + (int64_t)vi[1] * 7);
+        r = scl(1.0 / sig, sub(om, qrot(qinv(Tib.R), wI)));
+        // -R^T * (-hat(-w)) / sig = -R^T hat(w) / sig
+        m3 B = mmul(mT(qmat(Tib.R)), hat(wI));
+        for (int i = 0; i < 3; i++)
+          for (int j = 0; j < 3; j++) E.J[i][E.col[1] + j] = 0.0, E.J[i][E.col[1] + 3 + j] = -B.a[i][j] / sig;
+      }
+      for (int i = 0; i < 3; i++) E.J[i][E.col[0] + i] = 1.0 / sig;
+      E.e[0] = r.x, E.e[1] = r.y, E.e[2] = r.z;
+    } else if (FK == 5 || FK == 10) {  // imu calib RW / prior (residual padded to 23)
+      E.m = 23;
+      const int n = d.jac.size;
+      double dd[23];
+      for (int i = 0; i < 23; i++) E.e[i] = 0.0, dd[i] = 0.0;
+      if (FK == 5) {
+        imu_boxminus(d.var[6] + (int64_t)vi[1] * 32, d.var[6] + (int64_t)vi[0] * 32, d.jac, dd);
+        for (int i = 0; i < n; i++) {
+          E.e[i] = dd[i] * c[i];
+          E.J[i][E.col[0] + i] = -c[i];
+          E.J[i][E.col[1] + i] = c[i];
+        }
+      } else {
+        imu_boxminus(d.var[6] + (int64_t)vi[0] * 32, c, d.jac, dd);
+        for (int i = 0; i < n; i++) {
+          const double sq = sqrt(c[32 + i]);
+          E.e[i] = dd[i] * sq;
+          E.J[i][E.col[0] + i] = sq;
+        }
+      }
+    } else if (FK == 6 || FK == 11) {  // cam intrinsics RW / prior (residual padded to 17)
+      E.m = 17;
+      for (int i = 0; i < 17; i++) E.e[i] = 0.0;
+      const double* v = d.var[4] + (int64_t)vi[FK == 6 ? 1 : 0] * 24;
+      const double* b = FK == 6 ? d.var[4] + (int64_t)vi[0] * 24 : c;
+      const int np = (int)v[1];
+      double dd[17];
+      int i = 0;
+      for (; i < np; i++) dd[i] = v[9 + i] - b[9 + i];
+      if (v[7] != 0.0) dd[i++] = v[5] - b[5];
+      if (v[8] != 0.0) dd[i++] = v[6] - b[6];
+      const int nt = i;
+      for (int j = 0; j < nt; j++) {
+        const double sq = FK == 6 ? c[j] : sqrt(c[24 + j]);
+        E.e[j] = dd[j] * sq;
+        if (FK == 6) {
+          E.J[j][E.col[0] + j] = -sq;
+          E.J[j][E.col[1] + j] = sq;
+        } else {
+          E.J[j][E.col[0] + j] = sq;
+        }
+      }
+    } else {  // SE3 RW (7, 8), pose prior (9), SE3 priors (12, 13)
+      E.m = 6;
+      const int vk = (FK == 7 || FK == 13) ? 7 : (FK == 9 ? 1 : 5);
+      se3 err;
+      double sq[6];
+      if (FK == 7 || FK == 8) {
+        err = se3_mul(se3_load(d.var[vk] + (int64_t)vi[1] * 7), se3_inv(se3_load(d.var[vk] + (int64_t)vi[0] * 7)));
+        for (int i = 0; i < 6; i++) sq[i] = c[i];
+      } else {
+        err = se3_mul(se3_load(d.var[vk] + (int64_t)vi[0] * 7), se3_inv(se3_load(c)));
+        for (int i = 0; i < 6; i++) sq[i] = FK == 9 ? 1.0 : sqrt(c[7 + i]);
+      }
+      double lg[6], Ji[36];
+      se3_log(err, lg);
+      se3_leftJacInv(lg, Ji);
+      for (int i = 0; i < 6; i++) E.e[i] = lg[i] * sq[i];
+      const int cn = (FK == 7 || FK == 8) ? E.col[1] : E.col[0];
+      for (int i = 0; i < 6; i++)
+        for (int j = 0; j < 6; j++) E.J[i][cn + j] = sq[i] * Ji[i * 6 + j];
+      if (FK == 7 || FK == 8) {
+        double A[36];
+        se3_Adj(err, A);
+        for (int i = 0; i < 6; i++)
+          for (int j = 0; j < 6; j++) {
+            double x = 0;
+            for (int q = 0; q < 6; q++) x += Ji[i * 6 + q] * A[q * 6 + j];
+            E.J[i][E.col[0] + j] = -sq[i] * x;
+          }
+      }
+      if (FK == 9) {
+        whiten = true;
+        U = c + 43;
+      }
+    }
+    // whitening by a square root U of the precision (P = U^T U, row-major m x m)
+    const int m = E.m;
+    if (whiten) {
+      double te[kMaxM];
+      for (int i = 0; i < m; i++) {
+        double s = 0;
+        for (int q = 0; q < m; q++) s += U[i * m + q] * E.e[q];
+        te[i] = s;
+      }
+      for (int i = 0; i < m; i++) E.e[i] = te[i];
+      for (int j = 0; j < colc; j++) {
+        for (int i = 0; i < m; i++) {
+          double s = 0;
+          for (int q = 0; q < m; q++) s += U[i * m + q] * E.J[q][j];
+          te[i] = s;
+        }
+        for (int i = 0; i < m; i++) E.J[i][j] = te[i];
+      }
+    }
+    double sq = 0;
+    for (int i = 0; i < m; i++) sq += E.e[i] * E.e[i];
+    double rho, drho;
+    if (useImuLoss) huber_jet2(d.imu.a, d.imu.b, d.imu.k2, d.imu.h, sq, rho, drho);
+    else rho = sq, drho = 1.0;
+    if (a.mode == 2) {
+      acc[0] = 0.5 * (useImuLoss ? huber_val(d.imu.a, d.imu.b, d.imu.k2, d.imu.h, sq) : sq);
+    } else {
+      acc[0] = 0.5 * rho;
+      const double w = sqrt(drho);
+      for (int s = 0; s < nv; s++) {
+        if (E.red[s] < 0) continue;
+        const int64_t ro = d.rvOff[E.red[s]];
+        for (int i = 0; i < E.dim[s]; i++) {
+          double gsum = 0;
+          for (int r = 0; r < m; r++) gsum += E.J[r][E.col[s] + i] * E.e[r];
+          atomicAdd(a.gOut + ro + i, drho * gsum);
+        }
+        if (a.mode != 0) continue;
+        for (int t = 0; t < nv; t++) {
+          if (E.red[t] < 0) continue;
+          const int64_t co = d.rvOff[E.red[t]];
+          for (int i = 0; i < E.dim[s]; i++)
+            for (int j = 0; j < E.dim[t]; j++) {
+              const int64_t R = ro + i, Cc = co + j;
+              if (R < Cc) continue;
+              double hs = 0;
+              for (int r = 0; r < m; r++) hs += E.J[r][E.col[s] + i] * E.J[r][E.col[t] + j];
+              atomicAdd(tile_addr(d, R, Cc), w * w * hs);
+            }
+        }
+      }
+    }
+  }
+  block_sum_atomic<1>(acc, d.red + (a.mode == 2 ? 1 : 0));
+}
+
+// ------------------------------------------------------------------ launch wrappers
+void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st) {
+  if (hi <= lo) return;
+  const int64_t n = hi - lo;
+  hipLaunchKernelGGL(visual_lin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, updateCache,
+                     dontRetry, lo, hi);
+}
+void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st) {
+  if (hi <= lo) return;
+  const int64_t n = hi - lo;
+  hipLaunchKernelGGL(visual_cost_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, comparable,
+                     lo, hi);
+}
+
+template <int FK>
+static void launch_one(const Dev& d, int mode, double* gOut, hipStream_t st) {
+  const SmallFactors& f = d.sf[FK];
+  if (f.n == 0) return;
+  SmallArgs a{f.n, f.vars, f.consts, f.nc, mode, gOut};
+  hipLaunchKernelGGL(small_kernel<FK>, dim3((unsigned)((f.n + 63) / 64)), dim3(64), 0, st, d, a);
+}
+
+void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st) {
+  launch_one<1>(d, mode, gOut, st);
+  launch_one<2>(d, mode, gOut, st);
+  launch_one<3>(d, mode, gOut, st);
+  launch_one<4>(d, mode, gOut, st);
+  launch_one<5>(d, mode, gOut, st);
+  launch_one<6>(d, mode, gOut, st);
+  launch_one<7>(d, mode, gOut, st);
+  launch_one<8>(d, mode, gOut, st);
+  launch_one<9>(d, mode, gOut, st);
+  launch_one<10>(d, mode, gOut, st);
+  launch_one<11>(d, mode, gOut, st);
+  launch_one<12>(d, mode, gOut, st);
+  launch_one<13>(d, mode, gOut, st);
+}
+
+}  // namespace viba
