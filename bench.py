@@ -1,0 +1,158 @@
+#!/usr/bin/env python
+"""LM iterations/s of the MI355X VI-BA engine on the synthetic config-C problem.
+
+Metric (BASELINE.json): "LM iterations/sec (and ms/iter) on 10k-pose/300k-landmark VI-BA".
+One step = one iteration of Optimizer::optimize (Optimizer.cpp:800-1097): linearize all factors,
+damp + Schur-eliminate landmarks + factor + solve the reduced system, box-plus, cost pass, and the
+LM accept/reject (+ rescaled / sub-step attempts when the step is bad), as driven by vb_optimize.
+
+    python bench.py [--gpus N --steps K --warmup W --config C]
+
+N > 1 runs under torch.distributed (one rank per GPU): landmarks are sharded in time-banded
+ranges, every rank linearizes/eliminates its shard, the partial reduced systems are summed on
+rank 0 over RCCL, rank 0 factors/solves and broadcasts the reduced step.
+Prints one JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# kernel families of vb_profile_kernel
+KF_VISUAL_LIN, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACKSUB, KF_COST = range(9)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix peak (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def visual_bytes_per_launch(p, nobs: int) -> float:
+    """Algorithmic HBM bytes of one visual linearize launch: per observation
+    48 B of constants, 6 int32 indices, the cached cost (read+write), the point (24 B) and the 72-plane
+    whitened Jacobian record written (576 B); shared variables (poses, velocities, calibration) once."""
+    per_obs = 48 + 6 * 4 + 16 + 24 + 72 * 8
+    shared = sum(p.vars[k].nbytes for k in (1, 2, 4, 5))
+    return nobs * per_obs + shared
+
+
+def cpu_baseline(full_kf: int, sample_kf: int = 1000):
+    """Oracle (single-threaded CPU restatement) on a time slice of the same workload; one LM iteration,
+    extrapolated linearly to the full problem (all phases are linear in #rigs at fixed band)."""
+    from oracle.refcpu import RefEngine
+    from visual_inertial_bundle_adjustment_amd import synth
+    frac = sample_kf / full_kf
+    cfg = synth.config("C", n_kf=sample_kf, n_lm=int(round(300000 * frac)))
+    p = synth.generate(cfg)
+    e = RefEngine(imu_calib_options=p.imu_calib_options)
+    synth.load_into(e, p)
+    t0 = time.perf_counter()
+    e.linearize(True, False)
+    e.damp_factor_solve(1e-5)
+    e.backup()
+    e.apply_step(0)
+    e.cost(True)
+    dt = time.perf_counter() - t0
+    per_iter_full = dt / frac
+    return {"value": 1.0 / per_iter_full, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+            "sample": f"one LM iteration of oracle/refcpu on a {sample_kf}-rig/{cfg.n_lm}-landmark/"
+                      f"{p.num_obs}-obs slice of config C ({dt:.2f} s), extrapolated x{1/frac:.0f} "
+                      "(linear in rigs at fixed band)",
+            "ms_per_step": per_iter_full * 1e3}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-family", type=int, default=KF_GEMM)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        from visual_inertial_bundle_adjustment_amd.distributed import run_sharded
+        return run_sharded(args, rank, world, local)
+
+    from visual_inertial_bundle_adjustment_amd import synth
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
+
+    t = time.perf_counter()
+    p = synth.generate(synth.config(args.config))
+    log(f"[bench] config {args.config}: {p.summary()} (generated in {time.perf_counter() - t:.1f}s)")
+    t = time.perf_counter()
+    e = HipEngine(imu_calib_options=p.imu_calib_options, device=local)
+    synth.load_into(e, p)
+    st = e.problem_stats()
+    log(f"[bench] finalize {time.perf_counter() - t:.1f}s; reduced order {st[3]}, tiles {st[5]} "
+        f"({st[4]} tile columns), gemm pairs/factorization {st[6]}")
+
+    # run exactly W then K iterations of the optimize loop (convergence stops disabled)
+    def settings(n):
+        return Settings.default(max_num_iterations=n, stop_if_no_improvement_for=10**6,
+                                distance_from_troubled_iteration=0)
+    if args.warmup:
+        s = e.optimize(settings(args.warmup))
+        log(f"[bench] warmup {s.num_iterations} its, cost {s.initial_cost:.6g} -> {s.final_cost:.6g}")
+    e.profile_kernel(args.profile_family)
+    e.synchronize()
+    t0 = time.perf_counter()
+    s = e.optimize(settings(args.steps))
+    e.synchronize()
+    elapsed = time.perf_counter() - t0
+    launches, kms = e.kernel_time()
+    e.profile_kernel(-1)
+    iters = s.num_iterations
+    ph = e.phase_times()
+    log(f"[bench] timed {iters} its in {elapsed:.3f}s, cost {s.initial_cost:.6g} -> {s.final_cost:.6g}; "
+        f"last it: lin {ph.linearize_ms:.2f} schur {ph.schur_ms:.2f} factor {ph.factor_ms:.2f} "
+        f"solve {ph.solve_ms:.2f} step {ph.step_ms:.2f} cost {ph.cost_ms:.2f} ms")
+
+    # roofline of the profiled kernel family
+    avg_ms = kms / max(1, launches)
+    if args.profile_family == KF_GEMM:
+        flops = st[6] * 2.0 * 64 ** 3  # per factorization = one launch sequence; per launch below
+        per_launch = flops / max(1, st[4])
+        achieved = per_launch / (avg_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
+                "kernel": "gemm_update_kernel (tile syrk/gemm, v_mfma_f64_16x16x4_f64)",
+                "avg_launch_ms": avg_ms, "launches": launches}
+    else:
+        b = visual_bytes_per_launch(p, st[0])
+        achieved = b / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "visual_lin_kernel (Jacobian fill)", "avg_launch_ms": avg_ms, "launches": launches}
+    cpu = None
+    if not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(int(p.vars[1].shape[0]))
+        except Exception as ex:  # the baseline must never hide the GPU number
+            log(f"[bench] cpu baseline failed: {ex}")
+    ms = elapsed * 1e3 / max(1, iters)
+    out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
+           "unit": "LM iterations/s", "n_gpus": 1, "steps": iters, "warmup": args.warmup,
+           "ms_per_step": ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+           "dtype": "f64", "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
+           "config": {"workload": f"config {args.config}: {st[0]} obs, {st[1]} landmarks, "
+                                  f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",
+                      "rigs": int(p.vars[1].shape[0]), "landmarks": int(st[1]), "observations": int(st[0]),
+                      "parallelism": "single GPU"},
+           "roofline": roof, "cpu_baseline": cpu}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

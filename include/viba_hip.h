@@ -271,6 +271,16 @@ int vb_back_substitute(vb_handle h, double* model_cost_reduction_partial);
 /* the HIP stream of the handle (hipStream_t), for interop with torch / RCCL */
 void* vb_stream(vb_handle h);
 
+/* ---------------------------------------------------------------- measurement
+ * time every launch of one kernel family with HIP events on the handle's stream
+ * (0 visual linearize, 1 landmark eliminate, 2 Schur assembly, 3 potrf+trsm, 4 tile GEMM update,
+ *  5 forward solve, 6 backward solve, 7 point back-substitution, 8 visual cost, 9 small factors;
+ *  -1 disables); vb_kernel_time returns launches and summed device milliseconds since enabling */
+int vb_profile_kernel(vb_handle h, int family);
+int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
+/* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs, nSmallFactors, 0, 0] */
+int vb_problem_stats(vb_handle h, int64_t* out10);
+
 #ifdef __cplusplus
 }
 #endif

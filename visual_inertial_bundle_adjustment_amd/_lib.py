@@ -58,3 +58,18 @@ def load_hip_lib() -> C.CDLL:
     if _hip is None:
         _hip = _load(HIP_LIB)
     return _hip
+
+
+_amdhip = None
+
+
+def hip_stream_sync(stream) -> None:
+    """hipStreamSynchronize on a raw stream handle (libamdhip64)."""
+    global _amdhip
+    if _amdhip is None:
+        _amdhip = C.CDLL("libamdhip64.so")
+        _amdhip.hipStreamSynchronize.argtypes = [C.c_void_p]
+        _amdhip.hipStreamSynchronize.restype = C.c_int
+    rc = _amdhip.hipStreamSynchronize(stream)
+    if rc != 0:
+        raise RuntimeError(f"hipStreamSynchronize failed: {rc}")

@@ -20,15 +20,16 @@ void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo,
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
-void launch_schur(const Dev& d, double lambda, hipStream_t st);
+void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st);
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
-void launch_potrf_trsm(const Dev& d, const int32_t* colTiles, int n, double* diagScratch, hipStream_t st);
+void launch_potrf_trsm(const Dev& d, const int32_t* colTiles, int n, double* diagScratch, double* linv,
+                       hipStream_t st);
 void launch_gemm_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets,
                         int npairs, const double* diagScratch, hipStream_t st);
 void launch_pad_diag(const Dev& d, hipStream_t st);
-void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, double* b, double* x,
-                hipStream_t st);
-void launch_bwd(const Dev& d, int J, int32_t diagTile, const int32_t* rowTiles, const int32_t* rowCol, int n,
+void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
+                double* b, double* x, hipStream_t st);
+void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
                 double* t, double* x, hipStream_t st);
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st);
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t st);
@@ -206,17 +207,59 @@ struct vb_handle_s {
   std::vector<int32_t> rowTilesH, rowColH;
   int32_t *colTilesD = nullptr, *colRowsD = nullptr, *pairsD = nullptr, *targetsD = nullptr, *rowTilesD = nullptr,
           *rowColD = nullptr;
-  double *diagScratch = nullptr, *yvec = nullptr, *rhsWork = nullptr;
+  double *diagScratch = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool isRoot = true;
+  // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
+  hipGraphExec_t factorGraph = nullptr, solveGraph = nullptr;
+  bool useGraphs = true;
   // state
   bool linearized = false, factored = false;
   vb_phase_times times{};
   hipEvent_t ev[8];
+  // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
+  int profFamily = -1;
+  std::vector<hipEvent_t> profEv;
+  size_t profUsed = 0;
+  int64_t profLaunches = 0;
+  double profMs = 0.0;
 };
 
 namespace {
+
+// kernel families for vb_profile_kernel
+enum { KF_VISUAL_LIN = 0, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACKSUB, KF_VISUAL_COST,
+       KF_SMALL, KF_COUNT };
+
+inline void profBegin(vb_handle h, int fam) {
+  if (h->profFamily != fam) return;
+  if (h->profUsed + 2 > h->profEv.size()) {
+    for (int i = 0; i < 256; i++) {
+      hipEvent_t e;
+      (void)hipEventCreate(&e);
+      h->profEv.push_back(e);
+    }
+  }
+  (void)hipEventRecord(h->profEv[h->profUsed], h->st);
+}
+inline void profEnd(vb_handle h, int fam) {
+  if (h->profFamily != fam) return;
+  (void)hipEventRecord(h->profEv[h->profUsed + 1], h->st);
+  h->profUsed += 2;
+}
+// harvest recorded pairs (call after a stream synchronisation)
+void profHarvest(vb_handle h) {
+  if (h->profFamily < 0 || h->profUsed == 0) return;
+  (void)hipStreamSynchronize(h->st);
+  for (size_t i = 0; i < h->profUsed; i += 2) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, h->profEv[i], h->profEv[i + 1]);
+    h->profMs += ms;
+    h->profLaunches++;
+  }
+  h->profUsed = 0;
+}
 
 int checkErr(vb_handle h) {
   int32_t e = 0;
@@ -232,6 +275,7 @@ int checkErr(vb_handle h) {
 int readRed(vb_handle h, double* out, int i0, int n) {
   HIPCHK(hipMemcpyAsync(out, h->d.red + i0, n * sizeof(double), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
+  profHarvest(h);
   return 0;
 }
 
@@ -284,8 +328,21 @@ int doFinalize(vb_handle h) {
         }
       }
   }
-  for (int64_t p = 0; p < d.nvar[0]; p++)
-    if (lmOf[p] == -2) lmOf[p] = (int32_t)nPts++;
+  // landmark numbering: by the earliest rig that observes the point (time-banded landmark shards
+  // and locality of the Schur lists), ties by handle
+  {
+    std::vector<int64_t> firstRig(d.nvar[0], INT64_MAX);
+    const int64_t nv0 = (int64_t)h->fint[0].size();
+    for (int64_t f = 0; f < nv0; f++) {
+      const int32_t pt = h->fvars[0][f * 5], pose = h->fvars[0][f * 5 + 1];
+      if (lmOf[pt] == -2) firstRig[pt] = std::min<int64_t>(firstRig[pt], pose);
+    }
+    std::vector<int64_t> pts;
+    for (int64_t p = 0; p < d.nvar[0]; p++)
+      if (lmOf[p] == -2) pts.push_back(p);
+    std::stable_sort(pts.begin(), pts.end(), [&](int64_t a, int64_t b) { return firstRig[a] < firstRig[b]; });
+    for (int64_t p : pts) lmOf[p] = (int32_t)nPts++;
+  }
   // ---------------- reduced ordering: mean pose ordinal of co-occurring poses
   const int nRV = (int)red.size();
   std::vector<double> ks(nRV, 0.0), kc(nRV, 0.0);
@@ -390,6 +447,13 @@ int doFinalize(vb_handle h) {
         obCol[o * 4 + s] = blkCol[q];
       }
   }
+  // reduced row of every landmark panel column
+  std::vector<int32_t> pcRow(lmY[nPts] / 3);
+  for (int64_t l = 0; l < nPts; l++)
+    for (int64_t b = lmBlk[l]; b < lmBlk[l + 1]; b++) {
+      const int32_t r = blkRed[b];
+      for (int j = 0; j < h->rvDim[r]; j++) pcRow[lmY[l] / 3 + blkCol[b] + j] = (int32_t)(h->rvOff[r] + j);
+    }
   // incidence lists O(X), L(X)
   std::vector<int64_t> oxStart(nRV + 1, 0), lxStart(nRV + 1, 0);
   for (int64_t o = 0; o < nObs; o++)
@@ -541,7 +605,7 @@ int doFinalize(vb_handle h) {
     return VB_E_HIP;
   if (alloc0(&d.cache, nObs) || alloc0(&d.Jt, (size_t)kJPlanes * d.nObsPad)) return VB_E_HIP;
   if (upload(&d.lmObs, lmObs) || upload(&d.lmY, lmY) || upload(&d.lmBlk, lmBlk) || upload(&d.blkRed, blkRed) ||
-      upload(&d.blkCol, blkCol) || upload(&d.ptLm, lmOf))
+      upload(&d.blkCol, blkCol) || upload(&d.ptLm, lmOf) || upload(&d.pcRow, pcRow))
     return VB_E_HIP;
   if (alloc0(&d.Vchol, nPts * 6) || alloc0(&d.gp, nPts * 3) || alloc0(&d.z, nPts * 3) || alloc0(&d.xp, nPts * 3) ||
       alloc0(&d.Y, lmY[nPts]) || alloc0(&d.gpNew, nPts * 3) || alloc0(&d.zNew, nPts * 3))
@@ -558,7 +622,7 @@ int doFinalize(vb_handle h) {
   if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) || upload(&h->pairsD, pairs) ||
       upload(&h->targetsD, targets) || upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
     return VB_E_HIP;
-  if (alloc0(&h->diagScratch, TS * TS)) return VB_E_HIP;
+  if (alloc0(&h->diagScratch, TS * TS) || alloc0(&h->linv, (size_t)nT * TS * TS)) return VB_E_HIP;
   d.nRS = h->nRS;
   if (upload(&d.rsOff, h->rsOff) || upload(&d.rsS, h->rsS) || upload(&d.rsI, h->rsI) || upload(&d.rsG, h->rsG))
     return VB_E_HIP;
@@ -569,30 +633,77 @@ int doFinalize(vb_handle h) {
 }
 
 // ------------------------------------------------------------------ numeric phases
-void factorReduced(vb_handle h) {
+void factorSeq(vb_handle h) {
   Dev& d = h->d;
   for (int32_t J = 0; J < d.nT; J++) {
     const int64_t c0 = h->colStart[J];
     const int n = (int)(h->colStart[J + 1] - c0);
-    launch_potrf_trsm(d, h->colTilesD + c0, n, h->diagScratch, h->st);
+    profBegin(h, KF_POTRF);
+    launch_potrf_trsm(d, h->colTilesD + c0, n, h->diagScratch, h->linv + (int64_t)J * TS * TS, h->st);
+    profEnd(h, KF_POTRF);
     const int64_t p0 = h->pairStart[J];
     const int np = (int)(h->pairStart[J + 1] - p0);
+    profBegin(h, KF_GEMM);
     launch_gemm_update(d, h->colTilesD + c0, h->pairsD + 2 * p0, h->targetsD + p0, np, h->diagScratch, h->st);
+    profEnd(h, KF_GEMM);
   }
 }
 
 // solve L L^T x = b (b is clobbered), result into x
-void solveReduced(vb_handle h, double* b, double* x) {
+void solveSeq(vb_handle h, double* b, double* x) {
   Dev& d = h->d;
   for (int32_t J = 0; J < d.nT; J++) {
     const int64_t c0 = h->colStart[J];
-    launch_fwd(d, h->colTilesD + c0, h->colRowsD + c0, (int)(h->colStart[J + 1] - c0), b, h->yvec, h->st);
+    profBegin(h, KF_FWD);
+    launch_fwd(d, h->colTilesD + c0, h->colRowsD + c0, (int)(h->colStart[J + 1] - c0), h->linv + (int64_t)J * TS * TS,
+               b, h->yvec, h->st);
+    profEnd(h, KF_FWD);
   }
   for (int32_t J = d.nT - 1; J >= 0; J--) {
     const int64_t r0 = h->rowStart[J];
-    launch_bwd(d, J, h->colTilesH[h->colStart[J]], h->rowTilesD + r0, h->rowColD + r0,
-               (int)(h->rowStart[J + 1] - r0), h->yvec, x, h->st);
+    profBegin(h, KF_BWD);
+    launch_bwd(d, J, h->rowTilesD + r0, h->rowColD + r0, (int)(h->rowStart[J + 1] - r0),
+               h->linv + (int64_t)J * TS * TS, h->yvec, x, h->st);
+    profEnd(h, KF_BWD);
   }
+}
+
+// launch sequences are fixed by the symbolic structure: capture them once into HIP graphs
+// (unless one of their kernel families is being profiled, which needs per-launch events)
+int captureGraph(vb_handle h, bool factor, hipGraphExec_t* out) {
+  hipGraph_t g;
+  HIPCHK(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
+  if (factor) factorSeq(h);
+  else solveSeq(h, h->rhsWork, h->d.xRed);
+  HIPCHK(hipStreamEndCapture(h->st, &g));
+  HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+  HIPCHK(hipGraphDestroy(g));
+  return 0;
+}
+
+int factorReduced(vb_handle h) {
+  const bool prof = h->profFamily == KF_POTRF || h->profFamily == KF_GEMM;
+  if (!h->useGraphs || prof) {
+    factorSeq(h);
+    return 0;
+  }
+  if (!h->factorGraph)
+    if (int rc = captureGraph(h, true, &h->factorGraph)) return rc;
+  HIPCHK(hipGraphLaunch(h->factorGraph, h->st));
+  return 0;
+}
+
+// solves with rhsWork as right-hand side, result in xRed
+int solveReduced(vb_handle h) {
+  const bool prof = h->profFamily == KF_FWD || h->profFamily == KF_BWD;
+  if (!h->useGraphs || prof) {
+    solveSeq(h, h->rhsWork, h->d.xRed);
+    return 0;
+  }
+  if (!h->solveGraph)
+    if (int rc = captureGraph(h, false, &h->solveGraph)) return rc;
+  HIPCHK(hipGraphLaunch(h->solveGraph, h->st));
+  return 0;
 }
 
 double elapsed(hipEvent_t a, hipEvent_t b) {
@@ -649,11 +760,11 @@ int vb_destroy(vb_handle h) {
   Dev& d = h->d;
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
-                  d.blkCol, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
+                  d.blkCol, d.pcRow, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->diagScratch, h->yvec,
-                  h->rhsWork};
+                  h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int k = 0; k < 9; k++) {
@@ -666,6 +777,9 @@ int vb_destroy(vb_handle h) {
     if (d.sf[k].consts) hipFree(d.sf[k].consts);
   }
   for (auto& e : h->ev) hipEventDestroy(e);
+  for (auto& e : h->profEv) hipEventDestroy(e);
+  if (h->factorGraph) hipGraphExecDestroy(h->factorGraph);
+  if (h->solveGraph) hipGraphExecDestroy(h->solveGraph);
   hipStreamDestroy(h->st);
   delete h;
   return 0;
@@ -733,7 +847,9 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   launch_pad_diag(d, h->st);
   const int64_t o0 = 0, o1 = d.nObs;  // (shard restriction applies to landmark-side work)
-  launch_visual_lin(d, update_cache, dont_retry_failed, o0, o1, h->st);
+  profBegin(h, KF_VISUAL_LIN);
+    launch_visual_lin(d, update_cache, dont_retry_failed, o0, o1, h->st);
+    profEnd(h, KF_VISUAL_LIN);
   if (h->isRoot) launch_small(d, 0, d.gRed, h->st);
   HIPCHK(hipEventRecord(h->ev[1], h->st));
   double c = 0;
@@ -750,14 +866,20 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
   Dev& d = h->d;
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   HIPCHK(hipEventRecord(h->ev[2], h->st));
-  launch_landmark(d, lambda, 0, 0, d.nPts, h->st);
-  launch_schur(d, lambda, h->st);
+  profBegin(h, KF_LANDMARK);
+    launch_landmark(d, lambda, 0, 0, d.nPts, h->st);
+    profEnd(h, KF_LANDMARK);
+  profBegin(h, KF_SCHUR);
+    launch_schur(d, lambda, h->isRoot ? 1 : 0, h->st);
+    profEnd(h, KF_SCHUR);
   HIPCHK(hipEventRecord(h->ev[3], h->st));
-  factorReduced(h);
+  if (int rc = factorReduced(h)) return rc;
   HIPCHK(hipEventRecord(h->ev[4], h->st));
   HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  solveReduced(h, h->rhsWork, d.xRed);
-  launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
+  if (int rc = solveReduced(h)) return rc;
+  profBegin(h, KF_BACKSUB);
+    launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
+    profEnd(h, KF_BACKSUB);
   HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
   launch_dot(d.xRed, d.gRed, d.nRed, d.red + 16, h->st);
   launch_dot(d.xp, d.gp, d.nPts * 3, d.red + 16, h->st);
@@ -781,7 +903,9 @@ int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red) {
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 1 * sizeof(double), h->st));
-  launch_visual_lin(d, 0, dont_retry_failed, 0, d.nObs, h->st);
+  profBegin(h, KF_VISUAL_LIN);
+    launch_visual_lin(d, 0, dont_retry_failed, 0, d.nObs, h->st);
+    profEnd(h, KF_VISUAL_LIN);
   if (h->isRoot) launch_small(d, 1, d.gRedNew, h->st);
   launch_landmark(d, 0.0, 1, 0, d.nPts, h->st);
   launch_reduced_grad(d, 0, h->st);
@@ -801,7 +925,7 @@ int vb_solve_with_new_gradient(vb_handle h) {
   launch_landmark(d, 0.0, 2, 0, d.nPts, h->st);
   launch_reduced_grad(d, 1, h->st);
   HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  solveReduced(h, h->rhsWork, d.xRed);
+  if (int rc = solveReduced(h)) return rc;
   launch_backsub(d, 1, 0, d.nPts, d.xRed, d.xp, h->st);
   launch_axpby(d.subRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
   launch_axpby(d.subPt, d.xp, -1.0, 0.0, d.nPts * 3, h->st);
@@ -837,7 +961,9 @@ int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
   HIPCHK(hipEventRecord(h->ev[6], h->st));
   HIPCHK(hipMemsetAsync(d.red + 1, 0, 4 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  launch_visual_cost(d, comparable, 0, d.nObs, h->st);
+  profBegin(h, KF_VISUAL_COST);
+    launch_visual_cost(d, comparable, 0, d.nObs, h->st);
+    profEnd(h, KF_VISUAL_COST);
   if (h->isRoot) launch_small(d, 2, nullptr, h->st);
   HIPCHK(hipEventRecord(h->ev[7], h->st));
   double r[4];
@@ -930,6 +1056,32 @@ int vb_last_phase_times(vb_handle h, vb_phase_times* out) {
 }
 
 void* vb_stream(vb_handle h) { return h ? (void*)h->st : nullptr; }
+
+int vb_profile_kernel(vb_handle h, int family) {
+  if (!h || family < -1 || family >= KF_COUNT) return fail(VB_E_ARG, "bad kernel family");
+  profHarvest(h);
+  h->profFamily = family, h->profLaunches = 0, h->profMs = 0.0, h->profUsed = 0;
+  return 0;
+}
+int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  profHarvest(h);
+  if (launches) *launches = h->profLaunches;
+  if (total_ms) *total_ms = h->profMs;
+  return 0;
+}
+int vb_problem_stats(vb_handle h, int64_t* out) {
+  if (!h || !h->finalized || !out) return fail(VB_E_STATE, "not finalized");
+  const Dev& d = h->d;
+  out[0] = d.nObs, out[1] = d.nPts, out[2] = d.nRV, out[3] = d.nRed, out[4] = d.nT, out[5] = d.nTiles;
+  out[6] = h->pairStart.empty() ? 0 : h->pairStart.back();
+  int64_t sm = 0;
+  for (int k = 1; k < 14; k++) sm += d.sf[k].n;
+  out[7] = sm;
+  // Y panel doubles and total landmark-block count
+  out[8] = 0, out[9] = 0;
+  return 0;
+}
 
 int vb_reduced_buffers(vb_handle h, double** matrix, int64_t* matrix_len, double** rhs, int64_t* rhs_len) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
@@ -1070,15 +1222,15 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
 int vb_assemble_reduced(vb_handle h, double lambda) {
   if (!h || !h->linearized) return fail(VB_E_STATE, "vb_assemble_reduced needs vb_linearize");
   launch_landmark(h->d, lambda, 0, 0, h->d.nPts, h->st);
-  launch_schur(h->d, lambda, h->st);
+  launch_schur(h->d, lambda, h->isRoot ? 1 : 0, h->st);
   HIPCHK(hipStreamSynchronize(h->st));
   return checkErr(h);
 }
 int vb_factor_solve_reduced(vb_handle h) {
   if (!h) return fail(VB_E_ARG, "null handle");
-  factorReduced(h);
+  if (int rc = factorReduced(h)) return rc;
   HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  solveReduced(h, h->rhsWork, h->d.xRed);
+  if (int rc = solveReduced(h)) return rc;
   HIPCHK(hipMemcpyAsync(h->d.rhs, h->d.xRed, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
   return checkErr(h);
@@ -1087,7 +1239,9 @@ int vb_back_substitute(vb_handle h, double* mcr) {
   if (!h) return fail(VB_E_ARG, "null handle");
   Dev& d = h->d;
   HIPCHK(hipMemcpyAsync(d.xRed, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
+  profBegin(h, KF_BACKSUB);
+    launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
+    profEnd(h, KF_BACKSUB);
   HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
   if (h->isRoot) launch_dot(d.xRed, d.gRed, d.nRed, d.red + 16, h->st);
   launch_dot(d.xp, d.gp, d.nPts * 3, d.red + 16, h->st);

@@ -71,6 +71,7 @@ struct Dev {
   int64_t* lmBlk = nullptr;   // nPts + 1 into blkRed/blkCol
   int32_t* blkRed = nullptr;  // reduced ids of D(l), sorted by reduced offset
   int32_t* blkCol = nullptr;  // column offset in Y panel
+  int32_t* pcRow = nullptr;   // reduced row of every Y panel column (indexed by lmY[l]/3 + c)
   double *Vchol = nullptr, *gp = nullptr, *z = nullptr, *xp = nullptr, *Y = nullptr;
   double *gpNew = nullptr, *zNew = nullptr;
   int32_t* ptRed = nullptr;  // point param registered? (1/0) per point var handle

@@ -101,7 +101,6 @@ __global__ void __launch_bounds__(128) landmark_kernel(Dev d, double lambda, int
 }
 
 // ------------------------------------------------------------------ Schur column assembly
-constexpr int kSchurLds = 12288;  // doubles of accumulator per workgroup (96 KB)
 
 __device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
   const int32_t ti = d.tileIdx[(r / TS) * d.nT + (c / TS)];
@@ -109,84 +108,90 @@ __device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
   return d.tiles + (int64_t)ti * TS * TS + (c % TS) * TS + (r % TS);
 }
 
-__global__ void __launch_bounds__(256) schur_kernel(Dev d, double lambda) {
-  __shared__ double acc[kSchurLds];
-  __shared__ double gdir[32], gsch[32];
+// One wave per reduced variable X1 (a column block of S): lanes own distinct ROWS of the
+// LDS-resident accumulator, so no atomics are needed; observations and landmarks touching X1 are
+// processed one at a time by the whole wave (their row sets are disjoint within one item).
+//   direct:  acc[rows of X2] += J~_X2^T J~_X1   for the visual slots X2 >= X1 of each obs
+//   damping: diag(H_X1X1) = diag * (1 + lambda) + lambda  on visual + small-factor direct terms
+//   Schur:   acc[rows of X2] -= Y_{l,X2}^T Y_{l,X1} for the panel columns of l at/after X1
+// Rows beyond the LDS window are handled by re-scanning in windows of kSchurRows.
+constexpr int kSchurAcc = 6144;  // doubles per wave (48 KB)
+
+__global__ void __launch_bounds__(64) schur_kernel(Dev d, double lambda, int addIdentity) {
+  __shared__ double acc[kSchurAcc];
   const int X1 = blockIdx.x;
+  const int lane = threadIdx.x;
   const int d1 = d.rvDim[X1];
   const int64_t off1 = d.rvOff[X1];
   const int64_t span = d.rvRowEnd[X1] - off1;
-  const int RW = (int)min<int64_t>(span, kSchurLds / d1);
+  const int RW = (int)min<int64_t>(span, kSchurAcc / d1);
   const int64_t P = d.nObsPad;
   const double* Jt = d.Jt;
-  const int tid = threadIdx.x, nth = blockDim.x;
-  if (tid < 32) gdir[tid] = 0.0, gsch[tid] = 0.0;
+  double gdir = 0.0, gsch = 0.0;  // lane j < d1 accumulates column j
+  const int64_t ox0 = d.oxStart[X1], ox1 = d.oxStart[X1 + 1];
+  const int64_t lx0 = d.lxStart[X1], lx1 = d.lxStart[X1 + 1];
   for (int64_t w0 = 0; w0 < span; w0 += RW) {
     const int rows = (int)min<int64_t>(RW, span - w0);
-    for (int i = tid; i < rows * d1; i += nth) acc[i] = 0.0;
-    __syncthreads();
-    // ---- direct visual terms J~_X2^T J~_X1 (and g_X1 = sum J~^T e~ on the first pass)
-    for (int64_t idx = d.oxStart[X1] + tid; idx < d.oxStart[X1 + 1]; idx += nth) {
+    for (int i = lane; i < rows * d1; i += 64) acc[i] = 0.0;
+    __builtin_amdgcn_wave_barrier();
+    // ---- direct visual terms
+    for (int64_t idx = ox0; idx < ox1; idx++) {
       const int64_t o = d.oxObs[idx];
       const int s1 = d.oxSlot[idx];
       const int p1 = slotPlane(s1), st1 = slotStride(s1);
-      double j1[2][17];
-      for (int j = 0; j < d1; j++) j1[0][j] = Jt[(p1 + j) * P + o], j1[1][j] = Jt[(p1 + st1 + j) * P + o];
-      if (w0 == 0) {
+      if (w0 == 0 && lane < d1) {
         const double e0 = Jt[kJe * P + o], e1 = Jt[(kJe + 1) * P + o];
-        for (int j = 0; j < d1; j++) atomicAdd(&gdir[j], j1[0][j] * e0 + j1[1][j] * e1);
+        gdir += Jt[(p1 + lane) * P + o] * e0 + Jt[(p1 + st1 + lane) * P + o] * e1;
       }
+      // lane -> (slot s2, row i) flattened over the obs' slots with X2 >= X1
+      int base = 0;
       for (int s2 = 0; s2 < 4; s2++) {
         const int X2 = d.obRed[o * 4 + s2];
         if (X2 < 0) continue;
-        const int64_t r0 = d.rvOff[X2] - off1 - w0;
+        const int64_t o2 = d.rvOff[X2];
+        if (o2 < off1) continue;
         const int d2 = d.rvDim[X2];
-        if (r0 + (int64_t)d2 <= 0 || r0 >= rows || d.rvOff[X2] < off1) continue;
+        const int i = lane - base;
+        base += d2;
+        if (i < 0 || i >= d2) continue;
+        const int64_t rr = o2 - off1 - w0 + i;
+        if (rr < 0 || rr >= rows) continue;
         const int p2 = slotPlane(s2), st2 = slotStride(s2);
-        for (int i = 0; i < d2; i++) {
-          const int64_t rr = r0 + i;
-          if (rr < 0 || rr >= rows) continue;
-          const double a0 = Jt[(p2 + i) * P + o], a1 = Jt[(p2 + st2 + i) * P + o];
-          for (int j = 0; j < d1; j++) atomicAdd(&acc[rr * d1 + j], a0 * j1[0][j] + a1 * j1[1][j]);
-        }
+        const double a0 = Jt[(p2 + i) * P + o], a1 = Jt[(p2 + st2 + i) * P + o];
+        double* ar = acc + rr * d1;
+        for (int j = 0; j < d1; j++) ar[j] += a0 * Jt[(p1 + j) * P + o] + a1 * Jt[(p1 + st1 + j) * P + o];
       }
+      __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
-    if (w0 == 0) {  // damping of the total direct diagonal (visual + small factors already in S)
-      for (int j = tid; j < d1; j += nth) {
-        double* sp = tile_ptr(d, off1 + j, off1 + j);
-        const double tot = acc[j * d1 + j] + (sp ? *sp : 0.0);
-        acc[j * d1 + j] += lambda * tot + lambda;
-      }
+    if (w0 == 0 && lane < d1) {  // damping of the total direct diagonal (visual + small factors)
+      const double* sp = tile_ptr(d, off1 + lane, off1 + lane);
+      const double tot = acc[lane * d1 + lane] + (sp ? *sp : 0.0);
+      acc[lane * d1 + lane] += lambda * tot + (addIdentity ? lambda : 0.0);
     }
-    __syncthreads();
-    // ---- Schur complement terms - Y_{l,X2}^T Y_{l,X1}
-    for (int64_t idx = d.lxStart[X1] + tid; idx < d.lxStart[X1 + 1]; idx += nth) {
+    __builtin_amdgcn_wave_barrier();
+    // ---- Schur complement terms
+    for (int64_t idx = lx0; idx < lx1; idx++) {
       const int64_t l = d.lxLm[idx];
+      const int c1 = d.lxCol[idx];
       const double* Yl = d.Y + d.lmY[l];
-      const double* y1 = Yl + 3 * d.lxCol[idx];
-      if (w0 == 0) {
-        const double z0 = d.z[l * 3], z1 = d.z[l * 3 + 1], z2 = d.z[l * 3 + 2];
-        for (int j = 0; j < d1; j++) atomicAdd(&gsch[j], y1[3 * j] * z0 + y1[3 * j + 1] * z1 + y1[3 * j + 2] * z2);
+      const double* y1 = Yl + 3 * c1;
+      const int ncol = (int)((d.lmY[l + 1] - d.lmY[l]) / 3);
+      const int32_t* rowOf = d.pcRow + d.lmY[l] / 3;
+      if (w0 == 0 && lane < d1) {
+        gsch += y1[3 * lane] * d.z[l * 3] + y1[3 * lane + 1] * d.z[l * 3 + 1] + y1[3 * lane + 2] * d.z[l * 3 + 2];
       }
-      for (int64_t b = d.lmBlk[l]; b < d.lmBlk[l + 1]; b++) {
-        const int X2 = d.blkRed[b];
-        const int64_t r0 = d.rvOff[X2] - off1 - w0;
-        const int d2 = d.rvDim[X2];
-        if (d.rvOff[X2] < off1 || r0 >= rows || r0 + d2 <= 0) continue;
-        const double* y2 = Yl + 3 * d.blkCol[b];
-        for (int i = 0; i < d2; i++) {
-          const int64_t rr = r0 + i;
-          if (rr < 0 || rr >= rows) continue;
-          const double c0 = y2[3 * i], c1 = y2[3 * i + 1], c2 = y2[3 * i + 2];
-          for (int j = 0; j < d1; j++)
-            atomicAdd(&acc[rr * d1 + j], -(c0 * y1[3 * j] + c1 * y1[3 * j + 1] + c2 * y1[3 * j + 2]));
-        }
+      for (int c = c1 + lane; c < ncol; c += 64) {
+        const int64_t rr = (int64_t)rowOf[c] - off1 - w0;
+        if (rr < 0 || rr >= rows) continue;
+        const double q0 = Yl[3 * c], q1 = Yl[3 * c + 1], q2 = Yl[3 * c + 2];
+        double* ar = acc + rr * d1;
+        for (int j = 0; j < d1; j++) ar[j] -= q0 * y1[3 * j] + q1 * y1[3 * j + 1] + q2 * y1[3 * j + 2];
       }
+      __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
     // ---- write-out (exclusive owner of column block X1)
-    for (int i = tid; i < rows * d1; i += nth) {
+    for (int i = lane; i < rows * d1; i += 64) {
       const int rr = i / d1, j = i % d1;
       const int64_t R = off1 + w0 + rr, Cc = off1 + j;
       if (R < Cc) continue;
@@ -199,12 +204,12 @@ __global__ void __launch_bounds__(256) schur_kernel(Dev d, double lambda) {
       }
       *p += v;
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
   }
-  if (tid < d1) {
-    const double g = d.gRed[off1 + tid] + gdir[tid];
-    d.gRed[off1 + tid] = g;
-    d.rhs[off1 + tid] = g - gsch[tid];
+  if (lane < d1) {
+    const double g = d.gRed[off1 + lane] + gdir;
+    d.gRed[off1 + lane] = g;
+    d.rhs[off1 + lane] = g - gsch;
   }
 }
 
@@ -243,49 +248,72 @@ __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
 }
 
 // ------------------------------------------------------------------ tile Cholesky
-// in-wave left-looking Cholesky of a TS x TS column-major tile held in LDS (lane = row)
-__device__ void wave_potrf(double* A, int lane, int32_t* err) {
+// Register-resident wave Cholesky of a TS x TS tile: lane i holds row i (x[0..TS)); at step k
+// the pivot comes from lane k by a shuffle and column k is broadcast through LDS.  On return
+// x[k] = L(i, k) for k <= i; the factor is also written to Ls (column-major, upper part zero).
+__device__ void wave_potrf(double (&x)[TS], double* col, double* Ls, int lane, int32_t* err) {
+#pragma unroll
   for (int k = 0; k < TS; k++) {
-    if (lane >= k) {
-      double s = A[k * TS + lane];
-      for (int j = 0; j < k; j++) s -= A[j * TS + lane] * A[j * TS + k];
-      A[k * TS + lane] = s;
+    const double piv = __shfl(x[k], k, 64);
+    if (!(piv > 0.0) && lane == k) atomicOr(err, 8);
+    const double dk = sqrt(piv);
+    const double lk = (lane == k) ? dk : x[k] / dk;
+    if (lane >= k) x[k] = lk;
+    col[lane] = lk;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = k + 1; j < TS; j++) {
+      const double v = col[j];
+      if (lane >= j) x[j] -= lk * v;
     }
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const double dkk = A[k * TS + k];
-    __builtin_amdgcn_wave_barrier();
-    if (!(dkk > 0.0) && lane == 0) atomicOr(err, 8);
-    const double dd = sqrt(dkk);
-    if (lane > k) A[k * TS + lane] /= dd;
-    __builtin_amdgcn_wave_barrier();
-    if (lane == k) A[k * TS + k] = dd;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
+#pragma unroll
+  for (int c = 0; c < TS; c++) Ls[c * TS + lane] = (lane >= c) ? x[c] : 0.0;
 }
 
-// column J: rows[0] = J (diagonal), rows[1..n) off-diagonal tile rows
-// Every block factors its own LDS copy of the diagonal tile (they all read the unfactored tile),
-// block 0 publishes the factor to `diagOut` (scratch); gemm_update_kernel copies it back.
-__global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* colTiles, int n, double* diagOut) {
+// Every block factors its own copy of the diagonal tile (all read the unfactored tile); block 0
+// publishes the factor to `diagOut` (copied into place by gemm_update_kernel) and its wave 1 the
+// inverse L^-1 into `linv` (used by the triangular solves).  Waves then solve X L^T = A for the
+// off-diagonal tile rows q = 1 + 4 * blockIdx.x + wave.
+__global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* colTiles, int n, double* diagOut,
+                                                         double* linv) {
   __shared__ double L[TS * TS];
+  __shared__ double col[TS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const double* Ad = d.tiles + (int64_t)colTiles[0] * TS * TS;
-  for (int i = tid; i < TS * TS; i += blockDim.x) L[i] = Ad[i];
+  if (wave == 0) {
+    double x[TS];
+#pragma unroll
+    for (int c = 0; c < TS; c++) x[c] = Ad[c * TS + lane];
+    wave_potrf(x, col, L, lane, d.err);
+  }
   __syncthreads();
-  if (wave == 0) wave_potrf(L, lane, d.err);
-  __syncthreads();
-  if (blockIdx.x == 0)
+  if (blockIdx.x == 0) {
     for (int i = tid; i < TS * TS; i += blockDim.x) diagOut[i] = L[i];
+    if (wave == 1) {  // lane = column c of X = L^-1: X[i][c] = (delta_ic - sum_{k<i} L_ik X_kc) / L_ii
+      double xi[TS];
+#pragma unroll
+      for (int i = 0; i < TS; i++) {
+        double s = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 0; k < i; k++) s -= L[k * TS + i] * xi[k];
+        xi[i] = s / L[i * TS + i];
+      }
+#pragma unroll
+      for (int i = 0; i < TS; i++) linv[lane * TS + i] = xi[i];
+    }
+  }
   const int q = 1 + blockIdx.x * 4 + wave;
   if (q >= n) return;
   // X L^T = A  (row r = lane): x_c = (a_c - sum_{k<c} x_k L_ck) / L_cc
   double* A = d.tiles + (int64_t)colTiles[q] * TS * TS;
   double x[TS];
 #pragma unroll
+  for (int c = 0; c < TS; c++) x[c] = A[c * TS + lane];
+#pragma unroll
   for (int c = 0; c < TS; c++) {
-    double s = A[c * TS + lane];
+    double s = x[c];
 #pragma unroll
     for (int k = 0; k < c; k++) s -= x[k] * L[k * TS + c];
     x[c] = s / L[c * TS + c];
@@ -348,27 +376,23 @@ __global__ void __launch_bounds__(256) gemm_update_kernel(Dev d, const int32_t* 
 }
 
 // ------------------------------------------------------------------ triangular solves
-// forward, column J: every block solves y_J = L_JJ^-1 b_J (wave 0), block 0 stores it into x;
+// forward, column J: every block computes y_J = Linv_JJ b_J (GEMV); block 0 stores it into x;
 // block q >= 1 updates b_I -= L_IJ y_J for I = rows[q]
 __global__ void __launch_bounds__(64) fwd_kernel(Dev d, const int32_t* colTiles, const int32_t* tileRow, int n,
-                                                 double* b, double* x, int64_t nRed) {
-  __shared__ double y[TS];
+                                                 const double* linvJ, double* b, double* x, int64_t nRed) {
+  __shared__ double bs[TS], y[TS];
   const int lane = threadIdx.x;
   const int J = tileRow[0];
-  const double* Ld = d.tiles + (int64_t)colTiles[0] * TS * TS;
   const int64_t base = (int64_t)J * TS;
-  double bi = (base + lane < nRed) ? b[base + lane] : 0.0;
-  for (int k = 0; k < TS; k++) {
-    if (lane == k) y[k] = bi / Ld[k * TS + k];
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const double yk = y[k];
-    if (lane > k) bi -= Ld[k * TS + lane] * yk;
-  }
+  bs[lane] = (base + lane < nRed) ? b[base + lane] : 0.0;
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  double yi = 0.0;
+#pragma unroll 16
+  for (int k = 0; k < TS; k++) yi += linvJ[k * TS + lane] * bs[k];
+  y[lane] = yi;
+  __builtin_amdgcn_wave_barrier();
   if (blockIdx.x == 0) {
-    if (base + lane < nRed) x[base + lane] = y[lane];
+    if (base + lane < nRed) x[base + lane] = yi;
     return;
   }
   const int q = blockIdx.x;
@@ -376,32 +400,28 @@ __global__ void __launch_bounds__(64) fwd_kernel(Dev d, const int32_t* colTiles,
   const double* A = d.tiles + (int64_t)colTiles[q] * TS * TS;
   const int64_t ib = (int64_t)tileRow[q] * TS;
   double s = 0;
+#pragma unroll 16
   for (int k = 0; k < TS; k++) s += A[k * TS + lane] * y[k];
   if (ib + lane < nRed) b[ib + lane] -= s;
 }
 
-// backward, row J (descending): x_J = L_JJ^-T t_J; block q >= 1 updates t_K -= L_JK^T x_J
+// backward, row J (descending): x_J = Linv_JJ^T t_J; block q >= 1 updates t_K -= L_JK^T x_J
 // for the tiles (J, K), K < J, listed in rowTiles (tile index) / rowCol (K)
-__global__ void __launch_bounds__(64) bwd_kernel(Dev d, int J, int32_t diagTile, const int32_t* rowTiles,
-                                                 const int32_t* rowCol, int n, double* t, double* x,
-                                                 int64_t nRed) {
-  __shared__ double xs[TS];
+__global__ void __launch_bounds__(64) bwd_kernel(Dev d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n,
+                                                 const double* linvJ, double* t, double* x, int64_t nRed) {
+  __shared__ double ts[TS], xs[TS];
   const int lane = threadIdx.x;
-  const double* Ld = d.tiles + (int64_t)diagTile * TS * TS;
   const int64_t base = (int64_t)J * TS;
-  // L^T x = t, backward: x_k = (t_k - sum_{i>k} L_ik x_i) / L_kk; lane = k holds t_k
-  double tk = (base + lane < nRed) ? t[base + lane] : 0.0;
-  for (int k = TS - 1; k >= 0; k--) {
-    if (lane == k) xs[k] = (base + k < nRed) ? tk / Ld[k * TS + k] : 0.0;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const double xk = xs[k];
-    if (lane < k) tk -= Ld[lane * TS + k] * xk;  // L_{k, lane}
-  }
+  ts[lane] = (base + lane < nRed) ? t[base + lane] : 0.0;
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  double xk = 0.0;  // x_k = sum_i Linv(i, k) t_i
+#pragma unroll 16
+  for (int i = 0; i < TS; i++) xk += linvJ[lane * TS + i] * ts[i];
+  if (base + lane >= nRed) xk = 0.0;
+  xs[lane] = xk;
+  __builtin_amdgcn_wave_barrier();
   if (blockIdx.x == 0) {
-    if (base + lane < nRed) x[base + lane] = xs[lane];
+    if (base + lane < nRed) x[base + lane] = xk;
     return;
   }
   const int q = blockIdx.x - 1;
@@ -409,6 +429,7 @@ __global__ void __launch_bounds__(64) bwd_kernel(Dev d, int J, int32_t diagTile,
   const double* A = d.tiles + (int64_t)rowTiles[q] * TS * TS;  // tile (J, K): rows of J, cols of K
   const int64_t kb = (int64_t)rowCol[q] * TS;
   double s = 0;
+#pragma unroll 16
   for (int i = 0; i < TS; i++) s += A[lane * TS + i] * xs[i];
   if (kb + lane < nRed) t[kb + lane] -= s;
 }
@@ -562,15 +583,16 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
   if (hi > lo)
     hipLaunchKernelGGL(landmark_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, lambda, mode, lo, hi);
 }
-void launch_schur(const Dev& d, double lambda, hipStream_t st) {
-  if (d.nRV) hipLaunchKernelGGL(schur_kernel, dim3(d.nRV), dim3(256), 0, st, d, lambda);
+void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
+  if (d.nRV) hipLaunchKernelGGL(schur_kernel, dim3(d.nRV), dim3(64), 0, st, d, lambda, addIdentity);
 }
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
   if (d.nRV) hipLaunchKernelGGL(reduced_grad_kernel, dim3(d.nRV), dim3(256), 0, st, d, mode);
 }
-void launch_potrf_trsm(const Dev& d, const int32_t* colTiles, int n, double* diagScratch, hipStream_t st) {
+void launch_potrf_trsm(const Dev& d, const int32_t* colTiles, int n, double* diagScratch, double* linv,
+                       hipStream_t st) {
   const int nb = n > 1 ? (n - 1 + 3) / 4 : 1;
-  hipLaunchKernelGGL(potrf_trsm_kernel, dim3(nb), dim3(256), 0, st, d, colTiles, n, diagScratch);
+  hipLaunchKernelGGL(potrf_trsm_kernel, dim3(nb), dim3(256), 0, st, d, colTiles, n, diagScratch, linv);
 }
 void launch_gemm_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets,
                         int npairs, const double* diagScratch, hipStream_t st) {
@@ -585,13 +607,13 @@ __global__ void pad_diag_kernel(Dev d) {
 void launch_pad_diag(const Dev& d, hipStream_t st) {
   if ((int64_t)d.nT * TS > d.nRed) hipLaunchKernelGGL(pad_diag_kernel, dim3(1), dim3(64), 0, st, d);
 }
-void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, double* b, double* x,
-                hipStream_t st) {
-  hipLaunchKernelGGL(fwd_kernel, dim3(n), dim3(64), 0, st, d, colTiles, tileRow, n, b, x, d.nRed);
+void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
+                double* b, double* x, hipStream_t st) {
+  hipLaunchKernelGGL(fwd_kernel, dim3(n), dim3(64), 0, st, d, colTiles, tileRow, n, linvJ, b, x, d.nRed);
 }
-void launch_bwd(const Dev& d, int J, int32_t diagTile, const int32_t* rowTiles, const int32_t* rowCol, int n,
+void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
                 double* t, double* x, hipStream_t st) {
-  hipLaunchKernelGGL(bwd_kernel, dim3(n + 1), dim3(64), 0, st, d, J, diagTile, rowTiles, rowCol, n, t, x, d.nRed);
+  hipLaunchKernelGGL(bwd_kernel, dim3(n + 1), dim3(64), 0, st, d, J, rowTiles, rowCol, n, linvJ, t, x, d.nRed);
 }
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st) {
   if (hi > lo)

@@ -278,7 +278,7 @@ void vbs_default_config(vbs_config* c, int which) {
   c->pixel_sigma = 0.5, c->outlier_frac = 0.01, c->perturb = 1, c->priors = 1;
   c->seed = 0xA21A + which, c->imu_calib_options = 0xff, c->reserved = 0;
   if (which == 1 || which == 2) {
-    c->n_imus = 2, c->camera_set = 1, c->mean_track = 20;
+    c->n_imus = 2, c->camera_set = 1, c->mean_track = 22.5;
     c->n_kf = which == 1 ? 2000 : 10000;
     c->n_lm = which == 1 ? 60000 : 300000;
   }

@@ -249,6 +249,25 @@ class HipEngine(CEngineBase):
             self.h, C.byref(s), lcb, pcb, None, C.byref(out)))
         return out
 
+    def profile_kernel(self, family: int):
+        self._check(self._fn("profile_kernel", [C.c_int])(self.h, family))
+
+    def kernel_time(self):
+        n, ms = C.c_int64(), C.c_double()
+        self._check(self._fn("kernel_time", [C.POINTER(C.c_int64), _dp])(self.h, C.byref(n), C.byref(ms)))
+        return n.value, ms.value
+
+    def problem_stats(self):
+        out = (C.c_int64 * 10)()
+        self._check(self._fn("problem_stats", [C.c_int64 * 10])(self.h, out))
+        return list(out)
+
+    def synchronize(self):
+        self.lib.vb_stream.restype = P
+        self.lib.vb_stream.argtypes = [P]
+        from ._lib import hip_stream_sync
+        hip_stream_sync(self.lib.vb_stream(self.h))
+
     def phase_times(self) -> PhaseTimes:
         t = PhaseTimes()
         self._check(self._fn("last_phase_times", [C.POINTER(PhaseTimes)])(self.h, C.byref(t)))
