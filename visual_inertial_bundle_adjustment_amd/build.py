@@ -15,7 +15,7 @@ LIB = os.path.join(HERE, "lib")
 HIP_SOURCES = ["factors.hip", "solver.hip", "api.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("VIBA_OFFLOAD_ARCH", "gfx950")
-HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", "-pthread", "-Wall", "-Wno-unused-function",
              "-Wno-unused-variable", "-Wno-unused-but-set-variable", "-Wno-unused-value"]
 
 
@@ -57,7 +57,7 @@ def build(force: bool = False, verbose: bool = False) -> list[str]:
                 print(r.stderr)
     hip = os.path.join(LIB, "libviba_hip.so")
     if force or not _newer(hip, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", hip, *objs])
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", hip, *objs])
     out.append(hip)
     return out
 

@@ -6,9 +6,11 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/viba_hip.h"
@@ -22,10 +24,11 @@ void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st);
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
-void launch_potrf_trsm(const Dev& d, const int32_t* colTiles, int n, double* diagScratch, double* linv,
-                       hipStream_t st);
-void launch_gemm_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets,
-                        int npairs, const double* diagScratch, hipStream_t st);
+void launch_potrf(const Dev& d, const int32_t* colTiles, double* dinv, hipStream_t st);
+void launch_trsm(const Dev& d, const int32_t* colTiles, int n, const double* dinv, hipStream_t st);
+void launch_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets, int npairs,
+                   int fuseDiag, double* dinvNext, hipStream_t st);
+void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st);
 void launch_pad_diag(const Dev& d, hipStream_t st);
 void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
                 double* b, double* x, hipStream_t st);
@@ -176,9 +179,155 @@ int alloc0(T** dptr, size_t n) {
   return 0;
 }
 
-struct Timer {
-  hipEvent_t a, b;
+template <typename F>
+void parallelFor(int64_t n, F&& f) {
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(1u, std::thread::hardware_concurrency()), 16, n / 64 + 1}));
+  if (nt == 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++) th.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt); });
+  for (auto& x : th) x.join();
+}
+
+// Inputs of the Schur work-list build (host arrays of doFinalize)
+struct SchurInputs {
+  int nRV;
+  const int64_t* rvOff;
+  const int32_t* rvDim;
+  const int64_t *lmY, *lmBlk;
+  const int32_t *blkRed, *blkCol, *obRed;
+  const int64_t *oxStart, *lxStart;
+  const int32_t *oxObs, *oxSlot, *lxLm, *lxCol;
+  int64_t lmB, lmE;        // landmark shard
+  int64_t obB, obE;        // observations of the shard's landmarks
+  int64_t obFree;          // first observation of a non-eliminated (constant) point
+  bool root;               // root also owns the observations of constant points
 };
+
+// Schur work list: every coupled block pair (X1, X2) with off(X2) >= off(X1) and its entries
+//   landmark entries: (panel column of X1, panel column of X2) for every landmark seeing both
+//                     (X1 == X2: (panel column, landmark) — the RHS pass needs z_l)
+//   observation entries: (obs, slot1 | slot2 << 8) for every observation with both in its slots
+// Entries of one pair are contiguous and in landmark / observation order; pairs are in (X1, X2)
+// order.  Each pair's lists are split into work items of bounded cost.
+struct SchurLists {
+  std::vector<uint32_t> lmEnt;
+  std::vector<int32_t> obEnt;
+  std::vector<SchurItem> items;
+};
+
+void buildSchurLists(const SchurInputs& in, SchurLists& out) {
+  const int nRV = in.nRV;
+  std::vector<std::vector<int32_t>> part(nRV);
+  std::vector<std::vector<int64_t>> cntL(nRV), cntO(nRV);
+  auto inObs = [&](int64_t o) { return (o >= in.obB && o < in.obE) || (in.root && o >= in.obFree); };
+  auto blockPos = [&](int64_t l, int32_t X) {
+    return std::lower_bound(in.blkRed + in.lmBlk[l], in.blkRed + in.lmBlk[l + 1], X) - in.blkRed;
+  };
+  // visit(X1, onLm(pairSlot, col1, col2, l), onOb(pairSlot, o, s1, s2)) with partners mapped to slots
+  auto visit = [&](int X1, std::vector<int32_t>& slot, std::vector<int32_t>& P, auto&& onLm, auto&& onOb) {
+    auto slotOf = [&](int32_t X2) {
+      if (slot[X2] < 0) slot[X2] = (int32_t)P.size(), P.push_back(X2);
+      return slot[X2];
+    };
+    slotOf(X1);
+    for (int64_t idx = in.lxStart[X1]; idx < in.lxStart[X1 + 1]; idx++) {
+      const int64_t l = in.lxLm[idx];
+      if (l < in.lmB || l >= in.lmE) continue;
+      const int64_t cb = in.lmY[l] / 3;
+      const int64_t c1 = cb + in.lxCol[idx];
+      onLm(slot[X1], c1, l, l, true);
+      for (int64_t b = blockPos(l, X1) + 1; b < in.lmBlk[l + 1]; b++) onLm(slotOf(in.blkRed[b]), c1, cb + in.blkCol[b], l, false);
+    }
+    const int64_t off1 = in.rvOff[X1];
+    for (int64_t idx = in.oxStart[X1]; idx < in.oxStart[X1 + 1]; idx++) {
+      const int64_t o = in.oxObs[idx];
+      if (!inObs(o)) continue;
+      const int s1 = in.oxSlot[idx];
+      onOb(slot[X1], o, s1, s1);
+      for (int s2 = 0; s2 < 4; s2++) {
+        const int32_t X2 = in.obRed[o * 4 + s2];
+        if (X2 < 0 || s2 == s1 || in.rvOff[X2] <= off1) continue;
+        onOb(slotOf(X2), o, s1, s2);
+      }
+    }
+  };
+  // pass 1: partners and counts per X1 (partners sorted by X2 afterwards)
+  std::vector<std::vector<int32_t>> permOf(nRV);
+  parallelFor(nRV, [&](int64_t a, int64_t b) {
+    std::vector<int32_t> slot(nRV, -1);
+    for (int64_t X1 = a; X1 < b; X1++) {
+      std::vector<int32_t> P;
+      std::vector<int64_t> cl, co;
+      visit((int)X1, slot, P,
+            [&](int32_t s, int64_t, int64_t, int64_t, bool) {
+              if ((size_t)s >= cl.size()) cl.resize(s + 1, 0), co.resize(s + 1, 0);
+              cl[s]++;
+            },
+            [&](int32_t s, int64_t, int, int) {
+              if ((size_t)s >= cl.size()) cl.resize(s + 1, 0), co.resize(s + 1, 0);
+              co[s]++;
+            });
+      cl.resize(P.size(), 0), co.resize(P.size(), 0);
+      for (int32_t X2 : P) slot[X2] = -1;
+      std::vector<int32_t> perm(P.size());
+      std::iota(perm.begin(), perm.end(), 0);
+      std::sort(perm.begin(), perm.end(), [&](int32_t x, int32_t y) { return P[x] < P[y]; });
+      part[X1] = P, cntL[X1] = cl, cntO[X1] = co, permOf[X1] = perm;
+    }
+  });
+  // offsets (pairs in (X1, sorted X2) order)
+  std::vector<std::vector<int64_t>> offL(nRV), offO(nRV);
+  int64_t totL = 0, totO = 0;
+  for (int X1 = 0; X1 < nRV; X1++) {
+    offL[X1].resize(part[X1].size()), offO[X1].resize(part[X1].size());
+    for (int32_t s : permOf[X1]) {
+      offL[X1][s] = totL, offO[X1][s] = totO;
+      totL += cntL[X1][s], totO += cntO[X1][s];
+    }
+  }
+  out.lmEnt.assign(2 * totL, 0);
+  out.obEnt.assign(2 * totO, 0);
+  // pass 2: fill (same visiting order as pass 1, so slots coincide)
+  parallelFor(nRV, [&](int64_t a, int64_t b) {
+    std::vector<int32_t> slot(nRV, -1);
+    for (int64_t X1 = a; X1 < b; X1++) {
+      std::vector<int32_t> P;
+      std::vector<int64_t> curL = offL[X1], curO = offO[X1];
+      visit((int)X1, slot, P,
+            [&](int32_t s, int64_t c1, int64_t c2, int64_t l, bool diag) {
+              const int64_t e = curL[s]++;
+              out.lmEnt[2 * e] = (uint32_t)c1;
+              out.lmEnt[2 * e + 1] = (uint32_t)(diag ? l : c2);
+            },
+            [&](int32_t s, int64_t o, int s1, int s2) {
+              const int64_t e = curO[s]++;
+              out.obEnt[2 * e] = (int32_t)o;
+              out.obEnt[2 * e + 1] = s1 | (s2 << 8);
+            });
+      for (int32_t X2 : P) slot[X2] = -1;
+    }
+  });
+  // work items: bounded (entries x 64-entry output chunks)
+  out.items.clear();
+  for (int X1 = 0; X1 < nRV; X1++)
+    for (int32_t s : permOf[X1]) {
+      const int32_t X2 = part[X1][s];
+      const int chunks = (in.rvDim[X1] * in.rvDim[X2] + 63) / 64;
+      const int64_t maxE = std::max<int64_t>(16, 512 / chunks);
+      for (int kind = 0; kind < 2; kind++) {
+        const int64_t n = kind ? cntO[X1][s] : cntL[X1][s];
+        const int64_t o0 = kind ? offO[X1][s] : offL[X1][s];
+        for (int64_t k = 0; k < n; k += maxE) {
+          SchurItem it;
+          it.start = o0 + k, it.count = (int32_t)std::min<int64_t>(maxE, n - k), it.X1 = X1, it.X2 = X2, it.kind = kind;
+          out.items.push_back(it);
+        }
+      }
+    }
+}
 
 }  // namespace
 
@@ -199,7 +348,7 @@ struct vb_handle_s {
   std::vector<int32_t> rvKind, rvHandle, rvDim;
   std::vector<int64_t> rvOff;
   std::vector<int32_t> lmOfPoint;
-  int64_t nParams = 0, order = 0, nLmObs = 0;
+  int64_t nParams = 0, order = 0, nLmObs = 0, nLmEnt = 0, nObEnt = 0;
   std::vector<int64_t> colStart;   // per tile column into colTilesH / colRowsH
   std::vector<int32_t> colTilesH, colRowsH;
   std::vector<int64_t> pairStart;  // per tile column into pairs / targets
@@ -207,13 +356,14 @@ struct vb_handle_s {
   std::vector<int32_t> rowTilesH, rowColH;
   int32_t *colTilesD = nullptr, *colRowsD = nullptr, *pairsD = nullptr, *targetsD = nullptr, *rowTilesD = nullptr,
           *rowColD = nullptr;
-  double *diagScratch = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
+  double *dinv = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool isRoot = true;
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
   hipGraphExec_t factorGraph = nullptr, solveGraph = nullptr;
   bool useGraphs = true;
+  bool noFusePotrf = false;  // VIBA_NO_FUSE_POTRF=1: separate potrf launches (profiling)
   // state
   bool linearized = false, factored = false;
   vb_phase_times times{};
@@ -230,7 +380,7 @@ namespace {
 
 // kernel families for vb_profile_kernel
 enum { KF_VISUAL_LIN = 0, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACKSUB, KF_VISUAL_COST,
-       KF_SMALL, KF_COUNT };
+       KF_SMALL, KF_TRSM, KF_COUNT };
 
 inline void profBegin(vb_handle h, int fam) {
   if (h->profFamily != fam) return;
@@ -476,6 +626,24 @@ int doFinalize(vb_handle h) {
         lxLm[fl[r]] = (int32_t)l, lxCol[fl[r]] = blkCol[b], fl[r]++;
       }
   }
+  // ---------------- Schur work list of this handle's landmark shard
+  if (h->lmEnd < 0) h->lmBegin = 0, h->lmEnd = nPts;
+  if (h->lmBegin < 0 || h->lmEnd > nPts || h->lmBegin > h->lmEnd) return fail(VB_E_ARG, "bad landmark shard range");
+  SchurLists sl;
+  {
+    SchurInputs in{nRV, h->rvOff.data(), h->rvDim.data(), lmY.data(), lmBlk.data(), blkRed.data(), blkCol.data(),
+                   obRed.data(), oxStart.data(), lxStart.data(), oxObs.data(), oxSlot.data(), lxLm.data(),
+                   lxCol.data(), h->lmBegin, h->lmEnd, lmObs[h->lmBegin], lmObs[h->lmEnd], lmObs[nPts], h->isRoot};
+    buildSchurLists(in, sl);
+  }
+  // landmark-entry items first, then observation-entry items (launched separately)
+  std::stable_partition(sl.items.begin(), sl.items.end(), [](const SchurItem& it) { return it.kind == 0; });
+  d.nItems = (int64_t)sl.items.size();
+  d.nItemsLm = 0;
+  for (const SchurItem& it : sl.items) d.nItemsLm += it.kind == 0;
+  h->nLmEnt = (int64_t)sl.lmEnt.size() / 2, h->nObEnt = (int64_t)sl.obEnt.size() / 2;
+  if (upload(&d.items, sl.items) || upload(&d.lmEnt, sl.lmEnt) || upload(&d.obEnt, sl.obEnt)) return VB_E_HIP;
+  sl = SchurLists();
   // ---------------- couplings: row ends and the tile pattern
   const int32_t nT = (int32_t)((nRed + TS - 1) / TS);
   d.nT = nT;
@@ -622,31 +790,41 @@ int doFinalize(vb_handle h) {
   if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) || upload(&h->pairsD, pairs) ||
       upload(&h->targetsD, targets) || upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
     return VB_E_HIP;
-  if (alloc0(&h->diagScratch, TS * TS) || alloc0(&h->linv, (size_t)nT * TS * TS)) return VB_E_HIP;
+  if (alloc0(&h->dinv, (size_t)(nT + 1) * 1024) || alloc0(&h->linv, (size_t)nT * TS * TS)) return VB_E_HIP;
   d.nRS = h->nRS;
   if (upload(&d.rsOff, h->rsOff) || upload(&d.rsS, h->rsS) || upload(&d.rsI, h->rsI) || upload(&d.rsG, h->rsG))
     return VB_E_HIP;
   if (alloc0(&d.red, 64) || alloc0(&d.err, 4)) return VB_E_HIP;
   h->finalized = true;
-  if (h->lmEnd < 0) h->lmEnd = nPts;
   return 0;
 }
 
 // ------------------------------------------------------------------ numeric phases
 void factorSeq(vb_handle h) {
   Dev& d = h->d;
+  bool diagReady = false;  // L_JJ already factored by the previous column's update launch
   for (int32_t J = 0; J < d.nT; J++) {
     const int64_t c0 = h->colStart[J];
     const int n = (int)(h->colStart[J + 1] - c0);
-    profBegin(h, KF_POTRF);
-    launch_potrf_trsm(d, h->colTilesD + c0, n, h->diagScratch, h->linv + (int64_t)J * TS * TS, h->st);
-    profEnd(h, KF_POTRF);
+    if (!diagReady) {
+      profBegin(h, KF_POTRF);
+      launch_potrf(d, h->colTilesD + c0, h->dinv + (int64_t)J * 1024, h->st);
+      profEnd(h, KF_POTRF);
+    }
+    profBegin(h, KF_TRSM);
+    launch_trsm(d, h->colTilesD + c0, n, h->dinv + (int64_t)J * 1024, h->st);
+    profEnd(h, KF_TRSM);
     const int64_t p0 = h->pairStart[J];
     const int np = (int)(h->pairStart[J + 1] - p0);
+    // pair 0 is (1, 1): the tile (row of off-diagonal 1)^2, the next diagonal when that row is J + 1
+    const bool fuse = np > 0 && h->colRowsH[c0 + 1] == J + 1 && !h->noFusePotrf;
     profBegin(h, KF_GEMM);
-    launch_gemm_update(d, h->colTilesD + c0, h->pairsD + 2 * p0, h->targetsD + p0, np, h->diagScratch, h->st);
+    launch_update(d, h->colTilesD + c0, h->pairsD + 2 * p0, h->targetsD + p0, np, fuse ? 1 : 0,
+                  h->dinv + (int64_t)(J + 1) * 1024, h->st);
     profEnd(h, KF_GEMM);
+    diagReady = fuse;
   }
+  launch_diag_inverse(d, h->linv, h->st);
 }
 
 // solve L L^T x = b (b is clobbered), result into x
@@ -682,7 +860,7 @@ int captureGraph(vb_handle h, bool factor, hipGraphExec_t* out) {
 }
 
 int factorReduced(vb_handle h) {
-  const bool prof = h->profFamily == KF_POTRF || h->profFamily == KF_GEMM;
+  const bool prof = h->profFamily == KF_POTRF || h->profFamily == KF_GEMM || h->profFamily == KF_TRSM;
   if (!h->useGraphs || prof) {
     factorSeq(h);
     return 0;
@@ -747,6 +925,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipSetDevice(c.device));
   vb_handle h = new vb_handle_s();
   h->cfg = c;
+  if (const char* e = getenv("VIBA_NO_FUSE_POTRF")) h->noFusePotrf = e[0] == '1';
   HIPCHK(hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking));
   for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
   *out = h;
@@ -761,9 +940,9 @@ int vb_destroy(vb_handle h) {
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
-                  d.lxStart, d.lxLm, d.lxCol, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
+                  d.lxStart, d.lxLm, d.lxCol, d.items, d.lmEnt, d.obEnt, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
-                  h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->diagScratch, h->yvec,
+                  h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -831,8 +1010,9 @@ int64_t vb_reduced_order(vb_handle h) { return h ? h->d.nRed : -1; }
 int64_t vb_total_order(vb_handle h) { return h ? h->order : -1; }
 
 int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_root) {
-  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_set_landmark_shard needs a finalized handle");
-  if (lm_begin < 0 || lm_end > h->d.nPts || lm_begin > lm_end) return fail(VB_E_ARG, "bad landmark range");
+  if (!h) return fail(VB_E_ARG, "null handle");
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_landmark_shard must precede vb_finalize");
+  if (lm_begin < 0 || lm_begin > lm_end) return fail(VB_E_ARG, "bad landmark range");
   h->lmBegin = lm_begin, h->lmEnd = lm_end, h->isRoot = is_root != 0;
   return 0;
 }
@@ -869,6 +1049,7 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
   profBegin(h, KF_LANDMARK);
     launch_landmark(d, lambda, 0, 0, d.nPts, h->st);
     profEnd(h, KF_LANDMARK);
+  HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   profBegin(h, KF_SCHUR);
     launch_schur(d, lambda, h->isRoot ? 1 : 0, h->st);
     profEnd(h, KF_SCHUR);
@@ -1078,8 +1259,8 @@ int vb_problem_stats(vb_handle h, int64_t* out) {
   int64_t sm = 0;
   for (int k = 1; k < 14; k++) sm += d.sf[k].n;
   out[7] = sm;
-  // Y panel doubles and total landmark-block count
-  out[8] = 0, out[9] = 0;
+  // Schur work-list sizes: landmark-pair entries, observation-pair entries
+  out[8] = h->nLmEnt, out[9] = h->nObEnt;
   return 0;
 }
 
@@ -1222,6 +1403,7 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
 int vb_assemble_reduced(vb_handle h, double lambda) {
   if (!h || !h->linearized) return fail(VB_E_STATE, "vb_assemble_reduced needs vb_linearize");
   launch_landmark(h->d, lambda, 0, 0, h->d.nPts, h->st);
+  HIPCHK(hipMemsetAsync(h->d.rhs, 0, (size_t)h->d.nT * TS * sizeof(double), h->st));
   launch_schur(h->d, lambda, h->isRoot ? 1 : 0, h->st);
   HIPCHK(hipStreamSynchronize(h->st));
   return checkErr(h);

@@ -2,12 +2,14 @@
 // HBM layout (fp64 throughout, SoA where a kernel streams it):
 //   variables      var[kind]      rows of VB data size (3/7/3/3/24/7/32/7/4 doubles)
 //   visual obs     sorted by landmark; ob_* int32 index arrays + obC[6] (u, v, sqrtH 2x2)
-//   whitened J     Jt[plane * nObsPad + o], 72 planes (see kJ* below), written once per linearize
+//   whitened J     Jt[o * kJPlanes + plane]: one 72-double record per observation (see kJ* below),
+//                  written once per linearize; read per landmark (landmark_kernel) and per block pair
 //   landmarks      per point: Vchol[6], gp[3], z[3], xp[3]; Y panel 3 x d_l at Y + lmY[l]
 //   reduced system dense T x T column-major tiles (envelope / tile-sparse), tileIdx[I*nT+J]
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstddef>
 
 namespace viba {
 
@@ -39,6 +41,16 @@ struct SmallFactors {  // one kind
   int32_t* vars = nullptr;   // n * nv
   double* consts = nullptr;  // n * nc (+ whitening appended for IMU / pose prior)
   int nv = 0, nc = 0;
+};
+
+// One unit of Schur-assembly work: block pair (X2 >= X1 by offset) and a range of its entry list.
+// kind 0: landmark entries (uint2 panel columns col1, col2 — or (col1, landmark) when X1 == X2),
+// kind 1: observation entries (int2 obs, slot1 | slot2 << 8).
+struct SchurItem {
+  int64_t start;
+  int32_t count;
+  int32_t X1, X2;
+  int32_t kind;
 };
 
 struct Dev {
@@ -83,6 +95,11 @@ struct Dev {
   int64_t* lxStart = nullptr;
   int32_t* lxLm = nullptr;
   int32_t* lxCol = nullptr;
+  // Schur assembly work list (block pairs)
+  int64_t nItems = 0, nItemsLm = 0;  // items [0, nItemsLm) have kind 0
+  SchurItem* items = nullptr;
+  uint32_t* lmEnt = nullptr;  // 2 per entry
+  int32_t* obEnt = nullptr;   // 2 per entry
   // tiles
   int T = 64;
   int32_t nT = 0;

@@ -225,23 +225,23 @@ __global__ void __launch_bounds__(256) visual_lin_kernel(Dev d, int updateCache,
       double rho, drho;
       huber_jet2(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s, rho, drho);
       const double w = sqrt(drho);
-      Jt[(kJe + 0) * P + o] = w * v.e[0];
-      Jt[(kJe + 1) * P + o] = w * v.e[1];
+      Jt[o * kJPlanes + (kJe + 0)] = w * v.e[0];
+      Jt[o * kJPlanes + (kJe + 1)] = w * v.e[1];
 #pragma unroll
-      for (int i = 0; i < 6; i++) Jt[(kJpt + i) * P + o] = w * v.Jpt[i];
+      for (int i = 0; i < 6; i++) Jt[o * kJPlanes + (kJpt + i)] = w * v.Jpt[i];
 #pragma unroll
-      for (int i = 0; i < 12; i++) Jt[(kJpose + i) * P + o] = w * v.Jpose[i];
+      for (int i = 0; i < 12; i++) Jt[o * kJPlanes + (kJpose + i)] = w * v.Jpose[i];
 #pragma unroll
-      for (int i = 0; i < 12; i++) Jt[(kJextr + i) * P + o] = w * v.Jextr[i];
+      for (int i = 0; i < 12; i++) Jt[o * kJPlanes + (kJextr + i)] = w * v.Jextr[i];
 #pragma unroll
-      for (int i = 0; i < 34; i++) Jt[(kJintr + i) * P + o] = w * v.Jintr[i];
+      for (int i = 0; i < 34; i++) Jt[o * kJPlanes + (kJintr + i)] = w * v.Jintr[i];
 #pragma unroll
-      for (int i = 0; i < 6; i++) Jt[(kJvel + i) * P + o] = w * v.Jvel[i];
+      for (int i = 0; i < 6; i++) Jt[o * kJPlanes + (kJvel + i)] = w * v.Jvel[i];
       acc[0] = 0.5 * rho;
       if (updateCache) d.cache[o] = 0.5 * rho;
     } else {
 #pragma unroll 8
-      for (int i = 0; i < kJPlanes; i++) Jt[i * P + o] = 0.0;
+      for (int i = 0; i < kJPlanes; i++) Jt[o * kJPlanes + i] = 0.0;
     }
   }
   block_sum_atomic<1>(acc, d.red + 0);

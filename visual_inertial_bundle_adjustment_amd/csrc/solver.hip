@@ -41,9 +41,9 @@ __global__ void __launch_bounds__(128) landmark_kernel(Dev d, double lambda, int
   }
   double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
   for (int64_t o = o0; o < o1; o++) {
-    const double a0 = Jt[(kJpt + 0) * P + o], a1 = Jt[(kJpt + 1) * P + o], a2 = Jt[(kJpt + 2) * P + o];
-    const double b0 = Jt[(kJpt + 3) * P + o], b1 = Jt[(kJpt + 4) * P + o], b2 = Jt[(kJpt + 5) * P + o];
-    const double e0 = Jt[(kJe + 0) * P + o], e1 = Jt[(kJe + 1) * P + o];
+    const double a0 = Jt[o * kJPlanes + (kJpt + 0)], a1 = Jt[o * kJPlanes + (kJpt + 1)], a2 = Jt[o * kJPlanes + (kJpt + 2)];
+    const double b0 = Jt[o * kJPlanes + (kJpt + 3)], b1 = Jt[o * kJPlanes + (kJpt + 4)], b2 = Jt[o * kJPlanes + (kJpt + 5)];
+    const double e0 = Jt[o * kJPlanes + (kJe + 0)], e1 = Jt[o * kJPlanes + (kJe + 1)];
     g0 += a0 * e0 + b0 * e1, g1 += a1 * e0 + b1 * e1, g2 += a2 * e0 + b2 * e1;
     if (mode == 0) {
       v00 += a0 * a0 + b0 * b0, v10 += a1 * a0 + b1 * b0, v20 += a2 * a0 + b2 * b0;
@@ -75,15 +75,15 @@ __global__ void __launch_bounds__(128) landmark_kernel(Dev d, double lambda, int
   const int64_t ncol = (d.lmY[l + 1] - d.lmY[l]) / 3;
   for (int64_t c = 0; c < 3 * ncol; c++) Y[c] = 0.0;
   for (int64_t o = o0; o < o1; o++) {
-    const double a0 = Jt[(kJpt + 0) * P + o], a1 = Jt[(kJpt + 1) * P + o], a2 = Jt[(kJpt + 2) * P + o];
-    const double b0 = Jt[(kJpt + 3) * P + o], b1 = Jt[(kJpt + 4) * P + o], b2 = Jt[(kJpt + 5) * P + o];
+    const double a0 = Jt[o * kJPlanes + (kJpt + 0)], a1 = Jt[o * kJPlanes + (kJpt + 1)], a2 = Jt[o * kJPlanes + (kJpt + 2)];
+    const double b0 = Jt[o * kJPlanes + (kJpt + 3)], b1 = Jt[o * kJPlanes + (kJpt + 4)], b2 = Jt[o * kJPlanes + (kJpt + 5)];
     for (int s = 0; s < 4; s++) {
       const int col = d.obCol[o * 4 + s];
       if (col < 0) continue;
       const int dim = rv_dim(d, d.obRed[o * 4 + s]);
       const int pl = slotPlane(s), st = slotStride(s);
       for (int j = 0; j < dim; j++) {
-        const double x0 = Jt[(pl + j) * P + o], x1 = Jt[(pl + st + j) * P + o];
+        const double x0 = Jt[o * kJPlanes + (pl + j)], x1 = Jt[o * kJPlanes + (pl + st + j)];
         double* w = Y + 3 * (col + j);
         w[0] += a0 * x0 + b0 * x1;
         w[1] += a1 * x0 + b1 * x1;
@@ -108,109 +108,122 @@ __device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
   return d.tiles + (int64_t)ti * TS * TS + (c % TS) * TS + (r % TS);
 }
 
-// One wave per reduced variable X1 (a column block of S): lanes own distinct ROWS of the
-// LDS-resident accumulator, so no atomics are needed; observations and landmarks touching X1 are
-// processed one at a time by the whole wave (their row sets are disjoint within one item).
-//   direct:  acc[rows of X2] += J~_X2^T J~_X1   for the visual slots X2 >= X1 of each obs
-//   damping: diag(H_X1X1) = diag * (1 + lambda) + lambda  on visual + small-factor direct terms
-//   Schur:   acc[rows of X2] -= Y_{l,X2}^T Y_{l,X1} for the panel columns of l at/after X1
-// Rows beyond the LDS window are handled by re-scanning in windows of kSchurRows.
-constexpr int kSchurAcc = 6144;  // doubles per wave (48 KB)
+// Schur assembly over the block-pair work list (api.hip buildSchurLists).  One wave per work item
+// (X1, X2, entry range); lane e owns entry (i, j) = (e / d1, e % d1) of the d2 x d1 block S(X2, X1)
+// (64-entry chunks for larger blocks) and streams the item's entries:
+//   landmark entries:    S(X2, X1) -= Y_{l,X2}^T Y_{l,X1}            (3-row panel columns)
+//   observation entries: S(X2, X1) += J~_X2^T J~_X1  (2 whitened residual rows; diag * (1 + lambda))
+// The partial block is added to the tile store with fp64 atomics (a pair's entries may be split over
+// several items).  Diagonal items also produce the RHS pieces: gRed += J~^T e~, rhs -= Y^T z.
+// XCD-aware block id: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch), so
+// hand each XCD a contiguous range of work (bijective for any grid size)
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
+  const int64_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
 
-__global__ void __launch_bounds__(64) schur_kernel(Dev d, double lambda, int addIdentity) {
-  __shared__ double acc[kSchurAcc];
-  const int X1 = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int d1 = d.rvDim[X1];
-  const int64_t off1 = d.rvOff[X1];
-  const int64_t span = d.rvRowEnd[X1] - off1;
-  const int RW = (int)min<int64_t>(span, kSchurAcc / d1);
-  const int64_t P = d.nObsPad;
+__global__ void __launch_bounds__(256) schur_items_kernel(Dev d, double lambda, int64_t i0, int64_t i1) {
+  const int64_t it = i0 + xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (it >= i1) return;
+  const int lane = threadIdx.x & 63;
+  const SchurItem w = d.items[it];
+  const int X1 = w.X1, X2 = w.X2;
+  const int d1 = d.rvDim[X1], d2 = d.rvDim[X2];
+  const int64_t off1 = d.rvOff[X1], off2 = d.rvOff[X2];
+  const bool diag = X1 == X2;
+  const int ne = d1 * d2;
+  const int cnt = w.count;
   const double* Jt = d.Jt;
-  double gdir = 0.0, gsch = 0.0;  // lane j < d1 accumulates column j
-  const int64_t ox0 = d.oxStart[X1], ox1 = d.oxStart[X1 + 1];
-  const int64_t lx0 = d.lxStart[X1], lx1 = d.lxStart[X1 + 1];
-  for (int64_t w0 = 0; w0 < span; w0 += RW) {
-    const int rows = (int)min<int64_t>(RW, span - w0);
-    for (int i = lane; i < rows * d1; i += 64) acc[i] = 0.0;
-    __builtin_amdgcn_wave_barrier();
-    // ---- direct visual terms
-    for (int64_t idx = ox0; idx < ox1; idx++) {
-      const int64_t o = d.oxObs[idx];
-      const int s1 = d.oxSlot[idx];
-      const int p1 = slotPlane(s1), st1 = slotStride(s1);
-      if (w0 == 0 && lane < d1) {
-        const double e0 = Jt[kJe * P + o], e1 = Jt[(kJe + 1) * P + o];
-        gdir += Jt[(p1 + lane) * P + o] * e0 + Jt[(p1 + st1 + lane) * P + o] * e1;
+  const double* Y = d.Y;
+  const uint2* lent = reinterpret_cast<const uint2*>(d.lmEnt) + w.start;
+  const int2* oent = reinterpret_cast<const int2*>(d.obEnt) + w.start;
+  constexpr int U = 4;  // entries in flight per wave
+  for (int e0 = 0; e0 < ne; e0 += 64) {
+    const int e = min(e0 + lane, ne - 1);
+    const int i = e / d1, j = e - (e / d1) * d1;
+    double acc = 0.0;
+    if (w.kind == 0) {
+      int k = 0;
+      for (; k + U <= cnt; k += U) {
+        double p[U][3], q[U][3];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const uint2 en = lent[k + u];
+          const double* y1 = Y + 3 * (int64_t)en.x + 3 * j;
+          const double* y2 = Y + 3 * (int64_t)(diag ? en.x : en.y) + 3 * i;
+#pragma unroll
+          for (int c = 0; c < 3; c++) p[u][c] = y1[c], q[u][c] = y2[c];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) acc -= q[u][0] * p[u][0] + q[u][1] * p[u][1] + q[u][2] * p[u][2];
       }
-      // lane -> (slot s2, row i) flattened over the obs' slots with X2 >= X1
-      int base = 0;
-      for (int s2 = 0; s2 < 4; s2++) {
-        const int X2 = d.obRed[o * 4 + s2];
-        if (X2 < 0) continue;
-        const int64_t o2 = d.rvOff[X2];
-        if (o2 < off1) continue;
-        const int d2 = d.rvDim[X2];
-        const int i = lane - base;
-        base += d2;
-        if (i < 0 || i >= d2) continue;
-        const int64_t rr = o2 - off1 - w0 + i;
-        if (rr < 0 || rr >= rows) continue;
-        const int p2 = slotPlane(s2), st2 = slotStride(s2);
-        const double a0 = Jt[(p2 + i) * P + o], a1 = Jt[(p2 + st2 + i) * P + o];
-        double* ar = acc + rr * d1;
-        for (int j = 0; j < d1; j++) ar[j] += a0 * Jt[(p1 + j) * P + o] + a1 * Jt[(p1 + st1 + j) * P + o];
+      for (; k < cnt; k++) {
+        const uint2 en = lent[k];
+        const double* y1 = Y + 3 * (int64_t)en.x + 3 * j;
+        const double* y2 = Y + 3 * (int64_t)(diag ? en.x : en.y) + 3 * i;
+        acc -= y2[0] * y1[0] + y2[1] * y1[1] + y2[2] * y1[2];
       }
-      __builtin_amdgcn_wave_barrier();
+    } else {
+      int k = 0;
+      for (; k + U <= cnt; k += U) {
+        double a0[U], a1[U], b0[U], b1[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int2 en = oent[k + u];
+          const double* rec = Jt + (int64_t)en.x * kJPlanes;
+          const int s1 = en.y & 255, s2 = en.y >> 8;
+          const int p1 = slotPlane(s1) + j, p2 = slotPlane(s2) + i;
+          a0[u] = rec[p2], a1[u] = rec[p2 + slotStride(s2)];
+          b0[u] = rec[p1], b1[u] = rec[p1 + slotStride(s1)];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) acc += a0[u] * b0[u] + a1[u] * b1[u];
+      }
+      for (; k < cnt; k++) {
+        const int2 en = oent[k];
+        const double* rec = Jt + (int64_t)en.x * kJPlanes;
+        const int s1 = en.y & 255, s2 = en.y >> 8;
+        const int p1 = slotPlane(s1) + j, p2 = slotPlane(s2) + i;
+        acc += rec[p2] * rec[p1] + rec[p2 + slotStride(s2)] * rec[p1 + slotStride(s1)];
+      }
+      if (diag && i == j) acc *= 1.0 + lambda;
     }
-    if (w0 == 0 && lane < d1) {  // damping of the total direct diagonal (visual + small factors)
-      const double* sp = tile_ptr(d, off1 + lane, off1 + lane);
-      const double tot = acc[lane * d1 + lane] + (sp ? *sp : 0.0);
-      acc[lane * d1 + lane] += lambda * tot + (addIdentity ? lambda : 0.0);
+    if (e0 + lane < ne && (!diag || i >= j) && acc != 0.0) {
+      double* p = tile_ptr(d, off2 + i, off1 + j);
+      if (p) atomicAdd(p, acc);
+      else atomicOr(d.err, 4);
     }
-    __builtin_amdgcn_wave_barrier();
-    // ---- Schur complement terms
-    for (int64_t idx = lx0; idx < lx1; idx++) {
-      const int64_t l = d.lxLm[idx];
-      const int c1 = d.lxCol[idx];
-      const double* Yl = d.Y + d.lmY[l];
-      const double* y1 = Yl + 3 * c1;
-      const int ncol = (int)((d.lmY[l + 1] - d.lmY[l]) / 3);
-      const int32_t* rowOf = d.pcRow + d.lmY[l] / 3;
-      if (w0 == 0 && lane < d1) {
-        gsch += y1[3 * lane] * d.z[l * 3] + y1[3 * lane + 1] * d.z[l * 3 + 1] + y1[3 * lane + 2] * d.z[l * 3 + 2];
-      }
-      for (int c = c1 + lane; c < ncol; c += 64) {
-        const int64_t rr = (int64_t)rowOf[c] - off1 - w0;
-        if (rr < 0 || rr >= rows) continue;
-        const double q0 = Yl[3 * c], q1 = Yl[3 * c + 1], q2 = Yl[3 * c + 2];
-        double* ar = acc + rr * d1;
-        for (int j = 0; j < d1; j++) ar[j] -= q0 * y1[3 * j] + q1 * y1[3 * j + 1] + q2 * y1[3 * j + 2];
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    __builtin_amdgcn_wave_barrier();
-    // ---- write-out (exclusive owner of column block X1)
-    for (int i = lane; i < rows * d1; i += 64) {
-      const int rr = i / d1, j = i % d1;
-      const int64_t R = off1 + w0 + rr, Cc = off1 + j;
-      if (R < Cc) continue;
-      const double v = acc[i];
-      if (v == 0.0) continue;
-      double* p = tile_ptr(d, R, Cc);
-      if (!p) {
-        atomicOr(d.err, 4);
-        continue;
-      }
-      *p += v;
-    }
-    __builtin_amdgcn_wave_barrier();
   }
-  if (lane < d1) {
-    const double g = d.gRed[off1 + lane] + gdir;
-    d.gRed[off1 + lane] = g;
-    d.rhs[off1 + lane] = g - gsch;
+  if (!diag || lane >= d1) return;
+  const int j = lane;
+  double g = 0.0;
+  if (w.kind == 0) {
+    for (int k = 0; k < cnt; k++) {
+      const uint2 en = lent[k];
+      const double* y1 = Y + 3 * (int64_t)en.x + 3 * j;
+      const double* z = d.z + 3 * (int64_t)en.y;
+      g += y1[0] * z[0] + y1[1] * z[1] + y1[2] * z[2];
+    }
+    atomicAdd(d.rhs + off1 + j, -g);
+  } else {
+    for (int k = 0; k < cnt; k++) {
+      const int2 en = oent[k];
+      const double* rec = Jt + (int64_t)en.x * kJPlanes;
+      const int s1 = en.y & 255;
+      const int p1 = slotPlane(s1) + j;
+      g += rec[p1] * rec[kJe] + rec[p1 + slotStride(s1)] * rec[kJe + 1];
+    }
+    atomicAdd(d.gRed + off1 + j, g);
   }
+}
+
+// damping of the small-factor part of the diagonal (visual part: schur_items_kernel) and the
+// identity term (Optimizer.cpp:136-146 addDamping: H_ii += lambda * H_ii + lambda)
+__global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= d.nRed) return;
+  double* p = tile_ptr(d, r, r);
+  *p = *p * (1.0 + lambda) + (addIdentity ? lambda : 0.0);
 }
 
 // gradient-only (mode 0: gRedNew += sum J~^T e~) or new reduced RHS (mode 1: rhs = gRedNew - Y^T zNew)
@@ -228,9 +241,9 @@ __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
       const int64_t o = d.oxObs[idx];
       const int s1 = d.oxSlot[idx];
       const int p1 = slotPlane(s1), st1 = slotStride(s1);
-      const double e0 = d.Jt[kJe * P + o], e1 = d.Jt[(kJe + 1) * P + o];
+      const double e0 = d.Jt[o * kJPlanes + kJe], e1 = d.Jt[o * kJPlanes + (kJe + 1)];
       for (int j = 0; j < d1; j++)
-        atomicAdd(&g[j], d.Jt[(p1 + j) * P + o] * e0 + d.Jt[(p1 + st1 + j) * P + o] * e1);
+        atomicAdd(&g[j], d.Jt[o * kJPlanes + (p1 + j)] * e0 + d.Jt[o * kJPlanes + (p1 + st1 + j)] * e1);
     }
   } else {
     for (int64_t idx = d.lxStart[X1] + tid; idx < d.lxStart[X1 + 1]; idx += blockDim.x) {
@@ -248,131 +261,303 @@ __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
 }
 
 // ------------------------------------------------------------------ tile Cholesky
-// Register-resident wave Cholesky of a TS x TS tile: lane i holds row i (x[0..TS)); at step k
-// the pivot comes from lane k by a shuffle and column k is broadcast through LDS.  On return
-// x[k] = L(i, k) for k <= i; the factor is also written to Ls (column-major, upper part zero).
-__device__ void wave_potrf(double (&x)[TS], double* col, double* Ls, int lane, int32_t* err) {
-#pragma unroll
-  for (int k = 0; k < TS; k++) {
-    const double piv = __shfl(x[k], k, 64);
-    if (!(piv > 0.0) && lane == k) atomicOr(err, 8);
-    const double dk = sqrt(piv);
-    const double lk = (lane == k) ? dk : x[k] / dk;
-    if (lane >= k) x[k] = lk;
-    col[lane] = lk;
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int j = k + 1; j < TS; j++) {
-      const double v = col[j];
-      if (lane >= j) x[j] -= lk * v;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-#pragma unroll
-  for (int c = 0; c < TS; c++) Ls[c * TS + lane] = (lane >= c) ? x[c] : 0.0;
-}
-
-// Every block factors its own copy of the diagonal tile (all read the unfactored tile); block 0
-// publishes the factor to `diagOut` (copied into place by gemm_update_kernel) and its wave 1 the
-// inverse L^-1 into `linv` (used by the triangular solves).  Waves then solve X L^T = A for the
-// off-diagonal tile rows q = 1 + 4 * blockIdx.x + wave.
-__global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* colTiles, int n, double* diagOut,
-                                                         double* linv) {
-  __shared__ double L[TS * TS];
-  __shared__ double col[TS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const double* Ad = d.tiles + (int64_t)colTiles[0] * TS * TS;
-  if (wave == 0) {
-    double x[TS];
-#pragma unroll
-    for (int c = 0; c < TS; c++) x[c] = Ad[c * TS + lane];
-    wave_potrf(x, col, L, lane, d.err);
-  }
-  __syncthreads();
-  if (blockIdx.x == 0) {
-    for (int i = tid; i < TS * TS; i += blockDim.x) diagOut[i] = L[i];
-    if (wave == 1) {  // lane = column c of X = L^-1: X[i][c] = (delta_ic - sum_{k<i} L_ik X_kc) / L_ii
-      double xi[TS];
-#pragma unroll
-      for (int i = 0; i < TS; i++) {
-        double s = (i == lane) ? 1.0 : 0.0;
-#pragma unroll
-        for (int k = 0; k < i; k++) s -= L[k * TS + i] * xi[k];
-        xi[i] = s / L[i * TS + i];
-      }
-#pragma unroll
-      for (int i = 0; i < TS; i++) linv[lane * TS + i] = xi[i];
-    }
-  }
-  const int q = 1 + blockIdx.x * 4 + wave;
-  if (q >= n) return;
-  // X L^T = A  (row r = lane): x_c = (a_c - sum_{k<c} x_k L_ck) / L_cc
-  double* A = d.tiles + (int64_t)colTiles[q] * TS * TS;
-  double x[TS];
-#pragma unroll
-  for (int c = 0; c < TS; c++) x[c] = A[c * TS + lane];
-#pragma unroll
-  for (int c = 0; c < TS; c++) {
-    double s = x[c];
-#pragma unroll
-    for (int k = 0; k < c; k++) s -= x[k] * L[k * TS + c];
-    x[c] = s / L[c * TS + c];
-  }
-#pragma unroll
-  for (int c = 0; c < TS; c++) A[c * TS + lane] = x[c];
-}
+// Right-looking tile Cholesky, two launches per tile column J (factorSeq in api.hip):
+//   trsm_kernel    L_IJ = A_IJ L_JJ^-T for the off-diagonal tiles of column J
+//   update_kernel  A_IK -= L_IJ L_KJ^T for every pair I >= K of column J (fp64 MFMA); the block whose
+//                  target is the next diagonal tile (J+1, J+1) factors it right after its update, so
+//                  the next column's trsm finds L_{J+1,J+1} ready (potrf_kernel covers the columns
+//                  whose diagonal receives no update from the previous column, and column 0).
+// Inside a tile everything is blocked by 16 and runs on v_mfma_f64_16x16x4_f64, computed TRANSPOSED:
+// an accumulator D (lane l, register r) = D[(l >> 4) + 4 r][l & 15] is exactly the B operand of k-step
+// r (B[4 r + (l >> 4)][l & 15]), so chained products need no data movement.  The only scalar work is
+// the factor + inverse of the four 16 x 16 diagonal blocks (dinv[J]: 4 x 256 doubles, column-major).
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
-// A_IK -= L_IJ * L_KJ^T for every pair (I >= K) of off-diagonal rows of column J
-// the extra last block copies the factored diagonal tile from scratch into place
-__global__ void __launch_bounds__(256) gemm_update_kernel(Dev d, const int32_t* colTiles, const int32_t* pairs,
-                                                         const int32_t* targets, int npairs, const double* diagIn) {
-  __shared__ double LI[TS * TS];
-  __shared__ double LK[TS * TS];
-  const int p = blockIdx.x;
-  if (p == npairs) {
-    double* Ad = d.tiles + (int64_t)colTiles[0] * TS * TS;
-    for (int i = threadIdx.x; i < TS * TS; i += blockDim.x) Ad[i] = diagIn[i];
-    return;
+__device__ __forceinline__ double4_t mfma64(double a, double b, double4_t c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
+// 16 x 16 Cholesky, lane r holds row r in s[0..16) (lanes >= 16 compute garbage, ignored):
+// right-looking, column C broadcast from lanes by readlane.
+template <int C, int J>
+struct Upd16 {
+  static __device__ __forceinline__ void run(double (&s)[16], double lc) {
+    s[J] -= lc * readlane_d(lc, J);
+    Upd16<C, J + 1>::run(s, lc);
   }
+};
+template <int C>
+struct Upd16<C, 16> {
+  static __device__ __forceinline__ void run(double (&)[16], double) {}
+};
+// 1 / sqrt(x): v_rsq_f64 + two Newton steps (~1 ulp; the IEEE sqrt + divide sequences are ~40
+// dependent instructions on the factorization's serial chain)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * (1.5 - 0.5 * x * y * y);
+  y = y * (1.5 - 0.5 * x * y * y);
+  return y;
+}
+template <int C>
+struct Chol16 {
+  static __device__ __forceinline__ void run(double (&s)[16], double (&rd)[16], int lane, bool& bad) {
+    const double piv = readlane_d(s[C], C);
+    bad |= !(piv > 0.0);
+    const double y = rsqrt_nr(piv);
+    rd[C] = y;
+    const double lc = (lane == C) ? piv * y : s[C] * y;
+    s[C] = lc;
+    Upd16<C, C + 1>::run(s, lc);
+    Chol16<C + 1>::run(s, rd, lane, bad);
+  }
+};
+template <>
+struct Chol16<16> {
+  static __device__ __forceinline__ void run(double (&)[16], double (&)[16], int, bool&) {}
+};
+// x = column `lane` of L^-1 (L rows in s[] of lanes 0..15, rd = 1 / diag): right-looking forward
+// substitution
+template <int I, int J>
+struct InvUpd16 {
+  static __device__ __forceinline__ void run(double (&x)[16], const double (&s)[16]) {
+    x[J] -= readlane_d(s[I], J) * x[I];
+    InvUpd16<I, J + 1>::run(x, s);
+  }
+};
+template <int I>
+struct InvUpd16<I, 16> {
+  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16]) {}
+};
+template <int I>
+struct Inv16 {
+  static __device__ __forceinline__ void run(double (&x)[16], const double (&s)[16], const double (&rd)[16]) {
+    x[I] *= rd[I];
+    InvUpd16<I, I + 1>::run(x, s);
+    Inv16<I + 1>::run(x, s, rd);
+  }
+};
+template <>
+struct Inv16<16> {
+  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16], const double (&)[16]) {}
+};
+
+// Row block `w` (16 rows) of X = A L^-T, X overwriting A (both column-major TS x TS; A/L may be LDS or
+// global): for k = 0..3: X_k^T = Dinv_k (A_k^T - sum_{k2<k} L_{k,k2} X_k2^T).  Xt[k] keeps X_k^T.
+template <int NK>
+__device__ __forceinline__ void trsm_rowblock(double* A, const double* L, const double* dinv, int w, int lane,
+                                              double4_t (&Xt)[4]) {
+  const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < NK; k++) {
+    double4_t acc;
+#pragma unroll
+    for (int r = 0; r < 4; r++) acc[r] = A[(16 * k + lq + 4 * r) * TS + 16 * w + lr];
+#pragma unroll
+    for (int k2 = 0; k2 < k; k2++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) acc = mfma64(-L[(16 * k2 + 4 * s + lq) * TS + 16 * k + lr], Xt[k2][s], acc);
+    double4_t res = double4_t{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 4; s++) res = mfma64(dinv[k * 256 + (4 * s + lq) * 16 + lr], acc[s], res);
+    Xt[k] = res;
+  }
+}
+
+// Factor + invert the 16 x 16 diagonal block i of T (LDS) given S (its updated value, D layout):
+// writes L_ii into T and Dinv_i into dinvS (LDS) and dinvG (global, may be null).
+__device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS, double* dinvG, int i,
+                                       double4_t S, int lane, bool& bad) {
+  const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; r++) scratch[(lq + 4 * r) * 16 + lr] = S[r];  // row-major S[i'][j']
+  __builtin_amdgcn_wave_barrier();
+  double s[16], x[16], rd[16];
+#pragma unroll
+  for (int c = 0; c < 16; c++) s[c] = scratch[lr * 16 + c];
+  Chol16<0>::run(s, rd, lane, bad);
+#pragma unroll
+  for (int c = 0; c < 16; c++) x[c] = (c == lane) ? 1.0 : 0.0;
+  Inv16<0>::run(x, s, rd);
+  if (lane < 16) {
+#pragma unroll
+    for (int c = 0; c < 16; c++) T[(16 * i + c) * TS + 16 * i + lane] = (c <= lane) ? s[c] : 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const double v = (r >= lane) ? x[r] : 0.0;
+      dinvS[i * 256 + lane * 16 + r] = v;
+      if (dinvG) dinvG[i * 256 + lane * 16 + r] = v;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Blocked Cholesky of the TS x TS tile in LDS (one wave), left-looking by 16-row blocks i:
+// L_ik (k < i) by trsm_rowblock, then S = A_ii - sum_k L_ik L_ik^T and its 16 x 16 factor/inverse.
+template <int I>
+struct PotrfRow {
+  static __device__ __forceinline__ void run(double* T, double* scratch, double* dinvS, double* dinvG, int lane,
+                                             bool& bad) {
+    const int lr = lane & 15, lq = lane >> 4;
+    double4_t Lt[4];
+    trsm_rowblock<I>(T, T, dinvS, I, lane, Lt);
+    double4_t S;
+#pragma unroll
+    for (int r = 0; r < 4; r++) S[r] = T[(16 * I + lr) * TS + 16 * I + lq + 4 * r];  // lower part valid
+#pragma unroll
+    for (int k = 0; k < I; k++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) S = mfma64(-Lt[k][s], Lt[k][s], S);
+#pragma unroll
+    for (int k = 0; k < I; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) T[(16 * k + lq + 4 * r) * TS + 16 * I + lr] = Lt[k][r];
+    __builtin_amdgcn_wave_barrier();
+    diag16(T, scratch, dinvS, dinvG, I, S, lane, bad);
+    PotrfRow<I + 1>::run(T, scratch, dinvS, dinvG, lane, bad);
+  }
+};
+template <>
+struct PotrfRow<4> {
+  static __device__ __forceinline__ void run(double*, double*, double*, double*, int, bool&) {}
+};
+
+__device__ __forceinline__ void potrf_blocked(double* T, double* scratch, double* dinvS, double* dinvG, int lane,
+                                              int32_t* err) {
+  bool bad = false;
+  PotrfRow<0>::run(T, scratch, dinvS, dinvG, lane, bad);
+  if (bad && lane == 0) atomicOr(err, 8);
+}
+
+// factor the diagonal tile of column J in place (+ its 16 x 16 block inverses); one wave
+__global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* colTiles, double* dinvG) {
+  __shared__ double T[TS * TS];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[1024];
+  const int lane = threadIdx.x;
+  double* A = d.tiles + (int64_t)colTiles[0] * TS * TS;
+  {
+    double v[TS];
+#pragma unroll
+    for (int c = 0; c < TS; c++) v[c] = A[c * TS + lane];
+#pragma unroll
+    for (int c = 0; c < TS; c++) T[c * TS + lane] = v[c];
+  }
+  __builtin_amdgcn_wave_barrier();
+  potrf_blocked(T, scratch, dinvS, dinvG, lane, d.err);
+#pragma unroll
+  for (int c = 0; c < TS; c++) A[c * TS + lane] = T[c * TS + lane];
+}
+
+// X = A L_JJ^-T for tile q = blockIdx.x + 1 of the column; wave w = 16-row block (all on MFMA)
+__global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* colTiles, const double* dinv) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double* L = d.tiles + (int64_t)colTiles[0] * TS * TS;
+  double* A = d.tiles + (int64_t)colTiles[blockIdx.x + 1] * TS * TS;
+  double4_t Xt[4];
+  trsm_rowblock<4>(A, L, dinv, w, lane, Xt);
+  const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) A[(16 * k + lq + 4 * r) * TS + 16 * w + lr] = Xt[k][r];
+}
+
+// A_IK -= L_IJ L_KJ^T for pair blockIdx.x of column J.  Computed transposed, D = L_K L_I^T, so that
+// the MFMA output column (lane & 15) runs along the tile's contiguous row index: wave w owns the
+// 32 x 32 block (p in [32 (w >> 1), +32), q in [32 (w & 1), +32)) of C(q, p); operands are loaded
+// straight from the tile store in the v_mfma_f64_16x16x4_f64 layouts (A: lane -> (l & 15, l >> 4),
+// B: lane -> (l >> 4, l & 15)).  fuseDiag: block 0 (pair (1, 1) = tile (J+1, J+1)) then factors it.
+__global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* colTiles, const int32_t* pairs,
+                                                     const int32_t* targets, int fuseDiag, double* dinvNext) {
+  __shared__ double T[TS * TS];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[1024];
+  const int p = blockIdx.x;
   const int qi = pairs[2 * p], qk = pairs[2 * p + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const double* gI = d.tiles + (int64_t)colTiles[qi] * TS * TS;
-  const double* gK = d.tiles + (int64_t)colTiles[qk] * TS * TS;
-  for (int i = tid; i < TS * TS; i += blockDim.x) LI[i] = gI[i], LK[i] = gK[i];
-  __syncthreads();
-  const int mb = (wave >> 1) * 32, nb = (wave & 1) * 32;
-  double4_t c[2][2];
+  const double* LI = d.tiles + (int64_t)colTiles[qi] * TS * TS;
+  const double* LK = d.tiles + (int64_t)colTiles[qk] * TS * TS;
+  double* C = d.tiles + (int64_t)targets[p] * TS * TS;
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  double4_t acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
-    for (int b = 0; b < 2; b++) c[a][b] = double4_t{0, 0, 0, 0};
-  const int li = lane & 15, lk = lane >> 4;
-#pragma unroll 4
-  for (int kk = 0; kk < TS; kk += 4) {
-    const int kcol = kk + lk;
+    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
+  double cv[2][2][4];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) cv[a][b][r] = C[(pb + a * 16 + l4 + 4 * r) * TS + qb + b * 16 + l15];
+#pragma unroll
+  for (int t0 = 0; t0 < TS; t0 += 4) {
+    const int t = t0 + l4;
     double av[2], bv[2];
 #pragma unroll
-    for (int a = 0; a < 2; a++) av[a] = LI[kcol * TS + mb + a * 16 + li];
+    for (int a = 0; a < 2; a++) av[a] = LK[t * TS + pb + a * 16 + l15];
 #pragma unroll
-    for (int b = 0; b < 2; b++) bv[b] = LK[kcol * TS + nb + b * 16 + li];
+    for (int b = 0; b < 2; b++) bv[b] = LI[t * TS + qb + b * 16 + l15];
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
-      for (int b = 0; b < 2; b++) c[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], c[a][b], 0, 0, 0);
+      for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
   }
-  double* C = d.tiles + (int64_t)targets[p] * TS * TS;
+  const bool fuse = fuseDiag && p == 0;
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
-        const int row = mb + a * 16 + lk + 4 * r;
-        const int col = nb + b * 16 + li;
-        C[col * TS + row] -= c[a][b][r];
+        const int idx = (pb + a * 16 + l4 + 4 * r) * TS + qb + b * 16 + l15;
+        const double v = cv[a][b][r] - acc[a][b][r];
+        if (fuse) T[idx] = v;
+        else C[idx] = v;
       }
+  if (!fuse) return;
+  __syncthreads();
+  if (wave == 0) potrf_blocked(T, scratch, dinvS, dinvNext, lane, d.err);
+  __syncthreads();
+  for (int i = tid; i < TS * TS; i += 256) C[i] = T[i];
+}
+
+// Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
+// tile, lane = column c of X = L^-1): X[i][c] = (delta_ic - sum_{k<i} L_ik X_kc) / L_ii.
+// linv[J] is column-major; the triangular solves apply it as a GEMV.
+__global__ void __launch_bounds__(64) diag_inverse_kernel(Dev d, double* linv) {
+  __shared__ double L[TS * TS];
+  const int J = blockIdx.x, lane = threadIdx.x;
+  const double* Ad = d.tiles + (int64_t)d.tileIdx[(int64_t)J * d.nT + J] * TS * TS;
+  {
+    double v[TS];  // all loads in flight before the LDS stores
+#pragma unroll
+    for (int c = 0; c < TS; c++) v[c] = Ad[c * TS + lane];
+#pragma unroll
+    for (int c = 0; c < TS; c++) L[c * TS + lane] = v[c];
+  }
+  __syncthreads();
+  double xi[TS];
+#pragma unroll
+  for (int i = 0; i < TS; i++) {
+    double s = (i == lane) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < i; k++) s -= L[k * TS + i] * xi[k];
+    xi[i] = s / L[i * TS + i];
+  }
+  double* out = linv + (int64_t)J * TS * TS + lane * TS;
+#pragma unroll
+  for (int i = 0; i < TS; i++) out[i] = xi[i];
 }
 
 // ------------------------------------------------------------------ triangular solves
@@ -578,26 +763,39 @@ __global__ void __launch_bounds__(256) boxplus_reduced_kernel(Dev d, const doubl
 
 // ------------------------------------------------------------------ launch wrappers
 static inline unsigned blocks(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hipStream_t st);
 
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi > lo)
     hipLaunchKernelGGL(landmark_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, lambda, mode, lo, hi);
 }
+// S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry)
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
-  if (d.nRV) hipLaunchKernelGGL(schur_kernel, dim3(d.nRV), dim3(64), 0, st, d, lambda, addIdentity);
+  if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
+  if (d.nItemsLm)
+    hipLaunchKernelGGL(schur_items_kernel, dim3(blocks(d.nItemsLm, 4)), dim3(256), 0, st, d, lambda, (int64_t)0, d.nItemsLm);
+  if (d.nItems > d.nItemsLm)
+    hipLaunchKernelGGL(schur_items_kernel, dim3(blocks(d.nItems - d.nItemsLm, 4)), dim3(256), 0, st, d, lambda,
+                       d.nItemsLm, d.nItems);
+  launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
   if (d.nRV) hipLaunchKernelGGL(reduced_grad_kernel, dim3(d.nRV), dim3(256), 0, st, d, mode);
 }
-void launch_potrf_trsm(const Dev& d, const int32_t* colTiles, int n, double* diagScratch, double* linv,
-                       hipStream_t st) {
-  const int nb = n > 1 ? (n - 1 + 3) / 4 : 1;
-  hipLaunchKernelGGL(potrf_trsm_kernel, dim3(nb), dim3(256), 0, st, d, colTiles, n, diagScratch, linv);
+void launch_potrf(const Dev& d, const int32_t* colTiles, double* dinv, hipStream_t st) {
+  hipLaunchKernelGGL(potrf_kernel, dim3(1), dim3(64), 0, st, d, colTiles, dinv);
 }
-void launch_gemm_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets,
-                        int npairs, const double* diagScratch, hipStream_t st) {
-  hipLaunchKernelGGL(gemm_update_kernel, dim3(npairs + 1), dim3(256), 0, st, d, colTiles, pairs, targets, npairs,
-                     diagScratch);
+void launch_trsm(const Dev& d, const int32_t* colTiles, int n, const double* dinv, hipStream_t st) {
+  if (n > 1) hipLaunchKernelGGL(trsm_kernel, dim3(n - 1), dim3(256), 0, st, d, colTiles, dinv);
+}
+void launch_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets, int npairs,
+                   int fuseDiag, double* dinvNext, hipStream_t st) {
+  if (npairs > 0)
+    hipLaunchKernelGGL(update_kernel, dim3(npairs), dim3(256), 0, st, d, colTiles, pairs, targets, fuseDiag,
+                       dinvNext);
+}
+void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st) {
+  if (d.nT) hipLaunchKernelGGL(diag_inverse_kernel, dim3(d.nT), dim3(64), 0, st, d, linv);
 }
 // identity on the diagonal of the padding rows of the last tile (rows >= nRed)
 __global__ void pad_diag_kernel(Dev d) {
