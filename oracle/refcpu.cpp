@@ -1168,3 +1168,55 @@ int ref_boxplus_var(void* h, int kind, int64_t handle, const double* delta) {
 }
 int ref_var_tdim(void* h, int kind, int64_t handle) { return varTdim(*(Problem*)h, kind, (int)handle); }
 }
+
+// ---------------------------------------------------------------- test helpers (MotionIntegral KATs)
+// RVP packed as 11 doubles: q[x y z w], dV[3], dP[3], dt.  Restates the identities checked by the
+// reference's lib/motion/preintegration/tests/TestMotionIntegral.cpp against this oracle's
+// integrate / combine / uncombine / differentiate (ref_factors.hpp) and boxMinus / boxPlus
+// (MotionIntegral.cpp:14-26).
+namespace {
+RVP unpackRvp(const double* a) {
+  RVP r;
+  r.R = SO3::fromQ(a[0], a[1], a[2], a[3]);
+  r.dV = v3(a[4], a[5], a[6]);
+  r.dP = v3(a[7], a[8], a[9]);
+  r.dt = a[10];
+  return r;
+}
+void packRvp(const RVP& r, double* o) {
+  for (int i = 0; i < 4; i++) o[i] = r.R.q[i];
+  for (int i = 0; i < 3; i++) o[4 + i] = r.dV[i], o[7 + i] = r.dP[i];
+  o[10] = r.dt;
+}
+}  // namespace
+extern "C" {
+void ref_mi_integrate(const double* gyro, const double* accel, double dt, double* out) {
+  packRvp(integrate(v3(gyro[0], gyro[1], gyro[2]), v3(accel[0], accel[1], accel[2]), dt), out);
+}
+void ref_mi_combine(const double* a, const double* b, double* out) {
+  packRvp(combine(unpackRvp(a), unpackRvp(b)), out);
+}
+void ref_mi_uncombine_left(const double* c, const double* a, double* out) {
+  packRvp(uncombineLeft(unpackRvp(c), unpackRvp(a)), out);
+}
+void ref_mi_differentiate(const double* rvp, double* out9) {
+  RVPInterp ip = differentiate(unpackRvp(rvp));
+  for (int i = 0; i < 3; i++) out9[i] = ip.gyro[i], out9[3 + i] = ip.accel[i], out9[6 + i] = ip.dvel[i];
+}
+// boxMinus(a, b) = [log(R_a R_b^-1), dV_a - dV_b, dP_a - dP_b]   (MotionIntegral.cpp:14-18)
+void ref_mi_boxminus(const double* a, const double* b, double* out9) {
+  RVP A = unpackRvp(a), B = unpackRvp(b);
+  V3 w = so3_log(A.R * B.R.inverse());
+  for (int i = 0; i < 3; i++) out9[i] = w[i], out9[3 + i] = A.dV[i] - B.dV[i], out9[6 + i] = A.dP[i] - B.dP[i];
+}
+// boxPlus(b, delta) = {exp(delta_r) R_b, delta_v + dV_b, delta_p + dP_b}   (MotionIntegral.cpp:20-26)
+void ref_mi_boxplus(const double* b, const double* delta, double* out) {
+  RVP B = unpackRvp(b);
+  RVP r;
+  r.R = so3_exp(v3(delta[0], delta[1], delta[2])) * B.R;
+  r.dV = v3(delta[3], delta[4], delta[5]) + B.dV;
+  r.dP = v3(delta[6], delta[7], delta[8]) + B.dP;
+  r.dt = B.dt;
+  packRvp(r, out);
+}
+}  // extern "C"

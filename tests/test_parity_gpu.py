@@ -1,0 +1,146 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle on the same seeded inputs.
+
+Tolerances (fp64 throughout; differences come only from summation order — atomics in the Schur
+assembly, blocked Cholesky, reciprocal-sqrt pivots):
+  costs, model / back reductions   relative 1e-10 (accepted cost 1e-9)
+  gradient                         max-abs / max|ref| 1e-10
+  step, sub-step                   max-abs / max|ref| 1e-8 (sub-step 1e-7)
+  variables after the step         1e-10;   CostStats exact
+  LM trajectory (optimize)         same iteration count, final cost relative 1e-9
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle.refcpu import RefEngine
+from parity_util import make, make_spring_chain, one_step, rel, spring_positions
+from visual_inertial_bundle_adjustment_amd import synth
+from visual_inertial_bundle_adjustment_amd.kinds import NUM_VAR_KINDS, VAR_NAMES
+
+pytestmark = pytest.mark.gpu
+
+
+def hip():
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    return HipEngine
+
+
+def assert_step_parity(og, orf, step_tol=1e-8, sub_tol=1e-7):
+    for k in ("cost0", "model_red", "back_red", "cost_restored"):
+        assert abs(og[k] - orf[k]) <= 1e-10 * abs(orf[k]), (k, og[k], orf[k])
+    assert abs(og["cost1"] - orf["cost1"]) <= 1e-9 * abs(orf["cost1"])
+    assert tuple(og["stats1"]) == tuple(orf["stats1"])
+    assert np.allclose(og["ratios"], orf["ratios"], rtol=1e-8, atol=0)
+    for k in range(NUM_VAR_KINDS - 1):
+        if orf["step"][k].size == 0:
+            continue
+        assert rel(og["grad"][k], orf["grad"][k]) < 1e-10, VAR_NAMES[k]
+        assert rel(og["step"][k], orf["step"][k]) < step_tol, VAR_NAMES[k]
+        assert rel(og["substep"][k], orf["substep"][k]) < sub_tol, VAR_NAMES[k]
+        assert rel(og["vars1"][k], orf["vars1"][k]) < 1e-10, VAR_NAMES[k]
+
+
+@pytest.mark.parametrize("which", ["A", "miniB"])
+def test_one_lm_step_matches_oracle(which):
+    g, _ = make(hip(), which)
+    r, _ = make(RefEngine, which)
+    assert g.reduced_order() == r.reduced_order() and g.total_order() == r.total_order()
+    assert_step_parity(one_step(g), one_step(r))
+
+
+@pytest.mark.parametrize("which", ["A", "miniB"])
+def test_optimize_trajectory_matches_oracle(which):
+    g, _ = make(hip(), which)
+    r, _ = make(RefEngine, which)
+    sg, sr = g.optimize(), r.optimize()
+    assert sg.num_iterations == sr.num_iterations
+    assert sg.num_troubled_seqs == sr.num_troubled_seqs
+    assert abs(sg.initial_cost - sr.initial_cost) <= 1e-11 * sr.initial_cost
+    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
+    for k in range(1, NUM_VAR_KINDS - 1):
+        if len(g.get_vars(k)):
+            assert rel(g.get_vars(k), r.get_vars(k)) < 1e-7, VAR_NAMES[k]
+
+
+def test_golden_fixture_A():
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_A.npz")
+    gold = dict(np.load(path, allow_pickle=False))
+    g, _ = make(hip(), "A")
+    o = one_step(g)
+    assert abs(o["cost1"] - gold["cost1"]) <= 1e-9 * gold["cost1"]
+    for k, name in enumerate(VAR_NAMES[:-1]):
+        assert rel(o["step"][k], gold[f"step_{name}"]) < 1e-8, name
+
+
+def test_spring_chain_no_landmarks():  # TestOptimizer.Simple restated; empty point range
+    e = make_spring_chain(hip())
+    e.optimize()
+    x = spring_positions(e)
+    assert np.all(np.abs(np.diff(x) - 1.0) < 1e-8), x
+
+
+@pytest.mark.parametrize("mask", [0x03, 0x0F | 0x40])
+def test_imu_calib_subsets(mask):  # ImuCalibrationJacobianIndices with options switched off
+    g, _ = make(hip(), "miniB", imu_calib_options=mask)
+    r, _ = make(RefEngine, "miniB", imu_calib_options=mask)
+    assert g.reduced_order() == r.reduced_order()
+    assert_step_parity(one_step(g), one_step(r))
+
+
+def test_constant_points_and_calibration():
+    """constant points stay out of the elimination range; constant calibration leaves the
+    reduced system (Variable.h:225 kConstantVar)."""
+    p = synth.generate(synth.config("miniB"))
+    rng = np.random.default_rng(3)
+    p.const[0][rng.choice(len(p.const[0]), size=200, replace=False)] = 1
+    p.const[5][:] = 1  # camera extrinsics fixed
+    engines = []
+    for cls in (hip(), RefEngine):
+        e = cls(imu_calib_options=p.imu_calib_options)
+        synth.load_into(e, p)
+        engines.append(e)
+    assert engines[0].reduced_order() == engines[1].reduced_order()
+    assert_step_parity(one_step(engines[0]), one_step(engines[1]))
+
+
+def test_rolling_shutter_out_of_range_is_an_error():
+    """RollingShutterData::getEstimate throws when dt leaves the table (RollingShutterData.cpp:82-91):
+    the engine reports VB_E_RANGE instead of producing numbers."""
+    from visual_inertial_bundle_adjustment_amd.engine import VbError
+    p = synth.generate(synth.config("miniB"))
+    rs = np.flatnonzero(p.fivals[0] >= 0)
+    assert len(rs)
+    cams = p.vars[4].copy()
+    cams[:, 5] *= 100.0  # 100x readout time: rows map far outside the +-11.5 ms tables
+    p.vars[4] = cams
+    e = hip()(imu_calib_options=p.imu_calib_options)
+    synth.load_into(e, p)
+    with pytest.raises(VbError) as ex:
+        e.linearize(True, False)
+    assert ex.value.code == -5
+
+
+def test_full_size_properties_config_C():
+    """Config C (10k rigs / 300k landmarks / 6M obs) through size-independent properties:
+    linearize cost == cost pass at the same point; model reduction > 0; accepted step lowers the
+    cost; backup/restore restores the variables bit-exactly (the cost to the last ulp: its
+    reduction uses atomics)."""
+    g, p = make(hip(), "C")
+    c0 = g.linearize(True, False)
+    c_pass, _ = g.cost(False)
+    assert abs(c0 - c_pass) <= 1e-12 * c0
+    mr = g.damp_factor_solve(1e-5)
+    assert mr > 0
+    v0 = [g.get_vars(k) for k in (1, 4)]
+    g.backup()
+    g.apply_step(0)
+    c1, st = g.cost(True)
+    assert c1 < c0 and st[1] < 0.03 * st[0]
+    g.restore()
+    c_back, _ = g.cost(False)
+    assert abs(c_back - c_pass) <= 1e-14 * c_pass
+    for a, k in zip(v0, (1, 4)):
+        assert np.array_equal(a, g.get_vars(k))

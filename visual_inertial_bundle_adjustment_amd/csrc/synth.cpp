@@ -787,6 +787,21 @@ void* vbs_generate(const vbs_config* cfg) {
       for (int i = 0; i < 6; i++) ce[7 + i] = 1.0 / (5e-3 * 5e-3);
       g.fconst[13].insert(g.fconst[13].end(), ce, ce + 13);
     }
+    // pose priors (PriorFactor.cpp:21-66 addPosePrior): first rig and every 500th, prior = GT pose,
+    // full 6x6 precision (correlated translation/rotation, SPD)
+    const int64_t nRig = (int64_t)g.cst[1].size();
+    for (int64_t r = 0; r < nRig; r += 500) {
+      const int32_t v[1] = {(int32_t)r};
+      g.fvars[9].insert(g.fvars[9].end(), v, v + 1);
+      g.fint[9].push_back(-1);
+      double cp[43];
+      std::copy(&g.gt[1][r * 7], &g.gt[1][r * 7] + 7, cp);
+      for (int i = 0; i < 36; i++) cp[7 + i] = 0.0;
+      for (int i = 0; i < 6; i++) cp[7 + i * 6 + i] = i < 3 ? 1.0 / (1e-2 * 1e-2) : 1.0 / (1e-3 * 1e-3);
+      cp[7 + 0 * 6 + 4] = cp[7 + 4 * 6 + 0] = 2e3;  // t_x <-> r_y coupling
+      cp[7 + 1 * 6 + 2] = cp[7 + 2 * 6 + 1] = -1e3;
+      g.fconst[9].insert(g.fconst[9].end(), cp, cp + 43);
+    }
   }
   return G;
 }
