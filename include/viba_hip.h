@@ -254,31 +254,50 @@ int vb_optimize(vb_handle h, const vb_settings* s, vb_log_cb log, vb_prestep_cb 
                 vb_summary* out);
 int vb_last_phase_times(vb_handle h, vb_phase_times* out);
 
+/* applyStep without the normalisation: raw = {max ratio, sum ratio^2, sum ratio} over the variables
+ * this handle counts (a shard: its landmarks, + the reduced variables on the root), so that a
+ * multi-device caller can reduce them; vb_apply_step = raw normalised by vb_num_params */
+int vb_apply_step_raw(vb_handle h, int which, double raw[3]);
+int64_t vb_num_params(vb_handle h);   /* registered parameter blocks (Optimizer.cpp:1017 divisor) */
+
 /* ---------------------------------------------------------------- multi-device (landmark shards)
- * Restrict the visual factors this handle linearizes to landmarks [lm_begin, lm_end) and mark the
- * handle as a non-root shard (is_root = 0: small factors are skipped). The partial reduced system
- * is exchanged by the caller through the device pointers below (RCCL reduce in bench/driver). */
+ * each device owns the landmarks [lm_begin, lm_end) (landmark order = earliest
+ * observing rig, so shards are time bands), linearizes their visual factors and eliminates them;
+ * the root (is_root = 1) also owns the constant-point observations, every small factor (IMU, omega,
+ * random walks, priors) and the identity damping term.  Must precede vb_finalize.  The caller sums
+ * the partial reduced systems on the root between the calls below (distributed.py: point-to-point
+ * tile bands + reduce of the RHS over RCCL), the root factors/solves, and broadcasts x_red. */
 int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_root);
-/* device pointers + sizes (in doubles) of the reduced matrix storage and the reduced RHS */
+/* device pointers + sizes (in doubles) of the reduced matrix (tile store) and the reduced RHS */
 int vb_reduced_buffers(vb_handle h, double** matrix, int64_t* matrix_len, double** rhs,
                        int64_t* rhs_len);
-/* split of vb_damp_factor_solve for sharded use: (1) assemble/eliminate into the reduced buffers,
- * (2) factor + solve the reduced system (root), (3) back-substitute points from a given reduced
- * solution already placed in the rhs buffer */
+/* the contiguous range of the tile store this shard's partial reduced system can touch */
+int vb_shard_tile_range(vb_handle h, int64_t* first_double, int64_t* num_doubles);
+/* split of vb_damp_factor_solve (Optimizer.cpp:826-833) for sharded use:
+ * (1) partial damped Schur-reduced system + RHS of this shard, (2) root: factor + solve (x_red is
+ * left in the RHS buffer), (3) every shard: x_red (in the RHS buffer) -> its points' step and the
+ * partial model cost reduction (summed by the caller) */
 int vb_assemble_reduced(vb_handle h, double lambda);
 int vb_factor_solve_reduced(vb_handle h);
 int vb_back_substitute(vb_handle h, double* model_cost_reduction_partial);
+/* split of vb_solve_with_new_gradient (Optimizer.cpp:958-972) for sharded use, after
+ * vb_gradient_dot_step: (1) partial new RHS, (2) root: solve with the existing factor,
+ * (3) every shard: sub-step of its points (which = 1) */
+int vb_assemble_new_rhs(vb_handle h);
+int vb_solve_reduced(vb_handle h);
+int vb_back_substitute_which(vb_handle h, int which, double* model_cost_reduction_partial);
 /* the HIP stream of the handle (hipStream_t), for interop with torch / RCCL */
 void* vb_stream(vb_handle h);
 
 /* ---------------------------------------------------------------- measurement
  * time every launch of one kernel family with HIP events on the handle's stream
- * (0 visual linearize, 1 landmark eliminate, 2 Schur assembly, 3 potrf+trsm, 4 tile GEMM update,
- *  5 forward solve, 6 backward solve, 7 point back-substitution, 8 visual cost, 9 small factors;
- *  -1 disables); vb_kernel_time returns launches and summed device milliseconds since enabling */
+ * (0 visual linearize, 1 landmark eliminate, 2 Schur assembly, 3 standalone potrf, 4 tile GEMM
+ *  update (+ fused next-diagonal potrf), 5 forward solve, 6 backward solve, 7 point
+ *  back-substitution, 8 visual cost, 9 small factors, 10 tile trsm; -1 disables); vb_kernel_time returns launches and summed device milliseconds since enabling */
 int vb_profile_kernel(vb_handle h, int family);
 int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
-/* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs, nSmallFactors, 0, 0] */
+/* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs, nSmallFactors,
+ *  Schur landmark-pair entries, Schur observation-pair entries] */
 int vb_problem_stats(vb_handle h, int64_t* out10);
 
 #ifdef __cplusplus

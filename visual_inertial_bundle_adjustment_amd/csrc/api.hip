@@ -360,6 +360,7 @@ struct vb_handle_s {
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool isRoot = true;
+  int64_t itemTileLo = 0, itemTileHi = -1, tileFirst = 0, tileCount = 0;
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
   hipGraphExec_t factorGraph = nullptr, solveGraph = nullptr;
   bool useGraphs = true;
@@ -638,11 +639,25 @@ int doFinalize(vb_handle h) {
   }
   // landmark-entry items first, then observation-entry items (launched separately)
   std::stable_partition(sl.items.begin(), sl.items.end(), [](const SchurItem& it) { return it.kind == 0; });
+  d.lmB = h->lmBegin, d.lmE = h->lmEnd, d.root = h->isRoot ? 1 : 0;
+  d.obB = lmObs[h->lmBegin], d.obE = lmObs[h->lmEnd], d.obFree = lmObs[nPts];
   d.nItems = (int64_t)sl.items.size();
   d.nItemsLm = 0;
   for (const SchurItem& it : sl.items) d.nItemsLm += it.kind == 0;
   h->nLmEnt = (int64_t)sl.lmEnt.size() / 2, h->nObEnt = (int64_t)sl.obEnt.size() / 2;
   if (upload(&d.items, sl.items) || upload(&d.lmEnt, sl.lmEnt) || upload(&d.obEnt, sl.obEnt)) return VB_E_HIP;
+  // tiles this shard's Schur items touch (column-major tile order => one contiguous range)
+  {
+    int64_t lo = INT64_MAX, hi = -1;
+    const int32_t nTl = (int32_t)((nRed + TS - 1) / TS);
+    for (const SchurItem& it : sl.items) {
+      const int64_t o1 = h->rvOff[it.X1], o2 = h->rvOff[it.X2];
+      const int64_t J0 = o1 / TS, J1 = (o1 + h->rvDim[it.X1] - 1) / TS;
+      const int64_t I0 = o2 / TS, I1 = (o2 + h->rvDim[it.X2] - 1) / TS;
+      lo = std::min(lo, J0 * nTl + I0), hi = std::max(hi, J1 * nTl + I1);
+    }
+    h->itemTileLo = lo, h->itemTileHi = hi;  // packed (J, I) keys, mapped to tile indices below
+  }
   sl = SchurLists();
   // ---------------- couplings: row ends and the tile pattern
   const int32_t nT = (int32_t)((nRed + TS - 1) / TS);
@@ -717,6 +732,20 @@ int doFinalize(vb_handle h) {
     h->colStart[J + 1] = (int64_t)h->colTilesH.size();
   }
   d.nTiles = nTiles;
+  if (h->isRoot || h->itemTileHi < 0) {
+    h->tileFirst = 0, h->tileCount = h->isRoot ? nTiles : 0;
+  } else {  // first / last stored tile whose (J, I) key lies inside the touched key range
+    int64_t first = -1, last = -1;
+    for (int32_t J = 0; J < nT; J++)
+      for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
+        const int64_t key = (int64_t)J * nT + h->colRowsH[c];
+        if (key >= h->itemTileLo && key <= h->itemTileHi) {
+          if (first < 0) first = h->colTilesH[c];
+          last = h->colTilesH[c];
+        }
+      }
+    h->tileFirst = first < 0 ? 0 : first, h->tileCount = first < 0 ? 0 : last - first + 1;
+  }
   std::vector<int32_t> pairs, targets;
   h->pairStart.assign(nT + 1, 0);
   for (int32_t J = 0; J < nT; J++) {
@@ -800,6 +829,22 @@ int doFinalize(vb_handle h) {
 }
 
 // ------------------------------------------------------------------ numeric phases
+// visual kernels over this shard's observations (+ the root's constant-point observations)
+void visualLinShard(vb_handle h, int updateCache, int dontRetry) {
+  const Dev& d = h->d;
+  profBegin(h, KF_VISUAL_LIN);
+  launch_visual_lin(d, updateCache, dontRetry, d.obB, d.obE, h->st);
+  if (d.root) launch_visual_lin(d, updateCache, dontRetry, d.obFree, d.nObs, h->st);
+  profEnd(h, KF_VISUAL_LIN);
+}
+void visualCostShard(vb_handle h, int comparable) {
+  const Dev& d = h->d;
+  profBegin(h, KF_VISUAL_COST);
+  launch_visual_cost(d, comparable, d.obB, d.obE, h->st);
+  if (d.root) launch_visual_cost(d, comparable, d.obFree, d.nObs, h->st);
+  profEnd(h, KF_VISUAL_COST);
+}
+
 void factorSeq(vb_handle h) {
   Dev& d = h->d;
   bool diagReady = false;  // L_JJ already factored by the previous column's update launch
@@ -882,6 +927,23 @@ int solveReduced(vb_handle h) {
     if (int rc = captureGraph(h, false, &h->solveGraph)) return rc;
   HIPCHK(hipGraphLaunch(h->solveGraph, h->st));
   return 0;
+}
+
+// x_red (xRed) -> points of this shard (x_p = L^-T (z - Y x_c)), step = -x (which 0) or sub-step
+// (which 1), and the partial model-cost dot into red[16] (x_red . g_red partial + shard points)
+void backSubstitute(vb_handle h, int which) {
+  Dev& d = h->d;
+  const int64_t p0 = d.lmB * 3, np = (d.lmE - d.lmB) * 3;
+  profBegin(h, KF_BACKSUB);
+  launch_backsub(d, which, d.lmB, d.lmE, d.xRed, d.xp, h->st);
+  profEnd(h, KF_BACKSUB);
+  if (which == 0) {
+    (void)hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st);
+    launch_dot(d.xRed, d.gRed, d.nRed, d.red + 16, h->st);
+    launch_dot(d.xp + p0, d.gp + p0, np, d.red + 16, h->st);
+  }
+  launch_axpby(which ? d.subRed : d.stepRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
+  launch_axpby((which ? d.subPt : d.stepPt) + p0, d.xp + p0, -1.0, 0.0, np, h->st);
 }
 
 double elapsed(hipEvent_t a, hipEvent_t b) {
@@ -1025,11 +1087,8 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  launch_pad_diag(d, h->st);
-  const int64_t o0 = 0, o1 = d.nObs;  // (shard restriction applies to landmark-side work)
-  profBegin(h, KF_VISUAL_LIN);
-    launch_visual_lin(d, update_cache, dont_retry_failed, o0, o1, h->st);
-    profEnd(h, KF_VISUAL_LIN);
+  if (h->isRoot) launch_pad_diag(d, h->st);
+  visualLinShard(h, update_cache, dont_retry_failed);
   if (h->isRoot) launch_small(d, 0, d.gRed, h->st);
   HIPCHK(hipEventRecord(h->ev[1], h->st));
   double c = 0;
@@ -1047,8 +1106,8 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   HIPCHK(hipEventRecord(h->ev[2], h->st));
   profBegin(h, KF_LANDMARK);
-    launch_landmark(d, lambda, 0, 0, d.nPts, h->st);
-    profEnd(h, KF_LANDMARK);
+  launch_landmark(d, lambda, 0, d.lmB, d.lmE, h->st);
+  profEnd(h, KF_LANDMARK);
   HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   profBegin(h, KF_SCHUR);
     launch_schur(d, lambda, h->isRoot ? 1 : 0, h->st);
@@ -1058,14 +1117,7 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
   HIPCHK(hipEventRecord(h->ev[4], h->st));
   HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (int rc = solveReduced(h)) return rc;
-  profBegin(h, KF_BACKSUB);
-    launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
-    profEnd(h, KF_BACKSUB);
-  HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
-  launch_dot(d.xRed, d.gRed, d.nRed, d.red + 16, h->st);
-  launch_dot(d.xp, d.gp, d.nPts * 3, d.red + 16, h->st);
-  launch_axpby(d.stepRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
-  launch_axpby(d.stepPt, d.xp, -1.0, 0.0, d.nPts * 3, h->st);
+  backSubstitute(h, 0);
   HIPCHK(hipEventRecord(h->ev[5], h->st));
   double dotv = 0;
   if (int rc = readRed(h, &dotv, 16, 1)) return rc;
@@ -1084,15 +1136,13 @@ int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red) {
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 1 * sizeof(double), h->st));
-  profBegin(h, KF_VISUAL_LIN);
-    launch_visual_lin(d, 0, dont_retry_failed, 0, d.nObs, h->st);
-    profEnd(h, KF_VISUAL_LIN);
+  visualLinShard(h, 0, dont_retry_failed);
   if (h->isRoot) launch_small(d, 1, d.gRedNew, h->st);
-  launch_landmark(d, 0.0, 1, 0, d.nPts, h->st);
+  launch_landmark(d, 0.0, 1, d.lmB, d.lmE, h->st);
   launch_reduced_grad(d, 0, h->st);
   HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
   launch_dot(d.gRedNew, d.stepRed, d.nRed, d.red + 16, h->st);
-  launch_dot(d.gpNew, d.stepPt, d.nPts * 3, d.red + 16, h->st);
+  launch_dot(d.gpNew + d.lmB * 3, d.stepPt + d.lmB * 3, (d.lmE - d.lmB) * 3, d.red + 16, h->st);
   double dotv = 0;
   if (int rc = readRed(h, &dotv, 16, 1)) return rc;
   if (int rc = checkErr(h)) return rc;
@@ -1103,13 +1153,11 @@ int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red) {
 int vb_solve_with_new_gradient(vb_handle h) {
   if (!h || !h->factored) return fail(VB_E_STATE, "vb_solve_with_new_gradient needs a factorization");
   Dev& d = h->d;
-  launch_landmark(d, 0.0, 2, 0, d.nPts, h->st);
+  launch_landmark(d, 0.0, 2, d.lmB, d.lmE, h->st);
   launch_reduced_grad(d, 1, h->st);
   HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (int rc = solveReduced(h)) return rc;
-  launch_backsub(d, 1, 0, d.nPts, d.xRed, d.xp, h->st);
-  launch_axpby(d.subRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
-  launch_axpby(d.subPt, d.xp, -1.0, 0.0, d.nPts * 3, h->st);
+  backSubstitute(h, 1);
   HIPCHK(hipStreamSynchronize(h->st));
   return 0;
 }
@@ -1121,7 +1169,7 @@ int vb_scale_step(vb_handle h, double f) {
   return 0;
 }
 
-int vb_apply_step(vb_handle h, int which, double ratios[3]) {
+int vb_apply_step_raw(vb_handle h, int which, double raw[3]) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
   Dev& d = h->d;
   HIPCHK(hipEventRecord(h->ev[6], h->st));
@@ -1131,10 +1179,17 @@ int vb_apply_step(vb_handle h, int which, double ratios[3]) {
   double r[3];
   if (int rc = readRed(h, r, 8, 3)) return rc;
   h->times.step_ms = elapsed(h->ev[6], h->ev[7]);
+  if (raw) raw[0] = r[0], raw[1] = r[1], raw[2] = r[2];
+  return 0;
+}
+int vb_apply_step(vb_handle h, int which, double ratios[3]) {
+  double r[3];
+  if (int rc = vb_apply_step_raw(h, which, r)) return rc;
   const double n = (double)std::max<int64_t>(1, h->nParams);
   if (ratios) ratios[0] = r[0], ratios[1] = std::sqrt(r[1] / n), ratios[2] = r[2] / n;
   return 0;
 }
+int64_t vb_num_params(vb_handle h) { return h ? h->nParams : -1; }
 
 int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
@@ -1142,9 +1197,7 @@ int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
   HIPCHK(hipEventRecord(h->ev[6], h->st));
   HIPCHK(hipMemsetAsync(d.red + 1, 0, 4 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  profBegin(h, KF_VISUAL_COST);
-    launch_visual_cost(d, comparable, 0, d.nObs, h->st);
-    profEnd(h, KF_VISUAL_COST);
+  visualCostShard(h, comparable);
   if (h->isRoot) launch_small(d, 2, nullptr, h->st);
   HIPCHK(hipEventRecord(h->ev[7], h->st));
   double r[4];
@@ -1223,7 +1276,7 @@ int vb_get_gradient(vb_handle h, int kind, double* out) {
     Dev& d = h->d;
     HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
     if (h->isRoot) launch_small(d, 1, d.gRedNew, h->st);
-    launch_landmark(d, 0.0, 1, 0, d.nPts, h->st);
+    launch_landmark(d, 0.0, 1, d.lmB, d.lmE, h->st);
     launch_reduced_grad(d, 0, h->st);
     return getPerKind(h, d.gRedNew, d.gpNew, kind, out);
   }
@@ -1399,40 +1452,75 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
   return 0;
 }
 
-// sharded building blocks (landmark shards)
+// sharded building blocks (landmark shards).  The host controller
+// (distributed.py) sums the partial reduced systems / right-hand sides of all shards on the root
+// between these calls; every rank runs the same LM decisions.
+int vb_shard_tile_range(vb_handle h, int64_t* first_double, int64_t* num_doubles) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  if (first_double) *first_double = h->tileFirst * TS * TS;
+  if (num_doubles) *num_doubles = h->tileCount * TS * TS;
+  return 0;
+}
+// partial S (damped, Schur-reduced over this shard) in the tile store and partial RHS in rhs
 int vb_assemble_reduced(vb_handle h, double lambda) {
   if (!h || !h->linearized) return fail(VB_E_STATE, "vb_assemble_reduced needs vb_linearize");
-  launch_landmark(h->d, lambda, 0, 0, h->d.nPts, h->st);
-  HIPCHK(hipMemsetAsync(h->d.rhs, 0, (size_t)h->d.nT * TS * sizeof(double), h->st));
-  launch_schur(h->d, lambda, h->isRoot ? 1 : 0, h->st);
+  Dev& d = h->d;
+  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  launch_landmark(d, lambda, 0, d.lmB, d.lmE, h->st);
+  HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
+  launch_schur(d, lambda, h->isRoot ? 1 : 0, h->st);
   HIPCHK(hipStreamSynchronize(h->st));
-  return checkErr(h);
+  if (int rc = checkErr(h)) return rc;
+  h->linearized = false;
+  return 0;
 }
+// root: factor the (summed) tile store and solve with the (summed) rhs; x_red is left in rhs
 int vb_factor_solve_reduced(vb_handle h) {
-  if (!h) return fail(VB_E_ARG, "null handle");
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
   if (int rc = factorReduced(h)) return rc;
   HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (int rc = solveReduced(h)) return rc;
   HIPCHK(hipMemcpyAsync(h->d.rhs, h->d.xRed, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
-  return checkErr(h);
+  if (int rc = checkErr(h)) return rc;
+  h->factored = true;
+  return 0;
 }
-int vb_back_substitute(vb_handle h, double* mcr) {
-  if (!h) return fail(VB_E_ARG, "null handle");
+// root: solve with the existing factor, rhs -> x_red (left in rhs)
+int vb_solve_reduced(vb_handle h) {
+  if (!h || !h->factored) return fail(VB_E_STATE, "vb_solve_reduced needs a factorization");
+  HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  if (int rc = solveReduced(h)) return rc;
+  HIPCHK(hipMemcpyAsync(h->d.rhs, h->d.xRed, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+// x_red (broadcast into rhs) -> step (which 0) / sub-step (which 1) of this shard; which 0 also
+// returns the partial model cost reduction 0.5 (x_red . g_red_partial + x_p . g_p over the shard)
+int vb_back_substitute_which(vb_handle h, int which, double* mcr) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
   Dev& d = h->d;
   HIPCHK(hipMemcpyAsync(d.xRed, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  profBegin(h, KF_BACKSUB);
-    launch_backsub(d, 0, 0, d.nPts, d.xRed, d.xp, h->st);
-    profEnd(h, KF_BACKSUB);
-  HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
-  if (h->isRoot) launch_dot(d.xRed, d.gRed, d.nRed, d.red + 16, h->st);
-  launch_dot(d.xp, d.gp, d.nPts * 3, d.red + 16, h->st);
-  launch_axpby(d.stepRed, d.xRed, -1.0, 0.0, d.nRed, h->st);
-  launch_axpby(d.stepPt, d.xp, -1.0, 0.0, d.nPts * 3, h->st);
+  backSubstitute(h, which);
   double v = 0;
-  if (int rc = readRed(h, &v, 16, 1)) return rc;
+  if (which == 0) {
+    if (int rc = readRed(h, &v, 16, 1)) return rc;
+  } else {
+    HIPCHK(hipStreamSynchronize(h->st));
+  }
   if (mcr) *mcr = 0.5 * v;
   h->factored = true;
+  return 0;
+}
+int vb_back_substitute(vb_handle h, double* mcr) { return vb_back_substitute_which(h, 0, mcr); }
+// partial new reduced RHS of this shard (after vb_gradient_dot_step): rhs = gRedNew_part - Y^T zNew
+int vb_assemble_new_rhs(vb_handle h) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  Dev& d = h->d;
+  launch_landmark(d, 0.0, 2, d.lmB, d.lmE, h->st);
+  launch_reduced_grad(d, 1, h->st);
+  HIPCHK(hipStreamSynchronize(h->st));
   return 0;
 }
 

@@ -119,6 +119,11 @@ struct Dev {
   // scratch for reductions
   double* red = nullptr;  // 64 doubles
   int32_t* err = nullptr;  // error flags
+  // landmark shard of this handle (multi-GPU; the whole problem on a single GPU): landmarks
+  // [lmB, lmE), their observations [obB, obE); the root also owns the observations of constant
+  // points [obFree, nObs), every small factor and the reduced-variable step ratios
+  int64_t lmB = 0, lmE = 0, obB = 0, obE = 0, obFree = 0;
+  int32_t root = 1;
   // config
   LossParams reproj, imu;
   ImuIdx jac;

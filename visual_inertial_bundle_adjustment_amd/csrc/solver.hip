@@ -226,28 +226,32 @@ __global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
   *p = *p * (1.0 + lambda) + (addIdentity ? lambda : 0.0);
 }
 
-// gradient-only (mode 0: gRedNew += sum J~^T e~) or new reduced RHS (mode 1: rhs = gRedNew - Y^T zNew)
+// gradient-only (mode 0: gRedNew += sum J~^T e~ over this shard's observations) or new reduced RHS
+// (mode 1: rhs = gRedNew - sum Y^T zNew over this shard's landmarks)
+__device__ __forceinline__ bool shard_obs(const Dev& d, int64_t o) {
+  return (o >= d.obB && o < d.obE) || (d.root && o >= d.obFree);
+}
 __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
   __shared__ double g[32];
   const int X1 = blockIdx.x;
   const int d1 = d.rvDim[X1];
   const int64_t off1 = d.rvOff[X1];
-  const int64_t P = d.nObsPad;
   const int tid = threadIdx.x;
   if (tid < 32) g[tid] = 0.0;
   __syncthreads();
   if (mode == 0) {
     for (int64_t idx = d.oxStart[X1] + tid; idx < d.oxStart[X1 + 1]; idx += blockDim.x) {
       const int64_t o = d.oxObs[idx];
+      if (!shard_obs(d, o)) continue;
       const int s1 = d.oxSlot[idx];
+      const double* rec = d.Jt + o * kJPlanes;
       const int p1 = slotPlane(s1), st1 = slotStride(s1);
-      const double e0 = d.Jt[o * kJPlanes + kJe], e1 = d.Jt[o * kJPlanes + (kJe + 1)];
-      for (int j = 0; j < d1; j++)
-        atomicAdd(&g[j], d.Jt[o * kJPlanes + (p1 + j)] * e0 + d.Jt[o * kJPlanes + (p1 + st1 + j)] * e1);
+      for (int j = 0; j < d1; j++) atomicAdd(&g[j], rec[p1 + j] * rec[kJe] + rec[p1 + st1 + j] * rec[kJe + 1]);
     }
   } else {
     for (int64_t idx = d.lxStart[X1] + tid; idx < d.lxStart[X1 + 1]; idx += blockDim.x) {
       const int64_t l = d.lxLm[idx];
+      if (l < d.lmB || l >= d.lmE) continue;
       const double* y1 = d.Y + d.lmY[l] + 3 * d.lxCol[idx];
       const double z0 = d.zNew[l * 3], z1 = d.zNew[l * 3 + 1], z2 = d.zNew[l * 3 + 2];
       for (int j = 0; j < d1; j++) atomicAdd(&g[j], y1[3 * j] * z0 + y1[3 * j + 1] * z1 + y1[3 * j + 2] * z2);
@@ -687,7 +691,7 @@ __global__ void __launch_bounds__(256) boxplus_points_kernel(Dev d, const double
   double r = 0.0;
   if (h < d.nvar[0]) {
     const int l = d.ptLm[h];
-    if (l >= 0) {
+    if (l >= d.lmB && l < d.lmE) {
       double* v = d.var[0] + h * 3;
       const double* s = stepPt + (int64_t)l * 3;
       v[0] += s[0], v[1] += s[1], v[2] += s[2];
@@ -702,7 +706,7 @@ __global__ void __launch_bounds__(256) boxplus_points_kernel(Dev d, const double
 __global__ void __launch_bounds__(256) boxplus_reduced_kernel(Dev d, const double* stepRed) {
   const int X = blockIdx.x * blockDim.x + threadIdx.x;
   double r = 0.0;
-  if (X < d.nRV) {
+  if (X < d.nRV) {  // every shard applies the (identical) reduced step; only the root counts it
     const int kind = d.rvKind[X], h = d.rvHandle[X];
     const double* s = stepRed + d.rvOff[X];
     if (kind == 2 || kind == 3) {  // Vec3 (Variable.h:33-37)
@@ -758,7 +762,7 @@ __global__ void __launch_bounds__(256) boxplus_reduced_kernel(Dev d, const doubl
       for (int i = 0; i < J.size; i++) r = fmax(r, fabs(s[i]));
     }
   }
-  ratio_accum(d, r);
+  ratio_accum(d, d.root ? r : 0.0);
 }
 
 // ------------------------------------------------------------------ launch wrappers

@@ -1,0 +1,373 @@
+"""Landmark-sharded LM across devices, one process per GPU over torch.distributed.
+
+Every rank holds the whole problem but owns one time band of landmarks (landmarks ordered by their
+earliest observing rig, cut into contiguous ranges balanced by observation count): it linearizes the
+visual factors of its landmarks, eliminates them and forms its partial damped Schur-reduced system.
+The root (rank 0) also owns every small factor (IMU, omega, random walks, priors), the constant-point
+observations and the identity damping term.  Per LM iteration:
+
+  1. each rank: linearize (partial cost)                           -> all-reduce 1 scalar
+  2. each rank: partial reduced system S_r, RHS b_r                 (vb_assemble_reduced)
+  3. S = sum S_r on the root: each rank sends only the contiguous tile band its landmarks touch
+     (point-to-point over RCCL/xGMI), b = sum b_r by reduce
+  4. root: factor S, solve x_red                                    (vb_factor_solve_reduced)
+  5. broadcast x_red (reduced order x 8 B)
+  6. each rank: back-substitute its points, partial model reduction -> all-reduce 1 scalar
+  7. box-plus (every rank applies the reduced step; points per shard), step ratios -> all-reduce
+  8. cost pass (partial cost + CostStats)                           -> all-reduce 4 scalars
+The LM decisions (Optimizer.cpp:768-1106, restated by vb_optimize) run identically on every rank
+from the all-reduced scalars.  The bad-step path (step rescale, sub-step with the existing factor)
+uses the same pattern (vb_gradient_dot_step partial scalar; vb_assemble_new_rhs -> reduce ->
+root vb_solve_reduced -> broadcast -> vb_back_substitute_which(1)).
+
+The controller is engine-agnostic: the HIP engine (device buffers, RCCL) in production, the CPU
+oracle (host buffers, gloo) in the CPU tests.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import time
+
+import numpy as np
+
+from .engine import Settings, Summary
+
+
+# ------------------------------------------------------------------ buffers as torch tensors
+class _CudaArray:
+    """Minimal __cuda_array_interface__ exporter for a device pointer (no copy)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+
+def _tensor(ptr: int, n: int, device):
+    import torch
+    if n == 0:
+        return torch.zeros(0, dtype=torch.float64, device=device)
+    if device is None or device.type == "cpu":
+        return torch.from_numpy(np.ctypeslib.as_array((C.c_double * n).from_address(ptr)))
+    return torch.as_tensor(_CudaArray(ptr, n), device=device)
+
+
+class ShardComm:
+    """Collectives of the sharded LM.  `device` is where the engine's buffers live (a CUDA device
+    for the HIP engine, None for the oracle).  With the nccl backend (RCCL) device tensors go over
+    the wire directly; with gloo and device buffers they are staged through host memory."""
+
+    def __init__(self, rank: int, world: int, device=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.rank, self.world, self.device = rank, world, device
+        self.nccl = dist.get_backend() == "nccl"
+        self.sdev = device if self.nccl else None  # where scalar tensors live
+
+    # scalars
+    def sum(self, *vals):
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device=self.sdev)
+        self.dist.all_reduce(t)
+        return t.tolist()
+
+    def max(self, v):
+        t = self.torch.tensor([v], dtype=self.torch.float64, device=self.sdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return t.item()
+
+    def all_gather_obj(self, obj):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    # device / host buffers
+    def _staged(self, t):
+        return t if (self.nccl or t.device.type == "cpu") else t.cpu()
+
+    def reduce_to_root(self, t):
+        s = self._staged(t)
+        self.dist.reduce(s, dst=0)
+        if s is not t and self.rank == 0:
+            t.copy_(s)
+
+    def broadcast_from_root(self, t):
+        s = self._staged(t)
+        self.dist.broadcast(s, src=0)
+        if s is not t:
+            t.copy_(s)
+
+    def sum_bands_to_root(self, full, bands):
+        """full: this rank's matrix storage; bands[r] = (first, count) of rank r.  The root adds
+        every other rank's band into its own storage (point-to-point, overlapped)."""
+        dist = self.dist
+        if self.rank == 0:
+            bufs, ops = [], []
+            for r in range(1, self.world):
+                first, cnt = bands[r]
+                if cnt == 0:
+                    continue
+                b = self.torch.empty(cnt, dtype=self.torch.float64,
+                                     device=full.device if self.nccl else "cpu")
+                bufs.append((first, cnt, b))
+                ops.append(dist.P2POp(dist.irecv, b, r))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+            for first, cnt, b in bufs:
+                full[first:first + cnt] += b.to(full.device)
+        else:
+            first, cnt = bands[self.rank]
+            if cnt:
+                s = self._staged(full[first:first + cnt])
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, s.contiguous(), 0)]):
+                    w.wait()
+
+
+# ------------------------------------------------------------------ the sharded LM controller
+class ShardedOptimizer:
+    """Optimizer::optimize (Optimizer.cpp:768-1106) over landmark shards; mirrors vb_optimize."""
+
+    def __init__(self, engine, comm: ShardComm):
+        self.e, self.c = engine, comm
+        self.n_params = engine.num_params()
+        first, cnt = engine.shard_tile_range()
+        self.bands = comm.all_gather_obj((first, cnt))
+        self.sync = getattr(engine, "synchronize", lambda: None)
+
+    def _buffers(self):
+        m, nm, r, nr = self.e.reduced_buffers()
+        dev = self.c.device
+        return _tensor(m, nm, dev), _tensor(r, nr, dev)
+
+    # LM building blocks ---------------------------------------------------------------
+    def linearize(self, dont_retry):
+        return self.c.sum(self.e.linearize(True, dont_retry))[0]
+
+    def damp_factor_solve(self, lam):
+        e, c = self.e, self.c
+        e.assemble_reduced(lam)
+        S, b = self._buffers()
+        c.sum_bands_to_root(S, self.bands)
+        c.reduce_to_root(b)
+        self.sync_torch()
+        if c.rank == 0:
+            e.factor_solve_reduced()
+        S, b = self._buffers()
+        c.broadcast_from_root(b)
+        self.sync_torch()
+        return c.sum(e.back_substitute(0))[0]
+
+    def gradient_dot_step(self, dont_retry):
+        return self.c.sum(self.e.gradient_dot_step(dont_retry))[0]
+
+    def solve_with_new_gradient(self):
+        e, c = self.e, self.c
+        e.assemble_new_rhs()
+        _, b = self._buffers()
+        c.reduce_to_root(b)
+        self.sync_torch()
+        if c.rank == 0:
+            e.solve_reduced()
+        _, b = self._buffers()
+        c.broadcast_from_root(b)
+        self.sync_torch()
+        e.back_substitute(1)
+
+    def apply_step(self, which):
+        mx, sq, s = self.e.apply_step_raw(which)
+        mx = self.c.max(mx)
+        sq, s = self.c.sum(sq, s)
+        n = max(1, self.n_params)
+        return mx, math.sqrt(sq / n), s / n
+
+    def cost(self, comparable):
+        cost, st = self.e.cost(comparable)
+        out = self.c.sum(cost, *st)
+        return out[0], tuple(int(round(x)) for x in out[1:])
+
+    def sync_torch(self):
+        if self.c.device is not None and self.c.device.type != "cpu":
+            self.c.torch.cuda.synchronize(self.c.device)
+
+    # the loop ---------------------------------------------------------------------------
+    def optimize(self, s: Settings | None = None) -> Summary:
+        s = s or Settings.default()
+        e = self.e
+        damping = s.damping
+        it, last_impr, last_troubled = 0, 0, -10
+        initial_cost = final_cost = 0.0
+        troubled_start_damping, troubled_start, n_troubled, largest_troubled = damping, 0, 0, 0
+        dont_retry = False
+
+        def acceptable(st):
+            rate = st[1] / (st[0] + 1.0)
+            return rate < 0.03 and st[1] < st[2] * 2.0 + 50
+
+        while True:
+            prev_cost = self.linearize(dont_retry)
+            final_cost = prev_cost
+            if it == 0:
+                initial_cost = prev_cost
+            model_red = self.damp_factor_solve(damping)
+            if model_red < 0:  # Optimizer.cpp:835-854 (see vb_optimize)
+                damping *= s.damping_adjust_on_fail
+            e.backup()
+            ratios = self.apply_step(0)
+            new_cost, st = self.cost(True)
+            cost_red = prev_cost - new_cost
+            ratio_red_to_cost = cost_red / new_cost
+            ratio_red_to_exp = cost_red / model_red
+            applied = 1.0
+            ok_rate = acceptable(st)
+            if s.max_step_factor_attempts > 0 and (ratio_red_to_exp < s.min_relative_cost_reduction or not ok_rate):
+                back_red = self.gradient_dot_step(dont_retry)
+                sf = model_red / (model_red + back_red) if back_red > 0 else s.step_factor_decrease
+                for _ in range(s.max_step_factor_attempts):
+                    applied *= sf
+                    e.scale_step(sf)
+                    e.restore()
+                    self.apply_step(0)
+                    cost_f, st_f = self.cost(True)
+                    red_f = prev_cost - new_cost  # Optimizer.cpp:935
+                    r_f = red_f / (model_red * applied)
+                    if r_f >= s.min_relative_cost_reduction and acceptable(st_f):
+                        new_cost, st, cost_red, ratio_red_to_exp, ok_rate = cost_f, st_f, red_f, r_f, True
+                        break
+                    if s.try_sub_step:
+                        self.gradient_dot_step(dont_retry)
+                        self.solve_with_new_gradient()
+                        self.apply_step(1)
+                        cost_s, st_s = self.cost(True)
+                        red_s = prev_cost - cost_s
+                        r_s = red_s / (model_red * applied)
+                        if r_s >= s.min_relative_cost_reduction and acceptable(st_s):
+                            new_cost, st, cost_red, ratio_red_to_exp, ok_rate = cost_s, st_s, red_s, r_s, True
+                            break
+                    dont_retry = True
+                    sf = s.step_factor_decrease
+            tol = (ratio_red_to_cost < s.relative_cost_tolerance or cost_red < s.absolute_cost_tolerance
+                   or ratios[1] < s.variables_tolerance)
+            if new_cost > prev_cost or not ok_rate:
+                if last_troubled != it - 1:
+                    troubled_start_damping, troubled_start = damping, it
+                damping *= s.damping_adjust_on_fail
+                e.restore()
+                if damping > s.damping_max:
+                    break
+                last_troubled = it
+            else:
+                if last_troubled == it - 1 and troubled_start_damping < 1e1 and damping > 1e-3:
+                    n_troubled += 1
+                    largest_troubled = max(largest_troubled, it - troubled_start)
+                if ratio_red_to_exp >= s.min_relative_cost_reduction and applied > s.min_step_factor_for_good:
+                    damping = max(damping * s.damping_adjust_on_good_step, s.damping_min)
+                else:
+                    damping *= s.damping_adjust_on_average_step
+                final_cost = new_cost
+            it += 1
+            if not tol:
+                last_impr = it
+            if it >= last_impr + s.stop_if_no_improvement_for and it >= last_troubled + s.distance_from_troubled_iteration:
+                break
+            if it >= s.max_num_iterations:
+                break
+        out = Summary()
+        out.initial_cost, out.final_cost = initial_cost, final_cost
+        out.num_troubled_seqs, out.largest_troubled_seq, out.num_iterations = n_troubled, largest_troubled, it
+        return out
+
+
+# ------------------------------------------------------------------ shard boundaries
+def landmark_order(p):
+    """Landmark order of vb_finalize (api.hip): registered points by earliest observing rig, ties by
+    handle.  Returns (point handles in order, observations per landmark)."""
+    fv = p.fvars[0]
+    pts, poses = fv[:, 0].astype(np.int64), fv[:, 1].astype(np.int64)
+    keep = p.const[0][pts] == 0
+    pts, poses = pts[keep], poses[keep]
+    n = len(p.const[0])
+    first = np.full(n, np.iinfo(np.int64).max)
+    np.minimum.at(first, pts, poses)
+    cnt = np.bincount(pts, minlength=n)
+    handles = np.flatnonzero(cnt > 0)
+    order = handles[np.argsort(first[handles], kind="stable")]
+    return order, cnt[order]
+
+
+def shard_bounds(p, world: int):
+    """Contiguous landmark ranges balanced by observation count."""
+    _, cnt = landmark_order(p)
+    cum = np.concatenate([[0], np.cumsum(cnt)])
+    cuts = [0] + [int(np.searchsorted(cum, cum[-1] * k / world)) for k in range(1, world)] + [len(cnt)]
+    return [(cuts[r], cuts[r + 1]) for r in range(world)]
+
+
+# ------------------------------------------------------------------ bench entry (N > 1)
+def run_sharded(args, rank: int, world: int, local: int):
+    import json
+    import sys
+
+    import torch
+    import torch.distributed as dist
+
+    from . import synth
+    from .engine import HipEngine
+
+    def log(*a):
+        if rank == 0:
+            print(*a, file=sys.stderr, flush=True)
+
+    # test-only overrides (a 1-GPU box): VIBA_DIST_BACKEND=gloo, VIBA_DIST_SAME_DEVICE=1
+    backend = os.environ.get("VIBA_DIST_BACKEND", "nccl")
+    if os.environ.get("VIBA_DIST_SAME_DEVICE") == "1":
+        local = 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(backend)
+    p = synth.generate(synth.config(args.config))
+    lb, le = shard_bounds(p, world)[rank]
+    e = HipEngine(imu_calib_options=p.imu_calib_options, device=local)
+    e.set_landmark_shard(lb, le, rank == 0)
+    synth.load_into(e, p)
+    st = e.problem_stats()
+    log(f"[bench] {world} ranks, config {args.config}: {p.summary()}; rank 0 landmarks [{lb}, {le}), "
+        f"Schur entries lm {st[8]} obs {st[9]}")
+    comm = ShardComm(rank, world, dev)
+    opt = ShardedOptimizer(e, comm)
+
+    def settings(n):
+        return Settings.default(max_num_iterations=n, stop_if_no_improvement_for=10**6,
+                                distance_from_troubled_iteration=0)
+    if args.warmup:
+        opt.optimize(settings(args.warmup))
+    e.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    s = opt.optimize(settings(args.steps))
+    e.synchronize()
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = t.item()
+    iters = s.num_iterations
+    if rank == 0:
+        out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
+               "unit": "LM iterations/s", "n_gpus": world, "steps": iters, "warmup": args.warmup,
+               "ms_per_step": elapsed * 1e3 / max(1, iters), "higher_is_better": True, "scaling": "strong",
+               "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
+               "config": {"workload": f"config {args.config}: {st[0]} obs, {p.num_points} landmarks, "
+                                      f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",
+                          "parallelism": f"landmark shards x{world}, RCCL band reduce to rank 0"},
+               "roofline": None, "cpu_baseline": None,
+               "cost": [s.initial_cost, s.final_cost]}
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()

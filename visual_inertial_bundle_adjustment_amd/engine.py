@@ -183,6 +183,52 @@ class CEngineBase:
             self.h, which, kind, out.ctypes.data_as(_dp)))
         return out
 
+    # ---------------------------------------------------------------- landmark shards (multi-device)
+    def set_landmark_shard(self, lm_begin: int, lm_end: int, is_root: bool):
+        self._check(self._fn("set_landmark_shard", [C.c_int64, C.c_int64, C.c_int])(
+            self.h, lm_begin, lm_end, int(is_root)))
+
+    def num_params(self) -> int:
+        return self._fn("num_params", [], C.c_int64)(self.h)
+
+    def apply_step_raw(self, which=0):
+        r = (C.c_double * 3)()
+        self._check(self._fn("apply_step_raw", [C.c_int, C.c_double * 3])(self.h, which, r))
+        return tuple(r)
+
+    def assemble_reduced(self, lam: float):
+        self._check(self._fn("assemble_reduced", [C.c_double])(self.h, lam))
+
+    def factor_solve_reduced(self):
+        self._check(self._fn("factor_solve_reduced", [])(self.h))
+
+    def solve_reduced(self):
+        self._check(self._fn("solve_reduced", [])(self.h))
+
+    def assemble_new_rhs(self):
+        self._check(self._fn("assemble_new_rhs", [])(self.h))
+
+    def back_substitute(self, which=0) -> float:
+        m = C.c_double()
+        self._check(self._fn("back_substitute_which", [C.c_int, _dp])(self.h, which, C.byref(m)))
+        return m.value
+
+    def reduced_buffers(self):
+        """(matrix ptr, matrix len, rhs ptr, rhs len) in doubles: device pointers for the HIP
+        engine, host pointers for the oracle."""
+        m, r = P(), P()
+        nm, nr = C.c_int64(), C.c_int64()
+        self._check(self._fn("reduced_buffers", [C.POINTER(P), C.POINTER(C.c_int64), C.POINTER(P),
+                                                 C.POINTER(C.c_int64)])(
+            self.h, C.byref(m), C.byref(nm), C.byref(r), C.byref(nr)))
+        return m.value, nm.value, r.value, nr.value
+
+    def shard_tile_range(self):
+        a, n = C.c_int64(), C.c_int64()
+        self._check(self._fn("shard_tile_range", [C.POINTER(C.c_int64), C.POINTER(C.c_int64)])(
+            self.h, C.byref(a), C.byref(n)))
+        return a.value, n.value
+
     def get_gradient(self, kind: int) -> np.ndarray:
         out = np.zeros((self.nvars[kind], VAR_MAX_TANGENT[kind]))
         self._check(self._fn("get_gradient", [C.c_int, _dp])(self.h, kind,
