@@ -43,6 +43,18 @@ def visual_bytes_per_launch(p, nobs: int) -> float:
     return nobs * per_obs + shared
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this round
+    (profiles/pmc_summary.json, written by scripts/pmc_summary.py from separate FETCH_SIZE /
+    WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            return json.load(f)[kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(full_kf: int, sample_kf: int = 1000):
     """Oracle (single-threaded CPU restatement) on a time slice of the same workload; one LM iteration,
     extrapolated linearly to the full problem (all phases are linear in #rigs at fixed band)."""
@@ -119,22 +131,24 @@ def main():
         f"last it: lin {ph.linearize_ms:.2f} schur {ph.schur_ms:.2f} factor {ph.factor_ms:.2f} "
         f"solve {ph.solve_ms:.2f} step {ph.step_ms:.2f} cost {ph.cost_ms:.2f} ms")
 
-    # roofline of the profiled kernel family
+    # roofline of the profiled kernel family (average launch duration from HIP events on the engine
+    # stream, algorithmic work from the symbolic structure)
     avg_ms = kms / max(1, launches)
     if args.profile_family == KF_GEMM:
-        flops = st[6] * 2.0 * 64 ** 3  # per factorization = one launch sequence; per launch below
-        per_launch = flops / max(1, st[4])
+        # st[6] tile pairs per factorization, st[10] update launches per factorization
+        per_launch = st[6] * 2.0 * 64 ** 3 / max(1, st[10])
         achieved = per_launch / (avg_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
-                "kernel": "gemm_update_kernel (tile syrk/gemm, v_mfma_f64_16x16x4_f64)",
-                "avg_launch_ms": avg_ms, "launches": launches}
+                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": pmc_traffic("update_kernel"),
+                "kernel": "update_kernel (tile syrk/gemm on v_mfma_f64_16x16x4_f64, + fused next-diagonal potrf)",
+                "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches}
     else:
         b = visual_bytes_per_launch(p, st[0])
         achieved = b / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                "kernel": "visual_lin_kernel (Jacobian fill)", "avg_launch_ms": avg_ms, "launches": launches}
+                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("visual_lin_kernel"),
+                "kernel": "visual_lin_kernel (Jacobian fill)", "bytes_per_launch": b, "avg_launch_ms": avg_ms,
+                "launches": launches}
     cpu = None
     if not args.no_cpu_baseline:
         try:

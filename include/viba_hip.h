@@ -296,9 +296,10 @@ void* vb_stream(vb_handle h);
  *  back-substitution, 8 visual cost, 9 small factors, 10 tile trsm; -1 disables); vb_kernel_time returns launches and summed device milliseconds since enabling */
 int vb_profile_kernel(vb_handle h, int family);
 int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
-/* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs, nSmallFactors,
- *  Schur landmark-pair entries, Schur observation-pair entries] */
-int vb_problem_stats(vb_handle h, int64_t* out10);
+/* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs (per factorization),
+ *  nSmallFactors, Schur landmark-pair entries, Schur observation-pair entries,
+ *  update launches per factorization, trsm launches per factorization] */
+int vb_problem_stats(vb_handle h, int64_t* out12);
 
 #ifdef __cplusplus
 }

@@ -41,6 +41,9 @@ void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, h
 }  // namespace viba
 
 using namespace viba;
+namespace viba {
+ProfSlot g_prof;
+}
 
 namespace {
 
@@ -392,12 +395,12 @@ inline void profBegin(vb_handle h, int fam) {
       h->profEv.push_back(e);
     }
   }
-  (void)hipEventRecord(h->profEv[h->profUsed], h->st);
+  g_prof.start = h->profEv[h->profUsed], g_prof.stop = h->profEv[h->profUsed + 1], g_prof.consumed = false;
 }
 inline void profEnd(vb_handle h, int fam) {
   if (h->profFamily != fam) return;
-  (void)hipEventRecord(h->profEv[h->profUsed + 1], h->st);
-  h->profUsed += 2;
+  if (g_prof.consumed) h->profUsed += 2;  // the wrapper launched the family's kernel with the events
+  g_prof = ProfSlot();
 }
 // harvest recorded pairs (call after a stream synchronisation)
 void profHarvest(vb_handle h) {
@@ -988,6 +991,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   vb_handle h = new vb_handle_s();
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_FUSE_POTRF")) h->noFusePotrf = e[0] == '1';
+  if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
   HIPCHK(hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking));
   for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
   *out = h;
@@ -1304,7 +1308,7 @@ int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms) {
   if (total_ms) *total_ms = h->profMs;
   return 0;
 }
-int vb_problem_stats(vb_handle h, int64_t* out) {
+int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
   if (!h || !h->finalized || !out) return fail(VB_E_STATE, "not finalized");
   const Dev& d = h->d;
   out[0] = d.nObs, out[1] = d.nPts, out[2] = d.nRV, out[3] = d.nRed, out[4] = d.nT, out[5] = d.nTiles;
@@ -1314,6 +1318,13 @@ int vb_problem_stats(vb_handle h, int64_t* out) {
   out[7] = sm;
   // Schur work-list sizes: landmark-pair entries, observation-pair entries
   out[8] = h->nLmEnt, out[9] = h->nObEnt;
+  // launches per factorization: tile GEMM update, trsm
+  int64_t nu = 0, nt = 0;
+  for (int32_t J = 0; J < d.nT; J++) {
+    nu += h->pairStart[J + 1] > h->pairStart[J];
+    nt += h->colStart[J + 1] - h->colStart[J] > 1;
+  }
+  out[10] = nu, out[11] = nt;
   return 0;
 }
 

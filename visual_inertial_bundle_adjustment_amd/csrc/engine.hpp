@@ -7,6 +7,7 @@
 //   landmarks      per point: Vchol[6], gp[3], z[3], xp[3]; Y panel 3 x d_l at Y + lmY[l]
 //   reduced system dense T x T column-major tiles (envelope / tile-sparse), tileIdx[I*nT+J]
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstddef>
@@ -128,5 +129,24 @@ struct Dev {
   LossParams reproj, imu;
   ImuIdx jac;
 };
+
+// Kernel-family timing (vb_profile_kernel): the host arms an event pair before the launch wrapper of
+// the profiled family; the wrapper's main kernel is then launched with hipExtLaunchKernelGGL, whose
+// events timestamp that kernel's own execution (no dispatch gap), and disarms it.
+struct ProfSlot {
+  hipEvent_t start = nullptr, stop = nullptr;
+  bool consumed = false;
+};
+extern ProfSlot g_prof;
+
+template <typename K, typename... Args>
+inline void launchK(K kernel, dim3 grid, dim3 block, uint32_t shmem, hipStream_t st, Args... args) {
+  if (g_prof.start && !g_prof.consumed) {
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, g_prof.start, g_prof.stop, 0, args...);
+    g_prof.consumed = true;
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, shmem, st, args...);
+  }
+}
 
 }  // namespace viba

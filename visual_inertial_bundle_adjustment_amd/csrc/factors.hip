@@ -703,13 +703,13 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
   const int64_t n = hi - lo;
-  hipLaunchKernelGGL(visual_lin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, updateCache,
-                     dontRetry, lo, hi);
+  launchK(visual_lin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, updateCache, dontRetry, lo,
+          hi);
 }
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
   const int64_t n = hi - lo;
-  hipLaunchKernelGGL(visual_cost_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, comparable,
+  launchK(visual_cost_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, comparable,
                      lo, hi);
 }
 

@@ -771,13 +771,13 @@ void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hip
 
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi > lo)
-    hipLaunchKernelGGL(landmark_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, lambda, mode, lo, hi);
+    launchK(landmark_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, lambda, mode, lo, hi);
 }
 // S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry)
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
   if (d.nItemsLm)
-    hipLaunchKernelGGL(schur_items_kernel, dim3(blocks(d.nItemsLm, 4)), dim3(256), 0, st, d, lambda, (int64_t)0, d.nItemsLm);
+    launchK(schur_items_kernel, dim3(blocks(d.nItemsLm, 4)), dim3(256), 0, st, d, lambda, (int64_t)0, d.nItemsLm);
   if (d.nItems > d.nItemsLm)
     hipLaunchKernelGGL(schur_items_kernel, dim3(blocks(d.nItems - d.nItemsLm, 4)), dim3(256), 0, st, d, lambda,
                        d.nItemsLm, d.nItems);
@@ -787,15 +787,15 @@ void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
   if (d.nRV) hipLaunchKernelGGL(reduced_grad_kernel, dim3(d.nRV), dim3(256), 0, st, d, mode);
 }
 void launch_potrf(const Dev& d, const int32_t* colTiles, double* dinv, hipStream_t st) {
-  hipLaunchKernelGGL(potrf_kernel, dim3(1), dim3(64), 0, st, d, colTiles, dinv);
+  launchK(potrf_kernel, dim3(1), dim3(64), 0, st, d, colTiles, dinv);
 }
 void launch_trsm(const Dev& d, const int32_t* colTiles, int n, const double* dinv, hipStream_t st) {
-  if (n > 1) hipLaunchKernelGGL(trsm_kernel, dim3(n - 1), dim3(256), 0, st, d, colTiles, dinv);
+  if (n > 1) launchK(trsm_kernel, dim3(n - 1), dim3(256), 0, st, d, colTiles, dinv);
 }
 void launch_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets, int npairs,
                    int fuseDiag, double* dinvNext, hipStream_t st) {
   if (npairs > 0)
-    hipLaunchKernelGGL(update_kernel, dim3(npairs), dim3(256), 0, st, d, colTiles, pairs, targets, fuseDiag,
+    launchK(update_kernel, dim3(npairs), dim3(256), 0, st, d, colTiles, pairs, targets, fuseDiag,
                        dinvNext);
 }
 void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st) {
@@ -811,15 +811,15 @@ void launch_pad_diag(const Dev& d, hipStream_t st) {
 }
 void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
                 double* b, double* x, hipStream_t st) {
-  hipLaunchKernelGGL(fwd_kernel, dim3(n), dim3(64), 0, st, d, colTiles, tileRow, n, linvJ, b, x, d.nRed);
+  launchK(fwd_kernel, dim3(n), dim3(64), 0, st, d, colTiles, tileRow, n, linvJ, b, x, d.nRed);
 }
 void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
                 double* t, double* x, hipStream_t st) {
-  hipLaunchKernelGGL(bwd_kernel, dim3(n + 1), dim3(64), 0, st, d, J, rowTiles, rowCol, n, linvJ, t, x, d.nRed);
+  launchK(bwd_kernel, dim3(n + 1), dim3(64), 0, st, d, J, rowTiles, rowCol, n, linvJ, t, x, d.nRed);
 }
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st) {
   if (hi > lo)
-    hipLaunchKernelGGL(backsub_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, mode, lo, hi, xr, xp);
+    launchK(backsub_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, mode, lo, hi, xr, xp);
 }
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t st) {
   if (n > 0)

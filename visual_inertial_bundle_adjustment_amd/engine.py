@@ -304,8 +304,8 @@ class HipEngine(CEngineBase):
         return n.value, ms.value
 
     def problem_stats(self):
-        out = (C.c_int64 * 10)()
-        self._check(self._fn("problem_stats", [C.c_int64 * 10])(self.h, out))
+        out = (C.c_int64 * 12)()
+        self._check(self._fn("problem_stats", [C.c_int64 * 12])(self.h, out))
         return list(out)
 
     def synchronize(self):
