@@ -300,6 +300,9 @@ int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
  *  nSmallFactors, Schur landmark-pair entries, Schur observation-pair entries,
  *  update launches per factorization, trsm launches per factorization] */
 int vb_problem_stats(vb_handle h, int64_t* out12);
+/* tuning aid: average kernel time [us] of one factorization kernel on scratch tiles
+ * (which: 0 potrf, 1 trsm, 2 update + fused next-diagonal potrf, 3 update) */
+int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us);
 
 #ifdef __cplusplus
 }

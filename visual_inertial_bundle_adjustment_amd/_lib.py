@@ -4,7 +4,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_DIR = os.environ.get("VIBA_LIB_DIR", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib"))
 HIP_LIB = os.path.join(LIB_DIR, "libviba_hip.so")
 SYNTH_LIB = os.path.join(LIB_DIR, "libviba_synth.so")
 

@@ -1536,3 +1536,62 @@ int vb_assemble_new_rhs(vb_handle h) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- kernel micro-benchmark (tuning aid)
+// Times one launch of a factorization kernel on scratch tiles (random SPD diagonal tile, random
+// off-diagonal tiles), averaged over `iters` launches, kernel-exact (hipExtLaunchKernelGGL events).
+// which: 0 standalone potrf, 1 trsm (one tile), 2 update with fused next-diagonal potrf (one pair),
+// 3 update (one pair, no fusion)
+extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us) {
+  if (!h || !h->finalized || iters <= 0) return fail(VB_E_STATE, "vb_bench_kernel needs a finalized handle");
+  Dev d = h->d;  // copy: tiles / err redirected to scratch
+  std::vector<double> A(TS * TS), B(TS * TS);
+  uint64_t sd = 12345;
+  auto rnd = [&] { sd = sd * 6364136223846793005ULL + 1442695040888963407ULL; return ((sd >> 11) * 0x1.0p-53) - 0.5; };
+  std::vector<double> M(TS * TS);
+  for (auto& v : M) v = rnd();
+  for (int i = 0; i < TS; i++)
+    for (int j = 0; j < TS; j++) {
+      double s = (i == j) ? TS : 0.0;
+      for (int k = 0; k < TS; k++) s += M[i * TS + k] * M[j * TS + k];
+      A[j * TS + i] = s;
+    }
+  for (auto& v : B) v = rnd();
+  double *tiles = nullptr, *dinv = nullptr;
+  int32_t *colT = nullptr, *pairs = nullptr, *targ = nullptr;
+  HIPCHK(hipMalloc(&tiles, 4 * TS * TS * sizeof(double)));
+  HIPCHK(hipMalloc(&dinv, 2 * 1024 * sizeof(double)));
+  HIPCHK(hipMalloc(&colT, 4 * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&pairs, 2 * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&targ, sizeof(int32_t)));
+  const int32_t ct[4] = {0, 1, 2, 3}, pr[2] = {1, 1}, tg[1] = {2};
+  HIPCHK(hipMemcpy(colT, ct, sizeof(ct), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pairs, pr, sizeof(pr), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(targ, tg, sizeof(tg), hipMemcpyHostToDevice));
+  d.tiles = tiles;
+  hipEvent_t e0, e1;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  double total = 0;
+  const size_t tb = TS * TS * sizeof(double);
+  for (int it = 0; it < iters + 1; it++) {
+    // tile 0: SPD (factored first for trsm/update), tile 1: off-diagonal, tile 2: SPD target
+    HIPCHK(hipMemcpyAsync(tiles, A.data(), tb, hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(tiles + TS * TS, B.data(), tb, hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipMemcpyAsync(tiles + 2 * TS * TS, A.data(), tb, hipMemcpyHostToDevice, h->st));
+    if (which != 0) launch_potrf(d, colT, dinv, h->st);
+    g_prof.start = e0, g_prof.stop = e1, g_prof.consumed = false;
+    if (which == 0) launch_potrf(d, colT, dinv, h->st);
+    else if (which == 1) launch_trsm(d, colT, 2, dinv, h->st);
+    else launch_update(d, colT, pairs, targ, 1, which == 2 ? 1 : 0, dinv + 1024, h->st);
+    g_prof = ProfSlot();
+    HIPCHK(hipStreamSynchronize(h->st));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    if (it > 0) total += ms;  // first launch: warm-up
+  }
+  hipEventDestroy(e0), hipEventDestroy(e1);
+  hipFree(tiles), hipFree(dinv), hipFree(colT), hipFree(pairs), hipFree(targ);
+  if (avg_us) *avg_us = total * 1e3 / iters;
+  return 0;
+}

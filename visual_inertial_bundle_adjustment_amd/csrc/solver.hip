@@ -289,19 +289,13 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
 }
 
-// 16 x 16 Cholesky, lane r holds row r in s[0..16) (lanes >= 16 compute garbage, ignored):
-// right-looking, column C broadcast from lanes by readlane.
-template <int C, int J>
-struct Upd16 {
-  static __device__ __forceinline__ void run(double (&s)[16], double lc) {
-    s[J] -= lc * readlane_d(lc, J);
-    Upd16<C, J + 1>::run(s, lc);
-  }
-};
-template <int C>
-struct Upd16<C, 16> {
-  static __device__ __forceinline__ void run(double (&)[16], double) {}
-};
+// Broadcast lane J of each 16-lane row to the whole row: one v_mov_b64_dpp row_newbcast:J
+// (the 16 x 16 diagonal blocks live in lanes 0..15, one row / column per lane)
+template <int J>
+__device__ __forceinline__ double rowbcast(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xF, 0xF, true);
+}
+
 // 1 / sqrt(x): v_rsq_f64 + two Newton steps (~1 ulp; the IEEE sqrt + divide sequences are ~40
 // dependent instructions on the factorization's serial chain)
 __device__ __forceinline__ double rsqrt_nr(double x) {
@@ -310,47 +304,59 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
   y = y * (1.5 - 0.5 * x * y * y);
   return y;
 }
+
+// 16 x 16 Cholesky, lane r holds row r in s[0..16) (lanes >= 16 compute garbage, ignored):
+// right-looking; step C broadcasts the pivot and the scaled column by DPP.
+template <int C, int J>
+struct Upd16 {
+  static __device__ __forceinline__ void run(double (&s)[16], double lc) {
+    s[J] -= lc * rowbcast<J>(lc);
+    Upd16<C, J + 1>::run(s, lc);
+  }
+};
+template <int C>
+struct Upd16<C, 16> {
+  static __device__ __forceinline__ void run(double (&)[16], double) {}
+};
+// Row C of X = L^-1 (lane c holds column c of X in x[]), left-looking, once row C of L is complete:
+// X[C][c] = (delta_Cc - sum_{k<C} L[C][k] X[k][c]) / L[C][C], L[C][k] = s[k] of lane C (DPP)
+template <int C, int K>
+struct InvRow16 {
+  static __device__ __forceinline__ void run(double& a0, double& a1, const double (&x)[16], const double (&s)[16]) {
+    // opaque copy: rowbcast<C>(s[K]) equals step K's rowbcast<C>(l_K); letting the compiler reuse
+    // that value keeps ~120 broadcasts live across the steps and spills them
+    double sk = s[K];
+    asm volatile("" : "+v"(sk));
+    if constexpr (K % 2 == 0) a0 -= rowbcast<C>(sk) * x[K];
+    else a1 -= rowbcast<C>(sk) * x[K];
+    InvRow16<C, K + 1>::run(a0, a1, x, s);
+  }
+};
+template <int C>
+struct InvRow16<C, C> {
+  static __device__ __forceinline__ void run(double&, double&, const double (&)[16], const double (&)[16]) {}
+};
+// Step C: pivot, column C of L, rank-1 update of the trailing columns (right-looking), then row C
+// of L^-1 (left-looking) -- two independent dependency chains the scheduler interleaves.
 template <int C>
 struct Chol16 {
-  static __device__ __forceinline__ void run(double (&s)[16], double (&rd)[16], int lane, bool& bad) {
-    const double piv = readlane_d(s[C], C);
+  static __device__ __forceinline__ void run(double (&s)[16], double (&x)[16], int lane, bool& bad) {
+    const double piv = rowbcast<C>(s[C]);
     bad |= !(piv > 0.0);
     const double y = rsqrt_nr(piv);
-    rd[C] = y;
-    const double lc = (lane == C) ? piv * y : s[C] * y;
+    const double lc = ((lane & 15) == C) ? piv * y : s[C] * y;
     s[C] = lc;
     Upd16<C, C + 1>::run(s, lc);
-    Chol16<C + 1>::run(s, rd, lane, bad);
+    double a0 = ((lane & 15) == C) ? 1.0 : 0.0, a1 = 0.0;
+    InvRow16<C, 0>::run(a0, a1, x, s);
+    x[C] = (a0 + a1) * y;
+    __builtin_amdgcn_sched_barrier(0);  // keep each step's broadcasts in its step (register pressure)
+    Chol16<C + 1>::run(s, x, lane, bad);
   }
 };
 template <>
 struct Chol16<16> {
   static __device__ __forceinline__ void run(double (&)[16], double (&)[16], int, bool&) {}
-};
-// x = column `lane` of L^-1 (L rows in s[] of lanes 0..15, rd = 1 / diag): right-looking forward
-// substitution
-template <int I, int J>
-struct InvUpd16 {
-  static __device__ __forceinline__ void run(double (&x)[16], const double (&s)[16]) {
-    x[J] -= readlane_d(s[I], J) * x[I];
-    InvUpd16<I, J + 1>::run(x, s);
-  }
-};
-template <int I>
-struct InvUpd16<I, 16> {
-  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16]) {}
-};
-template <int I>
-struct Inv16 {
-  static __device__ __forceinline__ void run(double (&x)[16], const double (&s)[16], const double (&rd)[16]) {
-    x[I] *= rd[I];
-    InvUpd16<I, I + 1>::run(x, s);
-    Inv16<I + 1>::run(x, s, rd);
-  }
-};
-template <>
-struct Inv16<16> {
-  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16], const double (&)[16]) {}
 };
 
 // Row block `w` (16 rows) of X = A L^-T, X overwriting A (both column-major TS x TS; A/L may be LDS or
@@ -375,30 +381,30 @@ __device__ __forceinline__ void trsm_rowblock(double* A, const double* L, const 
   }
 }
 
+#ifdef VIBA_POTRF_TIMING
+__device__ long long g_potrf_t[32];
+#define POTRF_T(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_potrf_t[k] = (long long)__builtin_readcyclecounter(); } while (0)
+#else
+#define POTRF_T(k) do {} while (0)
+#endif
+
 // Factor + invert the 16 x 16 diagonal block i of T (LDS) given S (its updated value, D layout):
-// writes L_ii into T and Dinv_i into dinvS (LDS) and dinvG (global, may be null).
-__device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS, double* dinvG, int i,
-                                       double4_t S, int lane, bool& bad) {
+// writes L_ii into T and Dinv_i into dinvS (LDS)
+__device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS, int i, double4_t S, int lane,
+                                       bool& bad) {
   const int lr = lane & 15, lq = lane >> 4;
 #pragma unroll
   for (int r = 0; r < 4; r++) scratch[(lq + 4 * r) * 16 + lr] = S[r];  // row-major S[i'][j']
   __builtin_amdgcn_wave_barrier();
-  double s[16], x[16], rd[16];
+  double s[16], x[16];
 #pragma unroll
   for (int c = 0; c < 16; c++) s[c] = scratch[lr * 16 + c];
-  Chol16<0>::run(s, rd, lane, bad);
-#pragma unroll
-  for (int c = 0; c < 16; c++) x[c] = (c == lane) ? 1.0 : 0.0;
-  Inv16<0>::run(x, s, rd);
+  Chol16<0>::run(s, x, lane, bad);
   if (lane < 16) {
 #pragma unroll
     for (int c = 0; c < 16; c++) T[(16 * i + c) * TS + 16 * i + lane] = (c <= lane) ? s[c] : 0.0;
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const double v = (r >= lane) ? x[r] : 0.0;
-      dinvS[i * 256 + lane * 16 + r] = v;
-      if (dinvG) dinvG[i * 256 + lane * 16 + r] = v;
-    }
+    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = (r >= lane) ? x[r] : 0.0;
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -407,11 +413,12 @@ __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS
 // L_ik (k < i) by trsm_rowblock, then S = A_ii - sum_k L_ik L_ik^T and its 16 x 16 factor/inverse.
 template <int I>
 struct PotrfRow {
-  static __device__ __forceinline__ void run(double* T, double* scratch, double* dinvS, double* dinvG, int lane,
-                                             bool& bad) {
+  static __device__ __forceinline__ void run(double* T, double* scratch, double* dinvS, int lane, bool& bad) {
     const int lr = lane & 15, lq = lane >> 4;
     double4_t Lt[4];
+    POTRF_T(4 * I + 0);
     trsm_rowblock<I>(T, T, dinvS, I, lane, Lt);
+    POTRF_T(4 * I + 1);
     double4_t S;
 #pragma unroll
     for (int r = 0; r < 4; r++) S[r] = T[(16 * I + lr) * TS + 16 * I + lq + 4 * r];  // lower part valid
@@ -424,20 +431,31 @@ struct PotrfRow {
 #pragma unroll
       for (int r = 0; r < 4; r++) T[(16 * k + lq + 4 * r) * TS + 16 * I + lr] = Lt[k][r];
     __builtin_amdgcn_wave_barrier();
-    diag16(T, scratch, dinvS, dinvG, I, S, lane, bad);
-    PotrfRow<I + 1>::run(T, scratch, dinvS, dinvG, lane, bad);
+    POTRF_T(4 * I + 2);
+    diag16(T, scratch, dinvS, I, S, lane, bad);
+    POTRF_T(4 * I + 3);
+    PotrfRow<I + 1>::run(T, scratch, dinvS, lane, bad);
   }
 };
 template <>
 struct PotrfRow<4> {
-  static __device__ __forceinline__ void run(double*, double*, double*, double*, int, bool&) {}
+  static __device__ __forceinline__ void run(double*, double*, double*, int, bool&) {}
 };
 
-__device__ __forceinline__ void potrf_blocked(double* T, double* scratch, double* dinvS, double* dinvG, int lane,
-                                              int32_t* err) {
+// one wave; on return T holds L (upper part zero) and dinvS the four 16 x 16 diagonal inverses
+__device__ __forceinline__ void potrf_blocked(double* T, double* scratch, double* dinvS, int lane, int32_t* err) {
   bool bad = false;
-  PotrfRow<0>::run(T, scratch, dinvS, dinvG, lane, bad);
+  PotrfRow<0>::run(T, scratch, dinvS, lane, bad);
   if (bad && lane == 0) atomicOr(err, 8);
+}
+
+// copy n doubles LDS -> global with `nthreads` threads (pointer-stepped, bounded unroll: keeps the
+// compiler from materialising every address up front)
+__device__ __forceinline__ void lds_to_global(double* dst, const double* src, int n, int tid, int nthreads) {
+  double* p = dst + tid;
+  const double* q = src + tid;
+#pragma unroll 8
+  for (int i = tid; i < n; i += nthreads, p += nthreads, q += nthreads) *p = *q;
 }
 
 // factor the diagonal tile of column J in place (+ its 16 x 16 block inverses); one wave
@@ -446,6 +464,7 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* colTile
   __shared__ double scratch[256];
   __shared__ double dinvS[1024];
   const int lane = threadIdx.x;
+  POTRF_T(19);
   double* A = d.tiles + (int64_t)colTiles[0] * TS * TS;
   {
     double v[TS];
@@ -455,9 +474,12 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* colTile
     for (int c = 0; c < TS; c++) T[c * TS + lane] = v[c];
   }
   __builtin_amdgcn_wave_barrier();
-  potrf_blocked(T, scratch, dinvS, dinvG, lane, d.err);
-#pragma unroll
-  for (int c = 0; c < TS; c++) A[c * TS + lane] = T[c * TS + lane];
+  POTRF_T(16);
+  potrf_blocked(T, scratch, dinvS, lane, d.err);
+  POTRF_T(17);
+  lds_to_global(A, T, TS * TS, lane, 64);
+  lds_to_global(dinvG, dinvS, 1024, lane, 64);
+  POTRF_T(18);
 }
 
 // X = A L_JJ^-T for tile q = blockIdx.x + 1 of the column; wave w = 16-row block (all on MFMA)
@@ -531,9 +553,10 @@ __global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* colTi
       }
   if (!fuse) return;
   __syncthreads();
-  if (wave == 0) potrf_blocked(T, scratch, dinvS, dinvNext, lane, d.err);
+  if (wave == 0) potrf_blocked(T, scratch, dinvS, lane, d.err);
   __syncthreads();
-  for (int i = tid; i < TS * TS; i += 256) C[i] = T[i];
+  lds_to_global(C, T, TS * TS, tid, 256);
+  lds_to_global(dinvNext, dinvS, 1024, tid, 256);
 }
 
 // Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
@@ -837,3 +860,9 @@ void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, h
 }
 
 }  // namespace viba
+
+#ifdef VIBA_POTRF_TIMING
+extern "C" int vb_debug_potrf_times(long long* out32) {
+  return hipMemcpyFromSymbol(out32, HIP_SYMBOL(viba::g_potrf_t), 32 * sizeof(long long)) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -308,6 +308,11 @@ class HipEngine(CEngineBase):
         self._check(self._fn("problem_stats", [C.c_int64 * 12])(self.h, out))
         return list(out)
 
+    def bench_kernel(self, which: int, iters: int = 200) -> float:
+        us = C.c_double()
+        self._check(self._fn("bench_kernel", [C.c_int, C.c_int, _dp])(self.h, which, iters, C.byref(us)))
+        return us.value
+
     def synchronize(self):
         self.lib.vb_stream.restype = P
         self.lib.vb_stream.argtypes = [P]
