@@ -10,7 +10,6 @@
 #include <cstring>
 #include <numeric>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/viba_hip.h"
@@ -182,156 +181,6 @@ int alloc0(T** dptr, size_t n) {
   return 0;
 }
 
-template <typename F>
-void parallelFor(int64_t n, F&& f) {
-  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)std::max(1u, std::thread::hardware_concurrency()), 16, n / 64 + 1}));
-  if (nt == 1) {
-    f(0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (int t = 0; t < nt; t++) th.emplace_back([&, t] { f(n * t / nt, n * (t + 1) / nt); });
-  for (auto& x : th) x.join();
-}
-
-// Inputs of the Schur work-list build (host arrays of doFinalize)
-struct SchurInputs {
-  int nRV;
-  const int64_t* rvOff;
-  const int32_t* rvDim;
-  const int64_t *lmY, *lmBlk;
-  const int32_t *blkRed, *blkCol, *obRed;
-  const int64_t *oxStart, *lxStart;
-  const int32_t *oxObs, *oxSlot, *lxLm, *lxCol;
-  int64_t lmB, lmE;        // landmark shard
-  int64_t obB, obE;        // observations of the shard's landmarks
-  int64_t obFree;          // first observation of a non-eliminated (constant) point
-  bool root;               // root also owns the observations of constant points
-};
-
-// Schur work list: every coupled block pair (X1, X2) with off(X2) >= off(X1) and its entries
-//   landmark entries: (panel column of X1, panel column of X2) for every landmark seeing both
-//                     (X1 == X2: (panel column, landmark) — the RHS pass needs z_l)
-//   observation entries: (obs, slot1 | slot2 << 8) for every observation with both in its slots
-// Entries of one pair are contiguous and in landmark / observation order; pairs are in (X1, X2)
-// order.  Each pair's lists are split into work items of bounded cost.
-struct SchurLists {
-  std::vector<uint32_t> lmEnt;
-  std::vector<int32_t> obEnt;
-  std::vector<SchurItem> items;
-};
-
-void buildSchurLists(const SchurInputs& in, SchurLists& out) {
-  const int nRV = in.nRV;
-  std::vector<std::vector<int32_t>> part(nRV);
-  std::vector<std::vector<int64_t>> cntL(nRV), cntO(nRV);
-  auto inObs = [&](int64_t o) { return (o >= in.obB && o < in.obE) || (in.root && o >= in.obFree); };
-  auto blockPos = [&](int64_t l, int32_t X) {
-    return std::lower_bound(in.blkRed + in.lmBlk[l], in.blkRed + in.lmBlk[l + 1], X) - in.blkRed;
-  };
-  // visit(X1, onLm(pairSlot, col1, col2, l), onOb(pairSlot, o, s1, s2)) with partners mapped to slots
-  auto visit = [&](int X1, std::vector<int32_t>& slot, std::vector<int32_t>& P, auto&& onLm, auto&& onOb) {
-    auto slotOf = [&](int32_t X2) {
-      if (slot[X2] < 0) slot[X2] = (int32_t)P.size(), P.push_back(X2);
-      return slot[X2];
-    };
-    slotOf(X1);
-    for (int64_t idx = in.lxStart[X1]; idx < in.lxStart[X1 + 1]; idx++) {
-      const int64_t l = in.lxLm[idx];
-      if (l < in.lmB || l >= in.lmE) continue;
-      const int64_t cb = in.lmY[l] / 3;
-      const int64_t c1 = cb + in.lxCol[idx];
-      onLm(slot[X1], c1, l, l, true);
-      for (int64_t b = blockPos(l, X1) + 1; b < in.lmBlk[l + 1]; b++) onLm(slotOf(in.blkRed[b]), c1, cb + in.blkCol[b], l, false);
-    }
-    const int64_t off1 = in.rvOff[X1];
-    for (int64_t idx = in.oxStart[X1]; idx < in.oxStart[X1 + 1]; idx++) {
-      const int64_t o = in.oxObs[idx];
-      if (!inObs(o)) continue;
-      const int s1 = in.oxSlot[idx];
-      onOb(slot[X1], o, s1, s1);
-      for (int s2 = 0; s2 < 4; s2++) {
-        const int32_t X2 = in.obRed[o * 4 + s2];
-        if (X2 < 0 || s2 == s1 || in.rvOff[X2] <= off1) continue;
-        onOb(slotOf(X2), o, s1, s2);
-      }
-    }
-  };
-  // pass 1: partners and counts per X1 (partners sorted by X2 afterwards)
-  std::vector<std::vector<int32_t>> permOf(nRV);
-  parallelFor(nRV, [&](int64_t a, int64_t b) {
-    std::vector<int32_t> slot(nRV, -1);
-    for (int64_t X1 = a; X1 < b; X1++) {
-      std::vector<int32_t> P;
-      std::vector<int64_t> cl, co;
-      visit((int)X1, slot, P,
-            [&](int32_t s, int64_t, int64_t, int64_t, bool) {
-              if ((size_t)s >= cl.size()) cl.resize(s + 1, 0), co.resize(s + 1, 0);
-              cl[s]++;
-            },
-            [&](int32_t s, int64_t, int, int) {
-              if ((size_t)s >= cl.size()) cl.resize(s + 1, 0), co.resize(s + 1, 0);
-              co[s]++;
-            });
-      cl.resize(P.size(), 0), co.resize(P.size(), 0);
-      for (int32_t X2 : P) slot[X2] = -1;
-      std::vector<int32_t> perm(P.size());
-      std::iota(perm.begin(), perm.end(), 0);
-      std::sort(perm.begin(), perm.end(), [&](int32_t x, int32_t y) { return P[x] < P[y]; });
-      part[X1] = P, cntL[X1] = cl, cntO[X1] = co, permOf[X1] = perm;
-    }
-  });
-  // offsets (pairs in (X1, sorted X2) order)
-  std::vector<std::vector<int64_t>> offL(nRV), offO(nRV);
-  int64_t totL = 0, totO = 0;
-  for (int X1 = 0; X1 < nRV; X1++) {
-    offL[X1].resize(part[X1].size()), offO[X1].resize(part[X1].size());
-    for (int32_t s : permOf[X1]) {
-      offL[X1][s] = totL, offO[X1][s] = totO;
-      totL += cntL[X1][s], totO += cntO[X1][s];
-    }
-  }
-  out.lmEnt.assign(2 * totL, 0);
-  out.obEnt.assign(2 * totO, 0);
-  // pass 2: fill (same visiting order as pass 1, so slots coincide)
-  parallelFor(nRV, [&](int64_t a, int64_t b) {
-    std::vector<int32_t> slot(nRV, -1);
-    for (int64_t X1 = a; X1 < b; X1++) {
-      std::vector<int32_t> P;
-      std::vector<int64_t> curL = offL[X1], curO = offO[X1];
-      visit((int)X1, slot, P,
-            [&](int32_t s, int64_t c1, int64_t c2, int64_t l, bool diag) {
-              const int64_t e = curL[s]++;
-              out.lmEnt[2 * e] = (uint32_t)c1;
-              out.lmEnt[2 * e + 1] = (uint32_t)(diag ? l : c2);
-            },
-            [&](int32_t s, int64_t o, int s1, int s2) {
-              const int64_t e = curO[s]++;
-              out.obEnt[2 * e] = (int32_t)o;
-              out.obEnt[2 * e + 1] = s1 | (s2 << 8);
-            });
-      for (int32_t X2 : P) slot[X2] = -1;
-    }
-  });
-  // work items: bounded (entries x 64-entry output chunks)
-  out.items.clear();
-  for (int X1 = 0; X1 < nRV; X1++)
-    for (int32_t s : permOf[X1]) {
-      const int32_t X2 = part[X1][s];
-      const int chunks = (in.rvDim[X1] * in.rvDim[X2] + 63) / 64;
-      const int64_t maxE = std::max<int64_t>(16, 512 / chunks);
-      for (int kind = 0; kind < 2; kind++) {
-        const int64_t n = kind ? cntO[X1][s] : cntL[X1][s];
-        const int64_t o0 = kind ? offO[X1][s] : offL[X1][s];
-        for (int64_t k = 0; k < n; k += maxE) {
-          SchurItem it;
-          it.start = o0 + k, it.count = (int32_t)std::min<int64_t>(maxE, n - k), it.X1 = X1, it.X2 = X2, it.kind = kind;
-          out.items.push_back(it);
-        }
-      }
-    }
-}
-
 }  // namespace
 
 struct vb_handle_s {
@@ -363,7 +212,7 @@ struct vb_handle_s {
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool isRoot = true;
-  int64_t itemTileLo = 0, itemTileHi = -1, tileFirst = 0, tileCount = 0;
+  int64_t tileFirst = 0, tileCount = 0, nTileEnt = 0;
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
   hipGraphExec_t factorGraph = nullptr, solveGraph = nullptr;
   bool useGraphs = true;
@@ -630,38 +479,11 @@ int doFinalize(vb_handle h) {
         lxLm[fl[r]] = (int32_t)l, lxCol[fl[r]] = blkCol[b], fl[r]++;
       }
   }
-  // ---------------- Schur work list of this handle's landmark shard
+  // ---------------- this handle's landmark shard
   if (h->lmEnd < 0) h->lmBegin = 0, h->lmEnd = nPts;
   if (h->lmBegin < 0 || h->lmEnd > nPts || h->lmBegin > h->lmEnd) return fail(VB_E_ARG, "bad landmark shard range");
-  SchurLists sl;
-  {
-    SchurInputs in{nRV, h->rvOff.data(), h->rvDim.data(), lmY.data(), lmBlk.data(), blkRed.data(), blkCol.data(),
-                   obRed.data(), oxStart.data(), lxStart.data(), oxObs.data(), oxSlot.data(), lxLm.data(),
-                   lxCol.data(), h->lmBegin, h->lmEnd, lmObs[h->lmBegin], lmObs[h->lmEnd], lmObs[nPts], h->isRoot};
-    buildSchurLists(in, sl);
-  }
-  // landmark-entry items first, then observation-entry items (launched separately)
-  std::stable_partition(sl.items.begin(), sl.items.end(), [](const SchurItem& it) { return it.kind == 0; });
   d.lmB = h->lmBegin, d.lmE = h->lmEnd, d.root = h->isRoot ? 1 : 0;
   d.obB = lmObs[h->lmBegin], d.obE = lmObs[h->lmEnd], d.obFree = lmObs[nPts];
-  d.nItems = (int64_t)sl.items.size();
-  d.nItemsLm = 0;
-  for (const SchurItem& it : sl.items) d.nItemsLm += it.kind == 0;
-  h->nLmEnt = (int64_t)sl.lmEnt.size() / 2, h->nObEnt = (int64_t)sl.obEnt.size() / 2;
-  if (upload(&d.items, sl.items) || upload(&d.lmEnt, sl.lmEnt) || upload(&d.obEnt, sl.obEnt)) return VB_E_HIP;
-  // tiles this shard's Schur items touch (column-major tile order => one contiguous range)
-  {
-    int64_t lo = INT64_MAX, hi = -1;
-    const int32_t nTl = (int32_t)((nRed + TS - 1) / TS);
-    for (const SchurItem& it : sl.items) {
-      const int64_t o1 = h->rvOff[it.X1], o2 = h->rvOff[it.X2];
-      const int64_t J0 = o1 / TS, J1 = (o1 + h->rvDim[it.X1] - 1) / TS;
-      const int64_t I0 = o2 / TS, I1 = (o2 + h->rvDim[it.X2] - 1) / TS;
-      lo = std::min(lo, J0 * nTl + I0), hi = std::max(hi, J1 * nTl + I1);
-    }
-    h->itemTileLo = lo, h->itemTileHi = hi;  // packed (J, I) keys, mapped to tile indices below
-  }
-  sl = SchurLists();
   // ---------------- couplings: row ends and the tile pattern
   const int32_t nT = (int32_t)((nRed + TS - 1) / TS);
   d.nT = nT;
@@ -735,19 +557,109 @@ int doFinalize(vb_handle h) {
     h->colStart[J + 1] = (int64_t)h->colTilesH.size();
   }
   d.nTiles = nTiles;
-  if (h->isRoot || h->itemTileHi < 0) {
-    h->tileFirst = 0, h->tileCount = h->isRoot ? nTiles : 0;
-  } else {  // first / last stored tile whose (J, I) key lies inside the touched key range
-    int64_t first = -1, last = -1;
+  // ---------------- Schur assembly work by target tile (this shard's landmarks and observations)
+  {
+    constexpr int kChunkLm = 64, kChunkObs = 128;  // entries per work item (bounded cost)
+    std::vector<TileWork> works;
+    // landmark entries
+    struct Seg { int64_t t, c0, c1; };
+    std::vector<Seg> sg;
+    auto segments = [&](int64_t l) {  // panel columns split by the tile their reduced row falls in
+      sg.clear();
+      const int64_t cb = lmY[l] / 3, nc = (lmY[l + 1] - lmY[l]) / 3;
+      for (int64_t c = 0; c < nc; c++) {
+        const int64_t t = pcRow[cb + c] / TS;
+        if (sg.empty() || sg.back().t != t) sg.push_back({t, c, c + 1});
+        else sg.back().c1 = c + 1;
+      }
+    };
+    std::vector<int64_t> tcnt(nTiles + 1, 0);
+    for (int64_t l = h->lmBegin; l < h->lmEnd; l++) {
+      segments(l);
+      for (size_t a = 0; a < sg.size(); a++)
+        for (size_t b = 0; b <= a; b++) {
+          const int32_t ti = tileIdx[(size_t)sg[a].t * nT + sg[b].t];
+          if (ti < 0) return fail(VB_E_STATE, "internal: landmark tile outside the symbolic structure");
+          tcnt[ti + 1]++;
+        }
+    }
+    for (int64_t t = 0; t < nTiles; t++) tcnt[t + 1] += tcnt[t];
+    std::vector<TileEnt> ents(tcnt[nTiles]);
+    {
+      std::vector<int64_t> cur(tcnt.begin(), tcnt.end() - 1);
+      for (int64_t l = h->lmBegin; l < h->lmEnd; l++) {
+        segments(l);
+        const int64_t cb = lmY[l] / 3;
+        for (size_t a = 0; a < sg.size(); a++)
+          for (size_t b = 0; b <= a; b++) {
+            const int32_t ti = tileIdx[(size_t)sg[a].t * nT + sg[b].t];
+            TileEnt& e = ents[cur[ti]++];
+            e.colI = (uint32_t)(cb + sg[a].c0), e.nI = (uint16_t)(sg[a].c1 - sg[a].c0);
+            e.colJ = (uint32_t)(cb + sg[b].c0), e.nJ = (uint16_t)(sg[b].c1 - sg[b].c0);
+            e.lm = (uint32_t)l;
+          }
+      }
+    }
+    // observation groups: this shard's observations by their 4 reduced blocks (rig, camera)
+    std::vector<int32_t> gobs;
+    for (int64_t o = 0; o < nObs; o++)
+      if ((o >= d.obB && o < d.obE) || (h->isRoot && o >= d.obFree)) gobs.push_back((int32_t)o);
+    auto gkey = [&](int32_t o, int s) { return obRed[(int64_t)o * 4 + s]; };
+    std::stable_sort(gobs.begin(), gobs.end(), [&](int32_t a, int32_t b) {
+      for (int s = 0; s < 4; s++)
+        if (gkey(a, s) != gkey(b, s)) return gkey(a, s) < gkey(b, s);
+      return false;
+    });
+    std::vector<int64_t> gstart;
+    std::vector<int32_t> gred;
+    int64_t tlo = INT64_MAX, thi = -1;
+    for (size_t i = 0; i < gobs.size(); i++) {
+      bool fresh = i == 0;
+      for (int s = 0; s < 4 && !fresh; s++) fresh = gkey(gobs[i], s) != gkey(gobs[i - 1], s);
+      if (!fresh) continue;
+      gstart.push_back((int64_t)i);
+      for (int s = 0; s < 4; s++) gred.push_back(gkey(gobs[i], s));
+      for (int s = 0; s < 4; s++)  // tiles the group touches (for the shard's tile band)
+        for (int t = 0; t <= s; t++) {
+          int32_t A = gkey(gobs[i], s), B = gkey(gobs[i], t);
+          if (A < 0 || B < 0) continue;
+          if (h->rvOff[A] < h->rvOff[B]) std::swap(A, B);
+          for (int64_t I = h->rvOff[A] / TS; I <= (h->rvOff[A] + h->rvDim[A] - 1) / TS; I++)
+            for (int64_t J = h->rvOff[B] / TS; J <= std::min<int64_t>(I, (h->rvOff[B] + h->rvDim[B] - 1) / TS); J++) {
+              const int32_t tt = tileIdx[(size_t)I * nT + J];
+              if (tt >= 0) tlo = std::min<int64_t>(tlo, tt), thi = std::max<int64_t>(thi, tt);
+            }
+        }
+    }
+    gstart.push_back((int64_t)gobs.size());
+    d.nGroups = (int64_t)gred.size() / 4;
+    if (upload(&d.grpStart, gstart) || upload(&d.grpObs, gobs) || upload(&d.grpRed, gred)) return VB_E_HIP;
+    std::vector<int32_t> tobs;
+    std::vector<int64_t> ocnt(nTiles + 1, 0);
     for (int32_t J = 0; J < nT; J++)
       for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
-        const int64_t key = (int64_t)J * nT + h->colRowsH[c];
-        if (key >= h->itemTileLo && key <= h->itemTileHi) {
-          if (first < 0) first = h->colTilesH[c];
-          last = h->colTilesH[c];
+        const int32_t ti = h->colTilesH[c];
+        for (int kind = 0; kind < 1; kind++) {  // kind 1 (observations): groups above
+          const std::vector<int64_t>& cnt = kind ? ocnt : tcnt;
+          const int64_t n = cnt[ti + 1] - cnt[ti];
+          const int64_t ch = kind ? kChunkObs : kChunkLm;
+          for (int64_t k = 0; k < n; k += ch) {
+            TileWork w{};
+            w.tile = ti, w.I = h->colRowsH[c], w.J = J, w.count = (int32_t)std::min<int64_t>(ch, n - k);
+            w.start = cnt[ti] + k, w.kind = kind;
+            works.push_back(w);
+            tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti);
+          }
         }
       }
-    h->tileFirst = first < 0 ? 0 : first, h->tileCount = first < 0 ? 0 : last - first + 1;
+    // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
+    d.nTileWorks = (int64_t)works.size();
+    h->nTileEnt = (int64_t)ents.size(), h->nObEnt = d.nGroups;
+    if (upload(&d.tileWorks, works) || upload(&d.tileEnts, ents) || upload(&d.tileObs, tobs)) return VB_E_HIP;
+    // tiles this shard's partial system can touch (column-major tile order: one contiguous range)
+    if (h->isRoot) h->tileFirst = 0, h->tileCount = nTiles;
+    else if (thi < 0) h->tileFirst = 0, h->tileCount = 0;
+    else h->tileFirst = tlo, h->tileCount = thi - tlo + 1;
   }
   std::vector<int32_t> pairs, targets;
   h->pairStart.assign(nT + 1, 0);
@@ -1006,7 +918,7 @@ int vb_destroy(vb_handle h) {
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
-                  d.lxStart, d.lxLm, d.lxCol, d.items, d.lmEnt, d.obEnt, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
+                  d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
@@ -1317,7 +1229,7 @@ int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
   for (int k = 1; k < 14; k++) sm += d.sf[k].n;
   out[7] = sm;
   // Schur work-list sizes: landmark-pair entries, observation-pair entries
-  out[8] = h->nLmEnt, out[9] = h->nObEnt;
+  out[8] = h->nTileEnt, out[9] = h->nObEnt;
   // launches per factorization: tile GEMM update, trsm
   int64_t nu = 0, nt = 0;
   for (int32_t J = 0; J < d.nT; J++) {

@@ -44,14 +44,22 @@ struct SmallFactors {  // one kind
   int nv = 0, nc = 0;
 };
 
-// One unit of Schur-assembly work: block pair (X2 >= X1 by offset) and a range of its entry list.
-// kind 0: landmark entries (uint2 panel columns col1, col2 — or (col1, landmark) when X1 == X2),
-// kind 1: observation entries (int2 obs, slot1 | slot2 << 8).
-struct SchurItem {
-  int64_t start;
-  int32_t count;
-  int32_t X1, X2;
-  int32_t kind;
+// Schur assembly organised by target tile: each work item is one 64x64 tile (I, J) of the reduced
+// system and a chunk of its entry list, of one kind:
+//   kind 0, landmark entries (TileEnt): the landmark's panel-column ranges inside tile I and tile J
+//           (panel columns = columns of its Y = L^-1 W panel):   C_IJ -= Y_{l,I}^T Y_{l,J}
+//   kind 1, observation entries (int32 obs index): the two whitened residual rows of the observation
+//           restricted to tile I / J columns:                    C_IJ += J~_I^T J~_J (damped diagonal)
+// Diagonal tiles also produce the RHS pieces (kind 0: rhs -= Y^T z; kind 1: gRed += J~^T e~).
+struct TileEnt {
+  uint32_t colI, colJ;  // first panel column (global index lmY[l] / 3 + c) inside tile I / J
+  uint16_t nI, nJ;      // number of panel columns inside tile I / J
+  uint32_t lm;          // landmark
+};
+struct TileWork {
+  int32_t tile, I, J, count;
+  int64_t start;  // into tileEnts (kind 0) or tileObs (kind 1)
+  int32_t kind, pad;
 };
 
 struct Dev {
@@ -96,11 +104,17 @@ struct Dev {
   int64_t* lxStart = nullptr;
   int32_t* lxLm = nullptr;
   int32_t* lxCol = nullptr;
-  // Schur assembly work list (block pairs)
-  int64_t nItems = 0, nItemsLm = 0;  // items [0, nItemsLm) have kind 0
-  SchurItem* items = nullptr;
-  uint32_t* lmEnt = nullptr;  // 2 per entry
-  int32_t* obEnt = nullptr;   // 2 per entry
+  // Schur assembly work by target tile
+  int64_t nTileWorks = 0;
+  TileWork* tileWorks = nullptr;
+  TileEnt* tileEnts = nullptr;
+  int32_t* tileObs = nullptr;  // (unused: direct terms go through the observation groups)
+  // direct visual terms by observation group (observations sharing their 4 reduced blocks: one rig,
+  // one camera): grpStart[g] .. grpStart[g + 1] into grpObs, grpRed[4 g + slot] the blocks
+  int64_t nGroups = 0;
+  int64_t* grpStart = nullptr;
+  int32_t* grpObs = nullptr;
+  int32_t* grpRed = nullptr;
   // tiles
   int T = 64;
   int32_t nT = 0;

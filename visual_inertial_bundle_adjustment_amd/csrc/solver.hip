@@ -19,6 +19,10 @@ namespace viba {
 using namespace dev;
 
 constexpr int TS = 64;  // tile size (rows/cols of a dense reduced-system tile)
+typedef double double4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double4_t mfma64(double a, double b, double4_t c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
 
 __device__ inline int rv_dim(const Dev& d, int r) { return d.rvDim[r]; }
 
@@ -108,13 +112,21 @@ __device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
   return d.tiles + (int64_t)ti * TS * TS + (c % TS) * TS + (r % TS);
 }
 
-// Schur assembly over the block-pair work list (api.hip buildSchurLists).  One wave per work item
-// (X1, X2, entry range); lane e owns entry (i, j) = (e / d1, e % d1) of the d2 x d1 block S(X2, X1)
-// (64-entry chunks for larger blocks) and streams the item's entries:
-//   landmark entries:    S(X2, X1) -= Y_{l,X2}^T Y_{l,X1}            (3-row panel columns)
-//   observation entries: S(X2, X1) += J~_X2^T J~_X1  (2 whitened residual rows; diag * (1 + lambda))
-// The partial block is added to the tile store with fp64 atomics (a pair's entries may be split over
-// several items).  Diagonal items also produce the RHS pieces: gRed += J~^T e~, rhs -= Y^T z.
+// Schur assembly by target tile (api.hip builds the work list; engine.hpp TileWork / TileEnt).
+// One workgroup per work item: a 64 x 64 tile (I, J) of the reduced system and a chunk of its entries.
+// Each batch of entries is scattered into LDS as K = 32 rows x 64 tile rows (operands Yi for tile I,
+// Yj for tile J; the same buffer on diagonal tiles):
+//   kind 0, landmarks (8 per batch): rows = the 3 rows of Y = L^-1 W (+ 1 zero row)   C -= Yi^T Yj
+//   kind 1, observations (16 per batch): rows = the 2 whitened residual rows          C += Ji^T Jj
+// and multiplied on v_mfma_f64_16x16x4_f64, transposed (D = Yj^T Yi) so that the MFMA output column
+// (lane & 15) runs along the tile's contiguous row index q; wave w owns the 32 x 32 block
+// (p in 32 (w >> 1) .., q in 32 (w & 1) ..).  Chunks of one tile may run concurrently: fp64 atomics.
+// Diagonal tiles also emit the RHS pieces (kind 0: rhs -= Y^T z; kind 1: gRed += J~^T e~) and, for
+// kind 1, the damping of the direct visual diagonal (Optimizer.cpp:136-146: d (1 + lambda)).
+constexpr int kTK = 32;       // K rows per batch
+constexpr int kTB = kTK / 4;  // landmarks per batch
+constexpr int kOB = kTK / 2;  // observations per batch
+
 // XCD-aware block id: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch), so
 // hand each XCD a contiguous range of work (bijective for any grid size)
 __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
@@ -122,102 +134,223 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-__global__ void __launch_bounds__(256) schur_items_kernel(Dev d, double lambda, int64_t i0, int64_t i1) {
-  const int64_t it = i0 + xcd_block(blockIdx.x, gridDim.x) * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (it >= i1) return;
-  const int lane = threadIdx.x & 63;
-  const SchurItem w = d.items[it];
-  const int X1 = w.X1, X2 = w.X2;
-  const int d1 = d.rvDim[X1], d2 = d.rvDim[X2];
-  const int64_t off1 = d.rvOff[X1], off2 = d.rvOff[X2];
-  const bool diag = X1 == X2;
-  const int ne = d1 * d2;
-  const int cnt = w.count;
-  const double* Jt = d.Jt;
-  const double* Y = d.Y;
-  const uint2* lent = reinterpret_cast<const uint2*>(d.lmEnt) + w.start;
-  const int2* oent = reinterpret_cast<const int2*>(d.obEnt) + w.start;
-  constexpr int U = 4;  // entries in flight per wave
-  for (int e0 = 0; e0 < ne; e0 += 64) {
-    const int e = min(e0 + lane, ne - 1);
-    const int i = e / d1, j = e - (e / d1) * d1;
-    double acc = 0.0;
-    if (w.kind == 0) {
-      int k = 0;
-      for (; k + U <= cnt; k += U) {
-        double p[U][3], q[U][3];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const uint2 en = lent[k + u];
-          const double* y1 = Y + 3 * (int64_t)en.x + 3 * j;
-          const double* y2 = Y + 3 * (int64_t)(diag ? en.x : en.y) + 3 * i;
-#pragma unroll
-          for (int c = 0; c < 3; c++) p[u][c] = y1[c], q[u][c] = y2[c];
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) acc -= q[u][0] * p[u][0] + q[u][1] * p[u][1] + q[u][2] * p[u][2];
-      }
-      for (; k < cnt; k++) {
-        const uint2 en = lent[k];
-        const double* y1 = Y + 3 * (int64_t)en.x + 3 * j;
-        const double* y2 = Y + 3 * (int64_t)(diag ? en.x : en.y) + 3 * i;
-        acc -= y2[0] * y1[0] + y2[1] * y1[1] + y2[2] * y1[2];
-      }
-    } else {
-      int k = 0;
-      for (; k + U <= cnt; k += U) {
-        double a0[U], a1[U], b0[U], b1[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-          const int2 en = oent[k + u];
-          const double* rec = Jt + (int64_t)en.x * kJPlanes;
-          const int s1 = en.y & 255, s2 = en.y >> 8;
-          const int p1 = slotPlane(s1) + j, p2 = slotPlane(s2) + i;
-          a0[u] = rec[p2], a1[u] = rec[p2 + slotStride(s2)];
-          b0[u] = rec[p1], b1[u] = rec[p1 + slotStride(s1)];
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++) acc += a0[u] * b0[u] + a1[u] * b1[u];
-      }
-      for (; k < cnt; k++) {
-        const int2 en = oent[k];
-        const double* rec = Jt + (int64_t)en.x * kJPlanes;
-        const int s1 = en.y & 255, s2 = en.y >> 8;
-        const int p1 = slotPlane(s1) + j, p2 = slotPlane(s2) + i;
-        acc += rec[p2] * rec[p1] + rec[p2 + slotStride(s2)] * rec[p1 + slotStride(s1)];
-      }
-      if (diag && i == j) acc *= 1.0 + lambda;
+__device__ __forceinline__ void fill_landmarks(const Dev& d, const TileWork& wk, int b, bool diag, double* yi,
+                                               double* yj, double* zb, int tid) {
+  const int e0 = b * kTB, ne = min(kTB, wk.count - e0);
+  const int64_t rI = (int64_t)wk.I * TS, rJ = (int64_t)wk.J * TS;
+  for (int sl = tid; sl < ne * TS; sl += 256) {
+    const int eb = sl / TS, c = sl - eb * TS;
+    const TileEnt en = d.tileEnts[wk.start + e0 + eb];
+    if (c < en.nI) {
+      const int64_t col = (int64_t)en.colI + c;
+      const int row = (int)(d.pcRow[col] - rI);
+      const double* y = d.Y + 3 * col;
+      const double y0 = y[0], y1 = y[1], y2 = y[2];
+      yi[(4 * eb) * TS + row] = y0, yi[(4 * eb + 1) * TS + row] = y1, yi[(4 * eb + 2) * TS + row] = y2;
     }
-    if (e0 + lane < ne && (!diag || i >= j) && acc != 0.0) {
-      double* p = tile_ptr(d, off2 + i, off1 + j);
-      if (p) atomicAdd(p, acc);
-      else atomicOr(d.err, 4);
+    if (!diag && c < en.nJ) {
+      const int64_t col = (int64_t)en.colJ + c;
+      const int row = (int)(d.pcRow[col] - rJ);
+      const double* y = d.Y + 3 * col;
+      const double y0 = y[0], y1 = y[1], y2 = y[2];
+      yj[(4 * eb) * TS + row] = y0, yj[(4 * eb + 1) * TS + row] = y1, yj[(4 * eb + 2) * TS + row] = y2;
     }
-  }
-  if (!diag || lane >= d1) return;
-  const int j = lane;
-  double g = 0.0;
-  if (w.kind == 0) {
-    for (int k = 0; k < cnt; k++) {
-      const uint2 en = lent[k];
-      const double* y1 = Y + 3 * (int64_t)en.x + 3 * j;
-      const double* z = d.z + 3 * (int64_t)en.y;
-      g += y1[0] * z[0] + y1[1] * z[1] + y1[2] * z[2];
-    }
-    atomicAdd(d.rhs + off1 + j, -g);
-  } else {
-    for (int k = 0; k < cnt; k++) {
-      const int2 en = oent[k];
-      const double* rec = Jt + (int64_t)en.x * kJPlanes;
-      const int s1 = en.y & 255;
-      const int p1 = slotPlane(s1) + j;
-      g += rec[p1] * rec[kJe] + rec[p1 + slotStride(s1)] * rec[kJe + 1];
-    }
-    atomicAdd(d.gRed + off1 + j, g);
+    if (diag && c < 3) zb[4 * eb + c] = d.z[3 * (int64_t)en.lm + c];
   }
 }
 
-// damping of the small-factor part of the diagonal (visual part: schur_items_kernel) and the
+// observation rows: thread (e = tid / 16, sub = tid % 16) writes the columns sub, sub + 16, .. of
+// each reduced block of observation e that fall into the tile
+__device__ __forceinline__ void fill_obs_rows(const Dev& d, const double* rec, int64_t o, int64_t r0, int e, int sub,
+                                              double* y) {
+#pragma unroll
+  for (int sl = 0; sl < 4; sl++) {
+    const int32_t X = d.obRed[o * 4 + sl];
+    if (X < 0) continue;
+    const int64_t off = d.rvOff[X] - r0;
+    const int dim = d.rvDim[X];
+    const int pl = slotPlane(sl), st = slotStride(sl);
+    for (int j = sub; j < dim; j += 16) {
+      const int64_t row = off + j;
+      if (row < 0 || row >= TS) continue;
+      y[(2 * e) * TS + row] = rec[pl + j];
+      y[(2 * e + 1) * TS + row] = rec[pl + st + j];
+    }
+  }
+}
+__device__ __forceinline__ void fill_observations(const Dev& d, const TileWork& wk, int b, bool diag, double* yi,
+                                                  double* yj, double* zb, int tid) {
+  const int e0 = b * kOB, ne = min(kOB, wk.count - e0);
+  const int e = tid >> 4, sub = tid & 15;
+  if (e >= ne) return;
+  const int64_t o = d.tileObs[wk.start + e0 + e];
+  const double* rec = d.Jt + o * kJPlanes;
+  fill_obs_rows(d, rec, o, (int64_t)wk.I * TS, e, sub, yi);
+  if (!diag) fill_obs_rows(d, rec, o, (int64_t)wk.J * TS, e, sub, yj);
+  if (diag && sub < 2) zb[2 * e + sub] = rec[kJe + sub];
+}
+
+__global__ void __launch_bounds__(256) schur_tile_kernel(Dev d, double lambda) {
+  // single-buffered (32 KB LDS): the gathers' latency is hidden by resident workgroups
+  __shared__ double Yi[kTK * TS];
+  __shared__ double Yj[kTK * TS];
+  __shared__ double zb[kTK];
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
+  const TileWork wk = d.tileWorks[w];
+  const bool diag = wk.I == wk.J;
+  const bool obs = wk.kind == 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  const int nb = (wk.count + (obs ? kOB : kTB) - 1) / (obs ? kOB : kTB);
+  double4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
+  double racc = 0.0;
+  const double* yj = diag ? Yi : Yj;
+  for (int b = 0; b < nb; b++) {
+    for (int i = tid; i < kTK * TS; i += 256) {
+      Yi[i] = 0.0;
+      if (!diag) Yj[i] = 0.0;
+    }
+    if (tid < kTK) zb[tid] = 0.0;
+    __syncthreads();
+    if (obs) fill_observations(d, wk, b, diag, Yi, Yj, zb, tid);
+    else fill_landmarks(d, wk, b, diag, Yi, Yj, zb, tid);
+    __syncthreads();
+#pragma unroll
+    for (int k0 = 0; k0 < kTK; k0 += 4) {
+      double av[2], bv[2];
+#pragma unroll
+      for (int a = 0; a < 2; a++) av[a] = yj[(k0 + l4) * TS + pb + a * 16 + l15];
+#pragma unroll
+      for (int bb = 0; bb < 2; bb++) bv[bb] = Yi[(k0 + l4) * TS + qb + bb * 16 + l15];
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int bb = 0; bb < 2; bb++) acc[a][bb] = mfma64(av[a], bv[bb], acc[a][bb]);
+    }
+    if (diag && tid < TS) {
+#pragma unroll 8
+      for (int k = 0; k < kTK; k++) racc += Yi[k * TS + tid] * zb[k];
+    }
+    __syncthreads();
+  }
+  double* C = d.tiles + (int64_t)wk.tile * TS * TS;
+  const double sign = obs ? 1.0 : -1.0;
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int p = pb + a * 16 + l4 + 4 * r, q = qb + bb * 16 + l15;
+        double v = acc[a][bb][r];
+        if (obs && diag && p == q) v *= 1.0 + lambda;
+        if (v != 0.0) atomicAdd(C + p * TS + q, sign * v);
+      }
+  if (diag && tid < TS) {
+    const int64_t row = (int64_t)wk.I * TS + tid;
+    if (row < d.nRed && racc != 0.0) atomicAdd(obs ? d.gRed + row : d.rhs + row, obs ? racc : -racc);
+  }
+}
+
+// Direct visual terms by observation group (observations sharing their reduced blocks: one rig, one
+// camera).  Per group: H = sum_o J~_o^T J~_o over the 32 columns [pose 6 | extr 6 | intr <= 17 |
+// vel 3] and g = sum_o J~_o^T e~_o, on v_mfma_f64_16x16x4_f64 (K = the group's residual rows, 4 per
+// k-step = 2 observations; the 4 waves split K and reduce through LDS).  Lane l owns the columns
+// l & 15 and 16 + (l & 15); an accumulator D[m][n] (lane: n = l & 15, rows m = (l >> 4) + 4 r) is the
+// Gram block directly.  mode 0: H (diagonal damped by (1 + lambda)) into the tiles, g into gRed;
+// mode 1: g only into gRedNew (gradient pass of the bad-step path).
+constexpr int kGrpBase[4] = {0, 6, 12, 29};
+
+__device__ __forceinline__ int grp_col_row(const Dev& d, const int32_t* red, int c, int& plane, int& stride) {
+  const int s = c < 6 ? 0 : c < 12 ? 1 : c < 29 ? 2 : 3;
+  const int j = c - kGrpBase[s];
+  const int32_t X = red[s];
+  plane = slotPlane(s) + j, stride = slotStride(s);
+  if (X < 0 || j >= d.rvDim[X]) return -1;
+  return (int)(d.rvOff[X] + j);
+}
+
+__global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, int mode) {
+  __shared__ double red_[4][64][14];
+  const int64_t g = xcd_block(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int32_t* rv = d.grpRed + 4 * g;
+  int p0, s0, p1, s1;
+  const int row0 = grp_col_row(d, rv, l15, p0, s0);
+  const int row1 = grp_col_row(d, rv, 16 + l15, p1, s1);
+  const int64_t o0 = d.grpStart[g], n = d.grpStart[g + 1] - o0;
+  const int r = l4 & 1;
+  const int64_t nks = (n + 1) / 2;
+  double4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
+  double g0 = 0.0, g1 = 0.0;
+  const double* Jt = d.Jt;
+  for (int64_t ks = wave; ks < nks; ks += 4) {
+    const int64_t e = 2 * ks + (l4 >> 1);
+    double v0 = 0.0, v1 = 0.0, er = 0.0;
+    if (e < n) {
+      const double* rec = Jt + (int64_t)d.grpObs[o0 + e] * kJPlanes;
+      er = rec[kJe + r];
+      if (row0 >= 0) v0 = rec[p0 + r * s0];
+      if (row1 >= 0) v1 = rec[p1 + r * s1];
+    }
+    g0 += v0 * er, g1 += v1 * er;
+    if (mode == 0) {
+      a00 = mfma64(v0, v0, a00);
+      a10 = mfma64(v1, v0, a10);
+      a11 = mfma64(v1, v1, a11);
+    }
+  }
+  // reduce the 4 waves (and, for g, the 4 lane groups) through LDS
+  double* mine = red_[wave][lane];
+#pragma unroll
+  for (int k = 0; k < 4; k++) mine[k] = a00[k], mine[4 + k] = a10[k], mine[8 + k] = a11[k];
+  mine[12] = g0, mine[13] = g1;
+  __syncthreads();
+  if (wave != 0) return;
+  double t[14];
+#pragma unroll
+  for (int k = 0; k < 14; k++) t[k] = red_[0][lane][k] + red_[1][lane][k] + red_[2][lane][k] + red_[3][lane][k];
+  // g: lanes l15 of the 4 lane groups hold partial sums of the same columns
+  double gc0 = t[12], gc1 = t[13];
+#pragma unroll
+  for (int off = 16; off < 64; off += 16) {
+    gc0 += __shfl(t[12], (lane + off) & 63, 64);
+    gc1 += __shfl(t[13], (lane + off) & 63, 64);
+  }
+  double* gOut = mode == 0 ? d.gRed : d.gRedNew;
+  if (l4 == 0) {
+    if (row0 >= 0 && gc0 != 0.0) atomicAdd(gOut + row0, gc0);
+    if (row1 >= 0 && gc1 != 0.0) atomicAdd(gOut + row1, gc1);
+  }
+  if (mode != 0) return;
+  // H: D[m][n], m = l4 + 4 k (+16), n = l15 (+16); rows of m / n via the lanes that own those columns
+#pragma unroll
+  for (int blk = 0; blk < 3; blk++) {
+    const int mb = blk == 0 ? 0 : 16, nb = blk == 2 ? 16 : 0;
+    const int rn = nb ? row1 : row0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int m = l4 + 4 * k;
+      const int rm = __shfl(mb ? row1 : row0, m, 64);
+      double v = t[4 * blk + k];
+      if (rm < 0 || rn < 0 || v == 0.0) continue;
+      if (rm == rn) v *= 1.0 + lambda;
+      else if (blk != 1 && rm < rn) continue;  // symmetric blocks: each pair once
+      const int64_t R = max(rm, rn), Cc = min(rm, rn);
+      double* pt = tile_ptr(d, R, Cc);
+      if (pt) atomicAdd(pt, v);
+      else atomicOr(d.err, 4);
+    }
+  }
+}
+
+// damping of the small-factor part of the diagonal (visual part: schur_tile_kernel) and the
 // identity term (Optimizer.cpp:136-146 addDamping: H_ii += lambda * H_ii + lambda)
 __global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -275,12 +408,6 @@ __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
 // an accumulator D (lane l, register r) = D[(l >> 4) + 4 r][l & 15] is exactly the B operand of k-step
 // r (B[4 r + (l >> 4)][l & 15]), so chained products need no data movement.  The only scalar work is
 // the factor + inverse of the four 16 x 16 diagonal blocks (dinv[J]: 4 x 256 doubles, column-major).
-
-typedef double double4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ double4_t mfma64(double a, double b, double4_t c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const int64_t b = __double_as_longlong(v);
@@ -799,14 +926,15 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
 // S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry)
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
-  if (d.nItemsLm)
-    launchK(schur_items_kernel, dim3(blocks(d.nItemsLm, 4)), dim3(256), 0, st, d, lambda, (int64_t)0, d.nItemsLm);
-  if (d.nItems > d.nItemsLm)
-    hipLaunchKernelGGL(schur_items_kernel, dim3(blocks(d.nItems - d.nItemsLm, 4)), dim3(256), 0, st, d, lambda,
-                       d.nItemsLm, d.nItems);
+  if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
+  if (d.nTileWorks) launchK(schur_tile_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
+  if (mode == 0) {  // visual gradient of this shard's observations, by observation group
+    if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, 0.0, 1);
+    return;
+  }
   if (d.nRV) hipLaunchKernelGGL(reduced_grad_kernel, dim3(d.nRV), dim3(256), 0, st, d, mode);
 }
 void launch_potrf(const Dev& d, const int32_t* colTiles, double* dinv, hipStream_t st) {
