@@ -34,6 +34,10 @@ void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, i
 void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
                 double* t, double* x, hipStream_t st);
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st);
+void launch_solve_persistent(const Dev& d, const int64_t* rowStart, const int32_t* rowTiles, const int32_t* rowCol,
+                             const int64_t* colStart, const int32_t* colTiles, const int32_t* colRows,
+                             const double* linv, const double* b, double* y, double* x, unsigned* flags, int G,
+                             hipStream_t st);
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t st);
 void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hipStream_t st);
 void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, hipStream_t st);
@@ -208,6 +212,10 @@ struct vb_handle_s {
   std::vector<int32_t> rowTilesH, rowColH;
   int32_t *colTilesD = nullptr, *colRowsD = nullptr, *pairsD = nullptr, *targetsD = nullptr, *rowTilesD = nullptr,
           *rowColD = nullptr;
+  int64_t *colStartD = nullptr, *rowStartD = nullptr;
+  unsigned* solveFlags = nullptr;
+  int numCUs = 256;
+  bool legacySolve = false;  // VIBA_SOLVE_LEGACY=1: one launch pair per tile column
   double *dinv = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
@@ -272,6 +280,7 @@ int checkErr(vb_handle h) {
   if (e & 2) return fail(VB_E_NUMERIC, "landmark 3x3 Cholesky breakdown");
   if (e & 8) return fail(VB_E_NUMERIC, "reduced system Cholesky breakdown (not positive definite)");
   if (e & 4) return fail(VB_E_STATE, "internal: Schur contribution outside the symbolic structure");
+  if (e & 16) return fail(VB_E_HIP, "internal: triangular-solve hand-off timed out");
   return 0;
 }
 
@@ -731,6 +740,9 @@ int doFinalize(vb_handle h) {
       alloc0(&d.stepRed, nPad) || alloc0(&d.stepPt, nPts * 3) || alloc0(&d.subRed, nPad) ||
       alloc0(&d.subPt, nPts * 3) || alloc0(&h->yvec, nPad) || alloc0(&h->rhsWork, nPad))
     return VB_E_HIP;
+  if (upload(&h->colStartD, h->colStart) || upload(&h->rowStartD, h->rowStart) ||
+      alloc0(&h->solveFlags, 2 * (size_t)nT))
+    return VB_E_HIP;
   if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) || upload(&h->pairsD, pairs) ||
       upload(&h->targetsD, targets) || upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
     return VB_E_HIP;
@@ -833,6 +845,14 @@ int factorReduced(vb_handle h) {
 
 // solves with rhsWork as right-hand side, result in xRed
 int solveReduced(vb_handle h) {
+  if (!h->legacySolve) {
+    Dev& d = h->d;
+    profBegin(h, KF_FWD);
+    launch_solve_persistent(d, h->rowStartD, h->rowTilesD, h->rowColD, h->colStartD, h->colTilesD, h->colRowsD, h->linv,
+                            h->rhsWork, h->yvec, d.xRed, h->solveFlags, h->numCUs, h->st);
+    profEnd(h, KF_FWD);
+    return 0;
+  }
   const bool prof = h->profFamily == KF_FWD || h->profFamily == KF_BWD;
   if (!h->useGraphs || prof) {
     solveSeq(h, h->rhsWork, h->d.xRed);
@@ -904,6 +924,12 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_FUSE_POTRF")) h->noFusePotrf = e[0] == '1';
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
+  if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
+      h->numCUs = prop.multiProcessorCount;
+  }
   HIPCHK(hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking));
   for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
   *out = h;
@@ -920,7 +946,7 @@ int vb_destroy(vb_handle h) {
                   d.blkCol, d.pcRow, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
-                  h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->dinv, h->yvec,
+                  h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->colStartD, h->rowStartD, h->solveFlags, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1075,7 +1101,7 @@ int vb_solve_with_new_gradient(vb_handle h) {
   if (int rc = solveReduced(h)) return rc;
   backSubstitute(h, 1);
   HIPCHK(hipStreamSynchronize(h->st));
-  return 0;
+  return checkErr(h);
 }
 
 int vb_scale_step(vb_handle h, double f) {

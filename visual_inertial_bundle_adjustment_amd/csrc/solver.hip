@@ -14,6 +14,7 @@
 //   fwd/bwd_kernel       tile triangular solves; backsub_kernel: points x_p = L^-T (z - Y x_c)
 #include "device_math.hpp"
 #include "engine.hpp"
+#include <algorithm>
 
 namespace viba {
 using namespace dev;
@@ -771,6 +772,138 @@ __global__ void __launch_bounds__(64) bwd_kernel(Dev d, int J, const int32_t* ro
 #pragma unroll 16
   for (int i = 0; i < TS; i++) s += A[lane * TS + i] * xs[i];
   if (kb + lane < nRed) t[kb + lane] -= s;
+}
+
+// ------------------------------------------------------------------ persistent triangular solves
+// One launch per direction (instead of one per tile column).  G resident workgroups; workgroup w owns
+// the tile rows J = w, w + G, .. (forward) or nT-1-w, nT-1-w-G, .. (backward) and processes them in
+// order, so every dependency is on a row an earlier-or-concurrent workgroup owns: no deadlock while
+// all G workgroups are resident (G <= CUs, 1 workgroup per CU).  Hand-off of a solved 64-vector
+// (MI355X_MICROARCH.md / cdna_hip_programming.md §6 Guideline 16, R1): the producer stores the payload
+// write-through (agent-scope relaxed atomic stores = global_store ... sc1), drains (s_waitcnt
+// vmcnt(0)), then one lane sets the flag (agent-scope atomic store); consumers poll the flag relaxed
+// with s_sleep and read the payload with sc1 loads only (never plain / flat loads of it).  Flags are
+// zeroed by a memset before every launch; spins are bounded (error flag 16 on timeout).
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) unsigned int guint;
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load((gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one wave waits until flag == 1; returns false on timeout
+__device__ __forceinline__ bool wait_flag(unsigned* flag, int lane, int32_t* err) {
+  unsigned v = 0;
+  if (lane == 0) {
+    for (unsigned spins = 0;; spins++) {
+      v = __hip_atomic_load((guint*)flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == 1u || spins > (1u << 24)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (v != 1u) atomicOr(err, 16);
+  }
+  v = __shfl(v, 0, 64);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the payload loads below the poll
+  return v == 1u;
+}
+__device__ __forceinline__ void publish(double* dst, double v, bool valid, unsigned* flag, int lane) {
+  if (valid) st_sc1(dst, v);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store((guint*)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// forward: y_J = Linv_JJ (b_J - sum_{K<J} L_JK y_K); the waves split the row's tiles (K ascending)
+__global__ void __launch_bounds__(256) fwd_persistent_kernel(Dev d, const int64_t* rowStart, const int32_t* rowTiles,
+                                                             const int32_t* rowCol, const double* linv, const double* b,
+                                                             double* y, unsigned* flags, int G) {
+  __shared__ double part[4][TS];
+  __shared__ double ys[4][TS];
+  __shared__ double ts[TS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int J = blockIdx.x; J < d.nT; J += G) {
+    double sacc = 0.0;
+    const int64_t r0 = rowStart[J], r1 = rowStart[J + 1];
+    for (int64_t idx = r0 + w; idx < r1; idx += 4) {
+      const int K = rowCol[idx];
+      const double* A = d.tiles + (int64_t)rowTiles[idx] * TS * TS;
+      double a[TS];
+#pragma unroll
+      for (int c = 0; c < TS; c++) a[c] = A[c * TS + lane];  // tile loads overlap the wait
+      if (!wait_flag(flags + K, lane, d.err)) return;
+      ys[w][lane] = ld_sc1(y + (int64_t)K * TS + lane);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int c = 0; c < TS; c++) sacc += a[c] * ys[w][c];
+      __builtin_amdgcn_wave_barrier();
+    }
+    part[w][lane] = sacc;
+    __syncthreads();
+    if (w == 0) {
+      const int64_t row = (int64_t)J * TS + lane;
+      ts[lane] = b[row] - (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
+      __builtin_amdgcn_wave_barrier();
+      const double* Li = linv + (int64_t)J * TS * TS;
+      double v = 0.0;
+#pragma unroll 16
+      for (int c = 0; c < TS; c++) v += Li[c * TS + lane] * ts[c];
+      publish(y + row, row < d.nRed ? v : 0.0, true, flags + J, lane);
+    }
+    __syncthreads();
+  }
+}
+
+// backward: x_J = Linv_JJ^T (y_J - sum_{I>J} L_IJ^T x_I); tiles of column J, I descending
+__global__ void __launch_bounds__(256) bwd_persistent_kernel(Dev d, const int64_t* colStart, const int32_t* colTiles,
+                                                             const int32_t* colRows, const double* linv, const double* yv,
+                                                             double* x, unsigned* flags, int G) {
+  __shared__ double part[4][TS];
+  __shared__ double xs[4][TS];
+  __shared__ double ts[TS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int J = d.nT - 1 - (int)blockIdx.x; J >= 0; J -= G) {
+    double sacc = 0.0;
+    const int64_t c0 = colStart[J], c1 = colStart[J + 1];
+    // off-diagonal tiles c0+1 .. c1-1 (rows I ascending): walk them descending, split over the waves
+    for (int64_t idx = c1 - 1 - w; idx > c0; idx -= 4) {
+      const int I = colRows[idx];
+      const double* A = d.tiles + (int64_t)colTiles[idx] * TS * TS;  // tile (I, J): A[q * TS + r] = L(r, q)
+      double a[TS];
+#pragma unroll
+      for (int r = 0; r < TS; r++) a[r] = A[lane * TS + r];
+      if (!wait_flag(flags + I, lane, d.err)) return;
+      xs[w][lane] = ld_sc1(x + (int64_t)I * TS + lane);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int r = 0; r < TS; r++) sacc += a[r] * xs[w][r];
+      __builtin_amdgcn_wave_barrier();
+    }
+    part[w][lane] = sacc;
+    __syncthreads();
+    if (w == 0) {
+      const int64_t row = (int64_t)J * TS + lane;
+      ts[lane] = yv[row] - (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
+      __builtin_amdgcn_wave_barrier();
+      const double* Li = linv + (int64_t)J * TS * TS;
+      double v = 0.0;
+#pragma unroll 16
+      for (int r = 0; r < TS; r++) v += Li[lane * TS + r] * ts[r];
+      publish(x + row, row < d.nRed ? v : 0.0, true, flags + J, lane);
+    }
+    __syncthreads();
+  }
+}
+
+void launch_solve_persistent(const Dev& d, const int64_t* rowStart, const int32_t* rowTiles, const int32_t* rowCol,
+                             const int64_t* colStart, const int32_t* colTiles, const int32_t* colRows,
+                             const double* linv, const double* b, double* y, double* x, unsigned* flags, int G,
+                             hipStream_t st) {
+  const int g = std::min<int>(G, d.nT);
+  (void)hipMemsetAsync(flags, 0, 2 * (size_t)d.nT * sizeof(unsigned), st);
+  launchK(fwd_persistent_kernel, dim3(g), dim3(256), 0, st, d, rowStart, rowTiles, rowCol, linv, b, y, flags, g);
+  launchK(bwd_persistent_kernel, dim3(g), dim3(256), 0, st, d, colStart, colTiles, colRows, linv, (const double*)y, x,
+          flags + d.nT, g);
 }
 
 // ------------------------------------------------------------------ point back-substitution
