@@ -108,7 +108,7 @@ def main():
     synth.load_into(e, p)
     st = e.problem_stats()
     log(f"[bench] finalize {time.perf_counter() - t:.1f}s; reduced order {st[3]}, tiles {st[5]} "
-        f"({st[4]} tile columns), gemm pairs/factorization {st[6]}, Schur entries: landmark-tile {st[8]}, obs-pair {st[9]}")
+        f"({st[4]} tile columns, {st[10]} levels), gemm pairs/factorization {st[6]}, Schur entries: landmark-tile {st[8]}, obs-pair {st[9]}")
 
     # run exactly W then K iterations of the optimize loop (convergence stops disabled)
     def settings(n):

@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <climits>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -23,12 +25,12 @@ void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st);
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
-void launch_potrf(const Dev& d, const int32_t* colTiles, double* dinv, hipStream_t st);
-void launch_trsm(const Dev& d, const int32_t* colTiles, int n, const double* dinv, hipStream_t st);
-void launch_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets, int npairs,
-                   int fuseDiag, double* dinvNext, hipStream_t st);
+void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st);
+void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
+                 hipStream_t st);
+void launch_update(const Dev& d, const int32_t* work, int n, hipStream_t st);
 void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st);
-void launch_pad_diag(const Dev& d, hipStream_t st);
+void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st);
 void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
                 double* b, double* x, hipStream_t st);
 void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
@@ -204,13 +206,18 @@ struct vb_handle_s {
   std::vector<int32_t> rvKind, rvHandle, rvDim;
   std::vector<int64_t> rvOff;
   std::vector<int32_t> lmOfPoint;
-  int64_t nParams = 0, order = 0, nLmObs = 0, nLmEnt = 0, nObEnt = 0;
+  int64_t nParams = 0, order = 0, nLmObs = 0, nLmEnt = 0, nObEnt = 0, nRedReal = 0, nParts = 0, nPadRows = 0;
+  int64_t* padRowsD = nullptr;  // reduced rows that belong to no variable (tile alignment of parts)
   std::vector<int64_t> colStart;   // per tile column into colTilesH / colRowsH
   std::vector<int32_t> colTilesH, colRowsH;
-  std::vector<int64_t> pairStart;  // per tile column into pairs / targets
+  std::vector<int64_t> lvP, lvT, lvU;  // per level into the potrf / trsm / update work arrays
+  int32_t nLevels = 0;
+  int64_t nPairs = 0;
+  int32_t *potrfTileD = nullptr, *potrfColD = nullptr, *trsmDiagD = nullptr, *trsmTargetD = nullptr,
+          *trsmColD = nullptr, *updD = nullptr;
   std::vector<int64_t> rowStart;   // per tile row into rowTilesH / rowColH
   std::vector<int32_t> rowTilesH, rowColH;
-  int32_t *colTilesD = nullptr, *colRowsD = nullptr, *pairsD = nullptr, *targetsD = nullptr, *rowTilesD = nullptr,
+  int32_t *colTilesD = nullptr, *colRowsD = nullptr, *rowTilesD = nullptr,
           *rowColD = nullptr;
   int64_t *colStartD = nullptr, *rowStartD = nullptr;
   unsigned* solveFlags = nullptr;
@@ -224,7 +231,6 @@ struct vb_handle_s {
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
   hipGraphExec_t factorGraph = nullptr, solveGraph = nullptr;
   bool useGraphs = true;
-  bool noFusePotrf = false;  // VIBA_NO_FUSE_POTRF=1: separate potrf launches (profiling)
   // state
   bool linearized = false, factored = false;
   vb_phase_times times{};
@@ -383,21 +389,136 @@ int doFinalize(vb_handle h) {
     if (red[a].first != red[b].first) return red[a].first < red[b].first;
     return red[a].second < red[b].second;
   });
-  std::vector<int> pos(nRV);
-  for (int i = 0; i < nRV; i++) pos[ord[i]] = i;
+  // ---------------- nested dissection over the time order (the ordering is ours)
+  // The time-ordered reduced system is a band (landmark tracks span up to ~60 rigs), whose Cholesky
+  // is a chain as long as the matrix.  Recursive bisection: cut the time order at half its
+  // dimension; the left variables coupled across the cut form the separator, ordered after both
+  // halves; each part starts on a tile boundary so that parts stay independent tile columns and the
+  // factorization runs level by level (factorSeq).  Any symmetric order is a valid Cholesky order:
+  // the separators only need to be sufficient, not minimal.
+  std::vector<int> tp(nRV);
+  for (int i = 0; i < nRV; i++) tp[ord[i]] = i;
+  std::vector<int> hiP(tp), loP(tp);
+  {
+    auto regPos = [&](int kind, int hh) -> int {
+      if (hh < 0 || kind == 0 || kind == 8 || redOf[kind][hh] < 0) return -1;
+      return tp[redOf[kind][hh]];
+    };
+    std::vector<int> lmLo(nPts, INT32_MAX), lmHi(nPts, -1);
+    const int64_t nv0 = (int64_t)h->fint[0].size();
+    auto obsPos = [&](int64_t f, int* ps) {
+      const int32_t* v = &h->fvars[0][f * 5];
+      ps[0] = regPos(1, v[1]), ps[1] = regPos(5, v[2]), ps[2] = regPos(4, v[3]);
+      ps[3] = h->fint[0][f] >= 0 ? regPos(2, v[4]) : -1;
+    };
+    for (int64_t f = 0; f < nv0; f++) {
+      int ps[4];
+      obsPos(f, ps);
+      const int l = lmOf[h->fvars[0][f * 5]];
+      int lo = INT32_MAX, hi = -1;
+      for (int k = 0; k < 4; k++)
+        if (ps[k] >= 0) lo = std::min(lo, ps[k]), hi = std::max(hi, ps[k]);
+      if (hi < 0) continue;
+      if (l >= 0) {
+        lmLo[l] = std::min(lmLo[l], lo), lmHi[l] = std::max(lmHi[l], hi);
+      } else {
+        for (int k = 0; k < 4; k++)
+          if (ps[k] >= 0) {
+            const int r = ord[ps[k]];
+            hiP[r] = std::max(hiP[r], hi), loP[r] = std::min(loP[r], lo);
+          }
+      }
+    }
+    for (int64_t f = 0; f < nv0; f++) {
+      const int l = lmOf[h->fvars[0][f * 5]];
+      if (l < 0 || lmHi[l] < 0) continue;
+      int ps[4];
+      obsPos(f, ps);
+      for (int k = 0; k < 4; k++)
+        if (ps[k] >= 0) {
+          const int r = ord[ps[k]];
+          hiP[r] = std::max(hiP[r], lmHi[l]), loP[r] = std::min(loP[r], lmLo[l]);
+        }
+    }
+    for (int fk = 1; fk < 14; fk++) {
+      const int nv = kNumVars[fk];
+      const int64_t n = (int64_t)h->fint[fk].size();
+      for (int64_t f = 0; f < n; f++) {
+        int lo = INT32_MAX, hi = -1;
+        for (int sl = 0; sl < nv; sl++) {
+          const int q = regPos(kFK[fk][sl], h->fvars[fk][f * nv + sl]);
+          if (q >= 0) lo = std::min(lo, q), hi = std::max(hi, q);
+        }
+        for (int sl = 0; sl < nv; sl++) {
+          const int q = regPos(kFK[fk][sl], h->fvars[fk][f * nv + sl]);
+          if (q >= 0) hiP[ord[q]] = std::max(hiP[ord[q]], hi), loP[ord[q]] = std::min(loP[ord[q]], lo);
+        }
+      }
+    }
+  }
+  std::vector<int> tdims(nRV);
+  for (int r = 0; r < nRV; r++) tdims[r] = tdimOf(red[r].first, red[r].second);
+  int64_t leafDims = 1024;
+  if (const char* e = getenv("VIBA_ND_LEAF")) leafDims = std::max<int64_t>(64, atoll(e));
+  if (getenv("VIBA_ND_OFF")) leafDims = INT64_MAX;
+  std::vector<int> nord;             // final order (registration indices)
+  std::vector<size_t> partBegin;     // parts (tile-aligned) in nord
+  std::function<void(std::vector<int>&)> dissect = [&](std::vector<int>& vs) {
+    int64_t dims = 0;
+    for (int r : vs) dims += tdims[r];
+    auto emit = [&](std::vector<int>& part) {
+      if (part.empty()) return;
+      partBegin.push_back(nord.size());
+      nord.insert(nord.end(), part.begin(), part.end());
+    };
+    if (dims <= leafDims || vs.size() < 4) return emit(vs);
+    int64_t acc = 0;
+    size_t k = 0;
+    while (k < vs.size() && acc + tdims[vs[k]] <= dims / 2) acc += tdims[vs[k++]];
+    if (k == 0 || k >= vs.size()) return emit(vs);
+    const int cut = tp[vs[k]];
+    std::vector<int> L, R(vs.begin() + k, vs.end()), S;
+    int64_t sd = 0;
+    for (size_t i = 0; i < k; i++) {
+      if (hiP[vs[i]] >= cut) S.push_back(vs[i]), sd += tdims[vs[i]];
+      else L.push_back(vs[i]);
+    }
+    if (L.empty() || 2 * sd > dims) return emit(vs);  // no useful separator
+    dissect(L);
+    dissect(R);
+    emit(S);
+  };
+  {
+    std::vector<int> all(ord.begin(), ord.end());
+    dissect(all);
+  }
   h->rvKind.resize(nRV), h->rvHandle.resize(nRV), h->rvDim.resize(nRV), h->rvOff.resize(nRV + 1);
-  int64_t off = 0;
-  for (int i = 0; i < nRV; i++) {
-    const auto [kind, hh] = red[ord[i]];
-    h->rvKind[i] = kind, h->rvHandle[i] = hh, h->rvDim[i] = tdimOf(kind, hh), h->rvOff[i] = off;
-    off += h->rvDim[i];
-    redOf[kind][hh] = i;
+  std::vector<int64_t> padRows;
+  int64_t off = 0, nRedReal = 0;
+  {
+    size_t pi = 0;
+    for (int i = 0; i < nRV; i++) {
+      if (pi < partBegin.size() && partBegin[pi] == (size_t)i) {  // parts start on a tile boundary
+        const int64_t a = (off + TS - 1) / TS * TS;
+        for (int64_t r = off; r < a; r++) padRows.push_back(r);
+        off = a, pi++;
+      }
+      const auto [kind, hh] = red[nord[i]];
+      h->rvKind[i] = kind, h->rvHandle[i] = hh, h->rvDim[i] = tdims[nord[i]], h->rvOff[i] = off;
+      off += h->rvDim[i], nRedReal += h->rvDim[i];
+      redOf[kind][hh] = i;
+    }
+    const int64_t a = (off + TS - 1) / TS * TS;
+    for (int64_t r = off; r < a; r++) padRows.push_back(r);
   }
   h->rvOff[nRV] = off;
   const int64_t nRed = off;
+  h->nRedReal = nRedReal, h->nParts = (int64_t)partBegin.size();
   d.nRV = nRV, d.nRed = nRed, d.nPts = nPts;
   h->nParams = nPts + nRV;
-  h->order = nPts * 3 + nRed;
+  h->order = nPts * 3 + nRedReal;
+  if (upload(&h->padRowsD, padRows)) return VB_E_HIP;
+  h->nPadRows = (int64_t)padRows.size();
 
   // ---------------- visual observations, sorted by landmark (constant-point obs at the end)
   const int64_t nObs = (int64_t)h->fint[0].size();
@@ -670,25 +791,51 @@ int doFinalize(vb_handle h) {
     else if (thi < 0) h->tileFirst = 0, h->tileCount = 0;
     else h->tileFirst = tlo, h->tileCount = thi - tlo + 1;
   }
-  std::vector<int32_t> pairs, targets;
-  h->pairStart.assign(nT + 1, 0);
-  for (int32_t J = 0; J < nT; J++) {
-    const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
-    for (int64_t qi = 1; qi < n; qi++)
-      for (int64_t qk = 1; qk <= qi; qk++) {
-        pairs.push_back((int32_t)qi), pairs.push_back((int32_t)qk);
-        const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
-        if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
-        targets.push_back(t);
-      }
-    h->pairStart[J + 1] = (int64_t)targets.size();
-  }
   h->rowStart.assign(nT + 1, 0);
   h->rowTilesH.clear(), h->rowColH.clear();
   for (int32_t J = 0; J < nT; J++) {
     for (int32_t K = 0; K < J; K++)
       if (tileIdx[(size_t)J * nT + K] >= 0) h->rowTilesH.push_back(tileIdx[(size_t)J * nT + K]), h->rowColH.push_back(K);
     h->rowStart[J + 1] = (int64_t)h->rowTilesH.size();
+  }
+  // ---------------- level schedule of the tile Cholesky: a column's level is one more than the
+  // levels of the columns that update it (its row tiles); the columns of one level are independent
+  // and are factored by one batched potrf, one batched trsm and one batched update launch
+  {
+    std::vector<int32_t> level(nT, 0);
+    int32_t nLev = 0;
+    for (int32_t J = 0; J < nT; J++) {
+      for (int64_t i = h->rowStart[J]; i < h->rowStart[J + 1]; i++) level[J] = std::max(level[J], level[h->rowColH[i]] + 1);
+      nLev = std::max(nLev, level[J] + 1);
+    }
+    std::vector<std::vector<int32_t>> cols(nLev);
+    for (int32_t J = 0; J < nT; J++) cols[level[J]].push_back(J);
+    std::vector<int32_t> pT, pC, tD, tT, tC;
+    std::vector<int32_t> upd;  // 4 per pair: LI tile, LK tile, target tile, atomic
+    h->lvP.assign(nLev + 1, 0), h->lvT.assign(nLev + 1, 0), h->lvU.assign(nLev + 1, 0);
+    std::vector<int32_t> stamp(nTiles, -1), hits(nTiles, 0);
+    for (int32_t L = 0; L < nLev; L++) {
+      for (int32_t J : cols[L]) {
+        const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+        pT.push_back(h->colTilesH[c0]), pC.push_back(J);
+        for (int64_t q = 1; q < n; q++) tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J);
+        for (int64_t qi = 1; qi < n; qi++)
+          for (int64_t qk = 1; qk <= qi; qk++) {
+            const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
+            if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
+            if (stamp[t] != L) stamp[t] = L, hits[t] = 0;
+            hits[t]++;
+            upd.insert(upd.end(), {h->colTilesH[c0 + qi], h->colTilesH[c0 + qk], t, 0});
+          }
+      }
+      for (int64_t u = h->lvU[L]; u < (int64_t)upd.size() / 4; u++) upd[4 * u + 3] = hits[upd[4 * u + 2]] > 1 ? 1 : 0;
+      h->lvP[L + 1] = (int64_t)pT.size(), h->lvT[L + 1] = (int64_t)tT.size(), h->lvU[L + 1] = (int64_t)upd.size() / 4;
+    }
+    h->nLevels = nLev;
+    h->nPairs = (int64_t)upd.size() / 4;
+    if (upload(&h->potrfTileD, pT) || upload(&h->potrfColD, pC) || upload(&h->trsmDiagD, tD) ||
+        upload(&h->trsmTargetD, tT) || upload(&h->trsmColD, tC) || upload(&h->updD, upd))
+      return VB_E_HIP;
   }
   // ---------------- small factors (+ whitening square roots)
   for (int fk = 1; fk < 14; fk++) {
@@ -743,8 +890,8 @@ int doFinalize(vb_handle h) {
   if (upload(&h->colStartD, h->colStart) || upload(&h->rowStartD, h->rowStart) ||
       alloc0(&h->solveFlags, 2 * (size_t)nT))
     return VB_E_HIP;
-  if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) || upload(&h->pairsD, pairs) ||
-      upload(&h->targetsD, targets) || upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
+  if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) ||
+      upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
     return VB_E_HIP;
   if (alloc0(&h->dinv, (size_t)(nT + 1) * 1024) || alloc0(&h->linv, (size_t)nT * TS * TS)) return VB_E_HIP;
   d.nRS = h->nRS;
@@ -774,27 +921,17 @@ void visualCostShard(vb_handle h, int comparable) {
 
 void factorSeq(vb_handle h) {
   Dev& d = h->d;
-  bool diagReady = false;  // L_JJ already factored by the previous column's update launch
-  for (int32_t J = 0; J < d.nT; J++) {
-    const int64_t c0 = h->colStart[J];
-    const int n = (int)(h->colStart[J + 1] - c0);
-    if (!diagReady) {
-      profBegin(h, KF_POTRF);
-      launch_potrf(d, h->colTilesD + c0, h->dinv + (int64_t)J * 1024, h->st);
-      profEnd(h, KF_POTRF);
-    }
+  for (int32_t L = 0; L < h->nLevels; L++) {
+    const int64_t p0 = h->lvP[L], t0 = h->lvT[L], u0 = h->lvU[L];
+    profBegin(h, KF_POTRF);
+    launch_potrf(d, h->potrfTileD + p0, h->potrfColD + p0, (int)(h->lvP[L + 1] - p0), h->dinv, h->st);
+    profEnd(h, KF_POTRF);
     profBegin(h, KF_TRSM);
-    launch_trsm(d, h->colTilesD + c0, n, h->dinv + (int64_t)J * 1024, h->st);
+    launch_trsm(d, h->trsmDiagD + t0, h->trsmTargetD + t0, h->trsmColD + t0, (int)(h->lvT[L + 1] - t0), h->dinv, h->st);
     profEnd(h, KF_TRSM);
-    const int64_t p0 = h->pairStart[J];
-    const int np = (int)(h->pairStart[J + 1] - p0);
-    // pair 0 is (1, 1): the tile (row of off-diagonal 1)^2, the next diagonal when that row is J + 1
-    const bool fuse = np > 0 && h->colRowsH[c0 + 1] == J + 1 && !h->noFusePotrf;
     profBegin(h, KF_GEMM);
-    launch_update(d, h->colTilesD + c0, h->pairsD + 2 * p0, h->targetsD + p0, np, fuse ? 1 : 0,
-                  h->dinv + (int64_t)(J + 1) * 1024, h->st);
+    launch_update(d, h->updD + 4 * u0, (int)(h->lvU[L + 1] - u0), h->st);
     profEnd(h, KF_GEMM);
-    diagReady = fuse;
   }
   launch_diag_inverse(d, h->linv, h->st);
 }
@@ -922,7 +1059,6 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipSetDevice(c.device));
   vb_handle h = new vb_handle_s();
   h->cfg = c;
-  if (const char* e = getenv("VIBA_NO_FUSE_POTRF")) h->noFusePotrf = e[0] == '1';
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
   if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
   {
@@ -946,7 +1082,7 @@ int vb_destroy(vb_handle h) {
                   d.blkCol, d.pcRow, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
-                  h->colRowsD, h->pairsD, h->targetsD, h->rowTilesD, h->rowColD, h->colStartD, h->rowStartD, h->solveFlags, h->dinv, h->yvec,
+                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1010,7 +1146,7 @@ int vb_finalize(vb_handle h) {
   return doFinalize(h);
 }
 
-int64_t vb_reduced_order(vb_handle h) { return h ? h->d.nRed : -1; }
+int64_t vb_reduced_order(vb_handle h) { return h ? h->nRedReal : -1; }
 int64_t vb_total_order(vb_handle h) { return h ? h->order : -1; }
 
 int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_root) {
@@ -1029,7 +1165,7 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  if (h->isRoot) launch_pad_diag(d, h->st);
+  if (h->isRoot) launch_pad_diag(d, h->padRowsD, h->nPadRows, h->st);
   visualLinShard(h, update_cache, dont_retry_failed);
   if (h->isRoot) launch_small(d, 0, d.gRed, h->st);
   HIPCHK(hipEventRecord(h->ev[1], h->st));
@@ -1250,18 +1386,14 @@ int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
   if (!h || !h->finalized || !out) return fail(VB_E_STATE, "not finalized");
   const Dev& d = h->d;
   out[0] = d.nObs, out[1] = d.nPts, out[2] = d.nRV, out[3] = d.nRed, out[4] = d.nT, out[5] = d.nTiles;
-  out[6] = h->pairStart.empty() ? 0 : h->pairStart.back();
+  out[6] = h->nPairs;
   int64_t sm = 0;
   for (int k = 1; k < 14; k++) sm += d.sf[k].n;
   out[7] = sm;
   // Schur work-list sizes: landmark-pair entries, observation-pair entries
   out[8] = h->nTileEnt, out[9] = h->nObEnt;
-  // launches per factorization: tile GEMM update, trsm
-  int64_t nu = 0, nt = 0;
-  for (int32_t J = 0; J < d.nT; J++) {
-    nu += h->pairStart[J + 1] > h->pairStart[J];
-    nt += h->colStart[J + 1] - h->colStart[J] > 1;
-  }
+  // levels of the tile Cholesky (update / trsm launches per factorization), pairs per factorization
+  const int64_t nu = h->nLevels, nt = h->nLevels;
   out[10] = nu, out[11] = nt;
   return 0;
 }
@@ -1478,8 +1610,7 @@ int vb_assemble_new_rhs(vb_handle h) {
 // ---------------------------------------------------------------- kernel micro-benchmark (tuning aid)
 // Times one launch of a factorization kernel on scratch tiles (random SPD diagonal tile, random
 // off-diagonal tiles), averaged over `iters` launches, kernel-exact (hipExtLaunchKernelGGL events).
-// which: 0 standalone potrf, 1 trsm (one tile), 2 update with fused next-diagonal potrf (one pair),
-// 3 update (one pair, no fusion)
+// which: 0 potrf, 1 trsm (one tile), 2/3 update (one pair)
 extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us) {
   if (!h || !h->finalized || iters <= 0) return fail(VB_E_STATE, "vb_bench_kernel needs a finalized handle");
   Dev d = h->d;  // copy: tiles / err redirected to scratch
@@ -1500,9 +1631,10 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
   HIPCHK(hipMalloc(&tiles, 4 * TS * TS * sizeof(double)));
   HIPCHK(hipMalloc(&dinv, 2 * 1024 * sizeof(double)));
   HIPCHK(hipMalloc(&colT, 4 * sizeof(int32_t)));
-  HIPCHK(hipMalloc(&pairs, 2 * sizeof(int32_t)));
+  HIPCHK(hipMalloc(&pairs, 4 * sizeof(int32_t)));
   HIPCHK(hipMalloc(&targ, sizeof(int32_t)));
-  const int32_t ct[4] = {0, 1, 2, 3}, pr[2] = {1, 1}, tg[1] = {2};
+  // potrf: tile 0 (col 0); trsm: diag 0 -> target 1; update: (LI 1, LK 1) -> target 2 (plain)
+  const int32_t ct[4] = {0, 0, 1, 0}, pr[4] = {1, 1, 2, 0}, tg[1] = {0};
   HIPCHK(hipMemcpy(colT, ct, sizeof(ct), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(pairs, pr, sizeof(pr), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(targ, tg, sizeof(tg), hipMemcpyHostToDevice));
@@ -1517,11 +1649,11 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
     HIPCHK(hipMemcpyAsync(tiles, A.data(), tb, hipMemcpyHostToDevice, h->st));
     HIPCHK(hipMemcpyAsync(tiles + TS * TS, B.data(), tb, hipMemcpyHostToDevice, h->st));
     HIPCHK(hipMemcpyAsync(tiles + 2 * TS * TS, A.data(), tb, hipMemcpyHostToDevice, h->st));
-    if (which != 0) launch_potrf(d, colT, dinv, h->st);
+    if (which != 0) launch_potrf(d, colT, targ, 1, dinv, h->st);
     g_prof.start = e0, g_prof.stop = e1, g_prof.consumed = false;
-    if (which == 0) launch_potrf(d, colT, dinv, h->st);
-    else if (which == 1) launch_trsm(d, colT, 2, dinv, h->st);
-    else launch_update(d, colT, pairs, targ, 1, which == 2 ? 1 : 0, dinv + 1024, h->st);
+    if (which == 0) launch_potrf(d, colT, targ, 1, dinv, h->st);
+    else if (which == 1) launch_trsm(d, colT, colT + 2, targ, 1, dinv, h->st);
+    else launch_update(d, pairs, 1, h->st);
     g_prof = ProfSlot();
     HIPCHK(hipStreamSynchronize(h->st));
     float ms = 0;

@@ -587,13 +587,16 @@ __device__ __forceinline__ void lds_to_global(double* dst, const double* src, in
 }
 
 // factor the diagonal tile of column J in place (+ its 16 x 16 block inverses); one wave
-__global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* colTiles, double* dinvG) {
+// factor diagonal tile tiles[b] in place (+ its 16 x 16 block inverses into dinv[cols[b]]); one
+// wave per tile, all the diagonal tiles of one level per launch
+__global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileList, const int32_t* cols, double* dinvAll) {
   __shared__ double T[TS * TS];
   __shared__ double scratch[256];
   __shared__ double dinvS[1024];
   const int lane = threadIdx.x;
   POTRF_T(19);
-  double* A = d.tiles + (int64_t)colTiles[0] * TS * TS;
+  double* A = d.tiles + (int64_t)tileList[blockIdx.x] * TS * TS;
+  double* dinvG = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
   {
     double v[TS];
 #pragma unroll
@@ -610,11 +613,14 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* colTile
   POTRF_T(18);
 }
 
-// X = A L_JJ^-T for tile q = blockIdx.x + 1 of the column; wave w = 16-row block (all on MFMA)
-__global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* colTiles, const double* dinv) {
+// X = A L_JJ^-T for target tile target[b] with diagonal tile diag[b] of column cols[b]; wave w =
+// 16-row block (all on MFMA); every off-diagonal tile of one level per launch
+__global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagList, const int32_t* targetList,
+                                                   const int32_t* cols, const double* dinvAll) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const double* L = d.tiles + (int64_t)colTiles[0] * TS * TS;
-  double* A = d.tiles + (int64_t)colTiles[blockIdx.x + 1] * TS * TS;
+  const double* L = d.tiles + (int64_t)diagList[blockIdx.x] * TS * TS;
+  double* A = d.tiles + (int64_t)targetList[blockIdx.x] * TS * TS;
+  const double* dinv = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
   double4_t Xt[4];
   trsm_rowblock<4>(A, L, dinv, w, lane, Xt);
   const int lr = lane & 15, lq = lane >> 4;
@@ -624,22 +630,19 @@ __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* colTile
     for (int r = 0; r < 4; r++) A[(16 * k + lq + 4 * r) * TS + 16 * w + lr] = Xt[k][r];
 }
 
-// A_IK -= L_IJ L_KJ^T for pair blockIdx.x of column J.  Computed transposed, D = L_K L_I^T, so that
-// the MFMA output column (lane & 15) runs along the tile's contiguous row index: wave w owns the
-// 32 x 32 block (p in [32 (w >> 1), +32), q in [32 (w & 1), +32)) of C(q, p); operands are loaded
-// straight from the tile store in the v_mfma_f64_16x16x4_f64 layouts (A: lane -> (l & 15, l >> 4),
-// B: lane -> (l >> 4, l & 15)).  fuseDiag: block 0 (pair (1, 1) = tile (J+1, J+1)) then factors it.
-__global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* colTiles, const int32_t* pairs,
-                                                     const int32_t* targets, int fuseDiag, double* dinvNext) {
-  __shared__ double T[TS * TS];
-  __shared__ double scratch[256];
-  __shared__ double dinvS[1024];
-  const int p = blockIdx.x;
-  const int qi = pairs[2 * p], qk = pairs[2 * p + 1];
+// Target -= L_I L_K^T for work item blockIdx.x = (LI tile, LK tile, target tile, atomic) -- every
+// tile pair of the columns of one level per launch.  Computed transposed, D = L_K L_I^T, so that the
+// MFMA output column (lane & 15) runs along the tile's contiguous row index: wave w owns the 32 x 32
+// block (p in [32 (w >> 1), +32), q in [32 (w & 1), +32)) of C(q, p); operands are loaded straight from
+// the tile store in the v_mfma_f64_16x16x4_f64 layouts.  `atomic`: the target also receives an update
+// from another column of the same level (fp64 atomics), else a plain read-modify-write.
+__global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* work) {
+  const int32_t* wk = work + 4 * (int64_t)blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const double* LI = d.tiles + (int64_t)colTiles[qi] * TS * TS;
-  const double* LK = d.tiles + (int64_t)colTiles[qk] * TS * TS;
-  double* C = d.tiles + (int64_t)targets[p] * TS * TS;
+  const double* LI = d.tiles + (int64_t)wk[0] * TS * TS;
+  const double* LK = d.tiles + (int64_t)wk[1] * TS * TS;
+  double* C = d.tiles + (int64_t)wk[2] * TS * TS;
+  const bool atomic = wk[3] != 0;
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
   const int l15 = lane & 15, l4 = lane >> 4;
   double4_t acc[2][2];
@@ -647,13 +650,6 @@ __global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* colTi
   for (int a = 0; a < 2; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
-  double cv[2][2][4];
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) cv[a][b][r] = C[(pb + a * 16 + l4 + 4 * r) * TS + qb + b * 16 + l15];
 #pragma unroll
   for (int t0 = 0; t0 < TS; t0 += 4) {
     const int t = t0 + l4;
@@ -667,7 +663,6 @@ __global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* colTi
 #pragma unroll
       for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
   }
-  const bool fuse = fuseDiag && p == 0;
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -675,16 +670,9 @@ __global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* colTi
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int idx = (pb + a * 16 + l4 + 4 * r) * TS + qb + b * 16 + l15;
-        const double v = cv[a][b][r] - acc[a][b][r];
-        if (fuse) T[idx] = v;
-        else C[idx] = v;
+        if (atomic) atomicAdd(C + idx, -acc[a][b][r]);
+        else C[idx] -= acc[a][b][r];
       }
-  if (!fuse) return;
-  __syncthreads();
-  if (wave == 0) potrf_blocked(T, scratch, dinvS, lane, d.err);
-  __syncthreads();
-  lds_to_global(C, T, TS * TS, tid, 256);
-  lds_to_global(dinvNext, dinvS, 1024, tid, 256);
 }
 
 // Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
@@ -1070,28 +1058,27 @@ void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
   }
   if (d.nRV) hipLaunchKernelGGL(reduced_grad_kernel, dim3(d.nRV), dim3(256), 0, st, d, mode);
 }
-void launch_potrf(const Dev& d, const int32_t* colTiles, double* dinv, hipStream_t st) {
-  launchK(potrf_kernel, dim3(1), dim3(64), 0, st, d, colTiles, dinv);
+void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st) {
+  if (n > 0) launchK(potrf_kernel, dim3(n), dim3(64), 0, st, d, tiles, cols, dinv);
 }
-void launch_trsm(const Dev& d, const int32_t* colTiles, int n, const double* dinv, hipStream_t st) {
-  if (n > 1) launchK(trsm_kernel, dim3(n - 1), dim3(256), 0, st, d, colTiles, dinv);
+void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
+                 hipStream_t st) {
+  if (n > 0) launchK(trsm_kernel, dim3(n), dim3(256), 0, st, d, diag, target, cols, dinv);
 }
-void launch_update(const Dev& d, const int32_t* colTiles, const int32_t* pairs, const int32_t* targets, int npairs,
-                   int fuseDiag, double* dinvNext, hipStream_t st) {
-  if (npairs > 0)
-    launchK(update_kernel, dim3(npairs), dim3(256), 0, st, d, colTiles, pairs, targets, fuseDiag,
-                       dinvNext);
+void launch_update(const Dev& d, const int32_t* work, int n, hipStream_t st) {
+  if (n > 0) launchK(update_kernel, dim3(n), dim3(256), 0, st, d, work);
 }
 void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st) {
   if (d.nT) hipLaunchKernelGGL(diag_inverse_kernel, dim3(d.nT), dim3(64), 0, st, d, linv);
 }
-// identity on the diagonal of the padding rows of the last tile (rows >= nRed)
-__global__ void pad_diag_kernel(Dev d) {
-  const int64_t r = d.nRed + threadIdx.x;
-  if (r < (int64_t)d.nT * TS) *tile_ptr(d, r, r) = 1.0;
+// identity on the diagonal of the padding rows (rows of no variable: tile alignment of the
+// nested-dissection parts, and the tail of the last tile)
+__global__ void pad_diag_kernel(Dev d, const int64_t* rows, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) *tile_ptr(d, rows[i], rows[i]) = 1.0;
 }
-void launch_pad_diag(const Dev& d, hipStream_t st) {
-  if ((int64_t)d.nT * TS > d.nRed) hipLaunchKernelGGL(pad_diag_kernel, dim3(1), dim3(64), 0, st, d);
+void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(pad_diag_kernel, dim3(blocks(n, 256)), dim3(256), 0, st, d, rows, n);
 }
 void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
                 double* b, double* x, hipStream_t st) {
