@@ -28,7 +28,7 @@ void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
 void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st);
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
                  hipStream_t st);
-void launch_update(const Dev& d, const int32_t* work, int n, hipStream_t st);
+void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st);
 void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st);
 void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
@@ -214,7 +214,8 @@ struct vb_handle_s {
   int32_t nLevels = 0;
   int64_t nPairs = 0;
   int32_t *potrfTileD = nullptr, *potrfColD = nullptr, *trsmDiagD = nullptr, *trsmTargetD = nullptr,
-          *trsmColD = nullptr, *updD = nullptr;
+          *trsmColD = nullptr, *updD = nullptr, *fanPairsD = nullptr;
+  std::vector<int32_t> fanPairs;  // host staging of fanPairsD (freed after upload)
   std::vector<int64_t> rowStart;   // per tile row into rowTilesH / rowColH
   std::vector<int32_t> rowTilesH, rowColH;
   int32_t *colTilesD = nullptr, *colRowsD = nullptr, *rowTilesD = nullptr,
@@ -810,32 +811,68 @@ int doFinalize(vb_handle h) {
     }
     std::vector<std::vector<int32_t>> cols(nLev);
     for (int32_t J = 0; J < nT; J++) cols[level[J]].push_back(J);
-    std::vector<int32_t> pT, pC, tD, tT, tC;
-    std::vector<int32_t> upd;  // 4 per pair: LI tile, LK tile, target tile, atomic
-    h->lvP.assign(nLev + 1, 0), h->lvT.assign(nLev + 1, 0), h->lvU.assign(nLev + 1, 0);
-    std::vector<int32_t> stamp(nTiles, -1), hits(nTiles, 0);
-    for (int32_t L = 0; L < nLev; L++) {
-      for (int32_t J : cols[L]) {
-        const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
-        pT.push_back(h->colTilesH[c0]), pC.push_back(J);
-        for (int64_t q = 1; q < n; q++) tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J);
+    // contributions by target: column K's pair (qi >= qk) of off-diagonal tiles updates the target
+    // tile (row qi, row qk) with L_{qi,K} L_{qk,K}^T (counting sort by target tile)
+    std::vector<int64_t> ccnt(nTiles + 1, 0);
+    for (int pass = 0; pass < 2; pass++) {
+      std::vector<int64_t> pos;
+      if (pass == 1) {
+        for (int64_t t = 0; t < nTiles; t++) ccnt[t + 1] += ccnt[t];
+        pos.assign(ccnt.begin(), ccnt.end() - 1);
+        h->fanPairs.assign(2 * (size_t)ccnt[nTiles], 0);
+      }
+      for (int32_t K = 0; K < nT; K++) {
+        const int64_t c0 = h->colStart[K], n = h->colStart[K + 1] - c0;
         for (int64_t qi = 1; qi < n; qi++)
           for (int64_t qk = 1; qk <= qi; qk++) {
             const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
             if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
-            if (stamp[t] != L) stamp[t] = L, hits[t] = 0;
-            hits[t]++;
-            upd.insert(upd.end(), {h->colTilesH[c0 + qi], h->colTilesH[c0 + qk], t, 0});
+            if (pass == 0) {
+              ccnt[t + 1]++;
+            } else {
+              const int64_t at = pos[t]++;
+              h->fanPairs[2 * at] = h->colTilesH[c0 + qi], h->fanPairs[2 * at + 1] = h->colTilesH[c0 + qk];
+            }
           }
       }
-      for (int64_t u = h->lvU[L]; u < (int64_t)upd.size() / 4; u++) upd[4 * u + 3] = hits[upd[4 * u + 2]] > 1 ? 1 : 0;
-      h->lvP[L + 1] = (int64_t)pT.size(), h->lvT[L + 1] = (int64_t)tT.size(), h->lvU[L + 1] = (int64_t)upd.size() / 4;
+    }
+    if (ccnt[nTiles] >= INT32_MAX) return fail(VB_E_STATE, "tile Cholesky too large (contribution count)");
+    // per level: fan-in of the level's column tiles, then potrf of its diagonals, then trsm.  A
+    // target's list is cut into near-equal chunks of at most `cs` contributions, cs chosen per level
+    // so the launch has ~fanWgs workgroups (>= 4 contributions per chunk: one per wave)
+    int64_t fanWgs = 2048;
+    if (const char* e = getenv("VIBA_FANIN_WGS")) fanWgs = std::max<int64_t>(64, atoll(e));
+    std::vector<int32_t> pT, pC, tD, tT, tC, fan;
+    h->lvP.assign(nLev + 1, 0), h->lvT.assign(nLev + 1, 0), h->lvU.assign(nLev + 1, 0);
+    for (int32_t L = 0; L < nLev; L++) {
+      int64_t total = 0;
+      for (int32_t J : cols[L])
+        for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
+      const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
+      for (int32_t J : cols[L]) {
+        const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+        pT.push_back(h->colTilesH[c0]), pC.push_back(J);
+        for (int64_t q = 1; q < n; q++) tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J);
+        for (int64_t q = 0; q < n; q++) {
+          const int32_t t = h->colTilesH[c0 + q];
+          const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
+          if (m == 0) continue;
+          const int64_t nch = (m + cs - 1) / cs;
+          for (int64_t k = 0; k < nch; k++) {
+            const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
+            fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
+          }
+        }
+      }
+      h->lvP[L + 1] = (int64_t)pT.size(), h->lvT[L + 1] = (int64_t)tT.size(), h->lvU[L + 1] = (int64_t)fan.size() / 4;
     }
     h->nLevels = nLev;
-    h->nPairs = (int64_t)upd.size() / 4;
+    h->nPairs = ccnt[nTiles];
     if (upload(&h->potrfTileD, pT) || upload(&h->potrfColD, pC) || upload(&h->trsmDiagD, tD) ||
-        upload(&h->trsmTargetD, tT) || upload(&h->trsmColD, tC) || upload(&h->updD, upd))
+        upload(&h->trsmTargetD, tT) || upload(&h->trsmColD, tC) || upload(&h->updD, fan) ||
+        upload(&h->fanPairsD, h->fanPairs))
       return VB_E_HIP;
+    std::vector<int32_t>().swap(h->fanPairs);
   }
   // ---------------- small factors (+ whitening square roots)
   for (int fk = 1; fk < 14; fk++) {
@@ -923,15 +960,15 @@ void factorSeq(vb_handle h) {
   Dev& d = h->d;
   for (int32_t L = 0; L < h->nLevels; L++) {
     const int64_t p0 = h->lvP[L], t0 = h->lvT[L], u0 = h->lvU[L];
+    profBegin(h, KF_GEMM);
+    launch_fanin(d, h->updD + 4 * u0, h->fanPairsD, (int)(h->lvU[L + 1] - u0), h->st);
+    profEnd(h, KF_GEMM);
     profBegin(h, KF_POTRF);
     launch_potrf(d, h->potrfTileD + p0, h->potrfColD + p0, (int)(h->lvP[L + 1] - p0), h->dinv, h->st);
     profEnd(h, KF_POTRF);
     profBegin(h, KF_TRSM);
     launch_trsm(d, h->trsmDiagD + t0, h->trsmTargetD + t0, h->trsmColD + t0, (int)(h->lvT[L + 1] - t0), h->dinv, h->st);
     profEnd(h, KF_TRSM);
-    profBegin(h, KF_GEMM);
-    launch_update(d, h->updD + 4 * u0, (int)(h->lvU[L + 1] - u0), h->st);
-    profEnd(h, KF_GEMM);
   }
   launch_diag_inverse(d, h->linv, h->st);
 }
@@ -1082,7 +1119,7 @@ int vb_destroy(vb_handle h) {
                   d.blkCol, d.pcRow, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
-                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->dinv, h->yvec,
+                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->fanPairsD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1633,11 +1670,15 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
   HIPCHK(hipMalloc(&colT, 4 * sizeof(int32_t)));
   HIPCHK(hipMalloc(&pairs, 4 * sizeof(int32_t)));
   HIPCHK(hipMalloc(&targ, sizeof(int32_t)));
-  // potrf: tile 0 (col 0); trsm: diag 0 -> target 1; update: (LI 1, LK 1) -> target 2 (plain)
-  const int32_t ct[4] = {0, 0, 1, 0}, pr[4] = {1, 1, 2, 0}, tg[1] = {0};
+  // potrf: tile 0 (col 0); trsm: diag 0 -> target 1; fan-in: 4 x (L_IK 1, L_JK 1) -> target 2 (plain)
+  const int32_t ct[4] = {0, 0, 1, 0}, pr[4] = {2, 0, 4, 0}, tg[1] = {0};
+  const int32_t fp[8] = {1, 1, 1, 1, 1, 1, 1, 1};
   HIPCHK(hipMemcpy(colT, ct, sizeof(ct), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(pairs, pr, sizeof(pr), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(targ, tg, sizeof(tg), hipMemcpyHostToDevice));
+  int32_t* fpD = nullptr;
+  HIPCHK(hipMalloc(&fpD, sizeof(fp)));
+  HIPCHK(hipMemcpy(fpD, fp, sizeof(fp), hipMemcpyHostToDevice));
   d.tiles = tiles;
   hipEvent_t e0, e1;
   HIPCHK(hipEventCreate(&e0));
@@ -1653,7 +1694,7 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
     g_prof.start = e0, g_prof.stop = e1, g_prof.consumed = false;
     if (which == 0) launch_potrf(d, colT, targ, 1, dinv, h->st);
     else if (which == 1) launch_trsm(d, colT, colT + 2, targ, 1, dinv, h->st);
-    else launch_update(d, pairs, 1, h->st);
+    else launch_fanin(d, pairs, fpD, 1, h->st);
     g_prof = ProfSlot();
     HIPCHK(hipStreamSynchronize(h->st));
     float ms = 0;
@@ -1661,7 +1702,7 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
     if (it > 0) total += ms;  // first launch: warm-up
   }
   hipEventDestroy(e0), hipEventDestroy(e1);
-  hipFree(tiles), hipFree(dinv), hipFree(colT), hipFree(pairs), hipFree(targ);
+  hipFree(tiles), hipFree(dinv), hipFree(colT), hipFree(pairs), hipFree(targ), hipFree(fpD);
   if (avg_us) *avg_us = total * 1e3 / iters;
   return 0;
 }

@@ -630,49 +630,121 @@ __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagLis
     for (int r = 0; r < 4; r++) A[(16 * k + lq + 4 * r) * TS + 16 * w + lr] = Xt[k][r];
 }
 
-// Target -= L_I L_K^T for work item blockIdx.x = (LI tile, LK tile, target tile, atomic) -- every
-// tile pair of the columns of one level per launch.  Computed transposed, D = L_K L_I^T, so that the
-// MFMA output column (lane & 15) runs along the tile's contiguous row index: wave w owns the 32 x 32
-// block (p in [32 (w >> 1), +32), q in [32 (w & 1), +32)) of C(q, p); operands are loaded straight from
-// the tile store in the v_mfma_f64_16x16x4_f64 layouts.  `atomic`: the target also receives an update
-// from another column of the same level (fp64 atomics), else a plain read-modify-write.
-__global__ void __launch_bounds__(256) update_kernel(Dev d, const int32_t* work) {
-  const int32_t* wk = work + 4 * (int64_t)blockIdx.x;
+// Fan-in (left-looking) update of target tile (I, J): A_IJ -= sum_K L_IK L_JK^T over one chunk of the
+// target's contribution list, computed at the level of column J (right before its potrf / trsm), so
+// the target is read and written once per chunk instead of once per contribution.
+// work[4 b .. 4 b + 4) = (target tile, first contribution, count, atomic); pairs[2 c] = L_IK tile,
+// pairs[2 c + 1] = L_JK tile; `atomic`: the target's list is split over several chunks.
+//
+// The four waves share every contribution: wave w owns the 32 x 32 block (p in [32 (w >> 1), +32),
+// q in [32 (w & 1), +32)) of the product, computed transposed (D = L_JK L_IK^T, so the MFMA output
+// column lane & 15 runs along the tile's contiguous row index).  Operands are staged per quarter
+// contribution (K = 16 columns of both tiles, 16 KB) by async global_load_lds (16 B per lane) into a
+// three-deep LDS ring (48 KB: three workgroups per CU): stage s + 1 is in flight while stage s feeds
+// v_mfma_f64_16x16x4_f64 and the CU's other workgroups cover the rest of the HBM latency (measured on
+// config C: K 16 x 3 buffers 41.6 TF/s, 16 x 4 40.2, 8 x 4 38.3, 32 x 3 35.0, 8 x 8 32.0 -- the
+// workgroups per CU matter more than the depth of one ring).  Writing stage s + R - 2 into buffer
+// (s + R - 2) % R is safe after one barrier per stage: its last reader was stage s - 2.  Odd columns
+// are stored rotated by 16 rows so each half-wave of a ds_read_b64 (two columns) hits all 64 banks.
+#ifndef VIBA_FAN_K
+#define VIBA_FAN_K 16
+#define VIBA_FAN_RING 3
+#endif
+constexpr int kFanK = VIBA_FAN_K;          // columns per stage
+constexpr int kFanRing = VIBA_FAN_RING;    // stages in the LDS ring (kFanRing - 2 in flight)
+constexpr int kStage = 2 * kFanK * TS;     // doubles per stage: [L_JK, L_IK][kFanK columns][64 rows]
+constexpr int kGlds = kStage / 128 / 4;    // global_load_lds per wave per stage (1 KB = 128 doubles each)
+
+__device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, int32_t start, int s, double* buf,
+                                            int wave, int lane) {
+  const int64_t c = start + s / (TS / kFanK);
+  const int k0 = (s % (TS / kFanK)) * kFanK;
+  // constant address space: scalar loads (lgkmcnt), so no vmcnt wait drains the LDS ring
+  const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
+  const int64_t tk = pc[2 * c + 1], ti = pc[2 * c];
+  const int hi = lane >> 5;
+  const int row = (2 * (lane & 31) - 16 * hi) & 63;
+#pragma unroll
+  for (int j = 0; j < kGlds; j++) {
+    const int i = wave * kGlds + j, tile = i / (kFanK / 2), cp = i % (kFanK / 2);  // 1 KB = 2 columns each
+    const double* src = d.tiles + (tile ? ti : tk) * TS * TS + (int64_t)(k0 + 2 * cp + hi) * TS + row;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(buf + tile * kFanK * TS + cp * 2 * TS),
+                                     16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
+  __shared__ double stg[kFanRing * kStage];
+  static_assert(kGlds * (kFanRing - 2) <= 63 && kFanRing <= 8 && kFanRing >= 3, "vmcnt range");
+  const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const double* LI = d.tiles + (int64_t)wk[0] * TS * TS;
-  const double* LK = d.tiles + (int64_t)wk[1] * TS * TS;
-  double* C = d.tiles + (int64_t)wk[2] * TS * TS;
-  const bool atomic = wk[3] != 0;
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
   const int l15 = lane & 15, l4 = lane >> 4;
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  double* C = d.tiles + (int64_t)wk[0] * TS * TS;
+  const int32_t start = wk[1], nst = (TS / kFanK) * wk[2];
+  const bool atomic = wk[3] != 0;
   double4_t acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
+  for (int s = 0; s < kFanRing - 2 && s < nst; s++) fanin_issue(d, pairs, start, s, stg + s * kStage, wave, lane);
+  for (int s = 0; s < nst; s++) {
+    if (s + kFanRing - 2 < nst)
+      fanin_issue(d, pairs, start, s + kFanRing - 2, stg + ((s + kFanRing - 2) % kFanRing) * kStage, wave, lane);
+    // this wave's part of stage s landed (later stages may stay in flight)
+    switch (min(kFanRing - 2, nst - 1 - s)) {
+      case 6: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * kGlds) : "memory"); break;
+      case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * kGlds) : "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * kGlds) : "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * kGlds) : "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kGlds) : "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * kGlds) : "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's
+    __builtin_amdgcn_sched_barrier(0);
+    const double* bk = stg + (s % kFanRing) * kStage;
+    const double* bi = bk + kFanK * TS;
 #pragma unroll
-  for (int t0 = 0; t0 < TS; t0 += 4) {
-    const int t = t0 + l4;
-    double av[2], bv[2];
+    for (int t0 = 0; t0 < kFanK; t0 += 4) {
+      const int t = t0 + l4, rot = (t & 1) * 16;
+      double av[2], bv[2];
 #pragma unroll
-    for (int a = 0; a < 2; a++) av[a] = LK[t * TS + pb + a * 16 + l15];
+      for (int a = 0; a < 2; a++) av[a] = bk[t * TS + ((pb + a * 16 + l15 + rot) & 63)];
 #pragma unroll
-    for (int b = 0; b < 2; b++) bv[b] = LI[t * TS + qb + b * 16 + l15];
+      for (int b = 0; b < 2; b++) bv[b] = bi[t * TS + ((qb + b * 16 + l15 + rot) & 63)];
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  double* Cw = C + (pb + l4) * TS + qb + l15;
+  if (atomic) {
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
-      for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) atomicAdd(Cw + (a * 16 + 4 * r) * TS + b * 16, -acc[a][b][r]);
+  } else {  // all 16 loads in flight, then the stores
+    double v[2][2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) v[a][b][r] = Cw[(a * 16 + 4 * r) * TS + b * 16];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + b * 16] = v[a][b][r] - acc[a][b][r];
   }
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int idx = (pb + a * 16 + l4 + 4 * r) * TS + qb + b * 16 + l15;
-        if (atomic) atomicAdd(C + idx, -acc[a][b][r]);
-        else C[idx] -= acc[a][b][r];
-      }
 }
 
 // Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
@@ -1065,8 +1137,8 @@ void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const
                  hipStream_t st) {
   if (n > 0) launchK(trsm_kernel, dim3(n), dim3(256), 0, st, d, diag, target, cols, dinv);
 }
-void launch_update(const Dev& d, const int32_t* work, int n, hipStream_t st) {
-  if (n > 0) launchK(update_kernel, dim3(n), dim3(256), 0, st, d, work);
+void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
+  if (n > 0) launchK(fanin_kernel, dim3(n), dim3(256), 0, st, d, work, pairs);
 }
 void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st) {
   if (d.nT) hipLaunchKernelGGL(diag_inverse_kernel, dim3(d.nT), dim3(64), 0, st, d, linv);
