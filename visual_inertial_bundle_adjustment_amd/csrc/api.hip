@@ -894,7 +894,13 @@ int doFinalize(vb_handle h) {
     }
     if (upload(&sf.vars, h->fvars[fk])) return VB_E_HIP;
     if (upload(&sf.consts, cs)) return VB_E_HIP;
+    sf.stage = d.nSmallStage;
+    d.nSmallStage += sf.n;
   }
+  if (h->isRoot && d.nSmallStage > 0 &&
+      (alloc0(&d.sJ, (size_t)d.nSmallStage * kSmallJ) || alloc0(&d.sE, (size_t)d.nSmallStage * kSmallE) ||
+       alloc0(&d.sMeta, (size_t)d.nSmallStage * kSmallMeta)))
+    return VB_E_HIP;
   // ---------------- uploads
   for (int k = 0; k < 9; k++) {
     if (upload(&d.var[k], h->data[k])) return VB_E_HIP;
@@ -1131,6 +1137,11 @@ int vb_destroy(vb_handle h) {
   for (int k = 0; k < 14; k++) {
     if (d.sf[k].vars) hipFree(d.sf[k].vars);
     if (d.sf[k].consts) hipFree(d.sf[k].consts);
+  }
+  {
+    if (d.sJ) hipFree(d.sJ);
+    if (d.sE) hipFree(d.sE);
+    if (d.sMeta) hipFree(d.sMeta);
   }
   for (auto& e : h->ev) hipEventDestroy(e);
   for (auto& e : h->profEv) hipEventDestroy(e);

@@ -42,7 +42,15 @@ struct SmallFactors {  // one kind
   int32_t* vars = nullptr;   // n * nv
   double* consts = nullptr;  // n * nc (+ whitening appended for IMU / pose prior)
   int nv = 0, nc = 0;
+  int64_t stage = 0;  // first staging slot of this kind (factors of all kinds share the staging)
 };
+// staging of the small (non-visual) factors between evaluation and assembly: per slot s
+//   sJ[s * kSmallJ ..]      raw Jacobian rows, row stride kSmallCols (m x colc used)
+//   sE[s * kSmallE ..]      [loss weight rho', whitened residual e (m)]
+//   sMeta[s * kSmallMeta ..] [m, colc, nslots, whitening offset into sf.consts (-1: none), kind,
+//                           reduced id x10, column x10, dim x10]
+constexpr int kSmallRows = 23, kSmallCols = 80;
+constexpr int kSmallJ = kSmallRows * kSmallCols, kSmallE = 24, kSmallMeta = 36;
 
 // Schur assembly organised by target tile: each work item is one 64x64 tile (I, J) of the reduced
 // system and a chunk of its entry list, of one kind:
@@ -127,6 +135,10 @@ struct Dev {
   double *stepRed = nullptr, *stepPt = nullptr, *subRed = nullptr, *subPt = nullptr;
   // small factors
   SmallFactors sf[14];
+  int64_t nSmallStage = 0;
+  double* sJ = nullptr;
+  double* sE = nullptr;
+  int32_t* sMeta = nullptr;
   // rolling shutter
   int32_t nRS = 0;
   int64_t* rsOff = nullptr;

@@ -287,15 +287,17 @@ __global__ void __launch_bounds__(256) visual_cost_kernel(Dev d, int comparable,
 }
 
 // ------------------------------------------------------------------ small factors
-constexpr int kMaxM = 23;
-constexpr int kMaxCols = 80;
+constexpr int kMaxM = kSmallRows;
+constexpr int kMaxCols = kSmallCols;
 
+// J points into the factor's staging slot (HBM): the evaluation writes its Jacobian blocks there
+// directly instead of into a 15 KB per-thread scratch array
 struct SmallEval {
   int m = 0;
   int nslot = 0;
   int col[10], dim[10], red[10];
   double e[kMaxM];
-  double J[kMaxM][kMaxCols];
+  double (*J)[kMaxCols];
 };
 
 __device__ inline void imu_boxminus(const double* v, const double* r, const ImuIdx& J, double* res) {
@@ -497,6 +499,8 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
   double acc[1] = {0.0};
   if (k < a.n) {
     SmallEval E;
+    const int64_t slot = d.sf[FK].stage + k;
+    E.J = (double(*)[kMaxCols])(d.sJ + slot * kSmallJ);
     const int nv = kNV[FK];
     const int32_t* vi = a.vars + k * nv;
     const double* c = a.consts + k * a.nc;
@@ -514,7 +518,8 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
       colc += E.dim[s];
       E.red[s] = d.redOf[kind][h];
     }
-    for (int i = 0; i < kMaxM; i++)
+    constexpr int mRows = (FK >= 1 && FK <= 3) ? 9 : FK == 4 ? 3 : (FK == 5 || FK == 10) ? 23 : (FK == 6 || FK == 11) ? 17 : 6;
+    for (int i = 0; i < mRows; i++)
       for (int j = 0; j < colc; j++) E.J[i][j] = 0.0;
     bool whiten = false;
     const double* U = nullptr;
@@ -643,7 +648,8 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
         U = c + 43;
       }
     }
-    // whitening by a square root U of the precision (P = U^T U, row-major m x m)
+    // whitening of the residual by a square root U of the precision (P = U^T U, row-major m x m);
+    // the Jacobian is whitened by small_assemble_kernel
     const int m = E.m;
     if (whiten) {
       double te[kMaxM];
@@ -653,14 +659,6 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
         te[i] = s;
       }
       for (int i = 0; i < m; i++) E.e[i] = te[i];
-      for (int j = 0; j < colc; j++) {
-        for (int i = 0; i < m; i++) {
-          double s = 0;
-          for (int q = 0; q < m; q++) s += U[i * m + q] * E.J[q][j];
-          te[i] = s;
-        }
-        for (int i = 0; i < m; i++) E.J[i][j] = te[i];
-      }
     }
     double sq = 0;
     for (int i = 0; i < m; i++) sq += E.e[i] * E.e[i];
@@ -671,32 +669,82 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
       acc[0] = 0.5 * (useImuLoss ? huber_val(d.imu.a, d.imu.b, d.imu.k2, d.imu.h, sq) : sq);
     } else {
       acc[0] = 0.5 * rho;
-      const double w = sqrt(drho);
-      for (int s = 0; s < nv; s++) {
-        if (E.red[s] < 0) continue;
-        const int64_t ro = d.rvOff[E.red[s]];
-        for (int i = 0; i < E.dim[s]; i++) {
-          double gsum = 0;
-          for (int r = 0; r < m; r++) gsum += E.J[r][E.col[s] + i] * E.e[r];
-          atomicAdd(a.gOut + ro + i, drho * gsum);
-        }
-        if (a.mode != 0) continue;
-        for (int t = 0; t < nv; t++) {
-          if (E.red[t] < 0) continue;
-          const int64_t co = d.rvOff[E.red[t]];
-          for (int i = 0; i < E.dim[s]; i++)
-            for (int j = 0; j < E.dim[t]; j++) {
-              const int64_t R = ro + i, Cc = co + j;
-              if (R < Cc) continue;
-              double hs = 0;
-              for (int r = 0; r < m; r++) hs += E.J[r][E.col[s] + i] * E.J[r][E.col[t] + j];
-              atomicAdd(tile_addr(d, R, Cc), w * w * hs);
-            }
-        }
-      }
+      double* se = d.sE + slot * kSmallE;
+      se[0] = drho;
+      for (int i = 0; i < m; i++) se[1 + i] = E.e[i];
+      int32_t* mt = d.sMeta + slot * kSmallMeta;
+      mt[0] = m, mt[1] = colc, mt[2] = nv, mt[3] = whiten ? (int32_t)(U - a.consts) : -1, mt[4] = FK;
+      for (int s = 0; s < nv; s++) mt[5 + s] = E.red[s], mt[15 + s] = E.col[s], mt[25 + s] = E.dim[s];
     }
   }
   block_sum_atomic<1>(acc, d.red + (a.mode == 2 ? 1 : 0));
+}
+
+// Assembly of the staged small factors, one wave per factor (4 per workgroup): whitened Jacobian
+// U J in LDS (lane = column), gradient rho' J^T e (mode 0 / 1) and, in mode 0, the Gauss-Newton
+// block rho' J^T J over the factor's non-constant columns, lane-parallel over the lower-triangle
+// entries, fp64 atomics into the reduced tiles (Optimizer.cpp:136-146 via the factor stores'
+// jacobian accumulation, InertialFactor / PriorFactor / RandomWalkFactor).
+__global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, double* gOut) {
+  __shared__ double Jl[4][kMaxM * kMaxCols];
+  __shared__ int32_t act[4][kMaxCols][2];  // active column: (staged column, reduced row)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t slot = (int64_t)blockIdx.x * 4 + wave;
+  if (slot >= d.nSmallStage) return;
+  const int32_t* mt = d.sMeta + slot * kSmallMeta;
+  const int m = mt[0], colc = mt[1], nv = mt[2], uoff = mt[3], fk = mt[4];
+  const double* Jg = d.sJ + slot * kSmallJ;
+  const double* se = d.sE + slot * kSmallE;
+  const double drho = se[0];
+  double* J = Jl[wave];
+  const double* U = uoff >= 0 ? d.sf[fk].consts + uoff : nullptr;
+  for (int j = lane; j < colc; j += 64) {
+    double col[kMaxM];
+#pragma unroll
+    for (int i = 0; i < kMaxM; i++) col[i] = i < m ? Jg[i * kMaxCols + j] : 0.0;
+    if (U) {
+      for (int i = 0; i < m; i++) {
+        double s = 0;
+        for (int q = 0; q < m; q++) s += U[i * m + q] * col[q];
+        J[i * kMaxCols + j] = s;
+      }
+    } else {
+      for (int i = 0; i < m; i++) J[i * kMaxCols + j] = col[i];
+    }
+  }
+  if (lane == 0) {
+    int n = 0;
+    for (int s = 0; s < nv; s++) {
+      const int red = mt[5 + s];
+      if (red < 0) continue;
+      const int64_t ro = d.rvOff[red];
+      for (int i = 0; i < mt[25 + s]; i++) act[wave][n][0] = mt[15 + s] + i, act[wave][n][1] = (int32_t)(ro + i), n++;
+    }
+    act[wave][kMaxCols - 1][1] = n;  // count (slot kMaxCols - 1 is never a column: colc <= 80 incl. scratch)
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const int A = act[wave][kMaxCols - 1][1];
+  for (int a = lane; a < A; a += 64) {
+    const int c = act[wave][a][0];
+    double g = 0;
+    for (int r = 0; r < m; r++) g += J[r * kMaxCols + c] * se[1 + r];
+    atomicAdd(gOut + act[wave][a][1], drho * g);
+  }
+  if (mode != 0) return;
+  const int P = A * (A + 1) / 2;
+  for (int p = lane; p < P; p += 64) {
+    int a = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+    while (a * (a + 1) / 2 > p) a--;
+    while ((a + 1) * (a + 2) / 2 <= p) a++;
+    const int b = p - a * (a + 1) / 2;
+    const int ca = act[wave][a][0], cb = act[wave][b][0];
+    double hs = 0;
+    for (int r = 0; r < m; r++) hs += J[r * kMaxCols + ca] * J[r * kMaxCols + cb];
+    int64_t R = act[wave][a][1], C = act[wave][b][1];
+    if (R < C) { const int64_t t = R; R = C; C = t; }
+    atomicAdd(tile_addr(d, R, C), drho * hs);
+  }
 }
 
 // ------------------------------------------------------------------ launch wrappers
@@ -713,6 +761,8 @@ void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hi
                      lo, hi);
 }
 
+void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
+
 template <int FK>
 static void launch_one(const Dev& d, int mode, double* gOut, hipStream_t st) {
   const SmallFactors& f = d.sf[FK];
@@ -722,6 +772,12 @@ static void launch_one(const Dev& d, int mode, double* gOut, hipStream_t st) {
 }
 
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st) {
+  launch_small_eval(d, mode, gOut, st);
+  if (mode != 2 && d.nSmallStage > 0)
+    launchK(small_assemble_kernel, dim3((unsigned)((d.nSmallStage + 3) / 4)), dim3(256), 0, st, d, mode, gOut);
+}
+
+void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st) {
   launch_one<1>(d, mode, gOut, st);
   launch_one<2>(d, mode, gOut, st);
   launch_one<3>(d, mode, gOut, st);
