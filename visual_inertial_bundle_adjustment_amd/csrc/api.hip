@@ -588,6 +588,30 @@ int doFinalize(vb_handle h) {
       const int32_t r = blkRed[b];
       for (int j = 0; j < h->rvDim[r]; j++) pcRow[lmY[l] / 3 + blkCol[b] + j] = (int32_t)(h->rvOff[r] + j);
     }
+  // panel column -> landmark block, landmark block -> its observation slots (landmark_kernel)
+  std::vector<int32_t> pcBlk(lmY[nPts] / 3);
+  std::vector<int64_t> bxStart(blkRed.size() + 1, 0);
+  std::vector<int32_t> bxEnt;
+  {
+    for (int64_t l = 0; l < nPts; l++)
+      for (int64_t b = lmBlk[l]; b < lmBlk[l + 1]; b++)
+        for (int j = 0; j < h->rvDim[blkRed[b]]; j++) pcBlk[lmY[l] / 3 + blkCol[b] + j] = (int32_t)b;
+    auto blockOf = [&](int64_t l, int64_t o, int s) {
+      return std::lower_bound(blkRed.begin() + lmBlk[l], blkRed.begin() + lmBlk[l + 1], obRed[o * 4 + s]) - blkRed.begin();
+    };
+    for (int64_t l = 0; l < nPts; l++)
+      for (int64_t o = lmObs[l]; o < lmObs[l + 1]; o++)
+        for (int s = 0; s < 4; s++)
+          if (obRed[o * 4 + s] >= 0) bxStart[blockOf(l, o, s) + 1]++;
+    for (size_t b = 0; b < blkRed.size(); b++) bxStart[b + 1] += bxStart[b];
+    bxEnt.resize(bxStart[blkRed.size()]);
+    std::vector<int64_t> fb(bxStart.begin(), bxStart.end() - 1);
+    if (nObs >= (int64_t(1) << 29)) return fail(VB_E_ARG, "too many visual observations (2^29)");
+    for (int64_t l = 0; l < nPts; l++)
+      for (int64_t o = lmObs[l]; o < lmObs[l + 1]; o++)
+        for (int s = 0; s < 4; s++)
+          if (obRed[o * 4 + s] >= 0) bxEnt[fb[blockOf(l, o, s)]++] = (int32_t)((o << 2) | s);
+  }
   // incidence lists O(X), L(X)
   std::vector<int64_t> oxStart(nRV + 1, 0), lxStart(nRV + 1, 0);
   for (int64_t o = 0; o < nObs; o++)
@@ -916,7 +940,8 @@ int doFinalize(vb_handle h) {
     return VB_E_HIP;
   if (alloc0(&d.cache, nObs) || alloc0(&d.Jt, (size_t)kJPlanes * d.nObsPad)) return VB_E_HIP;
   if (upload(&d.lmObs, lmObs) || upload(&d.lmY, lmY) || upload(&d.lmBlk, lmBlk) || upload(&d.blkRed, blkRed) ||
-      upload(&d.blkCol, blkCol) || upload(&d.ptLm, lmOf) || upload(&d.pcRow, pcRow))
+      upload(&d.blkCol, blkCol) || upload(&d.ptLm, lmOf) || upload(&d.pcRow, pcRow) || upload(&d.pcBlk, pcBlk) ||
+      upload(&d.bxStart, bxStart) || upload(&d.bxEnt, bxEnt))
     return VB_E_HIP;
   if (alloc0(&d.Vchol, nPts * 6) || alloc0(&d.gp, nPts * 3) || alloc0(&d.z, nPts * 3) || alloc0(&d.xp, nPts * 3) ||
       alloc0(&d.Y, lmY[nPts]) || alloc0(&d.gpNew, nPts * 3) || alloc0(&d.zNew, nPts * 3))
@@ -1122,7 +1147,7 @@ int vb_destroy(vb_handle h) {
   Dev& d = h->d;
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
-                  d.blkCol, d.pcRow, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
+                  d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->fanPairsD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->dinv, h->yvec,

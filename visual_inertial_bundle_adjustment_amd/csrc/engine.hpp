@@ -101,6 +101,9 @@ struct Dev {
   int32_t* blkRed = nullptr;  // reduced ids of D(l), sorted by reduced offset
   int32_t* blkCol = nullptr;  // column offset in Y panel
   int32_t* pcRow = nullptr;   // reduced row of every Y panel column (indexed by lmY[l]/3 + c)
+  int32_t* pcBlk = nullptr;   // landmark block (into blkRed/blkCol) of every Y panel column
+  int64_t* bxStart = nullptr; // per landmark block: its observation slots bxEnt[bxStart[b] ..)
+  int32_t* bxEnt = nullptr;   // (obs << 2) | slot
   double *Vchol = nullptr, *gp = nullptr, *z = nullptr, *xp = nullptr, *Y = nullptr;
   double *gpNew = nullptr, *zNew = nullptr;
   int32_t* ptRed = nullptr;  // point param registered? (1/0) per point var handle

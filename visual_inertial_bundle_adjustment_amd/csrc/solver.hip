@@ -28,38 +28,44 @@ __device__ __forceinline__ double4_t mfma64(double a, double b, double4_t c) {
 __device__ inline int rv_dim(const Dev& d, int r) { return d.rvDim[r]; }
 
 // ------------------------------------------------------------------ landmark elimination
-// mode 0: full (V, Cholesky, z, Y); mode 1: gradient only into gpNew; mode 2: zNew = L^-1 gpNew
-__global__ void __launch_bounds__(128) landmark_kernel(Dev d, double lambda, int mode, int64_t lo, int64_t hi) {
-  const int64_t l = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per landmark (Optimizer.cpp:136-146 restricted to the point block, then the point part
+// of the sparse elimination, Optimizer.cpp:200-231):
+//   lanes over the landmark's observations: V = sum Jp^T Jp, g = sum Jp^T e (record planes 0..7,
+//   64 B of each 576 B record), wave reduction; every lane then holds the damped 3 x 3 Cholesky L
+//   mode 0: lanes over the Y panel columns: W(:, c) = sum over the observation slots of the column's
+//   block of Jp^T J_x(:, j), Y(:, c) = L^-1 W(:, c) (no atomics: each column has one owner)
+//   mode 1: gradient only into gpNew
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+__global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int mode, int64_t lo, int64_t hi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= hi) return;
-  const int64_t P = d.nObsPad;
   const double* Jt = d.Jt;
   const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
-  if (mode == 2) {
-    const double* L = d.Vchol + l * 6;
-    const double* g = d.gpNew + l * 3;
-    const double z0 = g[0] / L[0];
-    const double z1 = (g[1] - L[1] * z0) / L[3];
-    const double z2 = (g[2] - L[2] * z0 - L[4] * z1) / L[5];
-    d.zNew[l * 3] = z0, d.zNew[l * 3 + 1] = z1, d.zNew[l * 3 + 2] = z2;
-    return;
-  }
   double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  for (int64_t o = o0; o < o1; o++) {
-    const double a0 = Jt[o * kJPlanes + (kJpt + 0)], a1 = Jt[o * kJPlanes + (kJpt + 1)], a2 = Jt[o * kJPlanes + (kJpt + 2)];
-    const double b0 = Jt[o * kJPlanes + (kJpt + 3)], b1 = Jt[o * kJPlanes + (kJpt + 4)], b2 = Jt[o * kJPlanes + (kJpt + 5)];
-    const double e0 = Jt[o * kJPlanes + (kJe + 0)], e1 = Jt[o * kJPlanes + (kJe + 1)];
+  for (int64_t o = o0 + lane; o < o1; o += 64) {
+    const double* r = Jt + o * kJPlanes;
+    const double e0 = r[kJe], e1 = r[kJe + 1];
+    const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
+    const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
     g0 += a0 * e0 + b0 * e1, g1 += a1 * e0 + b1 * e1, g2 += a2 * e0 + b2 * e1;
     if (mode == 0) {
       v00 += a0 * a0 + b0 * b0, v10 += a1 * a0 + b1 * b0, v20 += a2 * a0 + b2 * b0;
       v11 += a1 * a1 + b1 * b1, v21 += a2 * a1 + b2 * b1, v22 += a2 * a2 + b2 * b2;
     }
   }
+  g0 = wave_sum(g0), g1 = wave_sum(g1), g2 = wave_sum(g2);
   if (mode == 1) {
-    d.gpNew[l * 3] = g0, d.gpNew[l * 3 + 1] = g1, d.gpNew[l * 3 + 2] = g2;
+    if (lane == 0) d.gpNew[l * 3] = g0, d.gpNew[l * 3 + 1] = g1, d.gpNew[l * 3 + 2] = g2;
     return;
   }
-  d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
+  v00 = wave_sum(v00), v10 = wave_sum(v10), v20 = wave_sum(v20);
+  v11 = wave_sum(v11), v21 = wave_sum(v21), v22 = wave_sum(v22);
   v00 = v00 * (1.0 + lambda) + lambda;
   v11 = v11 * (1.0 + lambda) + lambda;
   v22 = v22 * (1.0 + lambda) + lambda;
@@ -70,39 +76,46 @@ __global__ void __launch_bounds__(128) landmark_kernel(Dev d, double lambda, int
   const double l21 = (v21 - l20 * l10) / l11;
   const double d22 = v22 - l20 * l20 - l21 * l21;
   const double l22 = sqrt(d22);
-  if (!(v00 > 0) || !(d11 > 0) || !(d22 > 0)) atomicOr(d.err, 2);
-  double* L = d.Vchol + l * 6;
-  L[0] = l00, L[1] = l10, L[2] = l20, L[3] = l11, L[4] = l21, L[5] = l22;
-  const double z0 = g0 / l00, z1 = (g1 - l10 * z0) / l11, z2 = (g2 - l20 * z0 - l21 * z1) / l22;
-  d.z[l * 3] = z0, d.z[l * 3 + 1] = z1, d.z[l * 3 + 2] = z2;
-  // W panel (3 x d_l) then Y = L^-1 W in place
+  if (lane == 0) {
+    if (!(v00 > 0) || !(d11 > 0) || !(d22 > 0)) atomicOr(d.err, 2);
+    double* L = d.Vchol + l * 6;
+    L[0] = l00, L[1] = l10, L[2] = l20, L[3] = l11, L[4] = l21, L[5] = l22;
+    const double z0 = g0 / l00, z1 = (g1 - l10 * z0) / l11, z2 = (g2 - l20 * z0 - l21 * z1) / l22;
+    d.z[l * 3] = z0, d.z[l * 3 + 1] = z1, d.z[l * 3 + 2] = z2;
+    d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
+  }
+  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
   double* Y = d.Y + d.lmY[l];
-  const int64_t ncol = (d.lmY[l + 1] - d.lmY[l]) / 3;
-  for (int64_t c = 0; c < 3 * ncol; c++) Y[c] = 0.0;
-  for (int64_t o = o0; o < o1; o++) {
-    const double a0 = Jt[o * kJPlanes + (kJpt + 0)], a1 = Jt[o * kJPlanes + (kJpt + 1)], a2 = Jt[o * kJPlanes + (kJpt + 2)];
-    const double b0 = Jt[o * kJPlanes + (kJpt + 3)], b1 = Jt[o * kJPlanes + (kJpt + 4)], b2 = Jt[o * kJPlanes + (kJpt + 5)];
-    for (int s = 0; s < 4; s++) {
-      const int col = d.obCol[o * 4 + s];
-      if (col < 0) continue;
-      const int dim = rv_dim(d, d.obRed[o * 4 + s]);
-      const int pl = slotPlane(s), st = slotStride(s);
-      for (int j = 0; j < dim; j++) {
-        const double x0 = Jt[o * kJPlanes + (pl + j)], x1 = Jt[o * kJPlanes + (pl + st + j)];
-        double* w = Y + 3 * (col + j);
-        w[0] += a0 * x0 + b0 * x1;
-        w[1] += a1 * x0 + b1 * x1;
-        w[2] += a2 * x0 + b2 * x1;
-      }
+  for (int64_t c = lane; c < ncol; c += 64) {
+    const int32_t b = d.pcBlk[cb + c];
+    const int j = (int)(c - d.blkCol[b]);
+    double w0 = 0, w1 = 0, w2 = 0;
+    for (int64_t e = d.bxStart[b]; e < d.bxStart[b + 1]; e++) {
+      const int32_t ent = d.bxEnt[e];
+      const int s = ent & 3;
+      const double* r = Jt + (int64_t)(ent >> 2) * kJPlanes;
+      const double x0 = r[slotPlane(s) + j], x1 = r[slotPlane(s) + slotStride(s) + j];
+      w0 += r[kJpt + 0] * x0 + r[kJpt + 3] * x1;
+      w1 += r[kJpt + 1] * x0 + r[kJpt + 4] * x1;
+      w2 += r[kJpt + 2] * x0 + r[kJpt + 5] * x1;
     }
+    const double y0 = w0 / l00;
+    const double y1 = (w1 - l10 * y0) / l11;
+    const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
+    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
   }
-  for (int64_t c = 0; c < ncol; c++) {
-    double* w = Y + 3 * c;
-    const double y0 = w[0] / l00;
-    const double y1 = (w[1] - l10 * y0) / l11;
-    const double y2 = (w[2] - l20 * y0 - l21 * y1) / l22;
-    w[0] = y0, w[1] = y1, w[2] = y2;
-  }
+}
+
+// mode 2: zNew = L^-1 gpNew, one thread per landmark
+__global__ void __launch_bounds__(256) landmark_z_kernel(Dev d, int64_t lo, int64_t hi) {
+  const int64_t l = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= hi) return;
+  const double* L = d.Vchol + l * 6;
+  const double* g = d.gpNew + l * 3;
+  const double z0 = g[0] / L[0];
+  const double z1 = (g[1] - L[1] * z0) / L[3];
+  const double z2 = (g[2] - L[2] * z0 - L[4] * z1) / L[5];
+  d.zNew[l * 3] = z0, d.zNew[l * 3 + 1] = z1, d.zNew[l * 3 + 2] = z2;
 }
 
 // ------------------------------------------------------------------ Schur column assembly
@@ -1113,8 +1126,9 @@ static inline unsigned blocks(int64_t n, int b) { return (unsigned)((n + b - 1) 
 void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hipStream_t st);
 
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st) {
-  if (hi > lo)
-    launchK(landmark_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, lambda, mode, lo, hi);
+  if (hi <= lo) return;
+  if (mode == 2) launchK(landmark_z_kernel, dim3(blocks(hi - lo, 256)), dim3(256), 0, st, d, lo, hi);
+  else launchK(landmark_kernel, dim3(blocks(hi - lo, 4)), dim3(256), 0, st, d, lambda, mode, lo, hi);
 }
 // S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry)
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
