@@ -29,8 +29,12 @@ def hip():
 
 
 def assert_step_parity(og, orf, step_tol=1e-8, sub_tol=1e-7):
-    for k in ("cost0", "model_red", "back_red", "cost_restored"):
+    for k in ("cost0", "cost_restored"):
         assert abs(og[k] - orf[k]) <= 1e-10 * abs(orf[k]), (k, og[k], orf[k])
+    # model_red and back_red (= g . step) are functions of the step, so they carry the step's
+    # tolerance (fp64 atomics reorder the reduced-system sums from run to run)
+    for k in ("model_red", "back_red"):
+        assert abs(og[k] - orf[k]) <= step_tol * abs(orf[k]), (k, og[k], orf[k])
     assert abs(og["cost1"] - orf["cost1"]) <= 1e-9 * abs(orf["cost1"])
     assert tuple(og["stats1"]) == tuple(orf["stats1"])
     assert np.allclose(og["ratios"], orf["ratios"], rtol=1e-8, atol=0)

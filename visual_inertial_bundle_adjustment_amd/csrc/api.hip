@@ -714,7 +714,6 @@ int doFinalize(vb_handle h) {
   d.nTiles = nTiles;
   // ---------------- Schur assembly work by target tile (this shard's landmarks and observations)
   {
-    constexpr int kChunkLm = 64, kChunkObs = 128;  // entries per work item (bounded cost)
     std::vector<TileWork> works;
     // landmark entries
     struct Seg { int64_t t, c0, c1; };
@@ -790,21 +789,23 @@ int doFinalize(vb_handle h) {
     d.nGroups = (int64_t)gred.size() / 4;
     if (upload(&d.grpStart, gstart) || upload(&d.grpObs, gobs) || upload(&d.grpRed, gred)) return VB_E_HIP;
     std::vector<int32_t> tobs;
-    std::vector<int64_t> ocnt(nTiles + 1, 0);
+    // work items: a tile's landmark entries in near-equal chunks of at most kChunkLm; `kind` = 1 when
+    // the tile is split over several items (fp64 atomics), else the item owns the tile (plain RMW)
+    int64_t kChunkLm = 256;
+    if (const char* e = getenv("VIBA_SCHUR_CHUNK")) kChunkLm = std::max<int64_t>(8, std::min<int64_t>(256, atoll(e)));
     for (int32_t J = 0; J < nT; J++)
       for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
         const int32_t ti = h->colTilesH[c];
-        for (int kind = 0; kind < 1; kind++) {  // kind 1 (observations): groups above
-          const std::vector<int64_t>& cnt = kind ? ocnt : tcnt;
-          const int64_t n = cnt[ti + 1] - cnt[ti];
-          const int64_t ch = kind ? kChunkObs : kChunkLm;
-          for (int64_t k = 0; k < n; k += ch) {
-            TileWork w{};
-            w.tile = ti, w.I = h->colRowsH[c], w.J = J, w.count = (int32_t)std::min<int64_t>(ch, n - k);
-            w.start = cnt[ti] + k, w.kind = kind;
-            works.push_back(w);
-            tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti);
-          }
+        const int64_t n = tcnt[ti + 1] - tcnt[ti];
+        if (n == 0) continue;
+        const int64_t nch = (n + kChunkLm - 1) / kChunkLm;
+        for (int64_t k = 0; k < nch; k++) {
+          TileWork w{};
+          const int64_t s0 = n * k / nch, s1 = n * (k + 1) / nch;
+          w.tile = ti, w.I = h->colRowsH[c], w.J = J, w.count = (int32_t)(s1 - s0);
+          w.start = tcnt[ti] + s0, w.kind = nch > 1 ? 1 : 0;
+          works.push_back(w);
+          tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti);
         }
       }
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)

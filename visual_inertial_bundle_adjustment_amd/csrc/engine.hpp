@@ -65,9 +65,9 @@ struct TileEnt {
   uint32_t lm;          // landmark
 };
 struct TileWork {
-  int32_t tile, I, J, count;
-  int64_t start;  // into tileEnts (kind 0) or tileObs (kind 1)
-  int32_t kind, pad;
+  int32_t tile, I, J, count;  // count <= 256 landmark entries
+  int64_t start;              // into tileEnts
+  int32_t kind, pad;          // kind 1: the tile is split over several items (atomic epilogue)
 };
 
 struct Dev {

@@ -127,19 +127,23 @@ __device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
 }
 
 // Schur assembly by target tile (api.hip builds the work list; engine.hpp TileWork / TileEnt).
-// One workgroup per work item: a 64 x 64 tile (I, J) of the reduced system and a chunk of its entries.
-// Each batch of entries is scattered into LDS as K = 32 rows x 64 tile rows (operands Yi for tile I,
-// Yj for tile J; the same buffer on diagonal tiles):
-//   kind 0, landmarks (8 per batch): rows = the 3 rows of Y = L^-1 W (+ 1 zero row)   C -= Yi^T Yj
-//   kind 1, observations (16 per batch): rows = the 2 whitened residual rows          C += Ji^T Jj
-// and multiplied on v_mfma_f64_16x16x4_f64, transposed (D = Yj^T Yi) so that the MFMA output column
-// (lane & 15) runs along the tile's contiguous row index q; wave w owns the 32 x 32 block
-// (p in 32 (w >> 1) .., q in 32 (w & 1) ..).  Chunks of one tile may run concurrently: fp64 atomics.
-// Diagonal tiles also emit the RHS pieces (kind 0: rhs -= Y^T z; kind 1: gRed += J~^T e~) and, for
-// kind 1, the damping of the direct visual diagonal (Optimizer.cpp:136-146: d (1 + lambda)).
+// One workgroup per work item: a 64 x 64 tile (I, J) of the reduced system and up to 256 of its
+// landmark entries (staged in LDS at the start).  Each batch of 8 landmarks is scattered into LDS as
+// K = 32 rows x 64 tile rows: landmark e owns rows 4 e .. 4 e + 2 (its Y = L^-1 W panel rows; row
+// 4 e + 3 stays zero), so one landmark is exactly one k-step of v_mfma_f64_16x16x4_f64 and the update
+// C -= Yi^T Yj is a sum of rank-3 16 x 16 block products.  The fill records, per landmark, which
+// 16-row blocks of tile I and of tile J its columns touch; a k-step's MFMA on block pair (a, b) runs
+// only when both are touched.  The gathers of batch b + 1 (pcRow, Y, z) are issued into registers
+// before batch b's MFMAs, so their latency overlaps the products.  Computed transposed (D = Yj^T Yi)
+// so the MFMA output column (lane & 15) runs along the tile's contiguous row index q; wave w owns the
+// 32 x 32 block (p in 32 (w >> 1) .., q in 32 (w & 1) ..).  Odd K rows are stored with the column
+// XOR 16, so the two 16-lane halves of each ds_read_b64 half-wave (K rows k, k + 1, 512 B apart) hit
+// disjoint banks.  The LDS image is zeroed once; after each batch the filling threads clear exactly
+// the entries they wrote.  A tile split over several items
+// (wk.kind) is updated with fp64 atomics, else by a plain read-modify-write.  Diagonal tiles also
+// emit rhs -= Y^T z.
 constexpr int kTK = 32;       // K rows per batch
 constexpr int kTB = kTK / 4;  // landmarks per batch
-constexpr int kOB = kTK / 2;  // observations per batch
 
 // XCD-aware block id: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch), so
 // hand each XCD a contiguous range of work (bijective for any grid size)
@@ -148,75 +152,54 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-__device__ __forceinline__ void fill_landmarks(const Dev& d, const TileWork& wk, int b, bool diag, double* yi,
-                                               double* yj, double* zb, int tid) {
-  const int e0 = b * kTB, ne = min(kTB, wk.count - e0);
-  const int64_t rI = (int64_t)wk.I * TS, rJ = (int64_t)wk.J * TS;
-  for (int sl = tid; sl < ne * TS; sl += 256) {
-    const int eb = sl / TS, c = sl - eb * TS;
-    const TileEnt en = d.tileEnts[wk.start + e0 + eb];
+struct SchurSlots {  // one thread's two fill slots of a batch, in registers
+  double yI[2][3], yJ[2][3], z[2];
+  int rowI[2], rowJ[2], eb[2], c[2];
+};
+
+__device__ __forceinline__ void schur_gather(const Dev& d, const TileEnt* ents, int count, int b, bool diag, int64_t rI,
+                                             int64_t rJ, int tid, SchurSlots& S) {
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const int sl = tid + 256 * k;
+    const int eb = sl / TS, c = sl - eb * TS, e = b * kTB + eb;
+    S.eb[k] = eb, S.c[k] = c, S.rowI[k] = -1, S.rowJ[k] = -1;
+    if (e >= count) continue;
+    const TileEnt en = ents[e];
     if (c < en.nI) {
       const int64_t col = (int64_t)en.colI + c;
-      const int row = (int)(d.pcRow[col] - rI);
+      S.rowI[k] = (int)(d.pcRow[col] - rI);
       const double* y = d.Y + 3 * col;
-      const double y0 = y[0], y1 = y[1], y2 = y[2];
-      yi[(4 * eb) * TS + row] = y0, yi[(4 * eb + 1) * TS + row] = y1, yi[(4 * eb + 2) * TS + row] = y2;
+      S.yI[k][0] = y[0], S.yI[k][1] = y[1], S.yI[k][2] = y[2];
     }
     if (!diag && c < en.nJ) {
       const int64_t col = (int64_t)en.colJ + c;
-      const int row = (int)(d.pcRow[col] - rJ);
+      S.rowJ[k] = (int)(d.pcRow[col] - rJ);
       const double* y = d.Y + 3 * col;
-      const double y0 = y[0], y1 = y[1], y2 = y[2];
-      yj[(4 * eb) * TS + row] = y0, yj[(4 * eb + 1) * TS + row] = y1, yj[(4 * eb + 2) * TS + row] = y2;
+      S.yJ[k][0] = y[0], S.yJ[k][1] = y[1], S.yJ[k][2] = y[2];
     }
-    if (diag && c < 3) zb[4 * eb + c] = d.z[3 * (int64_t)en.lm + c];
+    if (diag && c < 3) S.z[k] = d.z[3 * (int64_t)en.lm + c];
   }
-}
-
-// observation rows: thread (e = tid / 16, sub = tid % 16) writes the columns sub, sub + 16, .. of
-// each reduced block of observation e that fall into the tile
-__device__ __forceinline__ void fill_obs_rows(const Dev& d, const double* rec, int64_t o, int64_t r0, int e, int sub,
-                                              double* y) {
-#pragma unroll
-  for (int sl = 0; sl < 4; sl++) {
-    const int32_t X = d.obRed[o * 4 + sl];
-    if (X < 0) continue;
-    const int64_t off = d.rvOff[X] - r0;
-    const int dim = d.rvDim[X];
-    const int pl = slotPlane(sl), st = slotStride(sl);
-    for (int j = sub; j < dim; j += 16) {
-      const int64_t row = off + j;
-      if (row < 0 || row >= TS) continue;
-      y[(2 * e) * TS + row] = rec[pl + j];
-      y[(2 * e + 1) * TS + row] = rec[pl + st + j];
-    }
-  }
-}
-__device__ __forceinline__ void fill_observations(const Dev& d, const TileWork& wk, int b, bool diag, double* yi,
-                                                  double* yj, double* zb, int tid) {
-  const int e0 = b * kOB, ne = min(kOB, wk.count - e0);
-  const int e = tid >> 4, sub = tid & 15;
-  if (e >= ne) return;
-  const int64_t o = d.tileObs[wk.start + e0 + e];
-  const double* rec = d.Jt + o * kJPlanes;
-  fill_obs_rows(d, rec, o, (int64_t)wk.I * TS, e, sub, yi);
-  if (!diag) fill_obs_rows(d, rec, o, (int64_t)wk.J * TS, e, sub, yj);
-  if (diag && sub < 2) zb[2 * e + sub] = rec[kJe + sub];
 }
 
 __global__ void __launch_bounds__(256) schur_tile_kernel(Dev d, double lambda) {
-  // single-buffered (32 KB LDS): the gathers' latency is hidden by resident workgroups
   __shared__ double Yi[kTK * TS];
   __shared__ double Yj[kTK * TS];
   __shared__ double zb[kTK];
+  __shared__ uint32_t msk[kTB];  // bits 0-3: row blocks of tile I, 4-7: of tile J
+  __shared__ TileEnt ents[256];
   const int64_t w = xcd_block(blockIdx.x, gridDim.x);
   const TileWork wk = d.tileWorks[w];
   const bool diag = wk.I == wk.J;
-  const bool obs = wk.kind == 1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  const int nb = (wk.count + (obs ? kOB : kTB) - 1) / (obs ? kOB : kTB);
+  const int nb = (wk.count + kTB - 1) / kTB;
+  const int64_t rI = (int64_t)wk.I * TS, rJ = (int64_t)wk.J * TS;
+  if (tid < wk.count) ents[tid] = d.tileEnts[wk.start + tid];
+  for (int i = tid; i < kTK * TS; i += 256) Yi[i] = 0.0, Yj[i] = 0.0;
+  if (tid < kTK) zb[tid] = 0.0;
+  __syncthreads();
   double4_t acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; a++)
@@ -224,50 +207,93 @@ __global__ void __launch_bounds__(256) schur_tile_kernel(Dev d, double lambda) {
     for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
   double racc = 0.0;
   const double* yj = diag ? Yi : Yj;
+  SchurSlots S;
+  schur_gather(d, ents, wk.count, 0, diag, rI, rJ, tid, S);
   for (int b = 0; b < nb; b++) {
-    for (int i = tid; i < kTK * TS; i += 256) {
-      Yi[i] = 0.0;
-      if (!diag) Yj[i] = 0.0;
-    }
-    if (tid < kTK) zb[tid] = 0.0;
-    __syncthreads();
-    if (obs) fill_observations(d, wk, b, diag, Yi, Yj, zb, tid);
-    else fill_landmarks(d, wk, b, diag, Yi, Yj, zb, tid);
-    __syncthreads();
+    int posI[2], posJ[2];
 #pragma unroll
-    for (int k0 = 0; k0 < kTK; k0 += 4) {
+    for (int k = 0; k < 2; k++) {
+      const int eb = S.eb[k];
+      uint32_t bits = 0;
+      posI[k] = -1, posJ[k] = -1;
+      if (S.rowI[k] >= 0) {
+        const int p = 4 * eb * TS + S.rowI[k];
+        Yi[p] = S.yI[k][0], Yi[(p + TS) ^ 16] = S.yI[k][1], Yi[p + 2 * TS] = S.yI[k][2];
+        posI[k] = p;
+        bits |= 1u << (S.rowI[k] >> 4);
+      }
+      if (S.rowJ[k] >= 0) {
+        const int p = 4 * eb * TS + S.rowJ[k];
+        Yj[p] = S.yJ[k][0], Yj[(p + TS) ^ 16] = S.yJ[k][1], Yj[p + 2 * TS] = S.yJ[k][2];
+        posJ[k] = p;
+        bits |= 16u << (S.rowJ[k] >> 4);
+      }
+      if (diag) bits |= bits << 4;
+      // slot k of every lane of this wave belongs to landmark eb = wave + 4 k: OR the bits over
+      // the wave by ballot and store once (an LDS atomic from 64 lanes on one word serialises)
+      uint32_t wb = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) wb |= __ballot((bits >> i) & 1u) ? (1u << i) : 0u;
+      if (lane == 0) msk[eb] = wb;
+      if (diag && S.c[k] < 3 && b * kTB + eb < wk.count) zb[4 * eb + S.c[k]] = S.z[k];
+    }
+    __syncthreads();
+    if (b + 1 < nb) schur_gather(d, ents, wk.count, b + 1, diag, rI, rJ, tid, S);
+#pragma unroll
+    for (int eb = 0; eb < kTB; eb++) {
+      const uint32_t m = msk[eb];
+      if (m == 0) continue;
+      const int k0 = 4 * eb;
       double av[2], bv[2];
 #pragma unroll
-      for (int a = 0; a < 2; a++) av[a] = yj[(k0 + l4) * TS + pb + a * 16 + l15];
+      for (int a = 0; a < 2; a++) av[a] = yj[(k0 + l4) * TS + ((pb + a * 16 + l15) ^ ((l4 & 1) << 4))];
 #pragma unroll
-      for (int bb = 0; bb < 2; bb++) bv[bb] = Yi[(k0 + l4) * TS + qb + bb * 16 + l15];
+      for (int bb = 0; bb < 2; bb++) bv[bb] = Yi[(k0 + l4) * TS + ((qb + bb * 16 + l15) ^ ((l4 & 1) << 4))];
 #pragma unroll
       for (int a = 0; a < 2; a++)
 #pragma unroll
-        for (int bb = 0; bb < 2; bb++) acc[a][bb] = mfma64(av[a], bv[bb], acc[a][bb]);
+        for (int bb = 0; bb < 2; bb++)
+          if ((m >> (4 + (pb >> 4) + a)) & (m >> ((qb >> 4) + bb)) & 1u) acc[a][bb] = mfma64(av[a], bv[bb], acc[a][bb]);
     }
     if (diag && tid < TS) {
 #pragma unroll 8
-      for (int k = 0; k < kTK; k++) racc += Yi[k * TS + tid] * zb[k];
+      for (int k = 0; k < kTK; k++) racc += Yi[k * TS + (tid ^ ((k & 1) << 4))] * zb[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      if (posI[k] >= 0) Yi[posI[k]] = 0.0, Yi[(posI[k] + TS) ^ 16] = 0.0, Yi[posI[k] + 2 * TS] = 0.0;
+      if (posJ[k] >= 0) Yj[posJ[k]] = 0.0, Yj[(posJ[k] + TS) ^ 16] = 0.0, Yj[posJ[k] + 2 * TS] = 0.0;
     }
     __syncthreads();
   }
-  double* C = d.tiles + (int64_t)wk.tile * TS * TS;
-  const double sign = obs ? 1.0 : -1.0;
+  double* Cw = d.tiles + (int64_t)wk.tile * TS * TS + (pb + l4) * TS + qb + l15;
+  if (wk.kind) {
 #pragma unroll
-  for (int a = 0; a < 2; a++)
+    for (int a = 0; a < 2; a++)
 #pragma unroll
-    for (int bb = 0; bb < 2; bb++)
+      for (int bb = 0; bb < 2; bb++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int p = pb + a * 16 + l4 + 4 * r, q = qb + bb * 16 + l15;
-        double v = acc[a][bb][r];
-        if (obs && diag && p == q) v *= 1.0 + lambda;
-        if (v != 0.0) atomicAdd(C + p * TS + q, sign * v);
-      }
+        for (int r = 0; r < 4; r++)
+          if (acc[a][bb][r] != 0.0) atomicAdd(Cw + (a * 16 + 4 * r) * TS + bb * 16, -acc[a][bb][r]);
+  } else {
+    double v[2][2][4];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) v[a][bb][r] = Cw[(a * 16 + 4 * r) * TS + bb * 16];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + bb * 16] = v[a][bb][r] - acc[a][bb][r];
+  }
   if (diag && tid < TS) {
-    const int64_t row = (int64_t)wk.I * TS + tid;
-    if (row < d.nRed && racc != 0.0) atomicAdd(obs ? d.gRed + row : d.rhs + row, obs ? racc : -racc);
+    const int64_t row = rI + tid;
+    if (row < d.nRed && racc != 0.0) atomicAdd(d.rhs + row, -racc);
   }
 }
 
