@@ -2,8 +2,11 @@
 // HBM layout (fp64 throughout, SoA where a kernel streams it):
 //   variables      var[kind]      rows of VB data size (3/7/3/3/24/7/32/7/4 doubles)
 //   visual obs     sorted by landmark; ob_* int32 index arrays + obC[6] (u, v, sqrtH 2x2)
-//   whitened J     Jt[o * kJPlanes + plane]: one 72-double record per observation (see kJ* below),
-//                  written once per linearize; read per landmark (landmark_kernel) and per block pair
+//   whitened J     one 72-double record per observation in two regions (jt_plane below):
+//                  A = planes 0..31 (e, point, pose, extrinsics), B = planes 32..71 (intrinsics,
+//                  velocity), each record-contiguous, so a wave's records are one contiguous span of
+//                  each region (full-line stores from the LDS-staged visual_lin_kernel); read per
+//                  landmark (landmark_kernel), per observation group and per reduced block
 //   landmarks      per point: Vchol[6], gp[3], z[3], xp[3]; Y panel 3 x d_l at Y + lmY[l]
 //   reduced system dense T x T column-major tiles (envelope / tile-sparse), tileIdx[I*nT+J]
 #pragma once
@@ -22,6 +25,12 @@ constexpr int kJextr = 20;  // 2x6
 constexpr int kJintr = 32;  // 2x17
 constexpr int kJvel = 66;   // 2x3
 constexpr int kJPlanes = 72;
+constexpr int kJA = 32, kJB = 40;  // planes of region A / B
+// plane `plane` of observation o's record (Jt regions: A [nObsPad x kJA], then B [nObsPad x kJB]);
+// a slot's planes (slotPlane(s) .. + 2 * slotStride(s)) never straddle the regions
+__host__ __device__ inline const double* jt_plane(const double* Jt, int64_t nPad, int64_t o, int plane) {
+  return plane < kJA ? Jt + o * kJA + plane : Jt + nPad * kJA + o * kJB + (plane - kJA);
+}
 // slot order of an observation's reduced blocks
 constexpr int kSlotPose = 0, kSlotExtr = 1, kSlotIntr = 2, kSlotVel = 3;
 __host__ __device__ inline int slotPlane(int s) {

@@ -45,9 +45,12 @@ __device__ void block_sum_atomic(double (&v)[N], double* out) {
 }
 
 // ------------------------------------------------------------------ visual factor evaluation
+// Jintr (2 x 17, rows at 0 and 17) points into the caller's LDS staging (visual_lin_kernel): the
+// largest block stays out of registers; unused when WantJ is false
 struct VisOut {
   double e[2];
-  double Jpt[6], Jpose[12], Jextr[12], Jintr[34], Jvel[6];
+  double Jpt[6], Jpose[12], Jextr[12], Jvel[6];
+  double* Jintr;
 };
 
 // VisualFactor::operator() (VisualFactor.cpp:40-82) for T_bw given; Jacobians wrt point, the
@@ -141,14 +144,13 @@ __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se
         for (int k = 0; k < 6; k++) s += Jt[r * 6 + k] * (lg[k] / kEps);
         dE[r] = s;
       }
-      int idx = n + (estRO ? 1 : 0) + (estOff ? 1 : 0);
-      if (estOff) {
-        --idx;
-        o.Jintr[idx] = -dE[0], o.Jintr[17 + idx] = -dE[1];
-      }
-      if (estRO) {
-        --idx;
-        o.Jintr[idx] = dE[0] * tpf, o.Jintr[17 + idx] = dE[1] * tpf;
+      // columns after the n projection parameters: readout time (if estimated), then time offset;
+      // written by an unrolled select (a runtime index would put the whole record in scratch)
+      const int iRO = estRO ? n : -1, iOff = estOff ? n + (estRO ? 1 : 0) : -1;
+#pragma unroll
+      for (int j = 0; j < 17; j++) {
+        if (j == iOff) o.Jintr[j] = -dE[0], o.Jintr[17 + j] = -dE[1];
+        if (j == iRO) o.Jintr[j] = dE[0] * tpf, o.Jintr[17 + j] = dE[1] * tpf;
       }
     }
     // pose Jacobian: Jt * (Adj(T_AtT_Mid) + [0, hat(R_AtT_w (v dt + 0.5 dt^2 g))])
@@ -185,16 +187,31 @@ __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se
 }
 
 // ------------------------------------------------------------------ visual kernels
-// mode bits: 1 = update cache, 2 = dont retry failed
-__global__ void __launch_bounds__(256) visual_lin_kernel(Dev d, int updateCache, int dontRetry,
-                                                         int64_t lo, int64_t hi) {
-  const int64_t o = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Linearization of the visual factors, one observation per lane.  The whitened record is staged in
+// LDS per wave and written as full lines of the Jt regions (A: planes 0..31, B: 32..71): a wave's 64
+// records are one contiguous span of each region, so every 16 B store of the copy loop lands in a
+// line the wave writes completely (per-lane 576 B record stores wrote partial lines, read for
+// ownership: 2.5x the algorithmic HBM traffic).  LDS record strides 33 / 41 doubles are odd, so the
+// per-lane ds_write_b64 of one plane hits 32 distinct banks.
+typedef double double2_t __attribute__((ext_vector_type(2)));
+constexpr int kVisBlock = 128;  // two waves, 2 x 21 KB of staging
+
+__global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int updateCache, int dontRetry, int64_t lo,
+                                                               int64_t hi) {
+  __shared__ double stage[kVisBlock / 64][64 * (kJB + 1)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ob = lo + (int64_t)blockIdx.x * kVisBlock + wave * 64;  // the wave's first record
+  const int64_t o = ob + lane;
+  const int nrec = (int)max<int64_t>(0, min<int64_t>(64, hi - ob));
+  double* S = stage[wave];
   double acc[1] = {0.0};
+  VisOut v;
+  v.Jintr = S + lane * (kJB + 1);  // region-B position of the record (intrinsics are planes 32..65)
+  bool ok = false;
+  double w = 0.0;
   if (o < hi) {
-    double* Jt = d.Jt;
-    const int64_t P = d.nObsPad;
-    VisOut v;
-    bool ok = true, oor = false;
+    ok = true;
+    bool oor = false;
     const double c0 = d.cache[o];
     if (dontRetry && c0 < 0.0) {
       ok = false;
@@ -224,24 +241,54 @@ __global__ void __launch_bounds__(256) visual_lin_kernel(Dev d, int updateCache,
       const double s = v.e[0] * v.e[0] + v.e[1] * v.e[1];
       double rho, drho;
       huber_jet2(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s, rho, drho);
-      const double w = sqrt(drho);
-      Jt[o * kJPlanes + (kJe + 0)] = w * v.e[0];
-      Jt[o * kJPlanes + (kJe + 1)] = w * v.e[1];
-#pragma unroll
-      for (int i = 0; i < 6; i++) Jt[o * kJPlanes + (kJpt + i)] = w * v.Jpt[i];
-#pragma unroll
-      for (int i = 0; i < 12; i++) Jt[o * kJPlanes + (kJpose + i)] = w * v.Jpose[i];
-#pragma unroll
-      for (int i = 0; i < 12; i++) Jt[o * kJPlanes + (kJextr + i)] = w * v.Jextr[i];
-#pragma unroll
-      for (int i = 0; i < 34; i++) Jt[o * kJPlanes + (kJintr + i)] = w * v.Jintr[i];
-#pragma unroll
-      for (int i = 0; i < 6; i++) Jt[o * kJPlanes + (kJvel + i)] = w * v.Jvel[i];
+      w = sqrt(drho);
       acc[0] = 0.5 * rho;
       if (updateCache) d.cache[o] = 0.5 * rho;
-    } else {
-#pragma unroll 8
-      for (int i = 0; i < kJPlanes; i++) Jt[o * kJPlanes + i] = 0.0;
+    }
+  }
+  // region B (intrinsics already in place from the evaluation): scale by w, velocity, copy out
+  if (lane < nrec) {
+    double* r = S + lane * (kJB + 1);
+#pragma unroll
+    for (int i = 0; i < 34; i++) r[i] = ok ? w * r[i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) r[kJvel - kJA + i] = ok ? w * v.Jvel[i] : 0.0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    double* dst = d.Jt + d.nObsPad * kJA + ob * kJB;
+    for (int q = lane; q < nrec * (kJB / 2); q += 64) {
+      const int r = q / (kJB / 2), c = 2 * (q % (kJB / 2));
+      const double* src = S + r * (kJB + 1) + c;
+      *(double2_t*)(dst + r * kJB + c) = double2_t{src[0], src[1]};
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // region A: e (2), point (6), pose (12), extrinsics (12)
+  if (lane < nrec) {
+    double* r = S + lane * (kJA + 1);
+#pragma unroll
+    for (int i = 0; i < 2; i++) r[kJe + i] = ok ? w * v.e[i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) r[kJpt + i] = ok ? w * v.Jpt[i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) r[kJpose + i] = ok ? w * v.Jpose[i] : 0.0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) r[kJextr + i] = ok ? w * v.Jextr[i] : 0.0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    double* dst = d.Jt + ob * kJA;
+    for (int q = lane; q < nrec * (kJA / 2); q += 64) {
+      const int r = q / (kJA / 2), c = 2 * (q % (kJA / 2));
+      const double* src = S + r * (kJA + 1) + c;
+      *(double2_t*)(dst + r * kJA + c) = double2_t{src[0], src[1]};
     }
   }
   block_sum_atomic<1>(acc, d.red + 0);
@@ -253,6 +300,7 @@ __global__ void __launch_bounds__(256) visual_cost_kernel(Dev d, int comparable,
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   if (o < hi) {
     VisOut v;
+    v.Jintr = nullptr;
     bool oor = false, ok;
     const double* obsC = d.obC + o * 6;
     const int pt = d.obPt[o];
@@ -751,8 +799,8 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
   const int64_t n = hi - lo;
-  launchK(visual_lin_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, updateCache, dontRetry, lo,
-          hi);
+  launchK(visual_lin_kernel, dim3((unsigned)((n + kVisBlock - 1) / kVisBlock)), dim3(kVisBlock), 0, st, d, updateCache,
+          dontRetry, lo, hi);
 }
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;

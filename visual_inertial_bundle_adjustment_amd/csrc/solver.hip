@@ -49,7 +49,7 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
   const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
   double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
   for (int64_t o = o0 + lane; o < o1; o += 64) {
-    const double* r = Jt + o * kJPlanes;
+    const double* r = Jt + o * kJA;  // planes 0..7 live in region A
     const double e0 = r[kJe], e1 = r[kJe + 1];
     const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
     const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
@@ -93,8 +93,10 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
     for (int64_t e = d.bxStart[b]; e < d.bxStart[b + 1]; e++) {
       const int32_t ent = d.bxEnt[e];
       const int s = ent & 3;
-      const double* r = Jt + (int64_t)(ent >> 2) * kJPlanes;
-      const double x0 = r[slotPlane(s) + j], x1 = r[slotPlane(s) + slotStride(s) + j];
+      const int64_t o = ent >> 2;
+      const double* r = Jt + o * kJA;
+      const double* x = jt_plane(Jt, d.nObsPad, o, slotPlane(s) + j);
+      const double x0 = x[0], x1 = x[slotStride(s)];
       w0 += r[kJpt + 0] * x0 + r[kJpt + 3] * x1;
       w1 += r[kJpt + 1] * x0 + r[kJpt + 4] * x1;
       w2 += r[kJpt + 2] * x0 + r[kJpt + 5] * x1;
@@ -334,10 +336,10 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
     const int64_t e = 2 * ks + (l4 >> 1);
     double v0 = 0.0, v1 = 0.0, er = 0.0;
     if (e < n) {
-      const double* rec = Jt + (int64_t)d.grpObs[o0 + e] * kJPlanes;
-      er = rec[kJe + r];
-      if (row0 >= 0) v0 = rec[p0 + r * s0];
-      if (row1 >= 0) v1 = rec[p1 + r * s1];
+      const int64_t o = d.grpObs[o0 + e];
+      er = Jt[o * kJA + kJe + r];
+      if (row0 >= 0) v0 = jt_plane(Jt, d.nObsPad, o, p0)[r * s0];
+      if (row1 >= 0) v1 = jt_plane(Jt, d.nObsPad, o, p1)[r * s1];
     }
     g0 += v0 * er, g1 += v1 * er;
     if (mode == 0) {
@@ -417,9 +419,10 @@ __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
       const int64_t o = d.oxObs[idx];
       if (!shard_obs(d, o)) continue;
       const int s1 = d.oxSlot[idx];
-      const double* rec = d.Jt + o * kJPlanes;
-      const int p1 = slotPlane(s1), st1 = slotStride(s1);
-      for (int j = 0; j < d1; j++) atomicAdd(&g[j], rec[p1 + j] * rec[kJe] + rec[p1 + st1 + j] * rec[kJe + 1]);
+      const double* ea = d.Jt + o * kJA;
+      const double* x = jt_plane(d.Jt, d.nObsPad, o, slotPlane(s1));
+      const int st1 = slotStride(s1);
+      for (int j = 0; j < d1; j++) atomicAdd(&g[j], x[j] * ea[kJe] + x[st1 + j] * ea[kJe + 1]);
     }
   } else {
     for (int64_t idx = d.lxStart[X1] + tid; idx < d.lxStart[X1 + 1]; idx += blockDim.x) {
@@ -1007,22 +1010,25 @@ void launch_solve_persistent(const Dev& d, const int64_t* rowStart, const int32_
 
 // ------------------------------------------------------------------ point back-substitution
 // x_p = L^-T (z - sum_b Y_b x_b); mode 0 uses z, mode 1 uses zNew
-__global__ void __launch_bounds__(128) backsub_kernel(Dev d, int mode, int64_t lo, int64_t hi, const double* xr,
+// points x_p = L^-T (z - Y x_c) (Optimizer.cpp:200-231, back-substitution of the eliminated point
+// range): one wave per landmark, lanes over its Y panel columns (coalesced 24 B per lane; pcRow maps
+// a column to its reduced row), wave reduction, lane 0 solves the 3 x 3 system
+__global__ void __launch_bounds__(256) backsub_kernel(Dev d, int mode, int64_t lo, int64_t hi, const double* xr,
                                                       double* xp) {
-  const int64_t l = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= hi) return;
-  const double* zz = mode ? d.zNew : d.z;
-  double t0 = zz[l * 3], t1 = zz[l * 3 + 1], t2 = zz[l * 3 + 2];
-  const double* Yl = d.Y + d.lmY[l];
-  for (int64_t b = d.lmBlk[l]; b < d.lmBlk[l + 1]; b++) {
-    const int X = d.blkRed[b];
-    const double* yb = Yl + 3 * d.blkCol[b];
-    const double* xv = xr + d.rvOff[X];
-    for (int j = 0; j < d.rvDim[X]; j++) {
-      const double v = xv[j];
-      t0 -= yb[3 * j] * v, t1 -= yb[3 * j + 1] * v, t2 -= yb[3 * j + 2] * v;
-    }
+  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
+  const double* Y = d.Y + d.lmY[l];
+  double t0 = 0, t1 = 0, t2 = 0;
+  for (int64_t c = lane; c < ncol; c += 64) {
+    const double v = xr[d.pcRow[cb + c]];
+    t0 += Y[3 * c] * v, t1 += Y[3 * c + 1] * v, t2 += Y[3 * c + 2] * v;
   }
+  t0 = wave_sum(t0), t1 = wave_sum(t1), t2 = wave_sum(t2);
+  if (lane != 0) return;
+  const double* zz = mode ? d.zNew : d.z;
+  t0 = zz[l * 3] - t0, t1 = zz[l * 3 + 1] - t1, t2 = zz[l * 3 + 2] - t2;
   const double* L = d.Vchol + l * 6;
   const double x2 = t2 / L[5];
   const double x1 = (t1 - L[4] * x2) / L[3];
@@ -1202,7 +1208,7 @@ void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* row
 }
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st) {
   if (hi > lo)
-    launchK(backsub_kernel, dim3(blocks(hi - lo, 128)), dim3(128), 0, st, d, mode, lo, hi, xr, xp);
+    launchK(backsub_kernel, dim3(blocks(hi - lo, 4)), dim3(256), 0, st, d, mode, lo, hi, xr, xp);
 }
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t st) {
   if (n > 0)
