@@ -135,12 +135,14 @@ def main():
     # stream, algorithmic work from the symbolic structure)
     avg_ms = kms / max(1, launches)
     if args.profile_family == KF_GEMM:
-        # st[6] tile pairs per factorization, st[10] update launches per factorization
+        # st[6] tile-pair contributions per factorization (2 * 64^3 flops each), st[10] levels = fan-in
+        # launches per factorization
         per_launch = st[6] * 2.0 * 64 ** 3 / max(1, st[10])
         achieved = per_launch / (avg_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": pmc_traffic("update_kernel"),
-                "kernel": "update_kernel (tile syrk/gemm on v_mfma_f64_16x16x4_f64, + fused next-diagonal potrf)",
+                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": pmc_traffic("fanin_kernel"),
+                "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
+                          "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
                 "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches}
     else:
         b = visual_bytes_per_launch(p, st[0])
