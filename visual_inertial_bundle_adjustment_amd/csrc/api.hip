@@ -36,10 +36,10 @@ void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, i
 void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
                 double* t, double* x, hipStream_t st);
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st);
-void launch_solve_persistent(const Dev& d, const int64_t* rowStart, const int32_t* rowTiles, const int32_t* rowCol,
-                             const int64_t* colStart, const int32_t* colTiles, const int32_t* colRows,
-                             const double* linv, const double* b, double* y, double* x, unsigned* flags, int G,
-                             hipStream_t st);
+void launch_solve_fanout(const Dev& d, const int32_t* tasksF, int64_t nF, const int32_t* tasksB, int64_t nB,
+                         const int32_t* expF, const int32_t* expB, const int32_t* colTiles, const int32_t* colRows,
+                         const int32_t* rowTiles, const int32_t* rowCol, const double* linv, double* b, double* y,
+                         double* x, unsigned* flags, int G, hipStream_t st);
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t st);
 void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hipStream_t st);
 void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, hipStream_t st);
@@ -222,6 +222,8 @@ struct vb_handle_s {
           *rowColD = nullptr;
   int64_t *colStartD = nullptr, *rowStartD = nullptr;
   unsigned* solveFlags = nullptr;
+  int32_t *solveTasksFD = nullptr, *solveTasksBD = nullptr, *solveExpFD = nullptr, *solveExpBD = nullptr;
+  int64_t nSolveTasksF = 0, nSolveTasksB = 0;
   int numCUs = 256;
   bool legacySolve = false;  // VIBA_SOLVE_LEGACY=1: one launch pair per tile column
   double *dinv = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
@@ -836,6 +838,28 @@ int doFinalize(vb_handle h) {
     }
     std::vector<std::vector<int32_t>> cols(nLev);
     for (int32_t J = 0; J < nT; J++) cols[level[J]].push_back(J);
+    // fan-out triangular solve task lists (solver.hip fwd/bwd_fanout_kernel), by elimination level:
+    // every task of a level only waits on tasks of earlier levels (or the level's own diagonal task
+    // listed first), so the waves' in-flight window spans all independent subtrees of the level
+    {
+      std::vector<int32_t> tf, tb, ef(nT), eb(nT);
+      for (int32_t L = 0; L < nLev; L++)
+        for (int32_t K : cols[L]) {
+          tf.insert(tf.end(), {K, -1});
+          for (int64_t c = h->colStart[K] + 1; c < h->colStart[K + 1]; c++) tf.insert(tf.end(), {K, (int32_t)c});
+          ef[K] = (int32_t)(h->rowStart[K + 1] - h->rowStart[K]);
+          eb[K] = (int32_t)(h->colStart[K + 1] - h->colStart[K] - 1);
+        }
+      for (int32_t L = nLev - 1; L >= 0; L--)
+        for (int32_t J : cols[L]) {
+          tb.insert(tb.end(), {J, -1});
+          for (int64_t c = h->rowStart[J]; c < h->rowStart[J + 1]; c++) tb.insert(tb.end(), {J, (int32_t)c});
+        }
+      h->nSolveTasksF = (int64_t)tf.size() / 2, h->nSolveTasksB = (int64_t)tb.size() / 2;
+      if (upload(&h->solveTasksFD, tf) || upload(&h->solveTasksBD, tb) || upload(&h->solveExpFD, ef) ||
+          upload(&h->solveExpBD, eb))
+        return VB_E_HIP;
+    }
     // contributions by target: column K's pair (qi >= qk) of off-diagonal tiles updates the target
     // tile (row qi, row qk) with L_{qi,K} L_{qk,K}^T (counting sort by target tile)
     std::vector<int64_t> ccnt(nTiles + 1, 0);
@@ -957,7 +981,7 @@ int doFinalize(vb_handle h) {
       alloc0(&d.subPt, nPts * 3) || alloc0(&h->yvec, nPad) || alloc0(&h->rhsWork, nPad))
     return VB_E_HIP;
   if (upload(&h->colStartD, h->colStart) || upload(&h->rowStartD, h->rowStart) ||
-      alloc0(&h->solveFlags, 2 * (size_t)nT))
+      alloc0(&h->solveFlags, 4 * (size_t)nT))
     return VB_E_HIP;
   if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) ||
       upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
@@ -1054,8 +1078,9 @@ int solveReduced(vb_handle h) {
   if (!h->legacySolve) {
     Dev& d = h->d;
     profBegin(h, KF_FWD);
-    launch_solve_persistent(d, h->rowStartD, h->rowTilesD, h->rowColD, h->colStartD, h->colTilesD, h->colRowsD, h->linv,
-                            h->rhsWork, h->yvec, d.xRed, h->solveFlags, h->numCUs, h->st);
+    launch_solve_fanout(d, h->solveTasksFD, h->nSolveTasksF, h->solveTasksBD, h->nSolveTasksB, h->solveExpFD,
+                        h->solveExpBD, h->colTilesD, h->colRowsD, h->rowTilesD, h->rowColD, h->linv, h->rhsWork, h->yvec,
+                        d.xRed, h->solveFlags, h->numCUs, h->st);
     profEnd(h, KF_FWD);
     return 0;
   }
@@ -1151,7 +1176,7 @@ int vb_destroy(vb_handle h) {
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
-                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->fanPairsD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->dinv, h->yvec,
+                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->fanPairsD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->solveTasksFD, h->solveTasksBD, h->solveExpFD, h->solveExpBD, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);

@@ -916,96 +916,125 @@ __device__ __forceinline__ void publish(double* dst, double v, bool valid, unsig
   if (lane == 0) __hip_atomic_store((guint*)flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// forward: y_J = Linv_JJ (b_J - sum_{K<J} L_JK y_K); the waves split the row's tiles (K ascending)
-__global__ void __launch_bounds__(256) fwd_persistent_kernel(Dev d, const int64_t* rowStart, const int32_t* rowTiles,
-                                                             const int32_t* rowCol, const double* linv, const double* b,
-                                                             double* y, unsigned* flags, int G) {
-  __shared__ double part[4][TS];
-  __shared__ double ys[4][TS];
-  __shared__ double ts[TS];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int J = blockIdx.x; J < d.nT; J += G) {
-    double sacc = 0.0;
-    const int64_t r0 = rowStart[J], r1 = rowStart[J + 1];
-    for (int64_t idx = r0 + w; idx < r1; idx += 4) {
-      const int K = rowCol[idx];
-      const double* A = d.tiles + (int64_t)rowTiles[idx] * TS * TS;
+// Fan-out (right-looking) triangular solves, one persistent launch per direction.  Every wave walks
+// its share of a task list in topological order (task t -> wave t mod W):
+//   forward, per column K ascending: [diag K: wait until the cnt[K] = rows(K) updates of b_K landed,
+//     y_K = Linv_KK b_K, publish y_K + ready[K]] then one task per off-diagonal tile (I, K):
+//     wait ready[K], b_I -= L_IK y_K (agent-scope fp64 atomics), cnt[I] += 1
+//   backward, per row J descending: [diag J: wait cnt[J] = (off-diagonal tiles of column J),
+//     x_J = Linv_JJ^T y_J, publish] then per tile (J, K) of row J: wait ready[J], y_K -= L_JK^T x_J
+// A task waits only on tasks with smaller indices, so the smallest unfinished task can always run
+// (no deadlock with every wave resident: the grid is one workgroup per CU).  Tile operands are loaded
+// before the wait.  The critical path is the elimination-tree depth (~110 levels at config C), not
+// the longest row: a separator column's hundreds of row tiles are spread over all waves.
+// Hand-offs follow the guide's G16 recipe: payload by sc1 stores / agent atomics, s_waitcnt
+// vmcnt(0), then the flag or counter; consumers poll, then read the payload with sc1 loads.
+__device__ __forceinline__ bool wait_count(unsigned* c, unsigned expect, int lane, int32_t* err) {
+  unsigned v = 0;
+  if (lane == 0) {
+    for (unsigned spins = 0;; spins++) {
+      v = __hip_atomic_load((guint*)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v >= expect || spins > (1u << 24)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (v < expect) atomicOr(err, 16);
+  }
+  v = __shfl(v, 0, 64);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return v >= expect;
+}
+__device__ __forceinline__ void count_up(unsigned* c, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_add((guint*)c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void add_agent(double* p, double v) {
+  __hip_atomic_fetch_add((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void __launch_bounds__(256) fwd_fanout_kernel(Dev d, const int32_t* tasks, int64_t nTask,
+                                                         const int32_t* colTiles, const int32_t* colRows,
+                                                         const int32_t* expect, const double* linv, double* b,
+                                                         double* y, unsigned* ready, unsigned* cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t W = (int64_t)gridDim.x * 4;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < nTask; t += W) {
+    const int K = tasks[2 * t], c = tasks[2 * t + 1];
+    if (c < 0) {
+      const double* Li = linv + (int64_t)K * TS * TS;
       double a[TS];
 #pragma unroll
-      for (int c = 0; c < TS; c++) a[c] = A[c * TS + lane];  // tile loads overlap the wait
-      if (!wait_flag(flags + K, lane, d.err)) return;
-      ys[w][lane] = ld_sc1(y + (int64_t)K * TS + lane);
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int c = 0; c < TS; c++) sacc += a[c] * ys[w][c];
-      __builtin_amdgcn_wave_barrier();
-    }
-    part[w][lane] = sacc;
-    __syncthreads();
-    if (w == 0) {
-      const int64_t row = (int64_t)J * TS + lane;
-      ts[lane] = b[row] - (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
-      __builtin_amdgcn_wave_barrier();
-      const double* Li = linv + (int64_t)J * TS * TS;
+      for (int q = 0; q < TS; q++) a[q] = Li[q * TS + lane];
+      if (!wait_count(cnt + K, (unsigned)expect[K], lane, d.err)) return;
+      const int64_t row = (int64_t)K * TS + lane;
+      const double bk = ld_sc1(b + row);
       double v = 0.0;
-#pragma unroll 16
-      for (int c = 0; c < TS; c++) v += Li[c * TS + lane] * ts[c];
-      publish(y + row, row < d.nRed ? v : 0.0, true, flags + J, lane);
+#pragma unroll
+      for (int q = 0; q < TS; q++) v += a[q] * __shfl(bk, q, 64);
+      publish(y + row, row < d.nRed ? v : 0.0, true, ready + K, lane);
+    } else {
+      const int I = colRows[c];
+      const double* A = d.tiles + (int64_t)colTiles[c] * TS * TS;
+      double a[TS];
+#pragma unroll
+      for (int q = 0; q < TS; q++) a[q] = A[q * TS + lane];  // L(I row lane, K col q)
+      if (!wait_flag(ready + K, lane, d.err)) return;
+      const double yk = ld_sc1(y + (int64_t)K * TS + lane);
+      double v = 0.0;
+#pragma unroll
+      for (int q = 0; q < TS; q++) v += a[q] * __shfl(yk, q, 64);
+      add_agent(b + (int64_t)I * TS + lane, -v);
+      count_up(cnt + I, lane);
     }
-    __syncthreads();
   }
 }
 
-// backward: x_J = Linv_JJ^T (y_J - sum_{I>J} L_IJ^T x_I); tiles of column J, I descending
-__global__ void __launch_bounds__(256) bwd_persistent_kernel(Dev d, const int64_t* colStart, const int32_t* colTiles,
-                                                             const int32_t* colRows, const double* linv, const double* yv,
-                                                             double* x, unsigned* flags, int G) {
-  __shared__ double part[4][TS];
-  __shared__ double xs[4][TS];
-  __shared__ double ts[TS];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int J = d.nT - 1 - (int)blockIdx.x; J >= 0; J -= G) {
-    double sacc = 0.0;
-    const int64_t c0 = colStart[J], c1 = colStart[J + 1];
-    // off-diagonal tiles c0+1 .. c1-1 (rows I ascending): walk them descending, split over the waves
-    for (int64_t idx = c1 - 1 - w; idx > c0; idx -= 4) {
-      const int I = colRows[idx];
-      const double* A = d.tiles + (int64_t)colTiles[idx] * TS * TS;  // tile (I, J): A[q * TS + r] = L(r, q)
+__global__ void __launch_bounds__(256) bwd_fanout_kernel(Dev d, const int32_t* tasks, int64_t nTask,
+                                                         const int32_t* rowTiles, const int32_t* rowCol,
+                                                         const int32_t* expect, const double* linv, double* yv,
+                                                         double* x, unsigned* ready, unsigned* cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t W = (int64_t)gridDim.x * 4;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < nTask; t += W) {
+    const int J = tasks[2 * t], c = tasks[2 * t + 1];
+    if (c < 0) {
+      const double* Li = linv + (int64_t)J * TS * TS;
       double a[TS];
 #pragma unroll
-      for (int r = 0; r < TS; r++) a[r] = A[lane * TS + r];
-      if (!wait_flag(flags + I, lane, d.err)) return;
-      xs[w][lane] = ld_sc1(x + (int64_t)I * TS + lane);
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int r = 0; r < TS; r++) sacc += a[r] * xs[w][r];
-      __builtin_amdgcn_wave_barrier();
-    }
-    part[w][lane] = sacc;
-    __syncthreads();
-    if (w == 0) {
+      for (int r = 0; r < TS; r++) a[r] = Li[lane * TS + r];  // Linv^T
+      if (!wait_count(cnt + J, (unsigned)expect[J], lane, d.err)) return;
       const int64_t row = (int64_t)J * TS + lane;
-      ts[lane] = yv[row] - (part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane]);
-      __builtin_amdgcn_wave_barrier();
-      const double* Li = linv + (int64_t)J * TS * TS;
+      const double tj = ld_sc1(yv + row);
       double v = 0.0;
-#pragma unroll 16
-      for (int r = 0; r < TS; r++) v += Li[lane * TS + r] * ts[r];
-      publish(x + row, row < d.nRed ? v : 0.0, true, flags + J, lane);
+#pragma unroll
+      for (int r = 0; r < TS; r++) v += a[r] * __shfl(tj, r, 64);
+      publish(x + row, row < d.nRed ? v : 0.0, true, ready + J, lane);
+    } else {
+      const int K = rowCol[c];
+      const double* A = d.tiles + (int64_t)rowTiles[c] * TS * TS;  // tile (J, K): A[q * TS + r] = L(r, q)
+      double a[TS];
+#pragma unroll
+      for (int r = 0; r < TS; r++) a[r] = A[lane * TS + r];  // lane = column q of K
+      if (!wait_flag(ready + J, lane, d.err)) return;
+      const double xj = ld_sc1(x + (int64_t)J * TS + lane);
+      double v = 0.0;
+#pragma unroll
+      for (int r = 0; r < TS; r++) v += a[r] * __shfl(xj, r, 64);
+      add_agent(yv + (int64_t)K * TS + lane, -v);
+      count_up(cnt + K, lane);
     }
-    __syncthreads();
   }
 }
 
-void launch_solve_persistent(const Dev& d, const int64_t* rowStart, const int32_t* rowTiles, const int32_t* rowCol,
-                             const int64_t* colStart, const int32_t* colTiles, const int32_t* colRows,
-                             const double* linv, const double* b, double* y, double* x, unsigned* flags, int G,
-                             hipStream_t st) {
-  const int g = std::min<int>(G, d.nT);
-  (void)hipMemsetAsync(flags, 0, 2 * (size_t)d.nT * sizeof(unsigned), st);
-  launchK(fwd_persistent_kernel, dim3(g), dim3(256), 0, st, d, rowStart, rowTiles, rowCol, linv, b, y, flags, g);
-  launchK(bwd_persistent_kernel, dim3(g), dim3(256), 0, st, d, colStart, colTiles, colRows, linv, (const double*)y, x,
-          flags + d.nT, g);
+// rhs b (clobbered), y (clobbered) -> x; flags: 4 nT words (ready / count, forward and backward)
+void launch_solve_fanout(const Dev& d, const int32_t* tasksF, int64_t nF, const int32_t* tasksB, int64_t nB,
+                         const int32_t* expF, const int32_t* expB, const int32_t* colTiles, const int32_t* colRows,
+                         const int32_t* rowTiles, const int32_t* rowCol, const double* linv, double* b, double* y,
+                         double* x, unsigned* flags, int G, hipStream_t st) {
+  (void)hipMemsetAsync(flags, 0, 4 * (size_t)d.nT * sizeof(unsigned), st);
+  launchK(fwd_fanout_kernel, dim3(G), dim3(256), 0, st, d, tasksF, nF, colTiles, colRows, expF, linv, b, y, flags,
+          flags + d.nT);
+  launchK(bwd_fanout_kernel, dim3(G), dim3(256), 0, st, d, tasksB, nB, rowTiles, rowCol, expB, linv, y, x,
+          flags + 2 * d.nT, flags + 3 * d.nT);
 }
 
 // ------------------------------------------------------------------ point back-substitution
