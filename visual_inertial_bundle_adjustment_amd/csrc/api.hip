@@ -238,6 +238,10 @@ struct vb_handle_s {
   bool linearized = false, factored = false;
   vb_phase_times times{};
   hipEvent_t ev[8];
+  // side stream: the small (non-visual) factor kernels -- few waves, latency-bound -- run beside
+  // the visual kernels, forked after the buffer resets and joined before their first consumer
+  hipStream_t st2 = nullptr;
+  hipEvent_t evFork = nullptr, evJoin = nullptr;
   // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
   int profFamily = -1;
   std::vector<hipEvent_t> profEv;
@@ -996,6 +1000,18 @@ int doFinalize(vb_handle h) {
 }
 
 // ------------------------------------------------------------------ numeric phases
+// small factors (root only) on the side stream; joinSmall makes the main stream wait for them
+void forkSmall(vb_handle h, int mode, double* gOut) {
+  if (!h->isRoot) return;
+  (void)hipEventRecord(h->evFork, h->st);
+  (void)hipStreamWaitEvent(h->st2, h->evFork, 0);
+  launch_small(h->d, mode, gOut, h->st2);
+  (void)hipEventRecord(h->evJoin, h->st2);
+}
+void joinSmall(vb_handle h) {
+  if (h->isRoot) (void)hipStreamWaitEvent(h->st, h->evJoin, 0);
+}
+
 // visual kernels over this shard's observations (+ the root's constant-point observations)
 void visualLinShard(vb_handle h, int updateCache, int dontRetry) {
   const Dev& d = h->d;
@@ -1161,7 +1177,10 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
       h->numCUs = prop.multiProcessorCount;
   }
   HIPCHK(hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking));
   for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -1195,6 +1214,9 @@ int vb_destroy(vb_handle h) {
     if (d.sMeta) hipFree(d.sMeta);
   }
   for (auto& e : h->ev) hipEventDestroy(e);
+  if (h->evFork) hipEventDestroy(h->evFork);
+  if (h->evJoin) hipEventDestroy(h->evJoin);
+  if (h->st2) hipStreamSynchronize(h->st2), hipStreamDestroy(h->st2);
   for (auto& e : h->profEv) hipEventDestroy(e);
   if (h->factorGraph) hipGraphExecDestroy(h->factorGraph);
   if (h->solveGraph) hipGraphExecDestroy(h->solveGraph);
@@ -1265,8 +1287,9 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   if (h->isRoot) launch_pad_diag(d, h->padRowsD, h->nPadRows, h->st);
+  forkSmall(h, 0, d.gRed);
   visualLinShard(h, update_cache, dont_retry_failed);
-  if (h->isRoot) launch_small(d, 0, d.gRed, h->st);
+  joinSmall(h);
   HIPCHK(hipEventRecord(h->ev[1], h->st));
   double c = 0;
   if (int rc = readRed(h, &c, 0, 1)) return rc;
@@ -1313,8 +1336,9 @@ int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red) {
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 1 * sizeof(double), h->st));
+  forkSmall(h, 1, d.gRedNew);
   visualLinShard(h, 0, dont_retry_failed);
-  if (h->isRoot) launch_small(d, 1, d.gRedNew, h->st);
+  joinSmall(h);
   launch_landmark(d, 0.0, 1, d.lmB, d.lmE, h->st);
   launch_reduced_grad(d, 0, h->st);
   HIPCHK(hipMemsetAsync(d.red + 16, 0, 8 * sizeof(double), h->st));
@@ -1374,8 +1398,9 @@ int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
   HIPCHK(hipEventRecord(h->ev[6], h->st));
   HIPCHK(hipMemsetAsync(d.red + 1, 0, 4 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  forkSmall(h, 2, nullptr);
   visualCostShard(h, comparable);
-  if (h->isRoot) launch_small(d, 2, nullptr, h->st);
+  joinSmall(h);
   HIPCHK(hipEventRecord(h->ev[7], h->st));
   double r[4];
   if (int rc = readRed(h, r, 1, 4)) return rc;

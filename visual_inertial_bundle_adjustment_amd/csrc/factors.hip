@@ -541,9 +541,9 @@ __constant__ int kFK[14][10] = {
     {3, 7}, {6, 6}, {4, 4}, {7, 7}, {5, 5}, {1}, {6}, {4}, {5}, {7}};
 __constant__ int kNV[14] = {5, 6, 9, 10, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1};
 
+// evaluation of factor k of kind FK (k >= a.n: nothing); returns this lane's cost term
 template <int FK>
-__global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, int64_t k) {
   double acc[1] = {0.0};
   if (k < a.n) {
     SmallEval E;
@@ -725,7 +725,37 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallArgs a) {
       for (int s = 0; s < nv; s++) mt[5 + s] = E.red[s], mt[15 + s] = E.col[s], mt[25 + s] = E.dim[s];
     }
   }
-  block_sum_atomic<1>(acc, d.red + (a.mode == 2 ? 1 : 0));
+  return acc[0];
+}
+
+// all kinds in one launch: block b evaluates kind FK for the blocks [first[FK], first[FK + 1]) (one
+// lane per factor); a dispatch per block instead of 13 serial launches of a few waves each
+struct SmallLaunch {
+  SmallArgs a[14];
+  int32_t first[15];
+};
+__global__ void __launch_bounds__(64) small_kernel(Dev d, SmallLaunch L) {
+  const int b = blockIdx.x;
+  int fk = 1;
+  while (fk < 13 && b >= L.first[fk + 1]) fk++;
+  const int64_t k = (int64_t)(b - L.first[fk]) * 64 + threadIdx.x;
+  double acc[1] = {0.0};
+  switch (fk) {
+    case 1: acc[0] = small_eval<1>(d, L.a[1], k); break;
+    case 2: acc[0] = small_eval<2>(d, L.a[2], k); break;
+    case 3: acc[0] = small_eval<3>(d, L.a[3], k); break;
+    case 4: acc[0] = small_eval<4>(d, L.a[4], k); break;
+    case 5: acc[0] = small_eval<5>(d, L.a[5], k); break;
+    case 6: acc[0] = small_eval<6>(d, L.a[6], k); break;
+    case 7: acc[0] = small_eval<7>(d, L.a[7], k); break;
+    case 8: acc[0] = small_eval<8>(d, L.a[8], k); break;
+    case 9: acc[0] = small_eval<9>(d, L.a[9], k); break;
+    case 10: acc[0] = small_eval<10>(d, L.a[10], k); break;
+    case 11: acc[0] = small_eval<11>(d, L.a[11], k); break;
+    case 12: acc[0] = small_eval<12>(d, L.a[12], k); break;
+    default: acc[0] = small_eval<13>(d, L.a[13], k); break;
+  }
+  block_sum_atomic<1>(acc, d.red + (L.a[1].mode == 2 ? 1 : 0));
 }
 
 // Assembly of the staged small factors, one wave per factor (4 per workgroup): whitened Jacobian
@@ -809,36 +839,23 @@ void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hi
                      lo, hi);
 }
 
-void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
-
-template <int FK>
-static void launch_one(const Dev& d, int mode, double* gOut, hipStream_t st) {
-  const SmallFactors& f = d.sf[FK];
-  if (f.n == 0) return;
-  SmallArgs a{f.n, f.vars, f.consts, f.nc, mode, gOut};
-  hipLaunchKernelGGL(small_kernel<FK>, dim3((unsigned)((f.n + 63) / 64)), dim3(64), 0, st, d, a);
+void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st) {
+  SmallLaunch L{};
+  int32_t nb = 0;
+  for (int fk = 1; fk < 14; fk++) {
+    const SmallFactors& f = d.sf[fk];
+    L.a[fk] = SmallArgs{f.n, f.vars, f.consts, f.nc, mode, gOut};
+    L.first[fk] = nb;
+    nb += (int32_t)((f.n + 63) / 64);
+  }
+  L.first[14] = nb;
+  if (nb > 0) hipLaunchKernelGGL(small_kernel, dim3((unsigned)nb), dim3(64), 0, st, d, L);
 }
 
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st) {
   launch_small_eval(d, mode, gOut, st);
   if (mode != 2 && d.nSmallStage > 0)
     launchK(small_assemble_kernel, dim3((unsigned)((d.nSmallStage + 3) / 4)), dim3(256), 0, st, d, mode, gOut);
-}
-
-void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st) {
-  launch_one<1>(d, mode, gOut, st);
-  launch_one<2>(d, mode, gOut, st);
-  launch_one<3>(d, mode, gOut, st);
-  launch_one<4>(d, mode, gOut, st);
-  launch_one<5>(d, mode, gOut, st);
-  launch_one<6>(d, mode, gOut, st);
-  launch_one<7>(d, mode, gOut, st);
-  launch_one<8>(d, mode, gOut, st);
-  launch_one<9>(d, mode, gOut, st);
-  launch_one<10>(d, mode, gOut, st);
-  launch_one<11>(d, mode, gOut, st);
-  launch_one<12>(d, mode, gOut, st);
-  launch_one<13>(d, mode, gOut, st);
 }
 
 }  // namespace viba
