@@ -796,24 +796,49 @@ int doFinalize(vb_handle h) {
     if (upload(&d.grpStart, gstart) || upload(&d.grpObs, gobs) || upload(&d.grpRed, gred)) return VB_E_HIP;
     std::vector<int32_t> tobs;
     // work items: a tile's landmark entries in near-equal chunks of at most kChunkLm; `kind` = 1 when
-    // the tile is split over several items (fp64 atomics), else the item owns the tile (plain RMW)
-    int64_t kChunkLm = 256;
+    // the tile is split over several items (fp64 atomics), else the item owns the tile (plain RMW).
+    // With a landmark band B (VIBA_SCHUR_BAND), a tile's entries are also cut at multiples of B
+    // landmarks and the items are ordered by (band, tile): the items of one band run back to back on
+    // one XCD (xcd_block hands each XCD a contiguous item range), so the band's Y columns are
+    // gathered from L2 instead of being re-fetched once per tile pair.
+    int64_t kChunkLm = 256, band = 0;
     if (const char* e = getenv("VIBA_SCHUR_CHUNK")) kChunkLm = std::max<int64_t>(8, std::min<int64_t>(256, atoll(e)));
+    if (const char* e = getenv("VIBA_SCHUR_BAND")) band = std::max<int64_t>(0, atoll(e));
+    std::vector<int64_t> itemBand;
+    std::vector<int32_t> itemsPerTile(nTiles, 0);
     for (int32_t J = 0; J < nT; J++)
       for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
         const int32_t ti = h->colTilesH[c];
-        const int64_t n = tcnt[ti + 1] - tcnt[ti];
-        if (n == 0) continue;
-        const int64_t nch = (n + kChunkLm - 1) / kChunkLm;
-        for (int64_t k = 0; k < nch; k++) {
-          TileWork w{};
-          const int64_t s0 = n * k / nch, s1 = n * (k + 1) / nch;
-          w.tile = ti, w.I = h->colRowsH[c], w.J = J, w.count = (int32_t)(s1 - s0);
-          w.start = tcnt[ti] + s0, w.kind = nch > 1 ? 1 : 0;
-          works.push_back(w);
-          tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti);
+        int64_t e0 = tcnt[ti];
+        const int64_t eEnd = tcnt[ti + 1];
+        while (e0 < eEnd) {  // one band segment [e0, e1)
+          int64_t e1 = eEnd;
+          const int64_t bnd = band > 0 ? ents[e0].lm / band : 0;
+          if (band > 0)
+            while (e1 > e0 && (int64_t)ents[e1 - 1].lm / band != bnd) e1--;  // entries sorted by landmark
+          const int64_t n = e1 - e0, nch = (n + kChunkLm - 1) / kChunkLm;
+          for (int64_t k = 0; k < nch; k++) {
+            TileWork w{};
+            const int64_t s0 = n * k / nch, s1 = n * (k + 1) / nch;
+            w.tile = ti, w.I = h->colRowsH[c], w.J = J, w.count = (int32_t)(s1 - s0);
+            w.start = e0 + s0, w.kind = 0;
+            works.push_back(w);
+            itemBand.push_back(bnd);
+            itemsPerTile[ti]++;
+            tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti);
+          }
+          e0 = e1;
         }
       }
+    for (TileWork& w : works) w.kind = itemsPerTile[w.tile] > 1 ? 1 : 0;
+    if (band > 0) {
+      std::vector<size_t> ord(works.size());
+      for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
+      std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return itemBand[a] < itemBand[b]; });
+      std::vector<TileWork> sorted(works.size());
+      for (size_t i = 0; i < ord.size(); i++) sorted[i] = works[ord[i]];
+      works.swap(sorted);
+    }
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
     d.nTileWorks = (int64_t)works.size();
     h->nTileEnt = (int64_t)ents.size(), h->nObEnt = d.nGroups;

@@ -144,6 +144,9 @@ __device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
 // the entries they wrote.  A tile split over several items
 // (wk.kind) is updated with fp64 atomics, else by a plain read-modify-write.  Diagonal tiles also
 // emit rhs -= Y^T z.
+#ifndef VIBA_SCHUR_EXPT
+#define VIBA_SCHUR_EXPT 0  // diagnostic builds only: 1 = no MFMA, 2 = no gathers
+#endif
 constexpr int kTK = 32;       // K rows per batch
 constexpr int kTB = kTK / 4;  // landmarks per batch
 
@@ -168,6 +171,10 @@ __device__ __forceinline__ void schur_gather(const Dev& d, const TileEnt* ents, 
     S.eb[k] = eb, S.c[k] = c, S.rowI[k] = -1, S.rowJ[k] = -1;
     if (e >= count) continue;
     const TileEnt en = ents[e];
+#if VIBA_SCHUR_EXPT == 2  // diagnostic only: no gathers
+    if (c < en.nI) S.rowI[k] = c, S.yI[k][0] = S.yI[k][1] = S.yI[k][2] = 0.0;
+    if (!diag && c < en.nJ) S.rowJ[k] = c, S.yJ[k][0] = S.yJ[k][1] = S.yJ[k][2] = 0.0;
+#else
     if (c < en.nI) {
       const int64_t col = (int64_t)en.colI + c;
       S.rowI[k] = (int)(d.pcRow[col] - rI);
@@ -180,11 +187,12 @@ __device__ __forceinline__ void schur_gather(const Dev& d, const TileEnt* ents, 
       const double* y = d.Y + 3 * col;
       S.yJ[k][0] = y[0], S.yJ[k][1] = y[1], S.yJ[k][2] = y[2];
     }
+#endif
     if (diag && c < 3) S.z[k] = d.z[3 * (int64_t)en.lm + c];
   }
 }
 
-__global__ void __launch_bounds__(256) schur_tile_kernel(Dev d, double lambda) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) schur_tile_kernel(Dev d, double lambda) {
   __shared__ double Yi[kTK * TS];
   __shared__ double Yj[kTK * TS];
   __shared__ double zb[kTK];
@@ -209,6 +217,9 @@ __global__ void __launch_bounds__(256) schur_tile_kernel(Dev d, double lambda) {
     for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
   double racc = 0.0;
   const double* yj = diag ? Yi : Yj;
+  // row blocks this wave's quadrant reads: k-steps touching none of them are skipped whole; on a
+  // diagonal tile the strictly upper block pairs are never formed (only the lower triangle is used)
+  const uint32_t qmask = (3u << (4 + (pb >> 4))) | (3u << (qb >> 4));
   SchurSlots S;
   schur_gather(d, ents, wk.count, 0, diag, rI, rJ, tid, S);
   for (int b = 0; b < nb; b++) {
@@ -243,7 +254,7 @@ __global__ void __launch_bounds__(256) schur_tile_kernel(Dev d, double lambda) {
     if (b + 1 < nb) schur_gather(d, ents, wk.count, b + 1, diag, rI, rJ, tid, S);
 #pragma unroll
     for (int eb = 0; eb < kTB; eb++) {
-      const uint32_t m = msk[eb];
+      const uint32_t m = msk[eb] & qmask;
       if (m == 0) continue;
       const int k0 = 4 * eb;
       double av[2], bv[2];
@@ -255,7 +266,9 @@ __global__ void __launch_bounds__(256) schur_tile_kernel(Dev d, double lambda) {
       for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int bb = 0; bb < 2; bb++)
-          if ((m >> (4 + (pb >> 4) + a)) & (m >> ((qb >> 4) + bb)) & 1u) acc[a][bb] = mfma64(av[a], bv[bb], acc[a][bb]);
+          if (VIBA_SCHUR_EXPT != 1 && ((m >> (4 + (pb >> 4) + a)) & (m >> ((qb >> 4) + bb)) & 1u) &&
+              !(diag && (pb >> 4) + a > (qb >> 4) + bb))
+            acc[a][bb] = mfma64(av[a], bv[bb], acc[a][bb]);
     }
     if (diag && tid < TS) {
 #pragma unroll 8
