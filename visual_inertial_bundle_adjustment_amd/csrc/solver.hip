@@ -501,40 +501,20 @@ template <int C>
 struct Upd16<C, 16> {
   static __device__ __forceinline__ void run(double (&)[16], double) {}
 };
-// Row C of X = L^-1 (lane c holds column c of X in x[]), left-looking, once row C of L is complete:
-// X[C][c] = (delta_Cc - sum_{k<C} L[C][k] X[k][c]) / L[C][C], L[C][k] = s[k] of lane C (DPP)
-template <int C, int K>
-struct InvRow16 {
-  static __device__ __forceinline__ void run(double& a0, double& a1, const double (&x)[16], const double (&s)[16]) {
-    // opaque copy: rowbcast<C>(s[K]) equals step K's rowbcast<C>(l_K); letting the compiler reuse
-    // that value keeps ~120 broadcasts live across the steps and spills them
-    double sk = s[K];
-    asm volatile("" : "+v"(sk));
-    if constexpr (K % 2 == 0) a0 -= rowbcast<C>(sk) * x[K];
-    else a1 -= rowbcast<C>(sk) * x[K];
-    InvRow16<C, K + 1>::run(a0, a1, x, s);
-  }
-};
-template <int C>
-struct InvRow16<C, C> {
-  static __device__ __forceinline__ void run(double&, double&, const double (&)[16], const double (&)[16]) {}
-};
-// Step C: pivot, column C of L, rank-1 update of the trailing columns (right-looking), then row C
-// of L^-1 (left-looking) -- two independent dependency chains the scheduler interleaves.
+// Step C: pivot, column C of L, rank-1 update of the trailing columns (right-looking); invd[C] =
+// 1 / L_CC (the same value in every lane).  Only the pivot chain is serial here; the inverse is
+// formed afterwards (diag16), off this chain.
 template <int C>
 struct Chol16 {
-  static __device__ __forceinline__ void run(double (&s)[16], double (&x)[16], int lane, bool& bad) {
+  static __device__ __forceinline__ void run(double (&s)[16], double (&invd)[16], int lane, bool& bad) {
     const double piv = rowbcast<C>(s[C]);
     bad |= !(piv > 0.0);
     const double y = rsqrt_nr(piv);
+    invd[C] = y;
     const double lc = ((lane & 15) == C) ? piv * y : s[C] * y;
     s[C] = lc;
     Upd16<C, C + 1>::run(s, lc);
-    double a0 = ((lane & 15) == C) ? 1.0 : 0.0, a1 = 0.0;
-    InvRow16<C, 0>::run(a0, a1, x, s);
-    x[C] = (a0 + a1) * y;
-    __builtin_amdgcn_sched_barrier(0);  // keep each step's broadcasts in its step (register pressure)
-    Chol16<C + 1>::run(s, x, lane, bad);
+    Chol16<C + 1>::run(s, invd, lane, bad);
   }
 };
 template <>
@@ -571,18 +551,40 @@ __device__ long long g_potrf_t[32];
 #define POTRF_T(k) do {} while (0)
 #endif
 
-// Factor + invert the 16 x 16 diagonal block i of T (LDS) given S (its updated value, D layout):
-// writes L_ii into T and Dinv_i into dinvS (LDS)
+// Factor + invert the 16 x 16 diagonal block i of T (LDS) given S (its updated value, D layout; only
+// its lower triangle is valid): writes L_ii into T and Dinv_i into dinvS (LDS).  Cholesky first, lane
+// r holding row r (pivot chain only: DPP row broadcasts, v_rsq_f64 + Newton), then X = L^-1 with
+// lane c computing column c right-looking: once x_k is known every later row's accumulator takes its
+// term, so the serial chain is one FMA + one multiply per row (L from LDS by broadcast reads).
+// (A one-MFMA-per-pivot variant -- the rank-1 update as a v_mfma_f64_16x16x4_f64 on the D layout --
+// measured slower: each pivot then waits on a dependent MFMA + readlane, 7.9k vs 5.7k cycles.)
 __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS, int i, double4_t S, int lane,
                                        bool& bad) {
   const int lr = lane & 15, lq = lane >> 4;
 #pragma unroll
   for (int r = 0; r < 4; r++) scratch[(lq + 4 * r) * 16 + lr] = S[r];  // row-major S[i'][j']
   __builtin_amdgcn_wave_barrier();
-  double s[16], x[16];
+  double s[16], invd[16];
 #pragma unroll
   for (int c = 0; c < 16; c++) s[c] = scratch[lr * 16 + c];
-  Chol16<0>::run(s, x, lane, bad);
+  Chol16<0>::run(s, invd, lane, bad);
+  __builtin_amdgcn_wave_barrier();  // every lane has read S
+  if (lane < 16) {
+#pragma unroll
+    for (int c = 0; c < 16; c++) scratch[lane * 16 + c] = (c <= lane) ? s[c] : 0.0;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double acc[16], x[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = (r == lr) ? 1.0 : 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    x[k] = acc[k] * invd[k];
+#pragma unroll
+    for (int r = k + 1; r < 16; r++) acc[r] -= scratch[r * 16 + k] * x[k];
+  }
   if (lane < 16) {
 #pragma unroll
     for (int c = 0; c < 16; c++) T[(16 * i + c) * TS + 16 * i + lane] = (c <= lane) ? s[c] : 0.0;
