@@ -271,6 +271,18 @@ int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_
 /* device pointers + sizes (in doubles) of the reduced matrix (tile store) and the reduced RHS */
 int vb_reduced_buffers(vb_handle h, double** matrix, int64_t* matrix_len, double** rhs,
                        int64_t* rhs_len);
+/* exact tile set of a non-root shard's partial reduced system (the root's list is empty): tile
+ * indices ascending; tiles == NULL queries the count.  Replaces the band of vb_shard_tile_range
+ * for the exchange (ND ordering spreads a shard's contributions over its subtree and the separators
+ * above it).  Reference: the per-shard partial Hessian of SURVEY 8e (no reference counterpart: the
+ * reference is single-process). */
+int vb_shard_tiles(vb_handle h, int32_t* tiles, int64_t* n);
+/* gather this shard's tiles (vb_shard_tiles order) into an engine-owned device buffer of
+ * n * 64 * 64 doubles; synchronous */
+int vb_pack_shard_tiles(vb_handle h, double** buf, int64_t* len);
+/* root: add n packed tiles (device buffer, vb_pack_shard_tiles layout of the sender) into the tile
+ * store at the device-resident tile indices; synchronous */
+int vb_add_tiles(vb_handle h, const int32_t* tiles_dev, int64_t n, const double* buf_dev);
 /* the contiguous range of the tile store this shard's partial reduced system can touch */
 int vb_shard_tile_range(vb_handle h, int64_t* first_double, int64_t* num_doubles);
 /* split of vb_damp_factor_solve (Optimizer.cpp:826-833) for sharded use:

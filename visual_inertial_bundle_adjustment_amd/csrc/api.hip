@@ -29,6 +29,8 @@ void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
                  hipStream_t st);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
+void launch_tile_gather(const Dev& d, const int32_t* tiles, int64_t n, double* out, hipStream_t st);
+void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, const double* in, hipStream_t st);
 void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st);
 void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st);
 void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
@@ -231,6 +233,9 @@ struct vb_handle_s {
   int64_t lmBegin = 0, lmEnd = -1;
   bool isRoot = true;
   int64_t tileFirst = 0, tileCount = 0, nTileEnt = 0;
+  std::vector<int32_t> shardTiles;  // exact tiles of this (non-root) shard's partial system
+  int32_t* shardTilesD = nullptr;
+  double* shardPack = nullptr;      // packed copy of those tiles (vb_pack_shard_tiles)
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
   hipGraphExec_t factorGraph = nullptr, solveGraph = nullptr;
   bool useGraphs = true;
@@ -773,6 +778,7 @@ int doFinalize(vb_handle h) {
     std::vector<int64_t> gstart;
     std::vector<int32_t> gred;
     int64_t tlo = INT64_MAX, thi = -1;
+    std::vector<uint8_t> touched(nTiles, 0);
     for (size_t i = 0; i < gobs.size(); i++) {
       bool fresh = i == 0;
       for (int s = 0; s < 4 && !fresh; s++) fresh = gkey(gobs[i], s) != gkey(gobs[i - 1], s);
@@ -787,7 +793,7 @@ int doFinalize(vb_handle h) {
           for (int64_t I = h->rvOff[A] / TS; I <= (h->rvOff[A] + h->rvDim[A] - 1) / TS; I++)
             for (int64_t J = h->rvOff[B] / TS; J <= std::min<int64_t>(I, (h->rvOff[B] + h->rvDim[B] - 1) / TS); J++) {
               const int32_t tt = tileIdx[(size_t)I * nT + J];
-              if (tt >= 0) tlo = std::min<int64_t>(tlo, tt), thi = std::max<int64_t>(thi, tt);
+              if (tt >= 0) tlo = std::min<int64_t>(tlo, tt), thi = std::max<int64_t>(thi, tt), touched[tt] = 1;
             }
         }
     }
@@ -825,7 +831,7 @@ int doFinalize(vb_handle h) {
             works.push_back(w);
             itemBand.push_back(bnd);
             itemsPerTile[ti]++;
-            tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti);
+            tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti), touched[ti] = 1;
           }
           e0 = e1;
         }
@@ -843,10 +849,19 @@ int doFinalize(vb_handle h) {
     d.nTileWorks = (int64_t)works.size();
     h->nTileEnt = (int64_t)ents.size(), h->nObEnt = d.nGroups;
     if (upload(&d.tileWorks, works) || upload(&d.tileEnts, ents) || upload(&d.tileObs, tobs)) return VB_E_HIP;
-    // tiles this shard's partial system can touch (column-major tile order: one contiguous range)
+    // tiles this shard's partial system can touch: the enclosing range (vb_shard_tile_range) and the
+    // exact set (vb_shard_tiles: landmark and observation-group targets; the root, which also holds
+    // the small factors and the damping, receives rather than sends)
     if (h->isRoot) h->tileFirst = 0, h->tileCount = nTiles;
     else if (thi < 0) h->tileFirst = 0, h->tileCount = 0;
     else h->tileFirst = tlo, h->tileCount = thi - tlo + 1;
+    h->shardTiles.clear();
+    if (!h->isRoot)
+      for (int64_t t = 0; t < nTiles; t++)
+        if (touched[t]) h->shardTiles.push_back((int32_t)t);
+    if (!h->shardTiles.empty() &&
+        (upload(&h->shardTilesD, h->shardTiles) || alloc0(&h->shardPack, h->shardTiles.size() * (size_t)TS * TS)))
+      return VB_E_HIP;
   }
   h->rowStart.assign(nT + 1, 0);
   h->rowTilesH.clear(), h->rowColH.clear();
@@ -1220,7 +1235,7 @@ int vb_destroy(vb_handle h) {
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
-                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->fanPairsD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->solveTasksFD, h->solveTasksBD, h->solveExpFD, h->solveExpBD, h->dinv, h->yvec,
+                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->fanPairsD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->solveTasksFD, h->solveTasksBD, h->solveExpFD, h->solveExpBD, h->shardTilesD, h->shardPack, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1685,6 +1700,26 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
 // sharded building blocks (landmark shards).  The host controller
 // (distributed.py) sums the partial reduced systems / right-hand sides of all shards on the root
 // between these calls; every rank runs the same LM decisions.
+int vb_shard_tiles(vb_handle h, int32_t* tiles, int64_t* n) {
+  if (!h || !h->finalized || !n) return fail(VB_E_STATE, "not finalized");
+  *n = (int64_t)h->shardTiles.size();
+  if (tiles) std::copy(h->shardTiles.begin(), h->shardTiles.end(), tiles);
+  return 0;
+}
+int vb_pack_shard_tiles(vb_handle h, double** buf, int64_t* len) {
+  if (!h || !h->finalized || !buf || !len) return fail(VB_E_STATE, "not finalized");
+  const int64_t n = (int64_t)h->shardTiles.size();
+  if (n) launch_tile_gather(h->d, h->shardTilesD, n, h->shardPack, h->st);
+  HIPCHK(hipStreamSynchronize(h->st));
+  *buf = h->shardPack, *len = n * TS * TS;
+  return 0;
+}
+int vb_add_tiles(vb_handle h, const int32_t* tiles_dev, int64_t n, const double* buf_dev) {
+  if (!h || !h->finalized || n < 0 || (n && (!tiles_dev || !buf_dev))) return fail(VB_E_ARG, "bad vb_add_tiles arguments");
+  if (n) launch_tile_scatter_add(h->d, tiles_dev, n, buf_dev, h->st);
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
 int vb_shard_tile_range(vb_handle h, int64_t* first_double, int64_t* num_doubles) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
   if (first_double) *first_double = h->tileFirst * TS * TS;

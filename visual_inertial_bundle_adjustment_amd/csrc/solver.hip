@@ -1227,6 +1227,24 @@ void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const
                  hipStream_t st) {
   if (n > 0) launchK(trsm_kernel, dim3(n), dim3(256), 0, st, d, diag, target, cols, dinv);
 }
+// shard exchange (vb_pack_shard_tiles / vb_add_tiles): one block per listed tile
+__global__ void __launch_bounds__(256) tile_gather_kernel(Dev d, const int32_t* tiles, double* out) {
+  const double* src = d.tiles + (int64_t)tiles[blockIdx.x] * TS * TS;
+  double* dst = out + (int64_t)blockIdx.x * TS * TS;
+  for (int i = threadIdx.x; i < TS * TS; i += 256) dst[i] = src[i];
+}
+__global__ void __launch_bounds__(256) tile_scatter_add_kernel(Dev d, const int32_t* tiles, const double* in) {
+  double* dst = d.tiles + (int64_t)tiles[blockIdx.x] * TS * TS;
+  const double* src = in + (int64_t)blockIdx.x * TS * TS;
+  for (int i = threadIdx.x; i < TS * TS; i += 256) dst[i] += src[i];
+}
+void launch_tile_gather(const Dev& d, const int32_t* tiles, int64_t n, double* out, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(tile_gather_kernel, dim3((unsigned)n), dim3(256), 0, st, d, tiles, out);
+}
+void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, const double* in, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(tile_scatter_add_kernel, dim3((unsigned)n), dim3(256), 0, st, d, tiles, in);
+}
+
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
   if (n > 0) launchK(fanin_kernel, dim3(n), dim3(256), 0, st, d, work, pairs);
 }

@@ -98,6 +98,35 @@ class ShardComm:
         if s is not t:
             t.copy_(s)
 
+    def sum_tiles_to_root(self, engine, tile_lists):
+        """Sparse exchange: every non-root rank packs the tiles its partial system touches
+        (engine.pack_shard_tiles) and sends them point-to-point; the root adds each rank's packed
+        tiles into its tile store (engine.add_tiles).  tile_lists[r]: device int32 tensor of rank
+        r's tile indices (root side)."""
+        dist, torch = self.dist, self.torch
+        if self.rank == 0:
+            bufs, ops = [], []
+            for r in range(1, self.world):
+                n = int(tile_lists[r].numel())
+                if n == 0:
+                    continue
+                b = torch.empty(n * 64 * 64, dtype=torch.float64, device=self.device if self.nccl else "cpu")
+                bufs.append((r, n, b))
+                ops.append(dist.P2POp(dist.irecv, b, r))
+            if ops:
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+            for r, n, b in bufs:
+                b = b.to(self.device)
+                torch.cuda.synchronize(self.device)
+                engine.add_tiles(tile_lists[r].data_ptr(), n, b.data_ptr())
+        else:
+            ptr, n = engine.pack_shard_tiles()
+            if n:
+                s = self._staged(_tensor(ptr, n, self.device))
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, s, 0)]):
+                    w.wait()
+
     def sum_bands_to_root(self, full, bands):
         """full: this rank's matrix storage; bands[r] = (first, count) of rank r.  The root adds
         every other rank's band into its own storage (point-to-point, overlapped)."""
@@ -134,6 +163,12 @@ class ShardedOptimizer:
         self.n_params = engine.num_params()
         first, cnt = engine.shard_tile_range()
         self.bands = comm.all_gather_obj((first, cnt))
+        # HIP engine: exact tile sets (the nested-dissection order spreads a shard's contributions
+        # over its subtree and the separators above it, so the enclosing band is wide)
+        self.tile_lists = None
+        if hasattr(engine, "shard_tiles") and comm.device is not None and comm.device.type != "cpu":
+            lists = comm.all_gather_obj(engine.shard_tiles().tolist())
+            self.tile_lists = [comm.torch.tensor(t, dtype=comm.torch.int32, device=comm.device) for t in lists]
         self.sync = getattr(engine, "synchronize", lambda: None)
 
     def _buffers(self):
@@ -149,7 +184,11 @@ class ShardedOptimizer:
         e, c = self.e, self.c
         e.assemble_reduced(lam)
         S, b = self._buffers()
-        c.sum_bands_to_root(S, self.bands)
+        if self.tile_lists is not None:
+            self.sync_torch()
+            c.sum_tiles_to_root(e, self.tile_lists)
+        else:
+            c.sum_bands_to_root(S, self.bands)
         c.reduce_to_root(b)
         self.sync_torch()
         if c.rank == 0:

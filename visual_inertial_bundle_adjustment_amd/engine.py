@@ -308,6 +308,26 @@ class HipEngine(CEngineBase):
         self._check(self._fn("problem_stats", [C.c_int64 * 12])(self.h, out))
         return list(out)
 
+    # sparse shard exchange (HIP engine only; the oracle keeps the band of shard_tile_range)
+    def shard_tiles(self) -> np.ndarray:
+        n = C.c_int64()
+        self._check(self._fn("shard_tiles", [C.c_void_p, C.POINTER(C.c_int64)])(self.h, None, C.byref(n)))
+        out = np.zeros(n.value, dtype=np.int32)
+        if n.value:
+            self._check(self._fn("shard_tiles", [C.c_void_p, C.POINTER(C.c_int64)])(
+                self.h, out.ctypes.data_as(C.c_void_p), C.byref(n)))
+        return out
+
+    def pack_shard_tiles(self):
+        """(device pointer, length in doubles) of this shard's tiles packed in shard_tiles order."""
+        b, n = P(), C.c_int64()
+        self._check(self._fn("pack_shard_tiles", [C.POINTER(P), C.POINTER(C.c_int64)])(
+            self.h, C.byref(b), C.byref(n)))
+        return b.value, n.value
+
+    def add_tiles(self, tiles_dev: int, n: int, buf_dev: int):
+        self._check(self._fn("add_tiles", [C.c_void_p, C.c_int64, C.c_void_p])(self.h, tiles_dev, n, buf_dev))
+
     def bench_kernel(self, which: int, iters: int = 200) -> float:
         us = C.c_double()
         self._check(self._fn("bench_kernel", [C.c_int, C.c_int, _dp])(self.h, which, iters, C.byref(us)))
