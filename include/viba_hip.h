@@ -298,6 +298,34 @@ int vb_back_substitute(vb_handle h, double* model_cost_reduction_partial);
 int vb_assemble_new_rhs(vb_handle h);
 int vb_solve_reduced(vb_handle h);
 int vb_back_substitute_which(vb_handle h, int which, double* model_cost_reduction_partial);
+/* ---------------------------------------------------------------- multi-device (partitioned factorization)
+ * SURVEY.md §8f-1 (no reference counterpart: the reference factors on one host with BaSpaCho).  With
+ * vb_set_partition (before vb_finalize; world a power of two) the nested-dissection order gives rank
+ * r the subtree r levels below the top log2(world) separators; the separators ("ROOT" columns) are
+ * factored on rank 0.  Every landmark goes to the rank whose subtree its observations touch (none
+ * touches two), rank 0 for ROOT-only ones; rank r evaluates and eliminates its landmarks and the
+ * small factors writing its columns.  Per LM iteration (distributed.py PartitionedOptimizer):
+ *   vb_assemble_reduced -> vb_factor_part(0) -> vb_solve_part(0)
+ *   -> sum of ROOT tiles / ROOT rhs rows on rank 0 (vb_part_exchange 0 / 1 + reduce)
+ *   -> rank 0: vb_factor_part(1), vb_solve_part(1) -> broadcast ROOT rows of x (vb_part_exchange 2)
+ *   -> vb_solve_part(2) -> vb_share_x + all-reduce -> vb_back_substitute */
+int vb_set_partition(vb_handle h, int rank, int world);
+/* which 0: factor this rank's subtree columns (and apply their updates to its partial ROOT tiles);
+ * which 1 (rank 0, after the ROOT tiles were summed): factor the ROOT columns */
+int vb_factor_part(vb_handle h, int which);
+/* phase 0: forward solve over the subtree (rhs -> partial ROOT rows); 1 (rank 0): forward + backward
+ * over the ROOT columns; 2: backward over the subtree given the ROOT rows of x */
+int vb_solve_part(vb_handle h, int phase);
+/* what 0 ROOT tiles, 1 ROOT rows of the forward-solve work vector, 2 ROOT rows of x;
+ * dir 0 packs them into an engine-owned device buffer (returned), dir 1 writes that buffer back */
+int vb_part_exchange(vb_handle h, int what, int dir, double** buf, int64_t* len);
+/* x rows this rank solved (other rows zero) into the RHS buffer (returned) for an all-reduce sum;
+ * then vb_back_substitute reads x_red from that buffer */
+int vb_share_x(vb_handle h, double** xred, int64_t* len);
+/* [this rank's subtree tile columns, ROOT tile columns, fan-in contributions of its subtree schedule,
+ *  of the ROOT schedule (rank 0 only), ROOT tiles exchanged per factorization] */
+int vb_part_info(vb_handle h, int64_t* out5);
+
 /* the HIP stream of the handle (hipStream_t), for interop with torch / RCCL */
 void* vb_stream(vb_handle h);
 

@@ -19,38 +19,44 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, which, its, out_dir):
+def _worker(rank, world, port, which, its, out_dir, mode="shard"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "tests")]
     import torch
     import torch.distributed as dist
     from visual_inertial_bundle_adjustment_amd import synth
-    from visual_inertial_bundle_adjustment_amd.distributed import ShardComm, ShardedOptimizer, shard_bounds
+    from visual_inertial_bundle_adjustment_amd.distributed import (PartitionedOptimizer, ShardComm,
+                                                                    ShardedOptimizer, shard_bounds)
     from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if mode == "partition":
+        os.environ["VIBA_ND_LEAF"] = "128"  # miniB is small: finer dissection so 4 ranks get subtrees
     dist.init_process_group("gloo", rank=rank, world_size=world)
     p = synth.generate(synth.config(which))
     lb, le = shard_bounds(p, world)[rank]
     e = HipEngine(imu_calib_options=p.imu_calib_options, device=0)
-    e.set_landmark_shard(lb, le, rank == 0)
+    if mode == "partition":
+        e.set_partition(rank, world)
+        cls = PartitionedOptimizer
+    else:
+        e.set_landmark_shard(lb, le, rank == 0)
+        cls = ShardedOptimizer
     synth.load_into(e, p)
-    s = ShardedOptimizer(e, ShardComm(rank, world, torch.device("cuda", 0))).optimize(
-        Settings.default(max_num_iterations=its))
+    s = cls(e, ShardComm(rank, world, torch.device("cuda", 0))).optimize(Settings.default(max_num_iterations=its))
     res = {"iters": s.num_iterations, "initial": s.initial_cost, "final": s.final_cost}
+    if mode == "partition":
+        res["part"] = np.array(e.part_info())
     for k in range(1, 8):
         res[f"v{k}"] = e.get_vars(k)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("which,its", [("miniB", 8)])
-def test_two_shards_on_gpu_match_single_gpu(which, its, tmp_path):
+def _check_against_single(tmp_path, world, which, its):
     from parity_util import make, rel
     from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
-    world = 2
-    mp.spawn(_worker, args=(world, _free_port(), which, its, str(tmp_path)), nprocs=world, join=True)
     r = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
     e, _ = make(HipEngine, which)
     s = e.optimize(Settings.default(max_num_iterations=its))
@@ -62,3 +68,22 @@ def test_two_shards_on_gpu_match_single_gpu(which, its, tmp_path):
             ref = e.get_vars(kind)
             if len(ref):
                 assert rel(r[k][f"v{kind}"], ref) < 1e-7, kind
+
+
+@pytest.mark.parametrize("which,its", [("miniB", 8)])
+def test_two_shards_on_gpu_match_single_gpu(which, its, tmp_path):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), which, its, str(tmp_path)), nprocs=world, join=True)
+    _check_against_single(tmp_path, world, which, its)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_partitioned_factorization_matches_single_gpu(world, tmp_path):
+    """Subtree factorization per rank + ROOT separators on rank 0 (PartitionedOptimizer): the
+    same LM trajectory as the single-GPU engine (different summation order only)."""
+    which, its = "miniB", 8
+    mp.spawn(_worker, args=(world, _free_port(), which, its, str(tmp_path), "partition"), nprocs=world, join=True)
+    _check_against_single(tmp_path, world, which, its)
+    part = [np.load(tmp_path / f"rank{k}.npz")["part"] for k in range(world)]
+    assert sum(q[0] > 0 for q in part) >= 2, part  # subtrees factored on several ranks
+    assert part[0][1] > 0 and part[0][3] > 0, part[0]  # and rank 0 the ROOT separators

@@ -31,7 +31,8 @@ void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_tile_gather(const Dev& d, const int32_t* tiles, int64_t n, double* out, hipStream_t st);
 void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, const double* in, hipStream_t st);
-void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st);
+void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st);
+void launch_chunk_copy(double* base, const int32_t* idx, int64_t n, int chunk, double* buf, int mode, hipStream_t st);
 void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st);
 void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
                 double* b, double* x, hipStream_t st);
@@ -41,7 +42,8 @@ void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double
 void launch_solve_fanout(const Dev& d, const int32_t* tasksF, int64_t nF, const int32_t* tasksB, int64_t nB,
                          const int32_t* expF, const int32_t* expB, const int32_t* colTiles, const int32_t* colRows,
                          const int32_t* rowTiles, const int32_t* rowCol, const double* linv, double* b, double* y,
-                         double* x, unsigned* flags, int G, hipStream_t st);
+                         double* x, unsigned* flags, int G, hipStream_t st, int phases, const int32_t* pre,
+                         int64_t nPre);
 void launch_dot(const double* a, const double* b, int64_t n, double* out, hipStream_t st);
 void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hipStream_t st);
 void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, hipStream_t st);
@@ -191,6 +193,21 @@ int alloc0(T** dptr, size_t n) {
 
 }  // namespace
 
+// One tile-Cholesky schedule (factorSeq): per elimination level the potrf / trsm / fan-in work
+// lists (offsets lvP / lvT / lvU), the fan-in contribution pairs it indexes, and the fan-out solve
+// task lists over the same columns (solver.hip fwd/bwd_fanout_kernel).
+struct Sched {
+  std::vector<int64_t> lvP, lvT, lvU;
+  int32_t nLevels = 0;
+  int64_t nPairs = 0;
+  int32_t *potrfTileD = nullptr, *potrfColD = nullptr, *trsmDiagD = nullptr, *trsmTargetD = nullptr,
+          *trsmColD = nullptr, *updD = nullptr, *fanPairsD = nullptr;
+  int32_t *tasksFD = nullptr, *tasksBD = nullptr, *expFD = nullptr, *expBD = nullptr, *preReadyD = nullptr;
+  int64_t nF = 0, nB = 0, nPreReady = 0;  // preReady: rows whose x is known before the backward solve
+  hipGraphExec_t graph = nullptr;
+  bool built = false;
+};
+
 struct vb_handle_s {
   vb_config cfg;
   hipStream_t st = nullptr;
@@ -212,32 +229,37 @@ struct vb_handle_s {
   int64_t* padRowsD = nullptr;  // reduced rows that belong to no variable (tile alignment of parts)
   std::vector<int64_t> colStart;   // per tile column into colTilesH / colRowsH
   std::vector<int32_t> colTilesH, colRowsH;
-  std::vector<int64_t> lvP, lvT, lvU;  // per level into the potrf / trsm / update work arrays
+  // tile-Cholesky schedules: sch[0] the whole factorization (or, partitioned, this rank's subtree
+  // plus its partial fan-in into the ROOT targets), sch[1] the ROOT separators (partitioned, rank 0)
+  Sched sch[2];
   int32_t nLevels = 0;
   int64_t nPairs = 0;
-  int32_t *potrfTileD = nullptr, *potrfColD = nullptr, *trsmDiagD = nullptr, *trsmTargetD = nullptr,
-          *trsmColD = nullptr, *updD = nullptr, *fanPairsD = nullptr;
-  std::vector<int32_t> fanPairs;  // host staging of fanPairsD (freed after upload)
+  std::vector<int32_t> rootTiles, rootRows;  // partitioned: tiles of ROOT columns, ROOT tile rows
+  int32_t *rootTilesD = nullptr, *rootRowsD = nullptr;
+  double *rootPack = nullptr, *rowPack = nullptr;
+  int32_t* ownRowsD = nullptr;  // row blocks this rank solves (vb_share_x)
+  int64_t nOwnRows = 0;
+  double* ownPack = nullptr;
   std::vector<int64_t> rowStart;   // per tile row into rowTilesH / rowColH
   std::vector<int32_t> rowTilesH, rowColH;
   int32_t *colTilesD = nullptr, *colRowsD = nullptr, *rowTilesD = nullptr,
           *rowColD = nullptr;
   int64_t *colStartD = nullptr, *rowStartD = nullptr;
   unsigned* solveFlags = nullptr;
-  int32_t *solveTasksFD = nullptr, *solveTasksBD = nullptr, *solveExpFD = nullptr, *solveExpBD = nullptr;
-  int64_t nSolveTasksF = 0, nSolveTasksB = 0;
   int numCUs = 256;
   bool legacySolve = false;  // VIBA_SOLVE_LEGACY=1: one launch pair per tile column
   double *dinv = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool isRoot = true;
+  int partRank = 0, partWorld = 1;  // vb_set_partition (partitioned factorization), else 1
+  std::vector<int8_t> colOwner;     // per tile column: owning rank, partWorld = ROOT (rank 0)
   int64_t tileFirst = 0, tileCount = 0, nTileEnt = 0;
   std::vector<int32_t> shardTiles;  // exact tiles of this (non-root) shard's partial system
   int32_t* shardTilesD = nullptr;
   double* shardPack = nullptr;      // packed copy of those tiles (vb_pack_shard_tiles)
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
-  hipGraphExec_t factorGraph = nullptr, solveGraph = nullptr;
+  hipGraphExec_t solveGraph = nullptr;
   bool useGraphs = true;
   // state
   bool linearized = false, factored = false;
@@ -475,19 +497,31 @@ int doFinalize(vb_handle h) {
   if (getenv("VIBA_ND_OFF")) leafDims = INT64_MAX;
   std::vector<int> nord;             // final order (registration indices)
   std::vector<size_t> partBegin;     // parts (tile-aligned) in nord
-  std::function<void(std::vector<int>&)> dissect = [&](std::vector<int>& vs) {
+  // partitioned factorization (vb_set_partition, world = 2^k): the parts below depth k belong to
+  // the subtree (= rank) they descend from; the separators above, and any part emitted there, are
+  // ROOT parts (factored by rank 0)
+  const int world = h->partWorld;
+  int partK = 0;
+  while ((1 << partK) < world) partK++;
+  std::vector<int> partOwner;
+  std::function<void(std::vector<int>&, int, int, int)> dissect = [&](std::vector<int>& vs, int depth, int sub,
+                                                                      int own) {
+    if (own < 0 && depth == partK) own = sub;
     int64_t dims = 0;
     for (int r : vs) dims += tdims[r];
-    auto emit = [&](std::vector<int>& part) {
+    // a separator above depth k is ROOT; an undivided set above depth k is a whole subtree, so it
+    // goes to the first rank of the ranks below it
+    auto emit = [&](std::vector<int>& part, bool separator) {
       if (part.empty()) return;
       partBegin.push_back(nord.size());
+      partOwner.push_back(own >= 0 ? own : separator ? world : sub << (partK - depth));
       nord.insert(nord.end(), part.begin(), part.end());
     };
-    if (dims <= leafDims || vs.size() < 4) return emit(vs);
+    if (dims <= leafDims || vs.size() < 4) return emit(vs, false);
     int64_t acc = 0;
     size_t k = 0;
     while (k < vs.size() && acc + tdims[vs[k]] <= dims / 2) acc += tdims[vs[k++]];
-    if (k == 0 || k >= vs.size()) return emit(vs);
+    if (k == 0 || k >= vs.size()) return emit(vs, false);
     const int cut = tp[vs[k]];
     std::vector<int> L, R(vs.begin() + k, vs.end()), S;
     int64_t sd = 0;
@@ -495,14 +529,14 @@ int doFinalize(vb_handle h) {
       if (hiP[vs[i]] >= cut) S.push_back(vs[i]), sd += tdims[vs[i]];
       else L.push_back(vs[i]);
     }
-    if (L.empty() || 2 * sd > dims) return emit(vs);  // no useful separator
-    dissect(L);
-    dissect(R);
-    emit(S);
+    if (L.empty() || 2 * sd > dims) return emit(vs, false);  // no useful separator
+    dissect(L, depth + 1, 2 * sub, own);
+    dissect(R, depth + 1, 2 * sub + 1, own);
+    emit(S, true);
   };
   {
     std::vector<int> all(ord.begin(), ord.end());
-    dissect(all);
+    dissect(all, 0, 0, -1);
   }
   h->rvKind.resize(nRV), h->rvHandle.resize(nRV), h->rvDim.resize(nRV), h->rvOff.resize(nRV + 1);
   std::vector<int64_t> padRows;
@@ -525,6 +559,56 @@ int doFinalize(vb_handle h) {
   }
   h->rvOff[nRV] = off;
   const int64_t nRed = off;
+  // owner of every tile column (parts start on tile boundaries; trailing padding joins the last part)
+  {
+    const int64_t nTc = (nRed + TS - 1) / TS;
+    h->colOwner.assign(nTc, (int8_t)(partOwner.empty() ? 0 : partOwner.back()));
+    size_t pi = 0;
+    for (int i = 0; i < nRV; i++) {
+      while (pi + 1 < partBegin.size() && partBegin[pi + 1] <= (size_t)i) pi++;
+      const int64_t t0 = h->rvOff[i] / TS, t1 = (h->rvOff[i] + h->rvDim[i] - 1) / TS;
+      for (int64_t t = t0; t <= t1; t++) h->colOwner[t] = (int8_t)partOwner[pi];
+    }
+    // (parts start on tile boundaries and a part's alignment padding shares a tile with its last
+    // rows, so every tile column holds variables of exactly one part)
+  }
+  // partition mode: landmarks (and constant-point observations) go to the rank whose subtree
+  // interior they touch -- never two (a variable coupled across a cut is in that cut's separator);
+  // those touching only ROOT columns go to rank 0.  Landmarks are renumbered so every rank's are
+  // contiguous (stable: time order within a rank).
+  auto redOwner = [&](int kind, int32_t hh) -> int {
+    if (hh < 0 || kind == 8 || redOf[kind][hh] < 0) return -1;
+    const int i = redOf[kind][hh];
+    return h->colOwner[h->rvOff[i] / TS];
+  };
+  auto obsOwner = [&](int64_t f) {
+    const int32_t* v = &h->fvars[0][f * 5];
+    const int os[4] = {redOwner(1, v[1]), redOwner(5, v[2]), redOwner(4, v[3]), h->fint[0][f] >= 0 ? redOwner(2, v[4]) : -1};
+    for (int o : os)
+      if (o >= 0 && o < world) return o;
+    return 0;  // ROOT columns only (or none): rank 0
+  };
+  std::vector<int> lmRank(nPts, 0);
+  if (world > 1) {
+    const int64_t nv0 = (int64_t)h->fint[0].size();
+    std::vector<int> lmOwn(nPts, -1);
+    for (int64_t f = 0; f < nv0; f++) {
+      const int l = lmOf[h->fvars[0][f * 5]];
+      if (l < 0) continue;
+      lmOwn[l] = std::max(lmOwn[l], obsOwner(f));
+    }
+    std::vector<int32_t> byRank(nPts);
+    std::iota(byRank.begin(), byRank.end(), 0);
+    for (int64_t l = 0; l < nPts; l++) lmRank[l] = std::max(0, lmOwn[l]);
+    std::stable_sort(byRank.begin(), byRank.end(), [&](int32_t a, int32_t b) { return lmRank[a] < lmRank[b]; });
+    std::vector<int32_t> newIdx(nPts);
+    for (int64_t i = 0; i < nPts; i++) newIdx[byRank[i]] = (int32_t)i;
+    for (auto& x : lmOf)
+      if (x >= 0) x = newIdx[x];
+    std::vector<int> r2(nPts);
+    for (int64_t l = 0; l < nPts; l++) r2[newIdx[l]] = lmRank[l];
+    lmRank.swap(r2);
+  }
   h->nRedReal = nRedReal, h->nParts = (int64_t)partBegin.size();
   d.nRV = nRV, d.nRed = nRed, d.nPts = nPts;
   h->nParams = nPts + nRV;
@@ -538,7 +622,7 @@ int doFinalize(vb_handle h) {
   std::iota(perm.begin(), perm.end(), 0);
   auto lmKey = [&](int64_t f) -> int64_t {
     const int l = lmOf[h->fvars[0][f * 5]];
-    return l < 0 ? INT64_MAX : l;
+    return l < 0 ? (world > 1 ? INT64_MAX - world + obsOwner(f) : INT64_MAX) : l;
   };
   std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return lmKey(a) < lmKey(b); });
   d.nObs = nObs;
@@ -646,10 +730,27 @@ int doFinalize(vb_handle h) {
       }
   }
   // ---------------- this handle's landmark shard
+  if (world > 1) {  // partition mode: this rank's landmarks and constant-point observations
+    const int me = h->partRank;
+    int64_t a = 0;
+    while (a < nPts && lmRank[a] < me) a++;
+    int64_t b = a;
+    while (b < nPts && lmRank[b] == me) b++;
+    h->lmBegin = a, h->lmEnd = b, h->isRoot = me == 0;
+  }
   if (h->lmEnd < 0) h->lmBegin = 0, h->lmEnd = nPts;
   if (h->lmBegin < 0 || h->lmEnd > nPts || h->lmBegin > h->lmEnd) return fail(VB_E_ARG, "bad landmark shard range");
   d.lmB = h->lmBegin, d.lmE = h->lmEnd, d.root = h->isRoot ? 1 : 0;
   d.obB = lmObs[h->lmBegin], d.obE = lmObs[h->lmEnd], d.obFree = lmObs[nPts];
+  // constant-point observations of this handle: [fB, fE) (the root's whole tail unless partitioned)
+  d.fB = d.obFree, d.fE = h->isRoot ? nObs : d.obFree;
+  if (world > 1) {
+    int64_t a = d.obFree;
+    while (a < nObs && obsOwner(perm[a]) < h->partRank) a++;
+    int64_t b = a;
+    while (b < nObs && obsOwner(perm[b]) == h->partRank) b++;
+    d.fB = a, d.fE = b;
+  }
   // ---------------- couplings: row ends and the tile pattern
   const int32_t nT = (int32_t)((nRed + TS - 1) / TS);
   d.nT = nT;
@@ -768,7 +869,7 @@ int doFinalize(vb_handle h) {
     // observation groups: this shard's observations by their 4 reduced blocks (rig, camera)
     std::vector<int32_t> gobs;
     for (int64_t o = 0; o < nObs; o++)
-      if ((o >= d.obB && o < d.obE) || (h->isRoot && o >= d.obFree)) gobs.push_back((int32_t)o);
+      if ((o >= d.obB && o < d.obE) || (o >= d.fB && o < d.fE)) gobs.push_back((int32_t)o);
     auto gkey = [&](int32_t o, int s) { return obRed[(int64_t)o * 4 + s]; };
     std::stable_sort(gobs.begin(), gobs.end(), [&](int32_t a, int32_t b) {
       for (int s = 0; s < 4; s++)
@@ -882,90 +983,134 @@ int doFinalize(vb_handle h) {
     }
     std::vector<std::vector<int32_t>> cols(nLev);
     for (int32_t J = 0; J < nT; J++) cols[level[J]].push_back(J);
-    // fan-out triangular solve task lists (solver.hip fwd/bwd_fanout_kernel), by elimination level:
-    // every task of a level only waits on tasks of earlier levels (or the level's own diagonal task
-    // listed first), so the waves' in-flight window spans all independent subtrees of the level
-    {
-      std::vector<int32_t> tf, tb, ef(nT), eb(nT);
+    int64_t fanWgs = 2048;
+    if (const char* e = getenv("VIBA_FANIN_WGS")) fanWgs = std::max<int64_t>(64, atoll(e));
+    // Build one schedule.  colSel(J): columns factored here (potrf, trsm, solve diagonal tasks);
+    // tgtSel(J): fan-in targets in column J; srcSel(K): contributions from column K; preSel(J): rows
+    // whose x is known before the backward solve (their tile tasks run, they get no diagonal task).
+    auto build = [&](Sched& S, auto colSel, auto tgtSel, auto srcSel, auto preSel) -> int {
+      // contributions by target: column K's pair (qi >= qk) of off-diagonal tiles updates the target
+      // tile (row qi, row qk) with L_{qi,K} L_{qk,K}^T (counting sort by target tile; sources in
+      // level order, so every target's list runs from old to new columns)
+      std::vector<int64_t> ccnt(nTiles + 1, 0);
+      std::vector<int32_t> pairs;
+      for (int pass = 0; pass < 2; pass++) {
+        std::vector<int64_t> pos;
+        if (pass == 1) {
+          for (int64_t t = 0; t < nTiles; t++) ccnt[t + 1] += ccnt[t];
+          pos.assign(ccnt.begin(), ccnt.end() - 1);
+          pairs.assign(2 * (size_t)ccnt[nTiles], 0);
+        }
+        for (int32_t LK = 0; LK < nLev; LK++)
+          for (int32_t K : cols[LK]) {
+            if (!srcSel(K)) continue;
+            const int64_t c0 = h->colStart[K], n = h->colStart[K + 1] - c0;
+            for (int64_t qi = 1; qi < n; qi++)
+              for (int64_t qk = 1; qk <= qi; qk++) {
+                if (!tgtSel(h->colRowsH[c0 + qk])) continue;
+                const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
+                if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
+                if (pass == 0) {
+                  ccnt[t + 1]++;
+                } else {
+                  const int64_t at = pos[t]++;
+                  pairs[2 * at] = h->colTilesH[c0 + qi], pairs[2 * at + 1] = h->colTilesH[c0 + qk];
+                }
+              }
+          }
+      }
+      if (ccnt[nTiles] >= INT32_MAX) return fail(VB_E_STATE, "tile Cholesky too large (contribution count)");
+      // per level: fan-in of the level's target tiles, then potrf of its diagonals, then trsm.  A
+      // target's list is cut into near-equal chunks of at most `cs` contributions, cs chosen per
+      // level so the launch has ~fanWgs workgroups (>= 4 contributions per chunk: one per wave)
+      std::vector<int32_t> pT, pC, tD, tT, tC, fan;
+      S.lvP.assign(nLev + 1, 0), S.lvT.assign(nLev + 1, 0), S.lvU.assign(nLev + 1, 0);
+      for (int32_t L = 0; L < nLev; L++) {
+        int64_t total = 0;
+        for (int32_t J : cols[L])
+          if (tgtSel(J))
+            for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
+        const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
+        for (int32_t J : cols[L]) {
+          const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+          if (colSel(J)) {
+            pT.push_back(h->colTilesH[c0]), pC.push_back(J);
+            for (int64_t q = 1; q < n; q++) tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J);
+          }
+          if (!tgtSel(J)) continue;
+          for (int64_t q = 0; q < n; q++) {
+            const int32_t t = h->colTilesH[c0 + q];
+            const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
+            if (m == 0) continue;
+            const int64_t nch = (m + cs - 1) / cs;
+            for (int64_t k = 0; k < nch; k++) {
+              const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
+              fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
+            }
+          }
+        }
+        S.lvP[L + 1] = (int64_t)pT.size(), S.lvT[L + 1] = (int64_t)tT.size(), S.lvU[L + 1] = (int64_t)fan.size() / 4;
+      }
+      S.nLevels = nLev, S.nPairs = ccnt[nTiles];
+      // fan-out solve task lists, by elimination level: every task of a level only waits on tasks of
+      // earlier levels (or the level's own diagonal task listed first), so the waves' in-flight window
+      // spans all independent subtrees of the level
+      std::vector<int32_t> tf, tb, ef(nT, 0), eb(nT, 0), pre;
       for (int32_t L = 0; L < nLev; L++)
         for (int32_t K : cols[L]) {
+          if (!colSel(K)) continue;
           tf.insert(tf.end(), {K, -1});
           for (int64_t c = h->colStart[K] + 1; c < h->colStart[K + 1]; c++) tf.insert(tf.end(), {K, (int32_t)c});
-          ef[K] = (int32_t)(h->rowStart[K + 1] - h->rowStart[K]);
+          for (int64_t c = h->rowStart[K]; c < h->rowStart[K + 1]; c++) ef[K] += srcSel(h->rowColH[c]) ? 1 : 0;
           eb[K] = (int32_t)(h->colStart[K + 1] - h->colStart[K] - 1);
         }
       for (int32_t L = nLev - 1; L >= 0; L--)
         for (int32_t J : cols[L]) {
-          tb.insert(tb.end(), {J, -1});
-          for (int64_t c = h->rowStart[J]; c < h->rowStart[J + 1]; c++) tb.insert(tb.end(), {J, (int32_t)c});
+          const bool own = colSel(J), known = preSel(J);
+          if (own) tb.insert(tb.end(), {J, -1});
+          if (known) pre.push_back(J);
+          if (!own && !known) continue;
+          for (int64_t c = h->rowStart[J]; c < h->rowStart[J + 1]; c++)
+            if (colSel(h->rowColH[c])) tb.insert(tb.end(), {J, (int32_t)c});
         }
-      h->nSolveTasksF = (int64_t)tf.size() / 2, h->nSolveTasksB = (int64_t)tb.size() / 2;
-      if (upload(&h->solveTasksFD, tf) || upload(&h->solveTasksBD, tb) || upload(&h->solveExpFD, ef) ||
-          upload(&h->solveExpBD, eb))
+      S.nF = (int64_t)tf.size() / 2, S.nB = (int64_t)tb.size() / 2, S.nPreReady = (int64_t)pre.size();
+      if (upload(&S.potrfTileD, pT) || upload(&S.potrfColD, pC) || upload(&S.trsmDiagD, tD) ||
+          upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.updD, fan) ||
+          upload(&S.fanPairsD, pairs) || upload(&S.tasksFD, tf) || upload(&S.tasksBD, tb) ||
+          upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre))
+        return VB_E_HIP;
+      S.built = true;
+      return 0;
+    };
+    const int W = h->partWorld, me = h->partRank;
+    auto any = [](int32_t) { return true; };
+    auto none = [](int32_t) { return false; };
+    if (W <= 1) {
+      if (int rc = build(h->sch[0], any, any, any, none)) return rc;
+    } else {
+      auto own = [&](int32_t J) { return h->colOwner[J] == me; };
+      auto root = [&](int32_t J) { return h->colOwner[J] == W; };
+      auto ownOrRoot = [&](int32_t J) { return h->colOwner[J] == me || h->colOwner[J] == W; };
+      if (int rc = build(h->sch[0], own, ownOrRoot, own, root)) return rc;
+      if (me == 0)
+        if (int rc = build(h->sch[1], root, root, root, none)) return rc;
+      for (int32_t J = 0; J < nT; J++)
+        if (root(J)) {
+          h->rootRows.push_back(J);
+          for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) h->rootTiles.push_back(h->colTilesH[c]);
+        }
+      std::vector<int32_t> ownRows;
+      for (int32_t J = 0; J < nT; J++)
+        if (own(J) || (me == 0 && root(J))) ownRows.push_back(J);
+      h->nOwnRows = (int64_t)ownRows.size();
+      if (upload(&h->ownRowsD, ownRows) || alloc0(&h->ownPack, ownRows.size() * (size_t)TS + 1)) return VB_E_HIP;
+      if (upload(&h->rootTilesD, h->rootTiles) || upload(&h->rootRowsD, h->rootRows) ||
+          alloc0(&h->rootPack, h->rootTiles.size() * (size_t)TS * TS + 1) ||
+          alloc0(&h->rowPack, h->rootRows.size() * (size_t)TS + 1))
         return VB_E_HIP;
     }
-    // contributions by target: column K's pair (qi >= qk) of off-diagonal tiles updates the target
-    // tile (row qi, row qk) with L_{qi,K} L_{qk,K}^T (counting sort by target tile)
-    std::vector<int64_t> ccnt(nTiles + 1, 0);
-    for (int pass = 0; pass < 2; pass++) {
-      std::vector<int64_t> pos;
-      if (pass == 1) {
-        for (int64_t t = 0; t < nTiles; t++) ccnt[t + 1] += ccnt[t];
-        pos.assign(ccnt.begin(), ccnt.end() - 1);
-        h->fanPairs.assign(2 * (size_t)ccnt[nTiles], 0);
-      }
-      for (int32_t K = 0; K < nT; K++) {
-        const int64_t c0 = h->colStart[K], n = h->colStart[K + 1] - c0;
-        for (int64_t qi = 1; qi < n; qi++)
-          for (int64_t qk = 1; qk <= qi; qk++) {
-            const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
-            if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
-            if (pass == 0) {
-              ccnt[t + 1]++;
-            } else {
-              const int64_t at = pos[t]++;
-              h->fanPairs[2 * at] = h->colTilesH[c0 + qi], h->fanPairs[2 * at + 1] = h->colTilesH[c0 + qk];
-            }
-          }
-      }
-    }
-    if (ccnt[nTiles] >= INT32_MAX) return fail(VB_E_STATE, "tile Cholesky too large (contribution count)");
-    // per level: fan-in of the level's column tiles, then potrf of its diagonals, then trsm.  A
-    // target's list is cut into near-equal chunks of at most `cs` contributions, cs chosen per level
-    // so the launch has ~fanWgs workgroups (>= 4 contributions per chunk: one per wave)
-    int64_t fanWgs = 2048;
-    if (const char* e = getenv("VIBA_FANIN_WGS")) fanWgs = std::max<int64_t>(64, atoll(e));
-    std::vector<int32_t> pT, pC, tD, tT, tC, fan;
-    h->lvP.assign(nLev + 1, 0), h->lvT.assign(nLev + 1, 0), h->lvU.assign(nLev + 1, 0);
-    for (int32_t L = 0; L < nLev; L++) {
-      int64_t total = 0;
-      for (int32_t J : cols[L])
-        for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
-      const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
-      for (int32_t J : cols[L]) {
-        const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
-        pT.push_back(h->colTilesH[c0]), pC.push_back(J);
-        for (int64_t q = 1; q < n; q++) tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J);
-        for (int64_t q = 0; q < n; q++) {
-          const int32_t t = h->colTilesH[c0 + q];
-          const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
-          if (m == 0) continue;
-          const int64_t nch = (m + cs - 1) / cs;
-          for (int64_t k = 0; k < nch; k++) {
-            const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
-            fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
-          }
-        }
-      }
-      h->lvP[L + 1] = (int64_t)pT.size(), h->lvT[L + 1] = (int64_t)tT.size(), h->lvU[L + 1] = (int64_t)fan.size() / 4;
-    }
     h->nLevels = nLev;
-    h->nPairs = ccnt[nTiles];
-    if (upload(&h->potrfTileD, pT) || upload(&h->potrfColD, pC) || upload(&h->trsmDiagD, tD) ||
-        upload(&h->trsmTargetD, tT) || upload(&h->trsmColD, tC) || upload(&h->updD, fan) ||
-        upload(&h->fanPairsD, h->fanPairs))
-      return VB_E_HIP;
-    std::vector<int32_t>().swap(h->fanPairs);
+    h->nPairs = h->sch[0].nPairs + h->sch[1].nPairs;
   }
   // ---------------- small factors (+ whitening square roots)
   for (int fk = 1; fk < 14; fk++) {
@@ -990,7 +1135,7 @@ int doFinalize(vb_handle h) {
     sf.stage = d.nSmallStage;
     d.nSmallStage += sf.n;
   }
-  if (h->isRoot && d.nSmallStage > 0 &&
+  if ((h->isRoot || h->partWorld > 1) && d.nSmallStage > 0 &&
       (alloc0(&d.sJ, (size_t)d.nSmallStage * kSmallJ) || alloc0(&d.sE, (size_t)d.nSmallStage * kSmallE) ||
        alloc0(&d.sMeta, (size_t)d.nSmallStage * kSmallMeta)))
     return VB_E_HIP;
@@ -1019,6 +1164,11 @@ int doFinalize(vb_handle h) {
       upload(&d.lxStart, lxStart) || upload(&d.lxLm, lxLm) || upload(&d.lxCol, lxCol))
     return VB_E_HIP;
   if (upload(&d.tileIdx, tileIdx) || alloc0(&d.tiles, (size_t)nTiles * TS * TS)) return VB_E_HIP;
+  {
+    int8_t* co = nullptr;
+    if (upload(&co, h->colOwner)) return VB_E_HIP;
+    d.colOwner = co, d.myRank = h->partRank, d.world = h->partWorld;
+  }
   const size_t nPad = (size_t)nT * TS;
   if (alloc0(&d.gRed, nPad) || alloc0(&d.rhs, nPad) || alloc0(&d.xRed, nPad) || alloc0(&d.gRedNew, nPad) ||
       alloc0(&d.stepRed, nPad) || alloc0(&d.stepPt, nPts * 3) || alloc0(&d.subRed, nPad) ||
@@ -1041,15 +1191,16 @@ int doFinalize(vb_handle h) {
 
 // ------------------------------------------------------------------ numeric phases
 // small factors (root only) on the side stream; joinSmall makes the main stream wait for them
+bool smallHere(vb_handle h, int mode) { return h->isRoot || (h->partWorld > 1 && mode != 2); }
 void forkSmall(vb_handle h, int mode, double* gOut) {
-  if (!h->isRoot) return;
+  if (!smallHere(h, mode)) return;
   (void)hipEventRecord(h->evFork, h->st);
   (void)hipStreamWaitEvent(h->st2, h->evFork, 0);
   launch_small(h->d, mode, gOut, h->st2);
   (void)hipEventRecord(h->evJoin, h->st2);
 }
 void joinSmall(vb_handle h) {
-  if (h->isRoot) (void)hipStreamWaitEvent(h->st, h->evJoin, 0);
+  if (h->isRoot || h->partWorld > 1) (void)hipStreamWaitEvent(h->st, h->evJoin, 0);
 }
 
 // visual kernels over this shard's observations (+ the root's constant-point observations)
@@ -1057,32 +1208,32 @@ void visualLinShard(vb_handle h, int updateCache, int dontRetry) {
   const Dev& d = h->d;
   profBegin(h, KF_VISUAL_LIN);
   launch_visual_lin(d, updateCache, dontRetry, d.obB, d.obE, h->st);
-  if (d.root) launch_visual_lin(d, updateCache, dontRetry, d.obFree, d.nObs, h->st);
+  launch_visual_lin(d, updateCache, dontRetry, d.fB, d.fE, h->st);
   profEnd(h, KF_VISUAL_LIN);
 }
 void visualCostShard(vb_handle h, int comparable) {
   const Dev& d = h->d;
   profBegin(h, KF_VISUAL_COST);
   launch_visual_cost(d, comparable, d.obB, d.obE, h->st);
-  if (d.root) launch_visual_cost(d, comparable, d.obFree, d.nObs, h->st);
+  launch_visual_cost(d, comparable, d.fB, d.fE, h->st);
   profEnd(h, KF_VISUAL_COST);
 }
 
-void factorSeq(vb_handle h) {
+void factorSeq(vb_handle h, const Sched& S) {
   Dev& d = h->d;
-  for (int32_t L = 0; L < h->nLevels; L++) {
-    const int64_t p0 = h->lvP[L], t0 = h->lvT[L], u0 = h->lvU[L];
+  for (int32_t L = 0; L < S.nLevels; L++) {
+    const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
     profBegin(h, KF_GEMM);
-    launch_fanin(d, h->updD + 4 * u0, h->fanPairsD, (int)(h->lvU[L + 1] - u0), h->st);
+    launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
     profEnd(h, KF_GEMM);
     profBegin(h, KF_POTRF);
-    launch_potrf(d, h->potrfTileD + p0, h->potrfColD + p0, (int)(h->lvP[L + 1] - p0), h->dinv, h->st);
+    launch_potrf(d, S.potrfTileD + p0, S.potrfColD + p0, (int)(S.lvP[L + 1] - p0), h->dinv, h->st);
     profEnd(h, KF_POTRF);
     profBegin(h, KF_TRSM);
-    launch_trsm(d, h->trsmDiagD + t0, h->trsmTargetD + t0, h->trsmColD + t0, (int)(h->lvT[L + 1] - t0), h->dinv, h->st);
+    launch_trsm(d, S.trsmDiagD + t0, S.trsmTargetD + t0, S.trsmColD + t0, (int)(S.lvT[L + 1] - t0), h->dinv, h->st);
     profEnd(h, KF_TRSM);
   }
-  launch_diag_inverse(d, h->linv, h->st);
+  launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
 }
 
 // solve L L^T x = b (b is clobbered), result into x
@@ -1106,10 +1257,10 @@ void solveSeq(vb_handle h, double* b, double* x) {
 
 // launch sequences are fixed by the symbolic structure: capture them once into HIP graphs
 // (unless one of their kernel families is being profiled, which needs per-launch events)
-int captureGraph(vb_handle h, bool factor, hipGraphExec_t* out) {
+int captureGraph(vb_handle h, const Sched* S, hipGraphExec_t* out) {
   hipGraph_t g;
   HIPCHK(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
-  if (factor) factorSeq(h);
+  if (S) factorSeq(h, *S);
   else solveSeq(h, h->rhsWork, h->d.xRed);
   HIPCHK(hipStreamEndCapture(h->st, &g));
   HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
@@ -1117,26 +1268,32 @@ int captureGraph(vb_handle h, bool factor, hipGraphExec_t* out) {
   return 0;
 }
 
-int factorReduced(vb_handle h) {
+// factor the columns of schedule `which` (0: all, or this rank's subtree in partition mode; 1: ROOT)
+int factorReduced(vb_handle h, int which = 0) {
+  Sched& S = h->sch[which];
+  if (!S.built) return fail(VB_E_STATE, "no factorization schedule here (partition root on rank 0 only)");
   const bool prof = h->profFamily == KF_POTRF || h->profFamily == KF_GEMM || h->profFamily == KF_TRSM;
   if (!h->useGraphs || prof) {
-    factorSeq(h);
+    factorSeq(h, S);
     return 0;
   }
-  if (!h->factorGraph)
-    if (int rc = captureGraph(h, true, &h->factorGraph)) return rc;
-  HIPCHK(hipGraphLaunch(h->factorGraph, h->st));
+  if (!S.graph)
+    if (int rc = captureGraph(h, &S, &S.graph)) return rc;
+  HIPCHK(hipGraphLaunch(S.graph, h->st));
   return 0;
 }
 
-// solves with rhsWork as right-hand side, result in xRed
-int solveReduced(vb_handle h) {
-  if (!h->legacySolve) {
+// solves with rhsWork as right-hand side, result in xRed (schedule `which`, phases bit 0 forward,
+// bit 1 backward; a partitioned backward pass takes the ROOT rows of xRed as given)
+int solveReduced(vb_handle h, int which = 0, int phases = 3) {
+  Sched& S = h->sch[which];
+  if (!S.built) return fail(VB_E_STATE, "no solve schedule here (partition root on rank 0 only)");
+  if (!h->legacySolve || h->partWorld > 1) {
     Dev& d = h->d;
     profBegin(h, KF_FWD);
-    launch_solve_fanout(d, h->solveTasksFD, h->nSolveTasksF, h->solveTasksBD, h->nSolveTasksB, h->solveExpFD,
-                        h->solveExpBD, h->colTilesD, h->colRowsD, h->rowTilesD, h->rowColD, h->linv, h->rhsWork, h->yvec,
-                        d.xRed, h->solveFlags, h->numCUs, h->st);
+    launch_solve_fanout(d, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD,
+                        h->rowTilesD, h->rowColD, h->linv, h->rhsWork, h->yvec, d.xRed, h->solveFlags, h->numCUs,
+                        h->st, phases, S.preReadyD, S.nPreReady);
     profEnd(h, KF_FWD);
     return 0;
   }
@@ -1146,7 +1303,7 @@ int solveReduced(vb_handle h) {
     return 0;
   }
   if (!h->solveGraph)
-    if (int rc = captureGraph(h, false, &h->solveGraph)) return rc;
+    if (int rc = captureGraph(h, nullptr, &h->solveGraph)) return rc;
   HIPCHK(hipGraphLaunch(h->solveGraph, h->st));
   return 0;
 }
@@ -1235,7 +1392,7 @@ int vb_destroy(vb_handle h) {
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
-                  h->colRowsD, h->rowTilesD, h->rowColD, h->potrfTileD, h->potrfColD, h->trsmDiagD, h->trsmTargetD, h->trsmColD, h->updD, h->fanPairsD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->solveTasksFD, h->solveTasksBD, h->solveExpFD, h->solveExpBD, h->shardTilesD, h->shardPack, h->dinv, h->yvec,
+                  h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -1258,7 +1415,13 @@ int vb_destroy(vb_handle h) {
   if (h->evJoin) hipEventDestroy(h->evJoin);
   if (h->st2) hipStreamSynchronize(h->st2), hipStreamDestroy(h->st2);
   for (auto& e : h->profEv) hipEventDestroy(e);
-  if (h->factorGraph) hipGraphExecDestroy(h->factorGraph);
+  for (Sched& S : h->sch) {
+    void* sp[] = {S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.updD, S.fanPairsD,
+                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD};
+    for (void* p : sp)
+      if (p) hipFree(p);
+    if (S.graph) hipGraphExecDestroy(S.graph);
+  }
   if (h->solveGraph) hipGraphExecDestroy(h->solveGraph);
   hipStreamDestroy(h->st);
   delete h;
@@ -1326,7 +1489,7 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  if (h->isRoot) launch_pad_diag(d, h->padRowsD, h->nPadRows, h->st);
+  if (h->isRoot || h->partWorld > 1) launch_pad_diag(d, h->padRowsD, h->nPadRows, h->st);
   forkSmall(h, 0, d.gRed);
   visualLinShard(h, update_cache, dont_retry_failed);
   joinSmall(h);
@@ -1350,7 +1513,7 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
   profEnd(h, KF_LANDMARK);
   HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   profBegin(h, KF_SCHUR);
-    launch_schur(d, lambda, h->isRoot ? 1 : 0, h->st);
+    launch_schur(d, lambda, (h->isRoot || h->partWorld > 1) ? 1 : 0, h->st);
     profEnd(h, KF_SCHUR);
   HIPCHK(hipEventRecord(h->ev[3], h->st));
   if (int rc = factorReduced(h)) return rc;
@@ -1517,7 +1680,7 @@ int vb_get_gradient(vb_handle h, int kind, double* out) {
   if (h->linearized) {
     Dev& d = h->d;
     HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
-    if (h->isRoot) launch_small(d, 1, d.gRedNew, h->st);
+    if (smallHere(h, 1)) launch_small(d, 1, d.gRedNew, h->st);
     launch_landmark(d, 0.0, 1, d.lmB, d.lmE, h->st);
     launch_reduced_grad(d, 0, h->st);
     return getPerKind(h, d.gRedNew, d.gpNew, kind, out);
@@ -1733,7 +1896,7 @@ int vb_assemble_reduced(vb_handle h, double lambda) {
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   launch_landmark(d, lambda, 0, d.lmB, d.lmE, h->st);
   HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
-  launch_schur(d, lambda, h->isRoot ? 1 : 0, h->st);
+  launch_schur(d, lambda, (h->isRoot || h->partWorld > 1) ? 1 : 0, h->st);
   HIPCHK(hipStreamSynchronize(h->st));
   if (int rc = checkErr(h)) return rc;
   h->linearized = false;
@@ -1786,6 +1949,78 @@ int vb_assemble_new_rhs(vb_handle h) {
   launch_landmark(d, 0.0, 2, d.lmB, d.lmE, h->st);
   launch_reduced_grad(d, 1, h->st);
   HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
+}
+
+
+// ---------------- partitioned factorization (nested-dissection subtrees per rank)
+int vb_set_partition(vb_handle h, int rank, int world) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_partition must precede vb_finalize");
+  if (world < 1 || world > 64 || (world & (world - 1)) || rank < 0 || rank >= world)
+    return fail(VB_E_ARG, "vb_set_partition: world must be a power of two in [1, 64], 0 <= rank < world");
+  h->partRank = rank, h->partWorld = world;
+  return 0;
+}
+// which 0: this rank's subtree columns (+ their fan-in into the ROOT tiles); 1 (rank 0): ROOT columns
+int vb_factor_part(vb_handle h, int which) {
+  if (!h || !h->finalized || which < 0 || which > 1) return fail(VB_E_STATE, "vb_factor_part: bad state / schedule");
+  HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
+  if (int rc = factorReduced(h, which)) return rc;
+  HIPCHK(hipStreamSynchronize(h->st));
+  if (int rc = checkErr(h)) return rc;
+  h->factored = true;
+  return 0;
+}
+// phase 0: rhsWork = rhs, forward solve over this rank's subtree (partial ROOT rows of rhsWork);
+// 1 (rank 0): forward + backward over the ROOT columns (ROOT rows of rhsWork summed);
+// 2: backward over this rank's subtree (ROOT rows of xRed given)
+int vb_solve_part(vb_handle h, int phase) {
+  if (!h || !h->factored || phase < 0 || phase > 2) return fail(VB_E_STATE, "vb_solve_part: bad state / phase");
+  HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
+  if (phase == 0)
+    HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  if (int rc = solveReduced(h, phase == 1 ? 1 : 0, phase == 0 ? 1 : phase == 1 ? 3 : 2)) return rc;
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkErr(h);
+}
+// what 0: the ROOT-column tiles of the tile store, 1: ROOT rows of rhsWork, 2: ROOT rows of xRed;
+// dir 0 packs them into the engine-owned buffer (returned), dir 1 writes the buffer back
+int vb_part_exchange(vb_handle h, int what, int dir, double** buf, int64_t* len) {
+  if (!h || !h->finalized || what < 0 || what > 2 || dir < 0 || dir > 1 || !buf || !len)
+    return fail(VB_E_ARG, "bad vb_part_exchange arguments");
+  if (h->partWorld <= 1) return fail(VB_E_STATE, "vb_part_exchange needs vb_set_partition");
+  const bool tiles = what == 0;
+  const int32_t* idx = tiles ? h->rootTilesD : h->rootRowsD;
+  const int64_t n = tiles ? (int64_t)h->rootTiles.size() : (int64_t)h->rootRows.size();
+  double* base = tiles ? h->d.tiles : what == 1 ? h->rhsWork : h->d.xRed;
+  double* pk = tiles ? h->rootPack : h->rowPack;
+  launch_chunk_copy(base, idx, n, tiles ? TS * TS : TS, pk, dir == 0 ? 0 : 1, h->st);
+  HIPCHK(hipStreamSynchronize(h->st));
+  *buf = pk, *len = n * (tiles ? TS * TS : TS);
+  return 0;
+}
+// [subtree tile columns of this rank, ROOT tile columns, fan-in contributions of the local schedule,
+//  of the ROOT schedule (rank 0), ROOT tiles exchanged]
+int vb_part_info(vb_handle h, int64_t* out5) {
+  if (!h || !h->finalized || !out5) return fail(VB_E_STATE, "not finalized");
+  int64_t own = 0, root = 0;
+  for (int8_t o : h->colOwner) own += o == h->partRank, root += o == h->partWorld;
+  if (h->partWorld <= 1) own = (int64_t)h->colOwner.size(), root = 0;
+  out5[0] = own, out5[1] = root, out5[2] = h->sch[0].nPairs, out5[3] = h->sch[1].nPairs;
+  out5[4] = (int64_t)h->rootTiles.size();
+  return 0;
+}
+// after the backward phase: the rows this rank solved (its subtree; + ROOT on rank 0) of xRed, other
+// rows zeroed, into the rhs buffer (returned) -- the caller all-reduces it, then vb_back_substitute
+int vb_share_x(vb_handle h, double** xred, int64_t* len) {
+  if (!h || !h->finalized || !xred || !len) return fail(VB_E_ARG, "bad vb_share_x arguments");
+  Dev& d = h->d;
+  HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
+  launch_chunk_copy(d.xRed, h->ownRowsD, h->nOwnRows, TS, h->ownPack, 0, h->st);
+  launch_chunk_copy(d.rhs, h->ownRowsD, h->nOwnRows, TS, h->ownPack, 1, h->st);
+  HIPCHK(hipStreamSynchronize(h->st));
+  *xred = d.rhs, *len = (int64_t)d.nT * TS;
   return 0;
 }
 

@@ -159,14 +159,26 @@ struct Dev {
   double* red = nullptr;  // 64 doubles
   int32_t* err = nullptr;  // error flags
   // landmark shard of this handle (multi-GPU; the whole problem on a single GPU): landmarks
-  // [lmB, lmE), their observations [obB, obE); the root also owns the observations of constant
-  // points [obFree, nObs), every small factor and the reduced-variable step ratios
-  int64_t lmB = 0, lmE = 0, obB = 0, obE = 0, obFree = 0;
+  // [lmB, lmE), their observations [obB, obE), constant-point observations [fB, fE) (all of
+  // [obFree, nObs) on the root unless partitioned); the root also owns the reduced-variable step
+  // ratios and, unless partitioned, every small factor
+  int64_t lmB = 0, lmE = 0, obB = 0, obE = 0, obFree = 0, fB = 0, fE = 0;
   int32_t root = 1;
+  // partitioned factorization: owner of every tile column (world = ROOT, rank 0), this rank, world
+  // (world <= 1: not partitioned, every column is this handle's)
+  const int8_t* colOwner = nullptr;
+  int32_t myRank = 0, world = 1;
   // config
   LossParams reproj, imu;
   ImuIdx jac;
 };
+
+// partitioned factorization: does this handle assemble into tile column `col`?
+__device__ __forceinline__ bool owns_col(const Dev& d, int64_t col) {
+  if (d.world <= 1) return true;
+  const int o = d.colOwner[col];
+  return o == d.myRank || (o == d.world && d.myRank == 0);
+}
 
 // Kernel-family timing (vb_profile_kernel): the host arms an event pair before the launch wrapper of
 // the profiled family; the wrapper's main kernel is then launched with hipExtLaunchKernelGGL, whose

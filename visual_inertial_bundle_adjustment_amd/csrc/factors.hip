@@ -733,6 +733,7 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
 struct SmallLaunch {
   SmallArgs a[14];
   int32_t first[15];
+  int32_t countCost;  // the root counts the small factors' cost (partitioned: every rank evaluates)
 };
 __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallLaunch L) {
   const int b = blockIdx.x;
@@ -755,6 +756,7 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallLaunch L) {
     case 12: acc[0] = small_eval<12>(d, L.a[12], k); break;
     default: acc[0] = small_eval<13>(d, L.a[13], k); break;
   }
+  if (!L.countCost) acc[0] = 0.0;
   block_sum_atomic<1>(acc, d.red + (L.a[1].mode == 2 ? 1 : 0));
 }
 
@@ -807,7 +809,7 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
     const int c = act[wave][a][0];
     double g = 0;
     for (int r = 0; r < m; r++) g += J[r * kMaxCols + c] * se[1 + r];
-    atomicAdd(gOut + act[wave][a][1], drho * g);
+    if (owns_col(d, act[wave][a][1] / d.T)) atomicAdd(gOut + act[wave][a][1], drho * g);
   }
   if (mode != 0) return;
   const int P = A * (A + 1) / 2;
@@ -821,7 +823,7 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
     for (int r = 0; r < m; r++) hs += J[r * kMaxCols + ca] * J[r * kMaxCols + cb];
     int64_t R = act[wave][a][1], C = act[wave][b][1];
     if (R < C) { const int64_t t = R; R = C; C = t; }
-    atomicAdd(tile_addr(d, R, C), drho * hs);
+    if (owns_col(d, C / d.T)) atomicAdd(tile_addr(d, R, C), drho * hs);
   }
 }
 
@@ -849,6 +851,7 @@ void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st) {
     nb += (int32_t)((f.n + 63) / 64);
   }
   L.first[14] = nb;
+  L.countCost = d.root;
   if (nb > 0) hipLaunchKernelGGL(small_kernel, dim3((unsigned)nb), dim3(64), 0, st, d, L);
 }
 

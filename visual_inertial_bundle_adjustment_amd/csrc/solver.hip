@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
 // identity term (Optimizer.cpp:136-146 addDamping: H_ii += lambda * H_ii + lambda)
 __global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= d.nRed) return;
+  if (r >= d.nRed || !owns_col(d, r / TS)) return;
   double* p = tile_ptr(d, r, r);
   *p = *p * (1.0 + lambda) + (addIdentity ? lambda : 0.0);
 }
@@ -417,7 +417,7 @@ __global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
 // gradient-only (mode 0: gRedNew += sum J~^T e~ over this shard's observations) or new reduced RHS
 // (mode 1: rhs = gRedNew - sum Y^T zNew over this shard's landmarks)
 __device__ __forceinline__ bool shard_obs(const Dev& d, int64_t o) {
-  return (o >= d.obB && o < d.obE) || (d.root && o >= d.obFree);
+  return (o >= d.obB && o < d.obE) || (o >= d.fB && o < d.fE);
 }
 __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
   __shared__ double g[32];
@@ -807,9 +807,9 @@ __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, 
 // Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
 // tile, lane = column c of X = L^-1): X[i][c] = (delta_ic - sum_{k<i} L_ik X_kc) / L_ii.
 // linv[J] is column-major; the triangular solves apply it as a GEMV.
-__global__ void __launch_bounds__(64) diag_inverse_kernel(Dev d, double* linv) {
+__global__ void __launch_bounds__(64) diag_inverse_kernel(Dev d, const int32_t* cols, double* linv) {
   __shared__ double L[TS * TS];
-  const int J = blockIdx.x, lane = threadIdx.x;
+  const int J = cols ? cols[blockIdx.x] : (int)blockIdx.x, lane = threadIdx.x;
   const double* Ad = d.tiles + (int64_t)d.tileIdx[(int64_t)J * d.nT + J] * TS * TS;
   {
     double v[TS];  // all loads in flight before the LDS stores
@@ -1040,16 +1040,31 @@ __global__ void __launch_bounds__(256) bwd_fanout_kernel(Dev d, const int32_t* t
   }
 }
 
-// rhs b (clobbered), y (clobbered) -> x; flags: 4 nT words (ready / count, forward and backward)
+__global__ void set_ready_kernel(const int32_t* rows, int64_t n, unsigned* ready) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) ready[rows[i]] = 1u;
+}
+// rhs b (clobbered), y (clobbered) -> x; flags: 4 nT words (ready / count, forward and backward).
+// phases: bit 0 forward, bit 1 backward.  pre[0..nPre): rows whose x is already in x (the backward
+// pass of a partitioned solve: ROOT rows solved on rank 0), marked ready before the backward pass.
 void launch_solve_fanout(const Dev& d, const int32_t* tasksF, int64_t nF, const int32_t* tasksB, int64_t nB,
                          const int32_t* expF, const int32_t* expB, const int32_t* colTiles, const int32_t* colRows,
                          const int32_t* rowTiles, const int32_t* rowCol, const double* linv, double* b, double* y,
-                         double* x, unsigned* flags, int G, hipStream_t st) {
-  (void)hipMemsetAsync(flags, 0, 4 * (size_t)d.nT * sizeof(unsigned), st);
-  launchK(fwd_fanout_kernel, dim3(G), dim3(256), 0, st, d, tasksF, nF, colTiles, colRows, expF, linv, b, y, flags,
-          flags + d.nT);
-  launchK(bwd_fanout_kernel, dim3(G), dim3(256), 0, st, d, tasksB, nB, rowTiles, rowCol, expB, linv, y, x,
-          flags + 2 * d.nT, flags + 3 * d.nT);
+                         double* x, unsigned* flags, int G, hipStream_t st, int phases, const int32_t* pre,
+                         int64_t nPre) {
+  if (phases & 1) {
+    (void)hipMemsetAsync(flags, 0, 2 * (size_t)d.nT * sizeof(unsigned), st);
+    if (nF > 0)
+      launchK(fwd_fanout_kernel, dim3(G), dim3(256), 0, st, d, tasksF, nF, colTiles, colRows, expF, linv, b, y,
+              flags, flags + d.nT);
+  }
+  if (phases & 2) {
+    (void)hipMemsetAsync(flags + 2 * d.nT, 0, 2 * (size_t)d.nT * sizeof(unsigned), st);
+    if (nPre > 0) hipLaunchKernelGGL(set_ready_kernel, dim3((unsigned)((nPre + 255) / 256)), dim3(256), 0, st, pre, nPre, flags + 2 * d.nT);
+    if (nB > 0)
+      launchK(bwd_fanout_kernel, dim3(G), dim3(256), 0, st, d, tasksB, nB, rowTiles, rowCol, expB, linv, y, x,
+              flags + 2 * d.nT, flags + 3 * d.nT);
+  }
 }
 
 // ------------------------------------------------------------------ point back-substitution
@@ -1227,35 +1242,41 @@ void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const
                  hipStream_t st) {
   if (n > 0) launchK(trsm_kernel, dim3(n), dim3(256), 0, st, d, diag, target, cols, dinv);
 }
-// shard exchange (vb_pack_shard_tiles / vb_add_tiles): one block per listed tile
-__global__ void __launch_bounds__(256) tile_gather_kernel(Dev d, const int32_t* tiles, double* out) {
-  const double* src = d.tiles + (int64_t)tiles[blockIdx.x] * TS * TS;
-  double* dst = out + (int64_t)blockIdx.x * TS * TS;
-  for (int i = threadIdx.x; i < TS * TS; i += 256) dst[i] = src[i];
+// shard / partition exchange (vb_pack_shard_tiles, vb_add_tiles, vb_part_exchange): one block per
+// listed chunk (a 64 x 64 tile of the tile store, or a 64-row block of a reduced vector);
+// mode 0 gathers base -> buf, 1 scatters buf -> base, 2 adds buf into base
+__global__ void __launch_bounds__(256) chunk_copy_kernel(double* base, const int32_t* idx, int chunk, double* buf,
+                                                         int mode) {
+  double* a = base + (int64_t)idx[blockIdx.x] * chunk;
+  double* b = buf + (int64_t)blockIdx.x * chunk;
+  for (int i = threadIdx.x; i < chunk; i += 256) {
+    if (mode == 0) b[i] = a[i];
+    else if (mode == 1) a[i] = b[i];
+    else a[i] += b[i];
+  }
 }
-__global__ void __launch_bounds__(256) tile_scatter_add_kernel(Dev d, const int32_t* tiles, const double* in) {
-  double* dst = d.tiles + (int64_t)tiles[blockIdx.x] * TS * TS;
-  const double* src = in + (int64_t)blockIdx.x * TS * TS;
-  for (int i = threadIdx.x; i < TS * TS; i += 256) dst[i] += src[i];
+void launch_chunk_copy(double* base, const int32_t* idx, int64_t n, int chunk, double* buf, int mode, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(chunk_copy_kernel, dim3((unsigned)n), dim3(256), 0, st, base, idx, chunk, buf, mode);
 }
 void launch_tile_gather(const Dev& d, const int32_t* tiles, int64_t n, double* out, hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(tile_gather_kernel, dim3((unsigned)n), dim3(256), 0, st, d, tiles, out);
+  launch_chunk_copy(d.tiles, tiles, n, TS * TS, out, 0, st);
 }
 void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, const double* in, hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(tile_scatter_add_kernel, dim3((unsigned)n), dim3(256), 0, st, d, tiles, in);
+  launch_chunk_copy(d.tiles, tiles, n, TS * TS, const_cast<double*>(in), 2, st);
 }
 
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
   if (n > 0) launchK(fanin_kernel, dim3(n), dim3(256), 0, st, d, work, pairs);
 }
-void launch_diag_inverse(const Dev& d, double* linv, hipStream_t st) {
-  if (d.nT) hipLaunchKernelGGL(diag_inverse_kernel, dim3(d.nT), dim3(64), 0, st, d, linv);
+// inverses of the diagonal factor tiles of the listed columns (all columns if cols == nullptr)
+void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(diag_inverse_kernel, dim3((unsigned)n), dim3(64), 0, st, d, cols, linv);
 }
 // identity on the diagonal of the padding rows (rows of no variable: tile alignment of the
 // nested-dissection parts, and the tail of the last tile)
 __global__ void pad_diag_kernel(Dev d, const int64_t* rows, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) *tile_ptr(d, rows[i], rows[i]) = 1.0;
+  if (i < n && owns_col(d, rows[i] / TS)) *tile_ptr(d, rows[i], rows[i]) = 1.0;
 }
 void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(pad_diag_kernel, dim3(blocks(n, 256)), dim3(256), 0, st, d, rows, n);

@@ -318,6 +318,70 @@ class ShardedOptimizer:
         return out
 
 
+class PartitionedOptimizer(ShardedOptimizer):
+    """The sharded LM with the reduced factorization itself distributed: every
+    rank factors its nested-dissection subtree, rank 0 only the ROOT separators above them.  Engine
+    built with set_partition(rank, world) (world a power of two; include/viba_hip.h).  Per reduced
+    solve, instead of summing whole partial systems on rank 0:
+
+      local: factor_part(0); solve_part(0)                 (subtree factor, forward solve)
+      reduce ROOT tiles + ROOT rows of the forward vector to rank 0     (RCCL reduce, in place)
+      rank 0: factor_part(1); solve_part(1)                (ROOT factor, forward + backward)
+      broadcast ROOT rows of x; local: solve_part(2)       (subtree backward solve)
+      all-reduce x (each rank contributes the rows it solved), back-substitute the landmarks
+    """
+
+    def __init__(self, engine, comm: ShardComm):
+        self.e, self.c = engine, comm
+        self.n_params = engine.num_params()
+        self.tile_lists = None
+
+    def _exchange(self, what, reduce):
+        e, c = self.e, self.c
+        ptr, n = e.part_exchange(what, 0)
+        if n == 0:
+            return
+        t = _tensor(ptr, n, c.device)
+        if reduce:
+            c.reduce_to_root(t)
+        else:
+            c.broadcast_from_root(t)
+        self.sync_torch()
+        if reduce and c.rank != 0:
+            return
+        e.part_exchange(what, 1)
+
+    def _solve(self, which):
+        e, c = self.e, self.c
+        e.solve_part(0)
+        self._exchange(1, True)
+        if c.rank == 0:
+            e.solve_part(1)
+        self._exchange(2, False)
+        e.solve_part(2)
+        ptr, n = e.share_x()
+        x = _tensor(ptr, n, c.device)
+        s = c._staged(x)
+        c.dist.all_reduce(s)
+        if s is not x:
+            x.copy_(s)
+        self.sync_torch()
+        return e.back_substitute(which)
+
+    def damp_factor_solve(self, lam):
+        e, c = self.e, self.c
+        e.assemble_reduced(lam)
+        e.factor_part(0)
+        self._exchange(0, True)
+        if c.rank == 0:
+            e.factor_part(1)
+        return c.sum(self._solve(0))[0]
+
+    def solve_with_new_gradient(self):
+        self.e.assemble_new_rhs()
+        self._solve(1)
+
+
 # ------------------------------------------------------------------ shard boundaries
 def landmark_order(p):
     """Landmark order of vb_finalize (api.hip): registered points by earliest observing rig, ties by
