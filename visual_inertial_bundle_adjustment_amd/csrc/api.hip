@@ -3,6 +3,7 @@
 // (≙ Optimizer::optimize, Optimizer.cpp:768-1106).  All numeric work runs in HIP kernels on the
 // handle's stream; the host only orders launches, reads back scalars and takes LM decisions.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -678,6 +679,7 @@ int doFinalize(vb_handle h) {
   }
   // reduced row of every landmark panel column
   std::vector<int32_t> pcRow(lmY[nPts] / 3);
+  d.nYcol = lmY[nPts] / 3;
   for (int64_t l = 0; l < nPts; l++)
     for (int64_t b = lmBlk[l]; b < lmBlk[l + 1]; b++) {
       const int32_t r = blkRed[b];
@@ -863,6 +865,9 @@ int doFinalize(vb_handle h) {
             e.colI = (uint32_t)(cb + sg[a].c0), e.nI = (uint16_t)(sg[a].c1 - sg[a].c0);
             e.colJ = (uint32_t)(cb + sg[b].c0), e.nJ = (uint16_t)(sg[b].c1 - sg[b].c0);
             e.lm = (uint32_t)l;
+            e.maskI = e.maskJ = 0;
+            for (int64_t c = sg[a].c0; c < sg[a].c1; c++) e.maskI |= 1ull << (pcRow[cb + c] % TS);
+            for (int64_t c = sg[b].c0; c < sg[b].c1; c++) e.maskJ |= 1ull << (pcRow[cb + c] % TS);
           }
       }
     }
@@ -985,6 +990,7 @@ int doFinalize(vb_handle h) {
     for (int32_t J = 0; J < nT; J++) cols[level[J]].push_back(J);
     int64_t fanWgs = 2048;
     if (const char* e = getenv("VIBA_FANIN_WGS")) fanWgs = std::max<int64_t>(64, atoll(e));
+    const bool fanSort = getenv("VIBA_FAN_SORT") && atoi(getenv("VIBA_FAN_SORT")) != 0;
     // Build one schedule.  colSel(J): columns factored here (potrf, trsm, solve diagonal tasks);
     // tgtSel(J): fan-in targets in column J; srcSel(K): contributions from column K; preSel(J): rows
     // whose x is known before the backward solve (their tile tasks run, they get no diagonal task).
@@ -1048,6 +1054,21 @@ int doFinalize(vb_handle h) {
               fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
             }
           }
+        }
+        if (fanSort) {  // longest chunks first: the dispatcher hands them out in order (LPT)
+          const size_t u0 = (size_t)S.lvU[L];
+          std::vector<std::array<int32_t, 4>> q((fan.size() / 4) - u0);
+          for (size_t i = 0; i < q.size(); i++)
+            for (int k = 0; k < 4; k++) q[i][k] = fan[4 * (u0 + i) + k];
+          // within each XCD's contiguous range of the launch (solver.hip xcd_block)
+          const size_t nq = q.size(), qq = nq / 8, rr = nq % 8;
+          for (size_t x = 0, b0 = 0; x < 8; x++) {
+            const size_t len = qq + (x < rr ? 1 : 0);
+            std::stable_sort(q.begin() + b0, q.begin() + b0 + len, [](const auto& a, const auto& b) { return a[2] > b[2]; });
+            b0 += len;
+          }
+          for (size_t i = 0; i < q.size(); i++)
+            for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
         }
         S.lvP[L + 1] = (int64_t)pT.size(), S.lvT[L + 1] = (int64_t)tT.size(), S.lvU[L + 1] = (int64_t)fan.size() / 4;
       }

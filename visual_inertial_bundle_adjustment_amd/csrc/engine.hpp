@@ -72,6 +72,8 @@ struct TileEnt {
   uint32_t colI, colJ;  // first panel column (global index lmY[l] / 3 + c) inside tile I / J
   uint16_t nI, nJ;      // number of panel columns inside tile I / J
   uint32_t lm;          // landmark
+  uint64_t maskI, maskJ;  // tile rows (r % 64) of those columns; ascending, so row r is column
+                          // popcount(mask & ((1 << r) - 1)) of the run
 };
 struct TileWork {
   int32_t tile, I, J, count;  // count <= 256 landmark entries
@@ -110,6 +112,7 @@ struct Dev {
   int32_t* blkRed = nullptr;  // reduced ids of D(l), sorted by reduced offset
   int32_t* blkCol = nullptr;  // column offset in Y panel
   int32_t* pcRow = nullptr;   // reduced row of every Y panel column (indexed by lmY[l]/3 + c)
+  int64_t nYcol = 0;          // panel columns (lmY[nPts] / 3)
   int32_t* pcBlk = nullptr;   // landmark block (into blkRed/blkCol) of every Y panel column
   int64_t* bxStart = nullptr; // per landmark block: its observation slots bxEnt[bxStart[b] ..)
   int32_t* bxEnt = nullptr;   // (obs << 2) | slot

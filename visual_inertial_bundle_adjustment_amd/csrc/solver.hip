@@ -312,6 +312,137 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
 }
 
+// Schur assembly, register-operand form (no LDS images, no per-batch barriers).  Same work items and
+// quadrant split as schur_tile_kernel; every k-step is one landmark entry (k = lane >> 4 < 3 its
+// three coordinates), and each lane fetches its MFMA operands straight from the Y panel: row r of
+// the tile is the entry's column popcount(mask & ((1 << r) - 1)) when bit r of the entry's row mask
+// is set (rows of a landmark's run ascend with its columns), else 0.  Loads are unconditional (index
+// clamped) and selected afterwards, so the operands of group g + 1 (4 entries) are in flight while
+// group g runs on the MFMA pipe.  Block pairs an entry does not touch are skipped by scalar tests on
+// the (wave-uniform) masks.
+constexpr int kSG = 4;  // entries per prefetch group
+
+struct SchurOps {
+  double v[kSG][4];  // per entry: J-side rows pb + l15, pb + 16 + l15; I-side rows qb + l15, qb + 16 + l15
+};
+
+__device__ __forceinline__ double schur_opnd(const Dev& d, uint64_t m, uint32_t col, uint64_t bit, int kk, bool kv) {
+  const int c = __popcll(m & (bit - 1));
+  const int64_t idx = min<int64_t>(3 * ((int64_t)col + c) + kk, 3 * d.nYcol - 1);
+  const double y = d.Y[idx];
+  return (kv && (m & bit)) ? y : 0.0;
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) schur_tile2_kernel(Dev d, double lambda) {
+  __shared__ TileEnt ents[256];
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
+  const TileWork wk = d.tileWorks[w];
+  const bool diag = wk.I == wk.J;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  const int cnt = wk.count;
+  if (tid < cnt) ents[tid] = d.tileEnts[wk.start + tid];
+  __syncthreads();
+  double4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
+  const bool kv = l4 < 3;
+  const int kk = kv ? l4 : 0;
+  const uint64_t bA0 = 1ull << (pb + l15), bA1 = 1ull << (pb + 16 + l15);
+  const uint64_t bB0 = 1ull << (qb + l15), bB1 = 1ull << (qb + 16 + l15);
+  // on a diagonal tile only the lower-triangle block pairs are formed (wave pb 32 / qb 0 idles)
+  const bool skip01 = diag && (pb >> 4) > (qb >> 4) + 1, skip00 = diag && (pb >> 4) > (qb >> 4);
+  const bool skip11 = skip00, skip10 = diag && (pb >> 4) + 1 > (qb >> 4);
+  const int ng = (cnt + kSG - 1) / kSG;
+  auto load = [&](int g, SchurOps& R) {
+#pragma unroll
+    for (int i = 0; i < kSG; i++) {
+      const int e = min(g * kSG + i, cnt - 1);
+      const TileEnt& en = ents[e];
+      const uint64_t mI = en.maskI, mJ = diag ? en.maskI : en.maskJ;
+      const uint32_t cI = en.colI, cJ = diag ? en.colI : en.colJ;
+      R.v[i][0] = schur_opnd(d, mJ, cJ, bA0, kk, kv);
+      R.v[i][1] = schur_opnd(d, mJ, cJ, bA1, kk, kv);
+      R.v[i][2] = schur_opnd(d, mI, cI, bB0, kk, kv);
+      R.v[i][3] = schur_opnd(d, mI, cI, bB1, kk, kv);
+    }
+  };
+  auto comp = [&](int g, const SchurOps& R) {
+#pragma unroll
+    for (int i = 0; i < kSG; i++) {
+      const int e = g * kSG + i;
+      if (e >= cnt) break;
+      const uint64_t mI = uniform64(ents[e].maskI), mJ = diag ? mI : uniform64(ents[e].maskJ);
+      const bool j0 = (mJ >> pb) & 0xffffull, j1 = (mJ >> (pb + 16)) & 0xffffull;
+      const bool i0 = (mI >> qb) & 0xffffull, i1 = (mI >> (qb + 16)) & 0xffffull;
+      if (j0 && i0 && !skip00) acc[0][0] = mfma64(R.v[i][0], R.v[i][2], acc[0][0]);
+      if (j0 && i1 && !skip01) acc[0][1] = mfma64(R.v[i][0], R.v[i][3], acc[0][1]);
+      if (j1 && i0 && !skip10) acc[1][0] = mfma64(R.v[i][1], R.v[i][2], acc[1][0]);
+      if (j1 && i1 && !skip11) acc[1][1] = mfma64(R.v[i][1], R.v[i][3], acc[1][1]);
+    }
+  };
+  if (!(diag && pb > qb)) {
+    SchurOps RA, RB;
+    load(0, RA);
+    for (int g = 0; g < ng; g += 2) {
+      if (g + 1 < ng) load(g + 1, RB);
+      comp(g, RA);
+      if (g + 1 < ng) {
+        if (g + 2 < ng) load(g + 2, RA);
+        comp(g + 1, RB);
+      }
+    }
+  }
+  double* Cw = d.tiles + (int64_t)wk.tile * TS * TS + (pb + l4) * TS + qb + l15;
+  if (!(diag && pb > qb)) {
+    if (wk.kind) {
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+          for (int r = 0; r < 4; r++)
+            if (acc[a][bb][r] != 0.0) atomicAdd(Cw + (a * 16 + 4 * r) * TS + bb * 16, -acc[a][bb][r]);
+    } else {
+      double v[2][2][4];
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) v[a][bb][r] = Cw[(a * 16 + 4 * r) * TS + bb * 16];
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int bb = 0; bb < 2; bb++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + bb * 16] = v[a][bb][r] - acc[a][bb][r];
+    }
+  }
+  // diagonal tiles: rhs -= Y^T z (the idle wave: pb 32, qb 0), lane = tile row
+  if (diag && pb > qb) {
+    const uint64_t bit = 1ull << lane;
+    double racc = 0.0;
+    for (int e = 0; e < cnt; e++) {
+      const uint64_t m = ents[e].maskI;
+      if (!(m & bit)) continue;
+      const int64_t col = (int64_t)ents[e].colI + __popcll(m & (bit - 1));
+      const double* zz = d.z + 3 * (int64_t)ents[e].lm;
+      racc += d.Y[3 * col] * zz[0] + d.Y[3 * col + 1] * zz[1] + d.Y[3 * col + 2] * zz[2];
+    }
+    const int64_t row = (int64_t)wk.I * TS + lane;
+    if (row < d.nRed && racc != 0.0) atomicAdd(d.rhs + row, -racc);
+  }
+}
+
 // Direct visual terms by observation group (observations sharing their reduced blocks: one rig, one
 // camera).  Per group: H = sum_o J~_o^T J~_o over the 32 columns [pose 6 | extr 6 | intr <= 17 |
 // vel 3] and g = sum_o J~_o^T e~_o, on v_mfma_f64_16x16x4_f64 (K = the group's residual rows, 4 per
@@ -707,6 +838,9 @@ __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagLis
 #define VIBA_FAN_K 16
 #define VIBA_FAN_RING 3
 #endif
+#ifndef VIBA_FAN_LATE
+#define VIBA_FAN_LATE 1
+#endif
 constexpr int kFanK = VIBA_FAN_K;          // columns per stage
 constexpr int kFanRing = VIBA_FAN_RING;    // stages in the LDS ring (kFanRing - 2 in flight)
 constexpr int kStage = 2 * kFanK * TS;     // doubles per stage: [L_JK, L_IK][kFanK columns][64 rows]
@@ -733,7 +867,7 @@ __device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, 
 
 __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
   __shared__ double stg[kFanRing * kStage];
-  static_assert(kGlds * (kFanRing - 2) <= 63 && kFanRing <= 8 && kFanRing >= 3, "vmcnt range");
+  static_assert(kGlds * (kFanRing - 1) <= 63 && kFanRing <= 8 && kFanRing >= 3, "vmcnt range");
   const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
@@ -746,12 +880,20 @@ __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, 
   for (int a = 0; a < 2; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
-  for (int s = 0; s < kFanRing - 2 && s < nst; s++) fanin_issue(d, pairs, start, s, stg + s * kStage, wave, lane);
+#if VIBA_FAN_LATE
+  // issue-after-barrier: kFanRing - 1 stages in flight; stage s + R - 1 goes into the buffer of stage
+  // s - 1, whose readers all passed this iteration's barrier
+  constexpr int kAhead = kFanRing - 1;
+#else
+  constexpr int kAhead = kFanRing - 2;
+#endif
+  for (int s = 0; s < kAhead && s < nst; s++) fanin_issue(d, pairs, start, s, stg + s * kStage, wave, lane);
   for (int s = 0; s < nst; s++) {
-    if (s + kFanRing - 2 < nst)
-      fanin_issue(d, pairs, start, s + kFanRing - 2, stg + ((s + kFanRing - 2) % kFanRing) * kStage, wave, lane);
+#if !VIBA_FAN_LATE
+    if (s + kAhead < nst) fanin_issue(d, pairs, start, s + kAhead, stg + ((s + kAhead) % kFanRing) * kStage, wave, lane);
+#endif
     // this wave's part of stage s landed (later stages may stay in flight)
-    switch (min(kFanRing - 2, nst - 1 - s)) {
+    switch (min(kAhead - (VIBA_FAN_LATE ? 1 : 0), nst - 1 - s)) {
       case 6: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * kGlds) : "memory"); break;
       case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * kGlds) : "memory"); break;
       case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * kGlds) : "memory"); break;
@@ -762,6 +904,10 @@ __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, 
     }
     __builtin_amdgcn_s_barrier();  // ... and every other wave's
     __builtin_amdgcn_sched_barrier(0);
+#if VIBA_FAN_LATE
+    if (s + kAhead < nst) fanin_issue(d, pairs, start, s + kAhead, stg + ((s + kAhead) % kFanRing) * kStage, wave, lane);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     const double* bk = stg + (s % kFanRing) * kStage;
     const double* bi = bk + kFanK * TS;
 #pragma unroll
@@ -1225,7 +1371,11 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
   if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
-  if (d.nTileWorks) launchK(schur_tile_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+  static const int v2 = getenv("VIBA_SCHUR_V2") ? atoi(getenv("VIBA_SCHUR_V2")) : 0;
+  if (d.nTileWorks) {
+    if (v2) launchK(schur_tile2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else launchK(schur_tile_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+  }
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {

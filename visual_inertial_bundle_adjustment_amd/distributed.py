@@ -433,15 +433,31 @@ def run_sharded(args, rank: int, world: int, local: int):
     else:
         dist.init_process_group(backend)
     p = synth.generate(synth.config(args.config))
-    lb, le = shard_bounds(p, world)[rank]
+    # default: partitioned factorization (world a power of two); VIBA_MULTI=shard selects landmark
+    # shards with the whole reduced system factored on rank 0
+    mode = os.environ.get("VIBA_MULTI", "partition" if world & (world - 1) == 0 else "shard")
     e = HipEngine(imu_calib_options=p.imu_calib_options, device=local)
-    e.set_landmark_shard(lb, le, rank == 0)
+    if mode == "partition":
+        e.set_partition(rank, world)
+    else:
+        lb, le = shard_bounds(p, world)[rank]
+        e.set_landmark_shard(lb, le, rank == 0)
     synth.load_into(e, p)
     st = e.problem_stats()
-    log(f"[bench] {world} ranks, config {args.config}: {p.summary()}; rank 0 landmarks [{lb}, {le}), "
-        f"Schur entries lm {st[8]} obs {st[9]}")
     comm = ShardComm(rank, world, dev)
-    opt = ShardedOptimizer(e, comm)
+    if mode == "partition":
+        info = comm.all_gather_obj(e.part_info())
+        log(f"[bench] {world} ranks, config {args.config}: {p.summary()}; partitioned factorization: subtree "
+            f"columns {[i[0] for i in info]}, ROOT columns {info[0][1]} ({info[0][4]} tiles), contributions "
+            f"local {[i[2] for i in info]} root {info[0][3]}")
+        opt = PartitionedOptimizer(e, comm)
+        parallelism = (f"nested-dissection subtree x{world} (landmarks, factor, solves per rank), ROOT separators "
+                       f"on rank 0, RCCL reduce/broadcast of ROOT tiles and rows")
+    else:
+        log(f"[bench] {world} ranks, config {args.config}: {p.summary()}; landmark shards, Schur entries lm "
+            f"{st[8]} obs {st[9]}")
+        opt = ShardedOptimizer(e, comm)
+        parallelism = f"landmark shards x{world}, RCCL tile exchange to rank 0"
 
     def settings(n):
         return Settings.default(max_num_iterations=n, stop_if_no_improvement_for=10**6,
@@ -469,7 +485,7 @@ def run_sharded(args, rank: int, world: int, local: int):
                "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
                "config": {"workload": f"config {args.config}: {st[0]} obs, {p.num_points} landmarks, "
                                       f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",
-                          "parallelism": f"landmark shards x{world}, RCCL band reduce to rank 0"},
+                          "parallelism": parallelism},
                "roofline": None, "cpu_baseline": None,
                "cost": [s.initial_cost, s.final_cost]}
         print(json.dumps(out), flush=True)
