@@ -2,7 +2,8 @@
 """LM iterations/s of the MI355X VI-BA engine on the synthetic config-C problem.
 
 Metric (BASELINE.json): "LM iterations/sec (and ms/iter) on 10k-pose/300k-landmark VI-BA".
-One step = one iteration of Optimizer::optimize (Optimizer.cpp:800-1097): linearize all factors,
+One step = one iteration of Optimizer::optimize (Optimizer.cpp:800-1097) as ark_vi_ba drives it: the
+preStepCallback's rolling-shutter table rebuild from the IMU stream (main_AriaKit_ViBa.cpp:95-101), linearize all factors,
 damp + Schur-eliminate landmarks + factor + solve the reduced system, box-plus, cost pass, and the
 LM accept/reject (+ rescaled / sub-step attempts when the step is bad), as driven by vb_optimize.
 
@@ -64,8 +65,9 @@ def cpu_baseline(full_kf: int, sample_kf: int = 1000):
     cfg = synth.config("C", n_kf=sample_kf, n_lm=int(round(300000 * frac)))
     p = synth.generate(cfg)
     e = RefEngine(imu_calib_options=p.imu_calib_options)
-    synth.load_into(e, p)
+    synth.load_into(e, p, rs_device=True)
     t0 = time.perf_counter()
+    e.update_rs_tables()  # the preStepCallback's RollingShutterData::compute, as in the GPU iteration
     e.linearize(True, False)
     e.damp_factor_solve(1e-5)
     e.backup()
@@ -88,6 +90,9 @@ def main():
     ap.add_argument("--config", default="C")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-family", type=int, default=KF_GEMM)
+    ap.add_argument("--rs-tables", choices=("device", "host"), default="device",
+                    help="device: rebuild the rolling-shutter tables from the IMU stream at the start of every "
+                         "iteration (ark_vi_ba's preStepCallback); host: fixed precomputed tables")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,7 +110,7 @@ def main():
     log(f"[bench] config {args.config}: {p.summary()} (generated in {time.perf_counter() - t:.1f}s)")
     t = time.perf_counter()
     e = HipEngine(imu_calib_options=p.imu_calib_options, device=local)
-    synth.load_into(e, p)
+    synth.load_into(e, p, rs_device=args.rs_tables == "device")
     st = e.problem_stats()
     log(f"[bench] finalize {time.perf_counter() - t:.1f}s; reduced order {st[3]}, tiles {st[5]} "
         f"({st[4]} tile columns, {st[10]} levels), gemm pairs/factorization {st[6]}, Schur entries: landmark-tile {st[8]}, obs-pair {st[9]}")
@@ -129,7 +134,7 @@ def main():
     ph = e.phase_times()
     log(f"[bench] timed {iters} its in {elapsed:.3f}s, cost {s.initial_cost:.6g} -> {s.final_cost:.6g}; "
         f"last it: lin {ph.linearize_ms:.2f} schur {ph.schur_ms:.2f} factor {ph.factor_ms:.2f} "
-        f"solve {ph.solve_ms:.2f} step {ph.step_ms:.2f} cost {ph.cost_ms:.2f} ms")
+        f"solve {ph.solve_ms:.2f} step {ph.step_ms:.2f} cost {ph.cost_ms:.2f} rs-tables {ph.rs_update_ms:.3f} ms")
 
     # roofline of the profiled kernel family (average launch duration from HIP events on the engine
     # stream, algorithmic work from the symbolic structure)

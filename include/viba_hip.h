@@ -15,6 +15,10 @@
  *     (viba/problem/SingleSessionProblem.h:64-129)
  *   RollingShutterData::compute results                        vb_set_rs_tables
  *     (lib/motion/preintegration/RollingShutterData.cpp:16-65)
+ *   SingleSessionAdapter::initRollingShutterData /             vb_set_imu_measurements,
+ *     updateRollingShutterData (viba/single_session/             vb_set_rs_rigs,
+ *     InitCalibration.cpp:299-325), ark_vi_ba's preStepCallback  vb_update_rs_tables (and every
+ *     (interfaces/ark/main_AriaKit_ViBa.cpp:95-101)              vb_optimize iteration)
  *   registerPointVariables + registeredVariablesToElimination  vb_set_elim_points (implicit: the
  *     Range (SingleSessionProblem.cpp:41-45, Optimizer.cpp:31)   point kind is always eliminated)
  *   Optimizer::initSolver (Optimizer.cpp:166-207)              vb_finalize
@@ -185,6 +189,7 @@ typedef struct vb_cost_stats { /* CostStats (Factor.h:20-30) */
 
 typedef struct vb_phase_times { /* per-phase device time of the last LM iteration [ms] */
   double linearize_ms, schur_ms, factor_ms, solve_ms, step_ms, cost_ms, total_ms;
+  double rs_update_ms; /* device rolling-shutter table rebuild (0 with host tables) */
 } vb_phase_times;
 
 typedef void (*vb_log_cb)(const char* msg, void* user);
@@ -214,6 +219,25 @@ int vb_add_factors(vb_handle h, int kind, int64_t n, const int32_t* var_idx, con
  * gravity[3 * t] = gravityWorld */
 int vb_set_rs_tables(vb_handle h, int32_t n_tables, const int64_t* offsets, const double* samples,
                      const double* interp, const double* gravity);
+/* rolling-shutter tables rebuilt on the device instead: the IMU-0 measurement
+ * stream (ImuMeasurement, imu_types/ImuMeasurement.h:18-23; timestamps strictly increasing [ns],
+ * gyro[3 n] rad/s, accel[3 n] m/s^2, as SingleSessionAdapter::initRollingShutterData's
+ * imu0Measurements, InitCalibration.cpp:299-314) ... */
+int vb_set_imu_measurements(vb_handle h, int64_t n, const int64_t* timestamp_ns, const double* gyro_rad_sec,
+                            const double* accel_m_sec2);
+/* ... and per table t (= the rs_table index of the visual factors): the midpoint (the rig's calib-state
+ * timestamp) and half length [us] of RollingShutterData's constructor, the VB_VAR_IMU_CALIB handle
+ * whose model parameters integrate it (imuCalib(rig, 0), InitCalibration.cpp:321) and the gravity
+ * variable.  Replaces vb_set_rs_tables; both precede vb_finalize. */
+int vb_set_rs_rigs(vb_handle h, int32_t n_tables, const int64_t* midpoint_us, const int64_t* half_length_us,
+                   const int32_t* imu_calib, int32_t gravity_var);
+/* RollingShutterData::compute for every table from the current variables (RollingShutterData.cpp:16-65
+ * via updateRollingShutterData, InitCalibration.cpp:316-325); vb_optimize does this at the start of
+ * every iteration, as ark_vi_ba's preStepCallback.  VB_E_RANGE when the IMU data does not cover an
+ * interval (the reference throws in enumIntegrationSteps, PreIntegration.cpp:16-61). */
+int vb_update_rs_tables(vb_handle h);
+/* download table t: sample count, samples (11 doubles each, NULL to skip) and interpolants (9 each) */
+int vb_get_rs_table(vb_handle h, int32_t t, int32_t* n_samples, double* samples, double* interp);
 /* build the symbolic structure (≙ Optimizer::initSolver) and upload everything to HBM */
 int vb_finalize(vb_handle h);
 int64_t vb_reduced_order(vb_handle h);   /* order of the Schur-reduced (non-point) system */

@@ -3,6 +3,7 @@
 // CPU restatement of the viba/problem factor functors, the sensor models they call, and the
 // variable box-plus/box-minus operators.  Every function cites the reference lines it follows.
 #pragma once
+#include <algorithm>
 #include <optional>
 #include <stdexcept>
 #include "ref_math.hpp"
@@ -292,7 +293,8 @@ inline RVP integrate(const RVPInterp& ip, double dt) {  // :117-121
   r.dP = r.dP + dt * ip.dvel;
   return r;
 }
-// differentiate (MotionIntegral.cpp:88-115): used by the synthetic RS table generator
+// differentiate (MotionIntegral.cpp:88-115): RollingShutterData::compute's interpolants.  Divisions
+// by dtSec as the reference's Eigen `omega / rvp.dtSec` (not a reciprocal multiply).
 inline RVPInterp differentiate(const RVP& rvp) {
   V3 om = so3_log(rvp.R);
   const double th2 = sqnorm(om), th = std::sqrt(th2);
@@ -306,11 +308,12 @@ inline RVPInterp differentiate(const RVP& rvp) {
   }
   V3 ov = cross(om, rvp.dV);
   V3 ups = rvp.dV + q1 * ov + q2 * cross(om, ov);
-  RVP recon = integrate((1.0 / rvp.dt) * om, (1.0 / rvp.dt) * ups, rvp.dt);
+  auto div = [](const V3& a, double s) { return v3(a[0] / s, a[1] / s, a[2] / s); };
+  RVP recon = integrate(div(om, rvp.dt), div(ups, rvp.dt), rvp.dt);
   RVPInterp ip;
-  ip.gyro = (1.0 / rvp.dt) * om;
-  ip.accel = (1.0 / rvp.dt) * ups;
-  ip.dvel = (1.0 / rvp.dt) * (rvp.dP - recon.dP);
+  ip.gyro = div(om, rvp.dt);
+  ip.accel = div(ups, rvp.dt);
+  ip.dvel = div(rvp.dP - recon.dP, rvp.dt);
   return ip;
 }
 
@@ -320,6 +323,122 @@ struct RSTable {
   std::vector<RVPInterp> interp;
   V3 gravity{{0, 0, 0}};
 };
+
+// ------------------------------------------------------------------ RollingShutterData::compute
+// IMU measurement (imu_types/ImuMeasurement.h:18-23; the temperature is not on this path)
+struct ImuMeas {
+  int64_t tNs;
+  V3 gyro, accel;
+};
+
+// Eigen's 3x3 inverse (LU/InverseImpl.h compute_inverse_size3_helper): cofactors of column 0,
+// det = their dot with column 0, result(r, c) = cofactor(c, r) / det (by multiplying with 1 / det)
+inline void inv3_eigen(const double m[3][3], double r[3][3]) {
+  auto cof = [&](int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return m[i1][j1] * m[i2][j2] - m[i1][j2] * m[i2][j1];
+  };
+  const double c0 = cof(0, 0), c1 = cof(1, 0), c2 = cof(2, 0);
+  const double invdet = 1.0 / (c0 * m[0][0] + c1 * m[1][0] + c2 * m[2][0]);
+  r[0][0] = c0 * invdet, r[0][1] = c1 * invdet, r[0][2] = c2 * invdet;
+  r[1][0] = cof(0, 1) * invdet, r[1][1] = cof(1, 1) * invdet, r[1][2] = cof(2, 1) * invdet;
+  r[2][0] = cof(0, 2) * invdet, r[2][1] = cof(1, 2) * invdet, r[2][2] = cof(2, 2) * invdet;
+}
+
+// ImuMeasurementModelParameters::getCompensatedImuMeasurement (ImuMeasurementModelParameters.h:92-104):
+// w = (gyroScale * gyroNonorth)^-1 w_meas - b_g, a = (accelScale * accelNonorth)^-1 a_meas - b_a
+// (only the average signal of SignalStatistics is used)
+struct ImuCompensation {
+  double gInv[3][3], aInv[3][3];
+  V3 bg, ba;
+  explicit ImuCompensation(const ImuModel& m) {
+    double G[3][3], A[3][3];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) G[i][j] = m.d[0 + i] * m.gN(i, j), A[i][j] = m.d[3 + i] * m.aN(i, j);
+    inv3_eigen(G, gInv);
+    inv3_eigen(A, aInv);
+    bg = v3(m.d[6], m.d[7], m.d[8]);
+    ba = v3(m.d[9], m.d[10], m.d[11]);
+  }
+  static V3 mv(const double M[3][3], const V3& v) {
+    return v3(M[0][0] * v[0] + M[0][1] * v[1] + M[0][2] * v[2], M[1][0] * v[0] + M[1][1] * v[1] + M[1][2] * v[2],
+              M[2][0] * v[0] + M[2][1] * v[1] + M[2][2] * v[2]);
+  }
+  void apply(const V3& gU, const V3& aU, V3& g, V3& a) const {
+    g = mv(gInv, gU) - bg;
+    a = mv(aInv, aU) - ba;
+  }
+};
+
+// measIndex_GT (PreIntegration.cpp:16-27): first measurement with timestamp > tNs
+inline int64_t measIndexGT(const std::vector<ImuMeas>& meas, int64_t tNs) {
+  auto it = std::upper_bound(meas.begin(), meas.end(), tNs,
+                             [](int64_t t, const ImuMeas& m) { return t < m.tNs; });
+  if (it == meas.end()) throw std::runtime_error("measIndex_GT: unexpected, it == meas.end()");
+  return it - meas.begin();
+}
+
+// forEachIntegratedMeasurement (PreIntegration.cpp:309-343) over the steps of enumIntegrationSteps
+// (:29-120): f(prevRvp, atAccelBoundary, atGyroBoundary) before each step and once at the end
+template <class F>
+void forEachIntegratedMeasurement(const std::vector<ImuMeas>& meas, const ImuModel& model, int64_t timeStartUs,
+                                  int64_t timeEndUs, F&& f) {
+  const ImuCompensation comp(model);
+  const int64_t dtRefGyroNs = (int64_t)(model.dtGyro() * 1e9);
+  const int64_t dtRefAccelNs = (int64_t)(model.dtAccel() * 1e9);
+  const int64_t refStartNs = timeStartUs * 1000, refEndNs = timeEndUs * 1000;
+  const int64_t kMarginNs = 1000;
+  const int64_t gS = measIndexGT(meas, refStartNs + dtRefGyroNs + kMarginNs);
+  const int64_t gE = measIndexGT(meas, refEndNs + dtRefGyroNs - kMarginNs);
+  if (gS <= 0) throw std::runtime_error("enumIntegrationSteps: gyro index, not enough margin at beginning of interval");
+  const int64_t aS = measIndexGT(meas, refStartNs + dtRefAccelNs + kMarginNs);
+  const int64_t aE = measIndexGT(meas, refEndNs + dtRefAccelNs - kMarginNs);
+  if (aS <= 0) throw std::runtime_error("enumIntegrationSteps: accel index, not enough margin at beginning of interval");
+  RVP prev;
+  prev.R = SO3::fromQ(0, 0, 0, 1);
+  int64_t prevStamp = refStartNs;
+  for (int64_t gi = gS, ai = aS; gi <= gE && ai <= aE;) {
+    const ImuMeas &mg = meas[gi], &ma = meas[ai], &mgp = meas[gi - 1], &map = meas[ai - 1];
+    const int64_t adjG = mg.tNs - dtRefGyroNs, adjA = ma.tNs - dtRefAccelNs;
+    const int64_t endMeas = std::min(adjG, adjA);
+    const bool notFirst = gi > gS || ai > aS;
+    const bool newAccel = notFirst && (map.tNs - dtRefAccelNs == prevStamp);
+    const bool newGyro = notFirst && (mgp.tNs - dtRefGyroNs == prevStamp);
+    const int64_t endStamp = (gi >= gE && ai >= aE) ? refEndNs : endMeas;
+    const double dtSec = (endStamp - prevStamp) * 1e-9;
+    prevStamp = endStamp;
+    gi += (adjG == endMeas);
+    ai += (adjA == endMeas);
+    const bool atStart = prev.dt == 0.0;
+    f(prev, newAccel || atStart, newGyro || atStart);
+    V3 w, a;
+    comp.apply(mg.gyro, ma.accel, w, a);
+    prev = combine(prev, integrate(w, a, dtSec));
+  }
+  f(prev, true, true);
+}
+
+// RollingShutterData::compute (RollingShutterData.cpp:16-65): RVP samples at the gyro boundaries of
+// [mid - half, mid + half], relative to the midpoint, and the interpolant of every gap
+inline void rs_compute(RSTable& T, const std::vector<ImuMeas>& meas, const ImuModel& model, int64_t midUs,
+                       int64_t halfUs, const V3& gravity) {
+  T.gravity = gravity;
+  T.samples.clear();
+  forEachIntegratedMeasurement(meas, model, midUs - halfUs, midUs, [&](const RVP& r, bool, bool atGyro) {
+    if (atGyro) T.samples.push_back(r);
+  });
+  const RVP startToMid = T.samples.back();
+  T.samples.pop_back();
+  for (RVP& s : T.samples) s = uncombineLeft(s, startToMid);
+  forEachIntegratedMeasurement(meas, model, midUs, midUs + halfUs, [&](const RVP& r, bool, bool atGyro) {
+    if (atGyro) T.samples.push_back(r);
+  });
+  T.interp.clear();
+  for (size_t i = 1; i < T.samples.size(); i++) {
+    if (T.samples[i - 1].dt >= T.samples[i].dt) throw std::runtime_error("Wut?");
+    T.interp.push_back(differentiate(uncombineLeft(T.samples[i], T.samples[i - 1])));
+  }
+}
 
 struct RSEstimate {
   SE3 T_mid_atT;

@@ -76,6 +76,12 @@ struct Problem {
   std::vector<int32_t> fint[14];
   std::vector<double> fconst[14];
   std::vector<RSTable> rs;
+  // device-side table rebuild inputs (updateRollingShutterData, InitCalibration.cpp:316-325): the
+  // IMU-0 stream, per table the midpoint / half length [us] and the IMU calib variable, gravity var
+  std::vector<ImuMeas> imu;
+  std::vector<int64_t> rsMid, rsHalf;
+  std::vector<int32_t> rsCalib;
+  int32_t rsGravity = -1;
   bool finalized = false;
 
   // registration
@@ -866,6 +872,70 @@ int ref_set_rs_tables(void* h, int32_t nt, const int64_t* offsets, const double*
   return 0;
 }
 
+int ref_set_imu_measurements(void* h, int64_t n, const int64_t* tNs, const double* gyro, const double* accel) {
+  Problem& P = *(Problem*)h;
+  P.imu.resize(n);
+  for (int64_t i = 0; i < n; i++) {
+    P.imu[i].tNs = tNs[i];
+    P.imu[i].gyro = v3(gyro[3 * i], gyro[3 * i + 1], gyro[3 * i + 2]);
+    P.imu[i].accel = v3(accel[3 * i], accel[3 * i + 1], accel[3 * i + 2]);
+    if (i && tNs[i] <= tNs[i - 1]) return (g_err = "IMU timestamps must increase", -1);
+  }
+  return 0;
+}
+
+int ref_set_rs_rigs(void* h, int32_t nt, const int64_t* midUs, const int64_t* halfUs, const int32_t* calib,
+                    int32_t gravityVar) {
+  Problem& P = *(Problem*)h;
+  P.rsMid.assign(midUs, midUs + nt);
+  P.rsHalf.assign(halfUs, halfUs + nt);
+  P.rsCalib.assign(calib, calib + nt);
+  P.rsGravity = gravityVar;
+  P.rs.assign(nt, RSTable());
+  return 0;
+}
+
+// SingleSessionAdapter::updateRollingShutterData (InitCalibration.cpp:316-325): every table from the
+// current IMU calib (modelParams of the rig's IMU-0 calib variable) and gravity
+int ref_update_rs_tables(void* h) {
+  Problem& P = *(Problem*)h;
+  try {
+    const double* g = &P.data[8][(size_t)P.rsGravity * 4];
+    const V3 grav = v3(g[0], g[1], g[2]);
+    for (size_t t = 0; t < P.rsMid.size(); t++) {
+      ImuModel m;
+      std::copy(&P.data[6][(size_t)P.rsCalib[t] * 32], &P.data[6][(size_t)P.rsCalib[t] * 32] + 32, m.d);
+      rs_compute(P.rs[t], P.imu, m, P.rsMid[t], P.rsHalf[t], grav);
+    }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+
+// table t: sample count (samples / interp NULL) or the samples (11 doubles) and interpolants (9)
+int ref_get_rs_table(void* h, int32_t t, int32_t* n, double* samples, double* interp) {
+  Problem& P = *(Problem*)h;
+  if (t < 0 || t >= (int32_t)P.rs.size()) return (g_err = "bad table", -1);
+  const RSTable& T = P.rs[t];
+  *n = (int32_t)T.samples.size();
+  if (samples)
+    for (size_t i = 0; i < T.samples.size(); i++) {
+      const RVP& r = T.samples[i];
+      double* o = samples + 11 * i;
+      for (int k = 0; k < 4; k++) o[k] = r.R.q[k];
+      for (int k = 0; k < 3; k++) o[4 + k] = r.dV[k], o[7 + k] = r.dP[k];
+      o[10] = r.dt;
+    }
+  if (interp)
+    for (size_t i = 0; i < T.interp.size(); i++) {
+      double* o = interp + 9 * i;
+      for (int k = 0; k < 3; k++) o[k] = T.interp[i].gyro[k], o[3 + k] = T.interp[i].accel[k], o[6 + k] = T.interp[i].dvel[k];
+    }
+  return 0;
+}
+
 int ref_finalize(void* h) {
   try {
     finalize(*(Problem*)h);
@@ -1014,6 +1084,7 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
   };
   int rc;
   while (true) {
+    if (!P.rsMid.empty() && (rc = ref_update_rs_tables(h))) return rc;  // ark_vi_ba's preStepCallback
     if (pre) pre(it, user);
     double prevCost;
     if ((rc = ref_linearize(h, 1, dontRetry, &prevCost))) return rc;

@@ -148,3 +148,64 @@ def test_full_size_properties_config_C():
     assert abs(c_back - c_pass) <= 1e-14 * c_pass
     for a, k in zip(v0, (1, 4)):
         assert np.array_equal(a, g.get_vars(k))
+
+
+# ------------------------------------------------------------------ rolling-shutter tables rebuilt on
+# the device (rs.hip) against the oracle's RollingShutterData::compute restatement
+def _rs_pair(p):
+    out = []
+    for cls in (hip(), RefEngine):
+        e = cls(imu_calib_options=p.imu_calib_options)
+        synth.load_into(e, p, rs_device=True)
+        out.append(e)
+    return out
+
+
+def _assert_tables_equal(g, r, n_tables, tol=1e-12):
+    for t in range(n_tables):
+        sg, ig = g.get_rs_table(t)
+        sr, ir = r.get_rs_table(t)
+        assert sg.shape == sr.shape, t
+        assert rel(sg, sr) < tol and rel(ig, ir) < tol, t
+
+
+def test_rs_tables_rebuilt_on_device_match_oracle():
+    """Tables: every sample and interpolant within 1e-12 of the oracle's (only FMA contraction and
+    transcendental ulps differ); then one LM step on the rebuilt tables, and the tables again after
+    the step's IMU-calibration change."""
+    p = synth.generate(synth.config("miniB"))
+    g, r = _rs_pair(p)
+    nt = len(p.rs_mid)
+    _assert_tables_equal(g, r, nt)
+    og, orf = one_step(g), one_step(r)
+    assert_step_parity(og, orf)
+    g.apply_step(0), r.apply_step(0)
+    g.update_rs_tables(), r.update_rs_tables()
+    _assert_tables_equal(g, r, nt)
+
+
+def test_rs_rebuild_every_iteration_optimize_matches_oracle():
+    """vb_optimize rebuilds the tables at the start of every iteration (ark_vi_ba's preStepCallback,
+    main_AriaKit_ViBa.cpp:95-101): same LM trajectory as the oracle doing the same."""
+    p = synth.generate(synth.config("miniB"))
+    g, r = _rs_pair(p)
+    from visual_inertial_bundle_adjustment_amd.engine import Settings
+    s = Settings.default(max_num_iterations=8)
+    sg, sr = g.optimize(s), r.optimize(s)
+    assert sg.num_iterations == sr.num_iterations
+    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
+    assert g.phase_times().rs_update_ms > 0
+    _assert_tables_equal(g, r, len(p.rs_mid), tol=1e-9)
+
+
+def test_rs_rebuild_imu_gap_is_an_error():
+    """IMU stream ending before the last interval: VB_E_RANGE, as the oracle (the reference throws in
+    measIndex_GT, PreIntegration.cpp:16-27)."""
+    from visual_inertial_bundle_adjustment_amd.engine import VbError
+    p = synth.generate(synth.config("miniB"))
+    keep = p.imu_t < p.rs_mid[-1] * 1000
+    p.imu_t, p.imu_gyro, p.imu_accel = p.imu_t[keep], p.imu_gyro[keep], p.imu_accel[keep]
+    e = hip()(imu_calib_options=p.imu_calib_options)
+    with pytest.raises(VbError) as ex:
+        synth.load_into(e, p, rs_device=True)
+    assert ex.value.code == -5

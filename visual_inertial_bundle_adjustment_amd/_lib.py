@@ -44,7 +44,10 @@ def load_synth_lib() -> C.CDLL:
             f.argtypes = [P, C.c_int]
         lib.vbs_num_rs_tables.restype = C.c_int32
         lib.vbs_num_rs_tables.argtypes = [P]
-        for name in ("vbs_rs_offsets", "vbs_rs_samples", "vbs_rs_interp", "vbs_rs_gravity"):
+        lib.vbs_num_imu.restype = C.c_int64
+        lib.vbs_num_imu.argtypes = [P]
+        for name in ("vbs_rs_offsets", "vbs_rs_samples", "vbs_rs_interp", "vbs_rs_gravity", "vbs_imu_t",
+                     "vbs_imu_gyro", "vbs_imu_accel", "vbs_rs_mid", "vbs_rs_half", "vbs_rs_calib"):
             f = getattr(lib, name)
             f.restype = P
             f.argtypes = [P]

@@ -23,6 +23,7 @@ namespace viba {
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st);
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
+void launch_rs_build(const Dev& d, hipStream_t st);
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st);
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
@@ -219,6 +220,12 @@ struct vb_handle_s {
   int32_t nRS = 0;
   std::vector<int64_t> rsOff;
   std::vector<double> rsS, rsI, rsG;
+  // device rebuild of the tables (vb_set_imu_measurements / vb_set_rs_rigs)
+  std::vector<int64_t> imuT, rsMid, rsHalf;
+  std::vector<double> imuV;
+  std::vector<int32_t> rsCalib;
+  int32_t rsGravVar = -1;
+  bool rsDevice = false, rsTimed = false;
   bool finalized = false;
   Dev d;
   std::vector<void*> allocs;
@@ -265,7 +272,7 @@ struct vb_handle_s {
   // state
   bool linearized = false, factored = false;
   vb_phase_times times{};
-  hipEvent_t ev[8];
+  hipEvent_t ev[10];
   // side stream: the small (non-visual) factor kernels -- few waves, latency-bound -- run beside
   // the visual kernels, forked after the buffer resets and joined before their first consumer
   hipStream_t st2 = nullptr;
@@ -313,15 +320,26 @@ void profHarvest(vb_handle h) {
   h->profUsed = 0;
 }
 
+int checkRsErr(vb_handle h, int32_t e);
 int checkErr(vb_handle h) {
-  int32_t e = 0;
-  HIPCHK(hipMemcpyAsync(&e, h->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+  int32_t ee[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(ee, h->d.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
+  const int32_t e = ee[0];
+  if (int rc = checkRsErr(h, ee[1])) return rc;
   if (e & 1) return fail(VB_E_RANGE, "RollingShutterData::getEstimate: out of range");
   if (e & 2) return fail(VB_E_NUMERIC, "landmark 3x3 Cholesky breakdown");
   if (e & 8) return fail(VB_E_NUMERIC, "reduced system Cholesky breakdown (not positive definite)");
   if (e & 4) return fail(VB_E_STATE, "internal: Schur contribution outside the symbolic structure");
   if (e & 16) return fail(VB_E_HIP, "internal: triangular-solve hand-off timed out");
+  return 0;
+}
+
+// errors of the last device rolling-shutter rebuild (rs.hip): the reference throws there
+int checkRsErr(vb_handle h, int32_t e) {
+  if (e & 1) return fail(VB_E_RANGE, "enumIntegrationSteps: IMU measurements do not cover the rolling-shutter interval");
+  if (e & 2) return fail(VB_E_NUMERIC, "RollingShutterData::compute: non-increasing sample times");
+  if (e & 4) return fail(VB_E_STATE, "internal: rolling-shutter table capacity exceeded");
   return 0;
 }
 
@@ -1203,8 +1221,34 @@ int doFinalize(vb_handle h) {
     return VB_E_HIP;
   if (alloc0(&h->dinv, (size_t)(nT + 1) * 1024) || alloc0(&h->linv, (size_t)nT * TS * TS)) return VB_E_HIP;
   d.nRS = h->nRS;
-  if (upload(&d.rsOff, h->rsOff) || upload(&d.rsS, h->rsS) || upload(&d.rsI, h->rsI) || upload(&d.rsG, h->rsG))
-    return VB_E_HIP;
+  if (h->rsDevice) {
+    // table capacity: the IMU samples of [mid - half, mid + half] widened by 20 ms on both sides (the
+    // reference-time offsets of the calibration move the gyro boundaries by far less), + 4
+    const int64_t kWidenNs = 20000000;
+    h->rsOff.assign(h->nRS + 1, 0);
+    for (int32_t t = 0; t < h->nRS; t++) {
+      const int64_t a = (h->rsMid[t] - h->rsHalf[t]) * 1000 - kWidenNs, b = (h->rsMid[t] + h->rsHalf[t]) * 1000 + kWidenNs;
+      const int64_t cnt = std::upper_bound(h->imuT.begin(), h->imuT.end(), b) -
+                          std::lower_bound(h->imuT.begin(), h->imuT.end(), a);
+      h->rsOff[t + 1] = h->rsOff[t] + cnt + 4;
+    }
+    const int64_t ns = h->rsOff[h->nRS];
+    std::vector<int32_t> zeroN(h->nRS, 0);
+    if (upload(&d.rsOff, h->rsOff) || alloc0(&d.rsS, ns * 11) || alloc0(&d.rsI, (ns - h->nRS) * 9) ||
+        alloc0(&d.rsG, (size_t)h->nRS * 3) || upload(&d.rsN, zeroN) || upload(&d.imuT, h->imuT) ||
+        upload(&d.imuV, h->imuV) || upload(&d.rsMid, h->rsMid) || upload(&d.rsHalf, h->rsHalf) ||
+        upload(&d.rsCalib, h->rsCalib))
+      return VB_E_HIP;
+    d.nImu = (int64_t)h->imuT.size();
+    d.rsGravVar = h->rsGravVar;
+  } else {
+    std::vector<int32_t> cnt(h->nRS);
+    for (int32_t t = 0; t < h->nRS; t++) cnt[t] = (int32_t)(h->rsOff[t + 1] - h->rsOff[t]);
+    if (h->rsOff.empty()) h->rsOff.assign(1, 0);
+    if (upload(&d.rsOff, h->rsOff) || upload(&d.rsS, h->rsS) || upload(&d.rsI, h->rsI) || upload(&d.rsG, h->rsG) ||
+        upload(&d.rsN, cnt))
+      return VB_E_HIP;
+  }
   if (alloc0(&d.red, 64) || alloc0(&d.err, 4)) return VB_E_HIP;
   h->finalized = true;
   return 0;
@@ -1412,7 +1456,8 @@ int vb_destroy(vb_handle h) {
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
-                  d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.red, d.err, h->colTilesD,
+                  d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
+                  d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv};
   for (void* p : ptrs)
@@ -1473,6 +1518,7 @@ int vb_set_rs_tables(vb_handle h, int32_t nt, const int64_t* offsets, const doub
                      const double* gravity) {
   if (!h || nt < 0) return fail(VB_E_ARG, "bad vb_set_rs_tables arguments");
   if (h->finalized) return fail(VB_E_STATE, "vb_set_rs_tables after vb_finalize");
+  if (h->rsDevice) return fail(VB_E_STATE, "vb_set_rs_tables after vb_set_rs_rigs (tables are rebuilt on the device)");
   h->nRS = nt;
   h->rsOff.assign(offsets, offsets + nt + 1);
   const int64_t ns = offsets[nt];
@@ -1481,6 +1527,74 @@ int vb_set_rs_tables(vb_handle h, int32_t nt, const int64_t* offsets, const doub
   h->rsG.assign(gravity, gravity + nt * 3);
   for (int t = 0; t < nt; t++)
     if (offsets[t + 1] - offsets[t] < 2) return fail(VB_E_ARG, "RS table needs >= 2 samples");
+  return 0;
+}
+
+int vb_set_imu_measurements(vb_handle h, int64_t n, const int64_t* timestamp_ns, const double* gyro,
+                             const double* accel) {
+  if (!h || n < 0 || (n && (!timestamp_ns || !gyro || !accel))) return fail(VB_E_ARG, "bad vb_set_imu_measurements arguments");
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_imu_measurements after vb_finalize");
+  h->imuT.assign(timestamp_ns, timestamp_ns + n);
+  h->imuV.resize((size_t)n * 6);
+  for (int64_t i = 0; i < n; i++) {
+    if (i && timestamp_ns[i] <= timestamp_ns[i - 1]) return fail(VB_E_ARG, "IMU timestamps must increase");
+    for (int k = 0; k < 3; k++) h->imuV[6 * i + k] = gyro[3 * i + k], h->imuV[6 * i + 3 + k] = accel[3 * i + k];
+  }
+  return 0;
+}
+
+int vb_set_rs_rigs(vb_handle h, int32_t nt, const int64_t* mid_us, const int64_t* half_us, const int32_t* imu_calib,
+                   int32_t gravity_var) {
+  if (!h || nt < 0 || (nt && (!mid_us || !half_us || !imu_calib))) return fail(VB_E_ARG, "bad vb_set_rs_rigs arguments");
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_rs_rigs after vb_finalize");
+  if (h->imuT.empty() && nt) return fail(VB_E_STATE, "vb_set_rs_rigs needs vb_set_imu_measurements first");
+  const int64_t nCalib = (int64_t)h->data[6].size() / 32, nGrav = (int64_t)h->data[8].size() / 4;
+  if (gravity_var < 0 || gravity_var >= nGrav) return fail(VB_E_ARG, "vb_set_rs_rigs: unknown gravity variable");
+  for (int32_t t = 0; t < nt; t++) {
+    if (imu_calib[t] < 0 || imu_calib[t] >= nCalib) return fail(VB_E_ARG, "vb_set_rs_rigs: unknown IMU calibration");
+    if (half_us[t] <= 0) return fail(VB_E_ARG, "vb_set_rs_rigs: half length must be positive");
+  }
+  h->nRS = nt;
+  h->rsMid.assign(mid_us, mid_us + nt);
+  h->rsHalf.assign(half_us, half_us + nt);
+  h->rsCalib.assign(imu_calib, imu_calib + nt);
+  h->rsGravVar = gravity_var;
+  h->rsDevice = true;
+  h->rsS.clear(), h->rsI.clear(), h->rsG.clear(), h->rsOff.clear();
+  return 0;
+}
+
+// enqueue the rebuild; its errors surface at the next synchronising check (checkErr reads err[1])
+int rsUpdateAsync(vb_handle h) {
+  HIPCHK(hipMemsetAsync(h->d.err + 1, 0, sizeof(int32_t), h->st));
+  HIPCHK(hipEventRecord(h->ev[8], h->st));
+  launch_rs_build(h->d, h->st);
+  HIPCHK(hipEventRecord(h->ev[9], h->st));
+  h->rsTimed = true;
+  return 0;
+}
+
+int vb_update_rs_tables(vb_handle h) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_update_rs_tables before vb_finalize");
+  if (!h->rsDevice) return fail(VB_E_STATE, "vb_update_rs_tables without vb_set_rs_rigs");
+  if (int rc = rsUpdateAsync(h)) return rc;
+  int32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, h->d.err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkRsErr(h, e);
+}
+
+int vb_get_rs_table(vb_handle h, int32_t t, int32_t* n_samples, double* samples, double* interp) {
+  if (!h || !h->finalized || !n_samples) return fail(VB_E_STATE, "vb_get_rs_table before vb_finalize");
+  if (t < 0 || t >= h->nRS) return fail(VB_E_ARG, "vb_get_rs_table: bad table index");
+  int32_t n = 0;
+  HIPCHK(hipMemcpyAsync(&n, h->d.rsN + t, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  *n_samples = n;
+  const int64_t s0 = h->rsOff[t];
+  if (samples && n) HIPCHK(hipMemcpy(samples, h->d.rsS + s0 * 11, (size_t)n * 11 * sizeof(double), hipMemcpyDeviceToHost));
+  if (interp && n > 1)
+    HIPCHK(hipMemcpy(interp, h->d.rsI + (s0 - t) * 9, (size_t)(n - 1) * 9 * sizeof(double), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -1519,6 +1633,7 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   if (int rc = readRed(h, &c, 0, 1)) return rc;
   if (int rc = checkErr(h)) return rc;
   h->times.linearize_ms = elapsed(h->ev[0], h->ev[1]);
+  if (h->rsTimed) h->times.rs_update_ms = elapsed(h->ev[8], h->ev[9]), h->rsTimed = false;
   if (cost) *cost = c;
   h->linearized = true, h->factored = false;
   return 0;
@@ -1774,6 +1889,8 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
   char buf[512];
   while (true) {
     auto t0 = std::chrono::steady_clock::now();
+    // ark_vi_ba's preStepCallback (main_AriaKit_ViBa.cpp:95-101): updateRollingShutterData
+    if (h->rsDevice && (rc = rsUpdateAsync(h))) return rc;
     if (pre) pre(it, user);
     double prevCost;
     if ((rc = vb_linearize(h, 1, dontRetry, &prevCost))) return rc;

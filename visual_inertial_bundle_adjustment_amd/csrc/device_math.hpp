@@ -347,6 +347,37 @@ DEVI rvp combine(const rvp& a, const rvp& b) {
   return c;
 }
 
+// MotionIntegral.cpp:35-42
+DEVI rvp uncombine_left(const rvp& c, const rvp& a) {
+  const q4 ai = qinv(a.R);
+  rvp b;
+  b.R = qmul(ai, c.R);
+  b.dV = qrot(ai, sub(c.dV, a.dV));
+  b.dt = c.dt - a.dt;
+  b.dP = qrot(ai, sub(sub(c.dP, a.dP), scl(b.dt, a.dV)));
+  return b;
+}
+DEVI v3 vdiv(v3 a, double s) { return {a.x / s, a.y / s, a.z / s}; }
+// differentiate (MotionIntegral.cpp:88-115): out = [gyroRadSec, accelMSec2, deltaVelMSec]
+DEVI void differentiate(const rvp& r, double* out) {
+  const v3 om = qlog(r.R);
+  const double th2 = dot(om, om), th = sqrt(th2);
+  double q2;
+  if (th < 1e-3) {
+    q2 = 1.0 / 12.0 - th2 / (4.0 * 180.0) + (th2 * th2) / (16.0 * 1890.0);
+  } else {
+    const double h = th * 0.5;
+    q2 = (1.0 - h * cos(h) / sin(h)) / th2;
+  }
+  const v3 ov = cross(om, r.dV);
+  const v3 ups = add(add(r.dV, scl(-0.5, ov)), scl(q2, cross(om, ov)));
+  const v3 g = vdiv(om, r.dt), a = vdiv(ups, r.dt);
+  const rvp rec = integrate(g, a, r.dt);
+  const v3 dv = vdiv(sub(r.dP, rec.dP), r.dt);
+  out[0] = g.x, out[1] = g.y, out[2] = g.z, out[3] = a.x, out[4] = a.y, out[5] = a.z;
+  out[6] = dv.x, out[7] = dv.y, out[8] = dv.z;
+}
+
 // RollingShutterData::getEstimate (RollingShutterData.cpp:67-111); returns T_midImu_imuAtT,
 // sets *outOfRange when tDelta is outside the table (the reference throws there)
 DEVI se3 rs_estimate(const double* samples, const double* interp, int n, const double* grav,

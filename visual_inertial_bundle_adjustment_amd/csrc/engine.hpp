@@ -155,9 +155,20 @@ struct Dev {
   double* sE = nullptr;
   int32_t* sMeta = nullptr;
   // rolling shutter
+  // table t: samples rsS[11 * (rsOff[t] .. rsOff[t] + rsN[t])), interpolants rsI[9 * (rsOff[t] - t ..)),
+  // gravity rsG[3 t]; rsOff spaces the tables by their capacity when they are rebuilt on the device
   int32_t nRS = 0;
   int64_t* rsOff = nullptr;
+  int32_t* rsN = nullptr;
   double *rsS = nullptr, *rsI = nullptr, *rsG = nullptr;
+  // device rebuild inputs (rs.hip): IMU-0 stream (timestamps [ns], [gyro 3, accel 3] per sample),
+  // per table midpoint / half length [us] and IMU calib variable, the gravity variable
+  int64_t nImu = 0;
+  int64_t* imuT = nullptr;
+  double* imuV = nullptr;
+  int64_t *rsMid = nullptr, *rsHalf = nullptr;
+  int32_t* rsCalib = nullptr;
+  int32_t rsGravVar = 0;
   // scratch for reductions
   double* red = nullptr;  // 64 doubles
   int32_t* err = nullptr;  // error flags

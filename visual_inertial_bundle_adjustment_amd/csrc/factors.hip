@@ -112,7 +112,7 @@ __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se
   const double tpf = obsC[1] / cam[3] - 0.5;
   const double ro = cam[4] != 0.0 ? cam[5] : 0.0;
   const double dt = ro * tpf - cam[6];
-  const int64_t s0 = d.rsOff[rs], ns = d.rsOff[rs + 1] - s0;
+  const int64_t s0 = d.rsOff[rs], ns = d.rsN[rs];
   const double* S = d.rsS + s0 * 11;
   const double* I = d.rsI + (s0 - rs) * 9;
   const double* G = d.rsG + rs * 3;

@@ -31,6 +31,10 @@ struct Gen {
   std::vector<double> fconst[14];
   std::vector<int64_t> rsOff;
   std::vector<double> rsSamples, rsInterp, rsGravity;
+  // IMU-0 stream and per-table rebuild inputs (vb_set_imu_measurements / vb_set_rs_rigs)
+  std::vector<int64_t> imuT, rsMid, rsHalf;
+  std::vector<double> imuG, imuA;
+  std::vector<int32_t> rsCalib;
   std::mt19937_64 rng;
   std::normal_distribution<double> N01{0.0, 1.0};
   std::uniform_real_distribution<double> U01{0.0, 1.0};
@@ -48,6 +52,11 @@ Vec3 velAt(double t) {
   return {6.0 * 0.11 * std::cos(0.11 * t + 0.3) + 1.5 * 0.31 * std::cos(0.31 * t),
           6.0 * 0.09 * std::cos(0.09 * t + 1.9) - 1.5 * 0.27 * std::sin(0.27 * t),
           0.3 * 0.45 * std::cos(0.45 * t)};
+}
+Vec3 accAt(double t) {
+  return {-6.0 * 0.11 * 0.11 * std::sin(0.11 * t + 0.3) - 1.5 * 0.31 * 0.31 * std::sin(0.31 * t),
+          -6.0 * 0.09 * 0.09 * std::sin(0.09 * t + 1.9) - 1.5 * 0.27 * 0.27 * std::cos(0.27 * t),
+          -0.3 * 0.45 * 0.45 * std::sin(0.45 * t)};
 }
 Quat rotWB(double t) {  // R_world_body = Rz(yaw) Ry(pitch) Rx(roll)
   const double yaw = 0.15 * t + 0.8 * std::sin(0.21 * t);
@@ -507,6 +516,42 @@ void* vbs_generate(const vbs_config* cfg) {
       g.rsOff.push_back(g.rsOff.back() + nS);
       g.rsGravity.push_back(gravity.x), g.rsGravity.push_back(gravity.y), g.rsGravity.push_back(gravity.z);
     }
+    // IMU-0 measurement stream at 1 kHz for the device rebuild of the same tables: trajectory time 0
+    // is stamp kBaseNs; measurement i at stamp s_i carries the mean body rate over reference times
+    // (s_{i-1}, s_i] - dtReferenceGyro and the specific force at the middle of (s_{i-1}, s_i] -
+    // dtReferenceAccel, distorted by the GT calibration of the window:
+    // meas = diag(scale) nonorth (true + bias) (ImuMeasurementModelParameters.h:17-26), + white noise
+    // from a separate generator (the problem's own random sequence is unchanged)
+    const int64_t kBaseNs = 1000000000, kStepNs = 1000000;
+    const double tBeg = -half - 0.03, tEnd = (nKf - 1) * dtKf + half + 0.03;
+    std::mt19937_64 nrng(cfg->seed ^ 0x5EEDC0FFEEULL);
+    std::normal_distribution<double> nd(0.0, 1.0);
+    const double winSec = kfPerWin * dtKf;
+    for (int64_t i = (int64_t)std::floor(tBeg * 1e3); i <= (int64_t)std::ceil(tEnd * 1e3); i++) {
+      const int64_t st = kBaseNs + i * kStepNs;
+      const int w = std::min(nWin - 1, std::max(0, (int)std::floor(i * 1e-3 / winSec)));
+      const double* m = gtImu[w * nImu].data();
+      const double dtA = m[30], dtG = m[31];
+      const double a = (st - kStepNs - kBaseNs) * 1e-9 - dtG, b = (st - kBaseNs) * 1e-9 - dtG;
+      const Vec3 om = (1.0 / (b - a)) * qlog(qmul(qinv(rotWB(a)), rotWB(b)));
+      const double tc = (st - kStepNs / 2 - kBaseNs) * 1e-9 - dtA;
+      const Vec3 f = qrot(qinv(rotWB(tc)), accAt(tc) - gravity);
+      const double ov[3] = {om.x + m[6], om.y + m[7], om.z + m[8]};
+      const double fv[3] = {f.x + m[9], f.y + m[10], f.z + m[11]};
+      g.imuT.push_back(st);
+      for (int r = 0; r < 3; r++) {
+        double gm = 0, am = 0;
+        for (int c = 0; c < 3; c++) gm += m[12 + c * 3 + r] * ov[c], am += m[21 + c * 3 + r] * fv[c];
+        g.imuG.push_back(m[r] * gm + 1e-4 * nd(nrng));
+        g.imuA.push_back(m[3 + r] * am + 1e-3 * nd(nrng));
+      }
+    }
+    const int64_t halfUs = (int64_t)(2e3 + camSpan * 0.5e6);  // InitCalibration.cpp:307
+    for (int k = 0; k < nKf; k++) {
+      g.rsMid.push_back(kBaseNs / 1000 + (int64_t)std::llround(k * dtKf * 1e6));
+      g.rsHalf.push_back(halfUs);
+      g.rsCalib.push_back(std::min(nWin - 1, k / kfPerWin) * nImu);
+    }
   }
 
   // ---------------- points + visual factors
@@ -823,5 +868,12 @@ const int64_t* vbs_rs_offsets(void* h) { return ((Gen*)h)->rsOff.data(); }
 const double* vbs_rs_samples(void* h) { return ((Gen*)h)->rsSamples.data(); }
 const double* vbs_rs_interp(void* h) { return ((Gen*)h)->rsInterp.data(); }
 const double* vbs_rs_gravity(void* h) { return ((Gen*)h)->rsGravity.data(); }
+int64_t vbs_num_imu(void* h) { return (int64_t)((Gen*)h)->imuT.size(); }
+const int64_t* vbs_imu_t(void* h) { return ((Gen*)h)->imuT.data(); }
+const double* vbs_imu_gyro(void* h) { return ((Gen*)h)->imuG.data(); }
+const double* vbs_imu_accel(void* h) { return ((Gen*)h)->imuA.data(); }
+const int64_t* vbs_rs_mid(void* h) { return ((Gen*)h)->rsMid.data(); }
+const int64_t* vbs_rs_half(void* h) { return ((Gen*)h)->rsHalf.data(); }
+const int32_t* vbs_rs_calib(void* h) { return ((Gen*)h)->rsCalib.data(); }
 
 }  // extern "C"

@@ -245,6 +245,8 @@ class ShardedOptimizer:
             return rate < 0.03 and st[1] < st[2] * 2.0 + 50
 
         while True:
+            if getattr(e, "rs_device", False):  # ark_vi_ba's preStepCallback (vb_optimize does the same)
+                e.update_rs_tables()
             prev_cost = self.linearize(dont_retry)
             final_cost = prev_cost
             if it == 0:
@@ -442,7 +444,7 @@ def run_sharded(args, rank: int, world: int, local: int):
     else:
         lb, le = shard_bounds(p, world)[rank]
         e.set_landmark_shard(lb, le, rank == 0)
-    synth.load_into(e, p)
+    synth.load_into(e, p, rs_device=getattr(args, "rs_tables", "device") == "device")
     st = e.problem_stats()
     comm = ShardComm(rank, world, dev)
     if mode == "partition":

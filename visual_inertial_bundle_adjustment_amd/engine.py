@@ -66,7 +66,7 @@ class Summary(C.Structure):
 
 class PhaseTimes(C.Structure):
     _fields_ = [(n, C.c_double) for n in ("linearize_ms", "schur_ms", "factor_ms", "solve_ms",
-                                          "step_ms", "cost_ms", "total_ms")]
+                                          "step_ms", "cost_ms", "total_ms", "rs_update_ms")]
 
 
 LOG_CB = C.CFUNCTYPE(None, C.c_char_p, P)
@@ -127,6 +127,39 @@ class CEngineBase:
         f = self._fn("set_rs_tables", [C.c_int32, C.POINTER(C.c_int64), _dp, _dp, _dp])
         self._check(f(self.h, len(off) - 1, off.ctypes.data_as(C.POINTER(C.c_int64)),
                       s.ctypes.data_as(_dp), ip.ctypes.data_as(_dp), g.ctypes.data_as(_dp)))
+
+    def set_imu_measurements(self, timestamp_ns, gyro, accel):
+        """IMU-0 stream for the device rolling-shutter rebuild (vb_set_imu_measurements)."""
+        t = _arr(timestamp_ns, np.int64)
+        g, a = _arr(gyro, np.float64).reshape(-1, 3), _arr(accel, np.float64).reshape(-1, 3)
+        f = self._fn("set_imu_measurements", [C.c_int64, C.POINTER(C.c_int64), _dp, _dp])
+        self._check(f(self.h, len(t), t.ctypes.data_as(C.POINTER(C.c_int64)), g.ctypes.data_as(_dp),
+                      a.ctypes.data_as(_dp)))
+
+    def set_rs_rigs(self, midpoint_us, half_length_us, imu_calib, gravity_var=0):
+        """Per-table rebuild inputs (vb_set_rs_rigs): RollingShutterData's midpoint / half length and
+        the IMU calibration variable of updateRollingShutterData (InitCalibration.cpp:316-325)."""
+        m, hl = _arr(midpoint_us, np.int64), _arr(half_length_us, np.int64)
+        c = _arr(imu_calib, np.int32)
+        f = self._fn("set_rs_rigs", [C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                     C.POINTER(C.c_int32), C.c_int32])
+        self._check(f(self.h, len(m), m.ctypes.data_as(C.POINTER(C.c_int64)),
+                      hl.ctypes.data_as(C.POINTER(C.c_int64)), c.ctypes.data_as(C.POINTER(C.c_int32)),
+                      int(gravity_var)))
+
+    def update_rs_tables(self):
+        """RollingShutterData::compute of every table from the current variables."""
+        self._check(self._fn("update_rs_tables", [])(self.h))
+
+    def get_rs_table(self, t: int):
+        """(samples (n, 11), interpolants (n - 1, 9)) of table t."""
+        n = C.c_int32()
+        f = self._fn("get_rs_table", [C.c_int32, C.POINTER(C.c_int32), _dp, _dp])
+        self._check(f(self.h, t, C.byref(n), None, None))
+        s = np.zeros((n.value, 11))
+        ip = np.zeros((max(0, n.value - 1), 9))
+        self._check(f(self.h, t, C.byref(n), s.ctypes.data_as(_dp), ip.ctypes.data_as(_dp)))
+        return s, ip
 
     def finalize(self):
         self._check(self._fn("finalize", [])(self.h))
