@@ -238,6 +238,13 @@ int vb_set_rs_rigs(vb_handle h, int32_t n_tables, const int64_t* midpoint_us, co
 int vb_update_rs_tables(vb_handle h);
 /* download table t: sample count, samples (11 doubles each, NULL to skip) and interpolants (9 each) */
 int vb_get_rs_table(vb_handle h, int32_t t, int32_t* n_samples, double* samples, double* interp);
+/* refinePoints (viba/problem/PointRefinement.cpp:160-196, run by ark_vi_ba before optimize,
+ * main_AriaKit_ViBa.cpp:69): every point with visual factors takes up to 5 damped Gauss-Newton steps on
+ * those factors alone (optimizeOnePoint, :91-158), one wave per point on the device.  After vb_finalize
+ * (and vb_update_rs_tables when rebuilt on the device); whole-problem handles only.
+ * costs = {total start cost, total end cost}; stats = {failures, successful iterations, points with
+ * at least one iteration} (the reference's log line, :183-194); either may be NULL. */
+int vb_refine_points(vb_handle h, double* costs, int64_t* stats);
 /* build the symbolic structure (≙ Optimizer::initSolver) and upload everything to HBM */
 int vb_finalize(vb_handle h);
 int64_t vb_reduced_order(vb_handle h);   /* order of the Schur-reduced (non-point) system */

@@ -1194,6 +1194,157 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
   return 0;
 }
 
+// ---------------------------------------------------------------- refinePoints
+// viba/problem/PointRefinement.cpp:16-196: every point with visual factors gets up to 5 damped
+// Gauss-Newton steps on those factors alone (point Jacobian only, varGradHess of Factor.h:419-466).
+
+// Eigen::LDLT<Matrix3d>::solve: ldlt_inplace<Lower>::unblocked (diagonal pivoting by the largest
+// remaining |diagonal|, left-looking column update, A21 /= pivot), then P^T L^-T D^-1 L^-1 P b with
+// D^-1 as Eigen's pseudo-inverse (0 for |d| <= DBL_MIN)
+static void ldlt3_solve(const double Hl[6], const double b[3], double x[3]) {
+  double m[3][3] = {{Hl[0], Hl[1], Hl[2]}, {Hl[1], Hl[3], Hl[4]}, {Hl[2], Hl[4], Hl[5]}};
+  int tr[3];
+  for (int k = 0; k < 3; k++) {
+    int big = k;
+    for (int i = k + 1; i < 3; i++)
+      if (std::fabs(m[i][i]) > std::fabs(m[big][big])) big = i;
+    tr[k] = big;
+    if (big != k) {
+      for (int j = 0; j < 3; j++) std::swap(m[k][j], m[big][j]);
+      for (int i = 0; i < 3; i++) std::swap(m[i][k], m[i][big]);
+    }
+    double tmp[3];
+    for (int j = 0; j < k; j++) tmp[j] = m[j][j] * m[k][j];
+    for (int j = 0; j < k; j++) m[k][k] -= m[k][j] * tmp[j];
+    for (int i = k + 1; i < 3; i++) {
+      for (int j = 0; j < k; j++) m[i][k] -= m[i][j] * tmp[j];
+      if (m[k][k] != 0.0) m[i][k] /= m[k][k];
+    }
+  }
+  for (int i = 0; i < 3; i++) x[i] = b[i];
+  for (int k = 0; k < 3; k++)
+    if (tr[k] != k) std::swap(x[k], x[tr[k]]);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < i; j++) x[i] -= m[i][j] * x[j];
+  for (int i = 0; i < 3; i++) x[i] = std::fabs(m[i][i]) > 2.2250738585072014e-308 ? x[i] / m[i][i] : 0.0;
+  for (int i = 2; i >= 0; i--)
+    for (int j = i + 1; j < 3; j++) x[i] -= m[j][i] * x[j];
+  for (int k = 2; k >= 0; k--)
+    if (tr[k] != k) std::swap(x[k], x[tr[k]]);
+}
+
+// pointGradHess (PointRefinement.cpp:48-75)
+static double refineGradHess(Problem& P, const std::vector<int64_t>& fl, std::vector<double>& bk, bool update,
+                             double g[3], double H[6]) {
+  double cost = 0;
+  for (int i = 0; i < 3; i++) g[i] = 0;
+  for (int i = 0; i < 6; i++) H[i] = 0;
+  bool wants[5] = {true, false, false, false, false};
+  for (size_t q = 0; q < fl.size(); q++) {
+    EvalOut o = evalFactor(P, 0, fl[q], wants);
+    if (!o.fe.ok) {
+      if (update) bk[q] = -1.0;
+      continue;
+    }
+    double rho, drho;
+    o.loss->jet2(squaredError(o), rho, drho);
+    cost += 0.5 * rho;
+    if (update) bk[q] = 0.5 * rho;
+    const Mat& J = o.fe.J[0];  // 2 x 3
+    for (int c = 0; c < 3; c++) {
+      const double a0 = drho * J(0, c), a1 = drho * J(1, c);
+      g[c] += o.fe.e[0] * a0 + o.fe.e[1] * a1;
+    }
+    const int ij[6][2] = {{0, 0}, {1, 0}, {2, 0}, {1, 1}, {2, 1}, {2, 2}};
+    for (int t = 0; t < 6; t++) {
+      const int a = ij[t][0], b = ij[t][1];
+      H[t] += drho * J(0, a) * J(0, b) + drho * J(1, a) * J(1, b);
+    }
+  }
+  return cost;
+}
+
+// pointCost (PointRefinement.cpp:78-90)
+static double refineCost(Problem& P, const std::vector<int64_t>& fl, const std::vector<double>& bk) {
+  double cost = 0;
+  bool wants[5] = {false, false, false, false, false};
+  for (size_t q = 0; q < fl.size(); q++) {
+    if (bk[q] < 0) continue;
+    EvalOut o = evalFactor(P, 0, fl[q], wants);
+    cost += o.fe.ok ? 0.5 * o.loss->val(squaredError(o)) : bk[q];
+  }
+  return cost;
+}
+
+// refinePoints / optimizeOnePoint (PointRefinement.cpp:91-196); out = {start cost, end cost},
+// stats = {failures, successful iterations, points with >= 1 iteration}
+int ref_refine_points(void* h, double* out, int64_t* stats) {
+  Problem& P = *(Problem*)h;
+  try {
+    std::vector<std::vector<int64_t>> tracks(P.data[0].size() / 3);
+    for (int64_t k = 0; k < (int64_t)P.fint[0].size(); k++) tracks[P.fvars[0][(size_t)k * 5]].push_back(k);
+    constexpr double kLambda = 1e-5, kCostTol = 1e-8, kStepTol = 1e-6, kMinImpr = 0.2, kStepRed = 0.3;
+    double totStart = 0, totEnd = 0;
+    int64_t nFail = 0, nTotIts = 0, nAtLeastOne = 0;
+    std::vector<double> bk;
+    for (size_t pt = 0; pt < tracks.size(); pt++) {
+      const auto& fl = tracks[pt];
+      if (fl.empty()) continue;
+      bk.assign(fl.size(), 0.0);
+      double* X = &P.data[0][pt * 3];
+      double startCost = 0, endCost = 0;
+      int nIts = 0;
+      for (int i = 0; i < 5; i++) {
+        double g[3], H[6];
+        const double cost = refineGradHess(P, fl, bk, true, g, H);
+        if (i == 0) startCost = endCost = cost;
+        H[0] = H[0] * (1.0 + kLambda) + kLambda, H[3] = H[3] * (1.0 + kLambda) + kLambda;
+        H[5] = H[5] * (1.0 + kLambda) + kLambda;
+        double st[3];
+        ldlt3_solve(H, g, st);
+        for (double& v : st) v = -v;
+        const double Xb[3] = {X[0], X[1], X[2]};
+        bool success = false;
+        for (int c = 0; c < 3; c++) X[c] += st[c];
+        double newCost = refineCost(P, fl, bk);
+        const double modelDelta = st[0] * g[0] + st[1] * g[1] + st[2] * g[2];
+        if (-modelDelta < kCostTol) break;  // the step stays applied (PointRefinement.cpp:116-118)
+        if (newCost < cost + modelDelta * kMinImpr) {
+          success = true;
+        } else {
+          double ng[3], nH[6];
+          refineGradHess(P, fl, bk, false, ng, nH);
+          for (int c = 0; c < 3; c++) X[c] = Xb[c];
+          const double newDelta = st[0] * ng[0] + st[1] * ng[1] + st[2] * ng[2];
+          const double f = newDelta > 0 ? -modelDelta / (newDelta - modelDelta) : kStepRed;
+          for (double& v : st) v *= f;
+          for (int c = 0; c < 3; c++) X[c] += st[c];
+          newCost = refineCost(P, fl, bk);
+          if (newCost < cost + (st[0] * g[0] + st[1] * g[1] + st[2] * g[2]) * kMinImpr) success = true;
+          else for (int c = 0; c < 3; c++) X[c] = Xb[c];
+        }
+        if (success) {
+          nIts++;
+          endCost = newCost;
+        } else {
+          nIts = -1;
+          break;
+        }
+        if (st[0] * st[0] + st[1] * st[1] + st[2] * st[2] < kStepTol * kStepTol) break;
+      }
+      if (nIts < 0) nFail++;
+      else nTotIts += nIts, nAtLeastOne += nIts > 0;
+      totStart += startCost, totEnd += endCost;
+    }
+    out[0] = totStart, out[1] = totEnd;
+    stats[0] = nFail, stats[1] = nTotIts, stats[2] = nAtLeastOne;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+
 // raw evaluation of one factor (residual + Jacobians) for finite-difference Jacobian tests:
 // e_out[m], J_out[m * sum(tdims)] (blocks in var order, col-major per block); returns m or <0
 int ref_eval_factor(void* h, int fk, int64_t k, double* e_out, double* J_out) {

@@ -209,3 +209,17 @@ def test_rs_rebuild_imu_gap_is_an_error():
     with pytest.raises(VbError) as ex:
         synth.load_into(e, p, rs_device=True)
     assert ex.value.code == -5
+
+
+def test_refine_points_matches_oracle():
+    """refinePoints on the device (one wave per point) against the oracle's restatement
+    (PointRefinement.cpp:91-196): same totals and statistics, same refined points.  Tolerance 1e-9 on
+    the points: independent per-point Gauss-Newton iterations, differing only in summation order."""
+    p = synth.generate(synth.config("miniB"))
+    g, r = _rs_pair(p)
+    (sg, eg), stg = g.refine_points()
+    (sr, er), str_ = r.refine_points()
+    assert stg == str_
+    assert abs(sg - sr) <= 1e-10 * sr and abs(eg - er) <= 1e-9 * er
+    assert rel(g.get_vars(0), r.get_vars(0)) < 1e-9
+    assert_step_parity(one_step(g), one_step(r))  # the LM step from the refined points

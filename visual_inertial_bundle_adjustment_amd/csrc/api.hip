@@ -24,6 +24,8 @@ void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo,
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_rs_build(const Dev& d, hipStream_t st);
+void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gObs, const int32_t* gPt, int64_t nG,
+                          double* backups, double* acc, hipStream_t st);
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st);
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
@@ -226,6 +228,11 @@ struct vb_handle_s {
   std::vector<int32_t> rsCalib;
   int32_t rsGravVar = -1;
   bool rsDevice = false, rsTimed = false;
+  // point refinement groups (built at the first vb_refine_points): observations by point
+  int64_t nRefG = 0;
+  int64_t* refStartD = nullptr;
+  int32_t *refObsD = nullptr, *refPtD = nullptr;
+  double *refBackD = nullptr, *refAccD = nullptr;
   bool finalized = false;
   Dev d;
   std::vector<void*> allocs;
@@ -1459,7 +1466,7 @@ int vb_destroy(vb_handle h) {
                   d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
-                  h->rhsWork, h->linv};
+                  h->rhsWork, h->linv, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int k = 0; k < 9; k++) {
@@ -1582,6 +1589,45 @@ int vb_update_rs_tables(vb_handle h) {
   HIPCHK(hipMemcpyAsync(&e, h->d.err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
   return checkRsErr(h, e);
+}
+
+int vb_refine_points(vb_handle h, double* costs, int64_t* stats) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_refine_points before vb_finalize");
+  Dev& d = h->d;
+  if (h->partWorld > 1 || d.lmB != 0 || d.lmE != d.nPts || !h->isRoot)
+    return fail(VB_E_UNSUPPORTED, "vb_refine_points needs the whole problem on this handle (no shard / partition)");
+  if (!h->refStartD) {
+    // observations grouped by point variable (refinePoints' perPointTracks, PointRefinement.cpp:20-45),
+    // in device observation order
+    std::vector<int32_t> obPt(d.nObs);
+    if (d.nObs) HIPCHK(hipMemcpy(obPt.data(), d.obPt, d.nObs * sizeof(int32_t), hipMemcpyDeviceToHost));
+    const int64_t nP = d.nvar[0];
+    std::vector<int64_t> cnt(nP + 1, 0);
+    for (int32_t p : obPt) cnt[p + 1]++;
+    for (int64_t p = 0; p < nP; p++) cnt[p + 1] += cnt[p];
+    std::vector<int32_t> obs(d.nObs);
+    std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+    for (int64_t o = 0; o < d.nObs; o++) obs[pos[obPt[o]]++] = (int32_t)o;
+    std::vector<int64_t> gs(1, 0);
+    std::vector<int32_t> gp;
+    for (int64_t p = 0; p < nP; p++)
+      if (cnt[p + 1] > cnt[p]) gp.push_back((int32_t)p), gs.push_back(cnt[p + 1]);
+    h->nRefG = (int64_t)gp.size();
+    if (upload(&h->refStartD, gs) || upload(&h->refObsD, obs) || upload(&h->refPtD, gp) ||
+        alloc0(&h->refBackD, (size_t)d.nObs) || alloc0(&h->refAccD, 8))
+      return VB_E_HIP;
+  }
+  HIPCHK(hipMemsetAsync(h->refAccD, 0, 8 * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.err, 0, 2 * sizeof(int32_t), h->st));
+  launch_refine_points(d, h->refStartD, h->refObsD, h->refPtD, h->nRefG, h->refBackD, h->refAccD, h->st);
+  double acc[8];
+  HIPCHK(hipMemcpyAsync(acc, h->refAccD, sizeof(acc), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  if (int rc = checkErr(h)) return rc;
+  if (costs) costs[0] = acc[0], costs[1] = acc[1];
+  if (stats) stats[0] = (int64_t)acc[2], stats[1] = (int64_t)acc[3], stats[2] = (int64_t)acc[4];
+  h->linearized = false, h->factored = false;
+  return 0;
 }
 
 int vb_get_rs_table(vb_handle h, int32_t t, int32_t* n_samples, double* samples, double* interp) {

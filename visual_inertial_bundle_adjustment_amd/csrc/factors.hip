@@ -54,8 +54,9 @@ struct VisOut {
 };
 
 // VisualFactor::operator() (VisualFactor.cpp:40-82) for T_bw given; Jacobians wrt point, the
-// pose argument (2x6), extrinsics (2x6) and intrinsics (2x nparams)
-template <bool WantJ>
+// pose argument (2x6), extrinsics (2x6) and intrinsics (2x nparams); PointOnly: the point Jacobian
+// alone (point refinement, varGradHess of the point variable)
+template <bool WantJ, bool PointOnly = false>
 __device__ bool vis_eval(const double* obsC, v3 X, const se3& Tbw, const se3& Tcb, const double* cam,
                          VisOut& o) {
   v3 pRig = se3_act(Tbw, X);
@@ -77,6 +78,7 @@ __device__ bool vis_eval(const double* obsC, v3 X, const se3& Tbw, const se3& Tc
 #pragma unroll
       for (int j = 0; j < 3; j++)
         o.Jpt[r * 3 + j] = dW[r * 3] * Rcw.a[0][j] + dW[r * 3 + 1] * Rcw.a[1][j] + dW[r * 3 + 2] * Rcw.a[2][j];
+      if (PointOnly) continue;
       double A[3];
 #pragma unroll
       for (int j = 0; j < 3; j++)
@@ -94,6 +96,7 @@ __device__ bool vis_eval(const double* obsC, v3 X, const se3& Tbw, const se3& Tc
       o.Jextr[r * 6 + 4] = -B[0] * mc.z + B[2] * mc.x;
       o.Jextr[r * 6 + 5] = B[0] * mc.y - B[1] * mc.x;
     }
+    if (PointOnly) return true;
     const int n = (int)cam[1];
 #pragma unroll
     for (int j = 0; j < 17; j++) {
@@ -106,7 +109,7 @@ __device__ bool vis_eval(const double* obsC, v3 X, const se3& Tbw, const se3& Tc
 }
 
 // RollingShutterVisualFactor::operator() (VisualFactor.cpp:131-210)
-template <bool WantJ>
+template <bool WantJ, bool PointOnly = false>
 __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se3& Tbw, const se3& Tcb,
                         const double* cam, v3 vel, bool wantTime, bool wantVel, VisOut& o, bool* oor) {
   const double tpf = obsC[1] / cam[3] - 0.5;
@@ -122,8 +125,8 @@ __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se
   if (*oor) return false;
   se3 TAtTMid = se3_inv(TmidAtT);
   se3 TAtTw = se3_mul(TAtTMid, Tbw);
-  if (!vis_eval<WantJ>(obsC, X, TAtTw, Tcb, cam, o)) return false;
-  if (WantJ) {
+  if (!vis_eval<WantJ, PointOnly>(obsC, X, TAtTw, Tcb, cam, o)) return false;
+  if (WantJ && !PointOnly) {
     double Jt[12];  // wrt T_AtT_w
 #pragma unroll
     for (int i = 0; i < 12; i++) Jt[i] = o.Jpose[i];
@@ -825,6 +828,185 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
     if (R < C) { const int64_t t = R; R = C; C = t; }
     if (owns_col(d, C / d.T)) atomicAdd(tile_addr(d, R, C), drho * hs);
   }
+}
+
+// ------------------------------------------------------------------ point refinement
+// refinePoints (viba/problem/PointRefinement.cpp:91-196): per point a few damped Gauss-Newton steps on
+// its visual factors alone, before the LM loop (ark_vi_ba, main_AriaKit_ViBa.cpp:69).  One wave per
+// point (group g: observations gObs[gStart[g] .. gStart[g + 1]) of point variable gPt[g]), lanes over
+// the observations; backups[] holds pointGradHess's costBackups (PointRefinement.cpp:48-75) per slot.
+// acc[0..4] += start cost, end cost, failures, successful iterations, points with >= 1 iteration.
+__device__ __forceinline__ double refine_wave_sum(double x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+// one observation at point X: whitened residual (and 2x3 point Jacobian); false if the factor fails
+template <bool WantJ>
+__device__ bool refine_eval(const Dev& d, int64_t o, v3 X, VisOut& v) {
+  const double* obsC = d.obC + o * 6;
+  se3 Tbw = se3_load(d.var[1] + (int64_t)d.obPose[o] * 7);
+  se3 Tcb = se3_load(d.var[5] + (int64_t)d.obExtr[o] * 7);
+  const double* cam = d.var[4] + (int64_t)d.obIntr[o] * 24;
+  const int rs = d.obRS[o];
+  if (rs < 0) return vis_eval<WantJ, true>(obsC, X, Tbw, Tcb, cam, v);
+  const double* vp = d.var[2] + (int64_t)d.obVel[o] * 3;
+  bool oor = false;
+  const bool ok = rs_eval<WantJ, true>(d, obsC, rs, X, Tbw, Tcb, cam, mk(vp[0], vp[1], vp[2]), false, false, v, &oor);
+  if (oor) atomicOr(d.err, 1);
+  return ok;
+}
+
+// pointGradHess (PointRefinement.cpp:48-75): sum over the valid factors of 0.5 rho, rho' J^T e, rho' J^T J
+// (varGradHess, Factor.h:419-466); updateBackups: backups[q] = the factor's cost, -1 when it fails
+__device__ void refine_grad_hess(const Dev& d, const int32_t* obs, int64_t n, double* bk, v3 X, bool update,
+                                 double& cost, double g[3], double H[6]) {
+  const int lane = threadIdx.x & 63;
+  double c = 0, g0 = 0, g1 = 0, g2 = 0, h00 = 0, h10 = 0, h20 = 0, h11 = 0, h21 = 0, h22 = 0;
+  for (int64_t q = lane; q < n; q += 64) {
+    VisOut v;
+    v.Jintr = nullptr;
+    if (!refine_eval<true>(d, obs[q], X, v)) {
+      if (update) bk[q] = -1.0;
+      continue;
+    }
+    const double s = v.e[0] * v.e[0] + v.e[1] * v.e[1];
+    double rho, drho;
+    huber_jet2(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s, rho, drho);
+    c += 0.5 * rho;
+    if (update) bk[q] = 0.5 * rho;
+    const double a0 = drho * v.Jpt[0], a1 = drho * v.Jpt[1], a2 = drho * v.Jpt[2];
+    const double b0 = drho * v.Jpt[3], b1 = drho * v.Jpt[4], b2 = drho * v.Jpt[5];
+    g0 += v.e[0] * a0 + v.e[1] * b0, g1 += v.e[0] * a1 + v.e[1] * b1, g2 += v.e[0] * a2 + v.e[1] * b2;
+    h00 += a0 * v.Jpt[0] + b0 * v.Jpt[3], h10 += a1 * v.Jpt[0] + b1 * v.Jpt[3], h20 += a2 * v.Jpt[0] + b2 * v.Jpt[3];
+    h11 += a1 * v.Jpt[1] + b1 * v.Jpt[4], h21 += a2 * v.Jpt[1] + b2 * v.Jpt[4], h22 += a2 * v.Jpt[2] + b2 * v.Jpt[5];
+  }
+  cost = refine_wave_sum(c);
+  g[0] = refine_wave_sum(g0), g[1] = refine_wave_sum(g1), g[2] = refine_wave_sum(g2);
+  H[0] = refine_wave_sum(h00), H[1] = refine_wave_sum(h10), H[2] = refine_wave_sum(h20);
+  H[3] = refine_wave_sum(h11), H[4] = refine_wave_sum(h21), H[5] = refine_wave_sum(h22);
+}
+
+// pointCost (PointRefinement.cpp:78-90): factors whose backup is negative are skipped, a failing one
+// counts its backup
+__device__ double refine_cost(const Dev& d, const int32_t* obs, int64_t n, const double* bk, v3 X) {
+  const int lane = threadIdx.x & 63;
+  double c = 0;
+  for (int64_t q = lane; q < n; q += 64) {
+    if (bk[q] < 0) continue;
+    VisOut v;
+    v.Jintr = nullptr;
+    if (!refine_eval<false>(d, obs[q], X, v)) {
+      c += bk[q];
+      continue;
+    }
+    const double s = v.e[0] * v.e[0] + v.e[1] * v.e[1];
+    c += 0.5 * huber_val(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s);
+  }
+  return refine_wave_sum(c);
+}
+
+// Eigen::LDLT<Matrix3d>::solve (LDLT.h: ldlt_inplace<Lower>::unblocked with diagonal pivoting, then
+// P^T L^-T D^-1 L^-1 P b); H lower triangle [00, 10, 20, 11, 21, 22].  As oracle ldlt3_solve.
+__device__ void refine_ldlt_solve(const double Hl[6], const double b[3], double x[3]) {
+  double m[3][3] = {{Hl[0], Hl[1], Hl[2]}, {Hl[1], Hl[3], Hl[4]}, {Hl[2], Hl[4], Hl[5]}};
+  int tr[3];
+  for (int k = 0; k < 3; k++) {
+    int big = k;
+    for (int i = k + 1; i < 3; i++)
+      if (fabs(m[i][i]) > fabs(m[big][big])) big = i;
+    tr[k] = big;
+    if (big != k) {
+      for (int j = 0; j < 3; j++) { const double t = m[k][j]; m[k][j] = m[big][j]; m[big][j] = t; }
+      for (int i = 0; i < 3; i++) { const double t = m[i][k]; m[i][k] = m[i][big]; m[i][big] = t; }
+    }
+    double tmp[3];
+    for (int j = 0; j < k; j++) tmp[j] = m[j][j] * m[k][j];
+    for (int j = 0; j < k; j++) m[k][k] -= m[k][j] * tmp[j];
+    for (int i = k + 1; i < 3; i++) {
+      for (int j = 0; j < k; j++) m[i][k] -= m[i][j] * tmp[j];
+      if (m[k][k] != 0.0) m[i][k] /= m[k][k];
+    }
+  }
+  for (int i = 0; i < 3; i++) x[i] = b[i];
+  for (int k = 0; k < 3; k++)
+    if (tr[k] != k) { const double t = x[k]; x[k] = x[tr[k]]; x[tr[k]] = t; }
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < i; j++) x[i] -= m[i][j] * x[j];
+  for (int i = 0; i < 3; i++) x[i] = fabs(m[i][i]) > 2.2250738585072014e-308 ? x[i] / m[i][i] : 0.0;
+  for (int i = 2; i >= 0; i--)
+    for (int j = i + 1; j < 3; j++) x[i] -= m[j][i] * x[j];
+  for (int k = 2; k >= 0; k--)
+    if (tr[k] != k) { const double t = x[k]; x[k] = x[tr[k]]; x[tr[k]] = t; }
+}
+
+__global__ void __launch_bounds__(256) refine_points_kernel(Dev d, const int64_t* gStart, const int32_t* gObs,
+                                                            const int32_t* gPt, int64_t nG, double* backups,
+                                                            double* acc) {
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= nG) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t q0 = gStart[g], n = gStart[g + 1] - q0;
+  const int32_t* obs = gObs + q0;
+  double* bk = backups + q0;
+  double* Xp = d.var[0] + (int64_t)gPt[g] * 3;
+  v3 X = mk(Xp[0], Xp[1], Xp[2]);
+  constexpr double kLambda = 1e-5, kCostTol = 1e-8, kStepTol = 1e-6, kMinImpr = 0.2, kStepRed = 0.3;
+  double startCost = 0, endCost = 0;
+  int nIts = 0;
+  for (int i = 0; i < 5; i++) {
+    double cost, gr[3], H[6];
+    refine_grad_hess(d, obs, n, bk, X, true, cost, gr, H);
+    if (i == 0) startCost = endCost = cost;
+    H[0] = H[0] * (1.0 + kLambda) + kLambda, H[3] = H[3] * (1.0 + kLambda) + kLambda;
+    H[5] = H[5] * (1.0 + kLambda) + kLambda;
+    double st[3];
+    refine_ldlt_solve(H, gr, st);
+    st[0] = -st[0], st[1] = -st[1], st[2] = -st[2];
+    const v3 Xb = X;
+    bool success = false;
+    X = mk(X.x + st[0], X.y + st[1], X.z + st[2]);
+    double newCost = refine_cost(d, obs, n, bk, X);
+    const double modelDelta = st[0] * gr[0] + st[1] * gr[1] + st[2] * gr[2];
+    if (-modelDelta < kCostTol) break;  // nothing to do (the step stays applied, as the reference)
+    if (newCost < cost + modelDelta * kMinImpr) {
+      success = true;
+    } else {  // reduced step
+      double nc, ng[3], nH[6];
+      refine_grad_hess(d, obs, n, bk, X, false, nc, ng, nH);
+      X = Xb;
+      const double newDelta = st[0] * ng[0] + st[1] * ng[1] + st[2] * ng[2];
+      const double f = newDelta > 0 ? -modelDelta / (newDelta - modelDelta) : kStepRed;
+      st[0] *= f, st[1] *= f, st[2] *= f;
+      X = mk(X.x + st[0], X.y + st[1], X.z + st[2]);
+      newCost = refine_cost(d, obs, n, bk, X);
+      if (newCost < cost + (st[0] * gr[0] + st[1] * gr[1] + st[2] * gr[2]) * kMinImpr) success = true;
+      else X = Xb;
+    }
+    if (success) {
+      nIts++;
+      endCost = newCost;
+    } else {
+      nIts = -1;
+      break;
+    }
+    if (st[0] * st[0] + st[1] * st[1] + st[2] * st[2] < kStepTol * kStepTol) break;
+  }
+  if (lane == 0) {
+    Xp[0] = X.x, Xp[1] = X.y, Xp[2] = X.z;
+    atomicAdd(acc + 0, startCost);
+    atomicAdd(acc + 1, endCost);
+    atomicAdd(acc + (nIts < 0 ? 2 : 3), nIts < 0 ? 1.0 : (double)nIts);
+    if (nIts > 0) atomicAdd(acc + 4, 1.0);
+  }
+}
+
+void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gObs, const int32_t* gPt, int64_t nG,
+                          double* backups, double* acc, hipStream_t st) {
+  if (nG > 0)
+    hipLaunchKernelGGL(refine_points_kernel, dim3((unsigned)((nG + 3) / 4)), dim3(256), 0, st, d, gStart, gObs, gPt, nG,
+                       backups, acc);
 }
 
 // ------------------------------------------------------------------ launch wrappers

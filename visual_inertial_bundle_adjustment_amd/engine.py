@@ -161,6 +161,14 @@ class CEngineBase:
         self._check(f(self.h, t, C.byref(n), s.ctypes.data_as(_dp), ip.ctypes.data_as(_dp)))
         return s, ip
 
+    def refine_points(self):
+        """refinePoints (PointRefinement.cpp:160-196): ((start cost, end cost), (failures, iterations,
+        points with >= 1 iteration))."""
+        c = (C.c_double * 2)()
+        st = (C.c_int64 * 3)()
+        self._check(self._fn("refine_points", [C.c_double * 2, C.c_int64 * 3])(self.h, c, st))
+        return (c[0], c[1]), tuple(st)
+
     def finalize(self):
         self._check(self._fn("finalize", [])(self.h))
 
