@@ -82,6 +82,32 @@ def cpu_baseline(full_kf: int, sample_kf: int = 1000):
             "ms_per_step": per_iter_full * 1e3}
 
 
+def mixed_vs_fp64(p, device, rs_device):
+    """Config E tolerance: one LM step (linearize, damp + factor + solve) from the same x0 on
+    the fp64 and the mixed-precision engines; ||delta_E - delta_C|| / ||delta_C|| over all variables, the
+    model cost reductions, and the costs after applying each step."""
+    import numpy as np
+    from visual_inertial_bundle_adjustment_amd import synth
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    out = {}
+    for prec in ("fp64", "mixed"):
+        e = HipEngine(imu_calib_options=p.imu_calib_options, device=device, precision=prec)
+        synth.load_into(e, p, rs_device=rs_device)
+        c0 = e.linearize(True, False)
+        mr = e.damp_factor_solve(1e-5)
+        step = np.concatenate([e.get_step(k).ravel() for k in range(8)])
+        e.backup()
+        e.apply_step(0)
+        c1, _ = e.cost(True)
+        out[prec] = (c0, mr, step, c1)
+        e.close()
+    (c0, mr, s64, c164), (_, mrm, smx, c1mx) = out["fp64"], out["mixed"]
+    return {"step_rel_l2": float(np.linalg.norm(smx - s64) / np.linalg.norm(s64)),
+            "step_rel_max": float(np.abs(smx - s64).max() / np.abs(s64).max()),
+            "model_reduction_rel": float(abs(mrm - mr) / abs(mr)),
+            "cost_after_step": {"fp64": c164, "mixed": c1mx}, "cost_before": c0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -90,6 +116,10 @@ def main():
     ap.add_argument("--config", default="C")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-family", type=int, default=KF_GEMM)
+    ap.add_argument("--precision", choices=("fp64", "mixed"), default="fp64",
+                    help="fp64 (the reference's arithmetic) or mixed (config E: fp32 Jacobian records and "
+                         "Schur-complement products, fp64 Cholesky); mixed also reports its first-step "
+                         "deviation from fp64")
     ap.add_argument("--refine", action="store_true",
                     help="run refinePoints before the LM loop, as ark_vi_ba (untimed; it changes the LM trajectory, "
                          "so the default times the loop from the generator's x0 like earlier rounds)")
@@ -112,7 +142,11 @@ def main():
     p = synth.generate(synth.config(args.config))
     log(f"[bench] config {args.config}: {p.summary()} (generated in {time.perf_counter() - t:.1f}s)")
     t = time.perf_counter()
-    e = HipEngine(imu_calib_options=p.imu_calib_options, device=local)
+    tolerance = None
+    if args.precision == "mixed":
+        tolerance = mixed_vs_fp64(p, local, args.rs_tables == "device")
+        log(f"[bench] mixed vs fp64, first LM step: {tolerance}")
+    e = HipEngine(imu_calib_options=p.imu_calib_options, device=local, precision=args.precision)
     synth.load_into(e, p, rs_device=args.rs_tables == "device")
     st = e.problem_stats()
     log(f"[bench] finalize {time.perf_counter() - t:.1f}s; reduced order {st[3]}, tiles {st[5]} "
@@ -176,15 +210,21 @@ def main():
         except Exception as ex:  # the baseline must never hide the GPU number
             log(f"[bench] cpu baseline failed: {ex}")
     ms = elapsed * 1e3 / max(1, iters)
+    if tolerance is not None:
+        out_extra = {"precision": "mixed (fp32 Jacobian records + Schur products, fp64 Cholesky)",
+                     "vs_fp64": tolerance}
+    else:
+        out_extra = {}
     out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
            "unit": "LM iterations/s", "n_gpus": 1, "steps": iters, "warmup": args.warmup,
            "ms_per_step": ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-           "dtype": "f64", "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
+           "dtype": "f64" if args.precision == "fp64" else "f32/f64",
+           "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
            "config": {"workload": f"config {args.config}: {st[0]} obs, {st[1]} landmarks, "
                                   f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",
                       "rigs": int(p.vars[1].shape[0]), "landmarks": int(st[1]), "observations": int(st[0]),
                       "parallelism": "single GPU"},
-           "roofline": roof, "cpu_baseline": cpu}
+           "roofline": roof, "cpu_baseline": cpu, **out_extra}
     print(json.dumps(out), flush=True)
 
 

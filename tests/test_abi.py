@@ -30,10 +30,11 @@ def test_header_declares_the_boundary():
         assert must in names
 
 
-def test_library_exports_every_declared_symbol():
-    lib = _lib.load_hip_lib()
+@pytest.mark.parametrize("mixed", [False, True])
+def test_library_exports_every_declared_symbol(mixed):
+    lib = _lib.load_hip_lib(mixed=mixed)
     missing = [n for n in declared_functions() if not hasattr(lib, n)]
-    assert not missing, f"libviba_hip.so does not export {missing}"
+    assert not missing, f"{'libviba_hip_mixed.so' if mixed else 'libviba_hip.so'} does not export {missing}"
 
 
 def test_library_is_gfx950_code_object():

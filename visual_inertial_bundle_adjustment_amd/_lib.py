@@ -6,10 +6,12 @@ import os
 
 LIB_DIR = os.environ.get("VIBA_LIB_DIR", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib"))
 HIP_LIB = os.path.join(LIB_DIR, "libviba_hip.so")
+HIP_LIB_MIXED = os.path.join(LIB_DIR, "libviba_hip_mixed.so")  # config E build (VIBA_MIXED=1)
 SYNTH_LIB = os.path.join(LIB_DIR, "libviba_synth.so")
 
 _synth = None
 _hip = None
+_hip_mixed = None
 
 
 class NativeLibraryMissing(RuntimeError):
@@ -55,9 +57,14 @@ def load_synth_lib() -> C.CDLL:
     return _synth
 
 
-def load_hip_lib() -> C.CDLL:
-    """Load the HIP product library. Raises NativeLibraryMissing when it was not built."""
-    global _hip
+def load_hip_lib(mixed: bool = False) -> C.CDLL:
+    """Load the HIP product library (fp64, or the config-E mixed-precision build). Raises
+    NativeLibraryMissing when it was not built."""
+    global _hip, _hip_mixed
+    if mixed:
+        if _hip_mixed is None:
+            _hip_mixed = _load(HIP_LIB_MIXED)
+        return _hip_mixed
     if _hip is None:
         _hip = _load(HIP_LIB)
     return _hip

@@ -1,6 +1,8 @@
 """In-tree build of the native libraries (no JIT, no cmake):
 
-    lib/libviba_hip.so    HIP kernels + C-ABI, gfx950 code objects (hipcc --offload-arch=gfx950)
+    lib/libviba_hip.so    HIP kernels + C-ABI, gfx950 code objects (hipcc --offload-arch=gfx950), fp64
+    lib/libviba_hip_mixed.so  the same with -DVIBA_MIXED=1 (config E: fp32 Jacobian records / Schur
+                          products, fp64 Cholesky; csrc/engine.hpp)
     lib/libviba_synth.so  synthetic problem generator (g++)
 """
 from __future__ import annotations
@@ -45,24 +47,28 @@ def build(force: bool = False, verbose: bool = False) -> list[str]:
     if force or not _newer(synth, [src] + headers):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", synth, src])
     out.append(synth)
-    # HIP library: compile objects in parallel, then link
-    objs = []
+    # HIP libraries (fp64, mixed): compile objects in parallel, then link
+    variants = [("libviba_hip.so", LIB, []), ("libviba_hip_mixed.so", os.path.join(LIB, "mixed"), ["-DVIBA_MIXED=1"])]
+    objs = {name: [] for name, _, _ in variants}
     jobs = []
-    with cf.ThreadPoolExecutor(max_workers=3) as ex:
-        for s in HIP_SOURCES:
-            sp = os.path.join(CSRC, s)
-            o = os.path.join(LIB, s.replace(".hip", ".o"))
-            objs.append(o)
-            if force or not _newer(o, [sp] + headers):
-                jobs.append(ex.submit(_run, [HIPCC, *HIP_FLAGS, "-c", sp, "-o", o]))
+    with cf.ThreadPoolExecutor(max_workers=int(os.environ.get("VIBA_BUILD_JOBS", "6"))) as ex:
+        for name, odir, defs in variants:
+            os.makedirs(odir, exist_ok=True)
+            for s in HIP_SOURCES:
+                sp = os.path.join(CSRC, s)
+                o = os.path.join(odir, s.replace(".hip", ".o"))
+                objs[name].append(o)
+                if force or not _newer(o, [sp] + headers):
+                    jobs.append(ex.submit(_run, [HIPCC, *HIP_FLAGS, *defs, "-c", sp, "-o", o]))
         for j in jobs:
             r = j.result()
             if verbose and r.stderr:
                 print(r.stderr)
-    hip = os.path.join(LIB, "libviba_hip.so")
-    if force or not _newer(hip, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", hip, *objs])
-    out.append(hip)
+    for name, _, _ in variants:
+        hip = os.path.join(LIB, name)
+        if force or not _newer(hip, objs[name]):
+            _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", hip, *objs[name]])
+        out.append(hip)
     return out
 
 

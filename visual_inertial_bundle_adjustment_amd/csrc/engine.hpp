@@ -17,6 +17,21 @@
 
 namespace viba {
 
+// Precision build ("fp32 Jacobian accumulate + fp64 Cholesky"): VIBA_MIXED=1
+// (libviba_hip_mixed.so) stores the whitened visual Jacobian records and the landmark Y panels in fp32
+// and forms the Hessian products of the Schur complement (observation-group Gram blocks, landmark tile
+// products) on fp32 MFMA (v_mfma_f32_16x16x4_f32, twice the fp64 MFMA rate); Jacobians are evaluated in
+// fp64 and rounded once, gradients / RHS, point blocks, the reduced system, its Cholesky and the solves
+// stay fp64.  VIBA_MIXED=0 (libviba_hip.so) is fp64 end to end, as the reference.
+#ifndef VIBA_MIXED
+#define VIBA_MIXED 0
+#endif
+#if VIBA_MIXED
+typedef float rec_t;
+#else
+typedef double rec_t;
+#endif
+
 // planes of the whitened visual Jacobian record
 constexpr int kJe = 0;      // e0, e1
 constexpr int kJpt = 2;     // 2x3 point, row-major
@@ -28,7 +43,8 @@ constexpr int kJPlanes = 72;
 constexpr int kJA = 32, kJB = 40;  // planes of region A / B
 // plane `plane` of observation o's record (Jt regions: A [nObsPad x kJA], then B [nObsPad x kJB]);
 // a slot's planes (slotPlane(s) .. + 2 * slotStride(s)) never straddle the regions
-__host__ __device__ inline const double* jt_plane(const double* Jt, int64_t nPad, int64_t o, int plane) {
+template <typename T>
+__host__ __device__ inline T* jt_plane(T* Jt, int64_t nPad, int64_t o, int plane) {
   return plane < kJA ? Jt + o * kJA + plane : Jt + nPad * kJA + o * kJB + (plane - kJA);
 }
 // slot order of an observation's reduced blocks
@@ -103,7 +119,7 @@ struct Dev {
   int32_t* obCol = nullptr;  // 4 per obs (column offset in the landmark's Y panel, -1)
   double* obC = nullptr;     // 6 per obs
   double* cache = nullptr;   // ResultCache per obs
-  double* Jt = nullptr;
+  rec_t* Jt = nullptr;  // whitened visual Jacobian records (fp32 in the VIBA_MIXED build)
   // landmarks
   int64_t nPts = 0;
   int64_t* lmObs = nullptr;   // nPts + 1
@@ -116,7 +132,8 @@ struct Dev {
   int32_t* pcBlk = nullptr;   // landmark block (into blkRed/blkCol) of every Y panel column
   int64_t* bxStart = nullptr; // per landmark block: its observation slots bxEnt[bxStart[b] ..)
   int32_t* bxEnt = nullptr;   // (obs << 2) | slot
-  double *Vchol = nullptr, *gp = nullptr, *z = nullptr, *xp = nullptr, *Y = nullptr;
+  double *Vchol = nullptr, *gp = nullptr, *z = nullptr, *xp = nullptr;
+  rec_t* Y = nullptr;  // landmark panels Y = L^-1 W (fp32 in the VIBA_MIXED build)
   double *gpNew = nullptr, *zNew = nullptr;
   int32_t* ptRed = nullptr;  // point param registered? (1/0) per point var handle
   int32_t* ptLm = nullptr;   // point var handle -> landmark index (-1)

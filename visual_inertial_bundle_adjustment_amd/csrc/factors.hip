@@ -197,6 +197,10 @@ __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se
 // ownership: 2.5x the algorithmic HBM traffic).  LDS record strides 33 / 41 doubles are odd, so the
 // per-lane ds_write_b64 of one plane hits 32 distinct banks.
 typedef double double2_t __attribute__((ext_vector_type(2)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
+// two adjacent record planes, rounded to the record type
+__device__ __forceinline__ void store_planes(double* p, double a, double b) { *(double2_t*)p = double2_t{a, b}; }
+__device__ __forceinline__ void store_planes(float* p, double a, double b) { *(float2_t*)p = float2_t{(float)a, (float)b}; }
 constexpr int kVisBlock = 128;  // two waves, 2 x 21 KB of staging
 
 __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int updateCache, int dontRetry, int64_t lo,
@@ -261,11 +265,11 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   {
-    double* dst = d.Jt + d.nObsPad * kJA + ob * kJB;
+    rec_t* dst = d.Jt + d.nObsPad * kJA + ob * kJB;
     for (int q = lane; q < nrec * (kJB / 2); q += 64) {
       const int r = q / (kJB / 2), c = 2 * (q % (kJB / 2));
       const double* src = S + r * (kJB + 1) + c;
-      *(double2_t*)(dst + r * kJB + c) = double2_t{src[0], src[1]};
+      store_planes(dst + r * kJB + c, src[0], src[1]);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -287,11 +291,11 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   {
-    double* dst = d.Jt + ob * kJA;
+    rec_t* dst = d.Jt + ob * kJA;
     for (int q = lane; q < nrec * (kJA / 2); q += 64) {
       const int r = q / (kJA / 2), c = 2 * (q % (kJA / 2));
       const double* src = S + r * (kJA + 1) + c;
-      *(double2_t*)(dst + r * kJA + c) = double2_t{src[0], src[1]};
+      store_planes(dst + r * kJA + c, src[0], src[1]);
     }
   }
   block_sum_atomic<1>(acc, d.red + 0);

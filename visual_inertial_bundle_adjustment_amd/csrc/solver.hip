@@ -21,9 +21,25 @@ using namespace dev;
 
 constexpr int TS = 64;  // tile size (rows/cols of a dense reduced-system tile)
 typedef double double4_t __attribute__((ext_vector_type(4)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ double4_t mfma64(double a, double b, double4_t c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+// Hessian products of the Schur complement (observation-group Gram blocks, landmark tile products) in
+// the record precision: fp64 MFMA, or v_mfma_f32_16x16x4_f32 in the VIBA_MIXED build.  The two differ
+// in their C/D map: f64 D row = (lane >> 4) + 4 r, f32 D row = 4 (lane >> 4) + r (column lane & 15 in
+// both; A/B maps identical), so accumulator register r of lane l sits at D row kAccL4 (l >> 4) + kAccR r.
+#if VIBA_MIXED
+typedef float4_t hacc4_t;
+__device__ __forceinline__ hacc4_t mfma_h(float a, float b, hacc4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+constexpr int kAccL4 = 4, kAccR = 1;
+#else
+typedef double4_t hacc4_t;
+__device__ __forceinline__ hacc4_t mfma_h(double a, double b, hacc4_t c) { return mfma64(a, b, c); }
+constexpr int kAccL4 = 1, kAccR = 4;
+#endif
 
 __device__ inline int rv_dim(const Dev& d, int r) { return d.rvDim[r]; }
 
@@ -45,11 +61,11 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
   const int lane = threadIdx.x & 63;
   const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= hi) return;
-  const double* Jt = d.Jt;
+  const rec_t* Jt = d.Jt;
   const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
   double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
   for (int64_t o = o0 + lane; o < o1; o += 64) {
-    const double* r = Jt + o * kJA;  // planes 0..7 live in region A
+    const rec_t* r = Jt + o * kJA;  // planes 0..7 live in region A
     const double e0 = r[kJe], e1 = r[kJe + 1];
     const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
     const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
@@ -85,7 +101,7 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
     d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
   }
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  double* Y = d.Y + d.lmY[l];
+  rec_t* Y = d.Y + d.lmY[l];
   for (int64_t c = lane; c < ncol; c += 64) {
     const int32_t b = d.pcBlk[cb + c];
     const int j = (int)(c - d.blkCol[b]);
@@ -94,8 +110,8 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
       const int32_t ent = d.bxEnt[e];
       const int s = ent & 3;
       const int64_t o = ent >> 2;
-      const double* r = Jt + o * kJA;
-      const double* x = jt_plane(Jt, d.nObsPad, o, slotPlane(s) + j);
+      const rec_t* r = Jt + o * kJA;
+      const rec_t* x = jt_plane(Jt, d.nObsPad, o, slotPlane(s) + j);
       const double x0 = x[0], x1 = x[slotStride(s)];
       w0 += r[kJpt + 0] * x0 + r[kJpt + 3] * x1;
       w1 += r[kJpt + 1] * x0 + r[kJpt + 4] * x1;
@@ -158,7 +174,8 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
 }
 
 struct SchurSlots {  // one thread's two fill slots of a batch, in registers
-  double yI[2][3], yJ[2][3], z[2];
+  rec_t yI[2][3], yJ[2][3];
+  double z[2];
   int rowI[2], rowJ[2], eb[2], c[2];
 };
 
@@ -178,13 +195,13 @@ __device__ __forceinline__ void schur_gather(const Dev& d, const TileEnt* ents, 
     if (c < en.nI) {
       const int64_t col = (int64_t)en.colI + c;
       S.rowI[k] = (int)(d.pcRow[col] - rI);
-      const double* y = d.Y + 3 * col;
+      const rec_t* y = d.Y + 3 * col;
       S.yI[k][0] = y[0], S.yI[k][1] = y[1], S.yI[k][2] = y[2];
     }
     if (!diag && c < en.nJ) {
       const int64_t col = (int64_t)en.colJ + c;
       S.rowJ[k] = (int)(d.pcRow[col] - rJ);
-      const double* y = d.Y + 3 * col;
+      const rec_t* y = d.Y + 3 * col;
       S.yJ[k][0] = y[0], S.yJ[k][1] = y[1], S.yJ[k][2] = y[2];
     }
 #endif
@@ -193,8 +210,8 @@ __device__ __forceinline__ void schur_gather(const Dev& d, const TileEnt* ents, 
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) schur_tile_kernel(Dev d, double lambda) {
-  __shared__ double Yi[kTK * TS];
-  __shared__ double Yj[kTK * TS];
+  __shared__ rec_t Yi[kTK * TS];
+  __shared__ rec_t Yj[kTK * TS];
   __shared__ double zb[kTK];
   __shared__ uint32_t msk[kTB];  // bits 0-3: row blocks of tile I, 4-7: of tile J
   __shared__ TileEnt ents[256];
@@ -210,13 +227,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   for (int i = tid; i < kTK * TS; i += 256) Yi[i] = 0.0, Yj[i] = 0.0;
   if (tid < kTK) zb[tid] = 0.0;
   __syncthreads();
-  double4_t acc[2][2];
+  hacc4_t acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
-    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
+    for (int b = 0; b < 2; b++) acc[a][b] = hacc4_t{0, 0, 0, 0};
   double racc = 0.0;
-  const double* yj = diag ? Yi : Yj;
+  const rec_t* yj = diag ? Yi : Yj;
   // row blocks this wave's quadrant reads: k-steps touching none of them are skipped whole; on a
   // diagonal tile the strictly upper block pairs are never formed (only the lower triangle is used)
   const uint32_t qmask = (3u << (4 + (pb >> 4))) | (3u << (qb >> 4));
@@ -257,7 +274,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
       const uint32_t m = msk[eb] & qmask;
       if (m == 0) continue;
       const int k0 = 4 * eb;
-      double av[2], bv[2];
+      rec_t av[2], bv[2];
 #pragma unroll
       for (int a = 0; a < 2; a++) av[a] = yj[(k0 + l4) * TS + ((pb + a * 16 + l15) ^ ((l4 & 1) << 4))];
 #pragma unroll
@@ -268,11 +285,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
         for (int bb = 0; bb < 2; bb++)
           if (VIBA_SCHUR_EXPT != 1 && ((m >> (4 + (pb >> 4) + a)) & (m >> ((qb >> 4) + bb)) & 1u) &&
               !(diag && (pb >> 4) + a > (qb >> 4) + bb))
-            acc[a][bb] = mfma64(av[a], bv[bb], acc[a][bb]);
+            acc[a][bb] = mfma_h(av[a], bv[bb], acc[a][bb]);
     }
     if (diag && tid < TS) {
 #pragma unroll 8
-      for (int k = 0; k < kTK; k++) racc += Yi[k * TS + (tid ^ ((k & 1) << 4))] * zb[k];
+      for (int k = 0; k < kTK; k++) racc += (double)Yi[k * TS + (tid ^ ((k & 1) << 4))] * zb[k];
     }
     __syncthreads();
 #pragma unroll
@@ -282,7 +299,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
     }
     __syncthreads();
   }
-  double* Cw = d.tiles + (int64_t)wk.tile * TS * TS + (pb + l4) * TS + qb + l15;
+  double* Cw = d.tiles + (int64_t)wk.tile * TS * TS + (pb + kAccL4 * l4) * TS + qb + l15;
   if (wk.kind) {
 #pragma unroll
     for (int a = 0; a < 2; a++)
@@ -290,7 +307,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
       for (int bb = 0; bb < 2; bb++)
 #pragma unroll
         for (int r = 0; r < 4; r++)
-          if (acc[a][bb][r] != 0.0) atomicAdd(Cw + (a * 16 + 4 * r) * TS + bb * 16, -acc[a][bb][r]);
+          if (acc[a][bb][r] != 0.0) atomicAdd(Cw + (a * 16 + kAccR * r) * TS + bb * 16, -(double)acc[a][bb][r]);
   } else {
     double v[2][2][4];
 #pragma unroll
@@ -298,13 +315,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
 #pragma unroll
       for (int bb = 0; bb < 2; bb++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) v[a][bb][r] = Cw[(a * 16 + 4 * r) * TS + bb * 16];
+        for (int r = 0; r < 4; r++) v[a][bb][r] = Cw[(a * 16 + kAccR * r) * TS + bb * 16];
 #pragma unroll
     for (int a = 0; a < 2; a++)
 #pragma unroll
       for (int bb = 0; bb < 2; bb++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + bb * 16] = v[a][bb][r] - acc[a][bb][r];
+        for (int r = 0; r < 4; r++) Cw[(a * 16 + kAccR * r) * TS + bb * 16] = v[a][bb][r] - (double)acc[a][bb][r];
   }
   if (diag && tid < TS) {
     const int64_t row = rI + tid;
@@ -436,7 +453,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
       if (!(m & bit)) continue;
       const int64_t col = (int64_t)ents[e].colI + __popcll(m & (bit - 1));
       const double* zz = d.z + 3 * (int64_t)ents[e].lm;
-      racc += d.Y[3 * col] * zz[0] + d.Y[3 * col + 1] * zz[1] + d.Y[3 * col + 2] * zz[2];
+      racc += (double)d.Y[3 * col] * zz[0] + (double)d.Y[3 * col + 1] * zz[1] + (double)d.Y[3 * col + 2] * zz[2];
     }
     const int64_t row = (int64_t)wk.I * TS + lane;
     if (row < d.nRed && racc != 0.0) atomicAdd(d.rhs + row, -racc);
@@ -473,23 +490,23 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
   const int64_t o0 = d.grpStart[g], n = d.grpStart[g + 1] - o0;
   const int r = l4 & 1;
   const int64_t nks = (n + 1) / 2;
-  double4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
+  hacc4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
   double g0 = 0.0, g1 = 0.0;
-  const double* Jt = d.Jt;
+  const rec_t* Jt = d.Jt;
   for (int64_t ks = wave; ks < nks; ks += 4) {
     const int64_t e = 2 * ks + (l4 >> 1);
-    double v0 = 0.0, v1 = 0.0, er = 0.0;
+    rec_t v0 = 0, v1 = 0, er = 0;
     if (e < n) {
       const int64_t o = d.grpObs[o0 + e];
       er = Jt[o * kJA + kJe + r];
       if (row0 >= 0) v0 = jt_plane(Jt, d.nObsPad, o, p0)[r * s0];
       if (row1 >= 0) v1 = jt_plane(Jt, d.nObsPad, o, p1)[r * s1];
     }
-    g0 += v0 * er, g1 += v1 * er;
+    g0 += (double)v0 * er, g1 += (double)v1 * er;
     if (mode == 0) {
-      a00 = mfma64(v0, v0, a00);
-      a10 = mfma64(v1, v0, a10);
-      a11 = mfma64(v1, v1, a11);
+      a00 = mfma_h(v0, v0, a00);
+      a10 = mfma_h(v1, v0, a10);
+      a11 = mfma_h(v1, v1, a11);
     }
   }
   // reduce the 4 waves (and, for g, the 4 lane groups) through LDS
@@ -522,7 +539,7 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
     const int rn = nb ? row1 : row0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      const int m = l4 + 4 * k;
+      const int m = kAccL4 * l4 + kAccR * k;
       const int rm = __shfl(mb ? row1 : row0, m, 64);
       double v = t[4 * blk + k];
       if (rm < 0 || rn < 0 || v == 0.0) continue;
@@ -563,18 +580,19 @@ __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
       const int64_t o = d.oxObs[idx];
       if (!shard_obs(d, o)) continue;
       const int s1 = d.oxSlot[idx];
-      const double* ea = d.Jt + o * kJA;
-      const double* x = jt_plane(d.Jt, d.nObsPad, o, slotPlane(s1));
+      const rec_t* ea = d.Jt + o * kJA;
+      const rec_t* x = jt_plane(d.Jt, d.nObsPad, o, slotPlane(s1));
       const int st1 = slotStride(s1);
-      for (int j = 0; j < d1; j++) atomicAdd(&g[j], x[j] * ea[kJe] + x[st1 + j] * ea[kJe + 1]);
+      for (int j = 0; j < d1; j++) atomicAdd(&g[j], (double)x[j] * ea[kJe] + (double)x[st1 + j] * ea[kJe + 1]);
     }
   } else {
     for (int64_t idx = d.lxStart[X1] + tid; idx < d.lxStart[X1 + 1]; idx += blockDim.x) {
       const int64_t l = d.lxLm[idx];
       if (l < d.lmB || l >= d.lmE) continue;
-      const double* y1 = d.Y + d.lmY[l] + 3 * d.lxCol[idx];
+      const rec_t* y1 = d.Y + d.lmY[l] + 3 * d.lxCol[idx];
       const double z0 = d.zNew[l * 3], z1 = d.zNew[l * 3 + 1], z2 = d.zNew[l * 3 + 2];
-      for (int j = 0; j < d1; j++) atomicAdd(&g[j], y1[3 * j] * z0 + y1[3 * j + 1] * z1 + y1[3 * j + 2] * z2);
+      for (int j = 0; j < d1; j++)
+        atomicAdd(&g[j], (double)y1[3 * j] * z0 + (double)y1[3 * j + 1] * z1 + (double)y1[3 * j + 2] * z2);
     }
   }
   __syncthreads();
@@ -1224,7 +1242,7 @@ __global__ void __launch_bounds__(256) backsub_kernel(Dev d, int mode, int64_t l
   const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= hi) return;
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  const double* Y = d.Y + d.lmY[l];
+  const rec_t* Y = d.Y + d.lmY[l];
   double t0 = 0, t1 = 0, t2 = 0;
   for (int64_t c = lane; c < ncol; c += 64) {
     const double v = xr[d.pcRow[cb + c]];

@@ -438,7 +438,7 @@ def run_sharded(args, rank: int, world: int, local: int):
     # default: partitioned factorization (world a power of two); VIBA_MULTI=shard selects landmark
     # shards with the whole reduced system factored on rank 0
     mode = os.environ.get("VIBA_MULTI", "partition" if world & (world - 1) == 0 else "shard")
-    e = HipEngine(imu_calib_options=p.imu_calib_options, device=local)
+    e = HipEngine(imu_calib_options=p.imu_calib_options, device=local, precision=getattr(args, "precision", "fp64"))
     if mode == "partition":
         e.set_partition(rank, world)
     else:
@@ -483,7 +483,7 @@ def run_sharded(args, rank: int, world: int, local: int):
         out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
                "unit": "LM iterations/s", "n_gpus": world, "steps": iters, "warmup": args.warmup,
                "ms_per_step": elapsed * 1e3 / max(1, iters), "higher_is_better": True, "scaling": "strong",
-               "vs_baseline": None, "dtype": "f64",
+               "vs_baseline": None, "dtype": "f64" if getattr(args, "precision", "fp64") == "fp64" else "f32/f64",
                "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
                "config": {"workload": f"config {args.config}: {st[0]} obs, {p.num_points} landmarks, "
                                       f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",

@@ -289,9 +289,14 @@ class HipEngine(CEngineBase):
                     ("tile", C.c_int32), ("reserved", C.c_int32)]
 
     def __init__(self, reproj_loss=(1.0, 3.0), imu_loss=(math.inf, math.inf), imu_calib_options=0xFF,
-                 device=0, tile=0):
+                 device=0, tile=0, precision="fp64"):
+        """precision: "fp64" (the reference's arithmetic) or "mixed" (SURVEY config E: fp32 Jacobian
+        records and Schur-complement products, fp64 Cholesky; libviba_hip_mixed.so)."""
         from ._lib import load_hip_lib
-        lib = load_hip_lib()
+        if precision not in ("fp64", "mixed"):
+            raise ValueError(f"precision must be 'fp64' or 'mixed', not {precision!r}")
+        self.precision = precision
+        lib = load_hip_lib(mixed=precision == "mixed")
         cfg = HipEngine.Config()
         lib.vb_default_config.argtypes = [P]
         lib.vb_default_config(C.byref(cfg))
