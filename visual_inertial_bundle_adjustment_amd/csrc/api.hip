@@ -896,6 +896,64 @@ int doFinalize(vb_handle h) {
           }
       }
     }
+    if (getenv("VIBA_SCHUR_STATS")) {  // analysis aid: MFMA counts of Schur tile-product schemes
+      auto blocks16 = [](uint64_t m) { int n = 0; for (int b = 0; b < 4; b++) n += ((m >> (16 * b)) & 0xffff) ? 1 : 0; return n; };
+      double cur = 0, grp = 0, dense = 0, useful = 0, grpTile = 0;
+      int64_t gsz[6] = {0, 0, 0, 0, 0, 0};
+      int64_t nGrp = 0;
+      for (int64_t t = 0; t < nTiles; t++) {
+        std::vector<std::pair<std::pair<uint64_t, uint64_t>, int>> sig;
+        for (int64_t e = tcnt[t]; e < tcnt[t + 1]; e++) {
+          const TileEnt& en = ents[e];
+          cur += (double)blocks16(en.maskI) * blocks16(en.maskJ);
+          useful += 3.0 * en.nI * en.nJ / 1024.0;
+          sig.push_back({{en.maskI, en.maskJ}, 1});
+        }
+        std::sort(sig.begin(), sig.end());
+        for (size_t i = 0; i < sig.size();) {
+          size_t j = i;
+          while (j < sig.size() && sig[j].first == sig[i].first) j++;
+          const int nI = __builtin_popcountll(sig[i].first.first), nJ = __builtin_popcountll(sig[i].first.second);
+          grp += std::ceil(3.0 * (j - i) / 4.0) * std::ceil(nI / 16.0) * std::ceil(nJ / 16.0);
+          grpTile += std::ceil(3.0 * (j - i) / 4.0) * blocks16(sig[i].first.first) * blocks16(sig[i].first.second);
+          gsz[std::min<size_t>(5, j - i <= 1 ? 0 : j - i <= 3 ? 1 : j - i <= 7 ? 2 : j - i <= 15 ? 3 : j - i <= 63 ? 4 : 5)] += j - i;
+          nGrp++;
+          i = j;
+        }
+        // dense K (3 rows per landmark, batches of 10 landmarks = 8 k-steps) in tile coordinates with
+        // the k-step's union mask, entries sorted by mask
+        {
+          std::vector<std::pair<uint64_t, uint64_t>> ms;
+          for (int64_t e = tcnt[t]; e < tcnt[t + 1]; e++) ms.push_back({ents[e].maskI, ents[e].maskJ});
+          std::sort(ms.begin(), ms.end());
+          for (size_t b0 = 0; b0 < ms.size(); b0 += 10)
+            for (int k = 0; k < 8; k++) {
+              uint64_t mi = 0, mj = 0;
+              for (int r = 4 * k; r < 4 * k + 4 && r < 30; r++) {
+                const size_t e = b0 + r / 3;
+                if (e < ms.size()) mi |= ms[e].first, mj |= ms[e].second;
+              }
+              dense += (double)blocks16(mi) * blocks16(mj);
+            }
+          std::vector<int> hist(8, 0);
+        }
+      }
+      fprintf(stderr, "[schur stats] entries %zu, MFMA-equivalents (16x16x4): current %.3g, dense-K union %.3g, "
+              "identical-mask groups %.3g in %lld groups (%.1f entries/group), useful %.3g\n",
+              ents.size(), cur, dense, grp, (long long)nGrp, (double)ents.size() / std::max<int64_t>(1, nGrp), useful);
+      fprintf(stderr, "[schur stats] identical-mask groups in tile coordinates (dense K) %.3g; entries in groups of "
+              "1 / 2-3 / 4-7 / 8-15 / 16-63 / 64+: %lld %lld %lld %lld %lld %lld\n", grpTile, (long long)gsz[0],
+              (long long)gsz[1], (long long)gsz[2], (long long)gsz[3], (long long)gsz[4], (long long)gsz[5]);
+    }
+    // compact Schur kinds: entries of a tile in runs of identical (maskI, maskJ) (solver.hip
+    // schur_run2_kernel / schur_run_kernel), by landmark within a run
+    if (schur_kind() == 0 || schur_kind() == 3)
+    for (int64_t t = 0; t < nTiles; t++)
+      std::sort(ents.begin() + tcnt[t], ents.begin() + tcnt[t + 1], [](const TileEnt& a, const TileEnt& b) {
+        if (a.maskI != b.maskI) return a.maskI < b.maskI;
+        if (a.maskJ != b.maskJ) return a.maskJ < b.maskJ;
+        return a.lm < b.lm;
+      });
     // observation groups: this shard's observations by their 4 reduced blocks (rig, camera)
     std::vector<int32_t> gobs;
     for (int64_t o = 0; o < nObs; o++)
@@ -934,48 +992,25 @@ int doFinalize(vb_handle h) {
     std::vector<int32_t> tobs;
     // work items: a tile's landmark entries in near-equal chunks of at most kChunkLm; `kind` = 1 when
     // the tile is split over several items (fp64 atomics), else the item owns the tile (plain RMW).
-    // With a landmark band B (VIBA_SCHUR_BAND), a tile's entries are also cut at multiples of B
-    // landmarks and the items are ordered by (band, tile): the items of one band run back to back on
-    // one XCD (xcd_block hands each XCD a contiguous item range), so the band's Y columns are
-    // gathered from L2 instead of being re-fetched once per tile pair.
-    int64_t kChunkLm = 256, band = 0;
+    // Items run in tile-column order (xcd_block hands each XCD a contiguous range of them).
+    int64_t kChunkLm = 256;
     if (const char* e = getenv("VIBA_SCHUR_CHUNK")) kChunkLm = std::max<int64_t>(8, std::min<int64_t>(256, atoll(e)));
-    if (const char* e = getenv("VIBA_SCHUR_BAND")) band = std::max<int64_t>(0, atoll(e));
-    std::vector<int64_t> itemBand;
     std::vector<int32_t> itemsPerTile(nTiles, 0);
     for (int32_t J = 0; J < nT; J++)
       for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
         const int32_t ti = h->colTilesH[c];
-        int64_t e0 = tcnt[ti];
-        const int64_t eEnd = tcnt[ti + 1];
-        while (e0 < eEnd) {  // one band segment [e0, e1)
-          int64_t e1 = eEnd;
-          const int64_t bnd = band > 0 ? ents[e0].lm / band : 0;
-          if (band > 0)
-            while (e1 > e0 && (int64_t)ents[e1 - 1].lm / band != bnd) e1--;  // entries sorted by landmark
-          const int64_t n = e1 - e0, nch = (n + kChunkLm - 1) / kChunkLm;
-          for (int64_t k = 0; k < nch; k++) {
-            TileWork w{};
-            const int64_t s0 = n * k / nch, s1 = n * (k + 1) / nch;
-            w.tile = ti, w.I = h->colRowsH[c], w.J = J, w.count = (int32_t)(s1 - s0);
-            w.start = e0 + s0, w.kind = 0;
-            works.push_back(w);
-            itemBand.push_back(bnd);
-            itemsPerTile[ti]++;
-            tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti), touched[ti] = 1;
-          }
-          e0 = e1;
+        const int64_t e0 = tcnt[ti], n = tcnt[ti + 1] - e0, nch = (n + kChunkLm - 1) / kChunkLm;
+        for (int64_t k = 0; k < nch; k++) {
+          TileWork w{};
+          const int64_t s0 = n * k / nch, s1 = n * (k + 1) / nch;
+          w.tile = ti, w.I = h->colRowsH[c], w.J = J, w.count = (int32_t)(s1 - s0);
+          w.start = e0 + s0, w.kind = 0;
+          works.push_back(w);
+          itemsPerTile[ti]++;
+          tlo = std::min<int64_t>(tlo, ti), thi = std::max<int64_t>(thi, ti), touched[ti] = 1;
         }
       }
     for (TileWork& w : works) w.kind = itemsPerTile[w.tile] > 1 ? 1 : 0;
-    if (band > 0) {
-      std::vector<size_t> ord(works.size());
-      for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
-      std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return itemBand[a] < itemBand[b]; });
-      std::vector<TileWork> sorted(works.size());
-      for (size_t i = 0; i < ord.size(); i++) sorted[i] = works[ord[i]];
-      works.swap(sorted);
-    }
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
     d.nTileWorks = (int64_t)works.size();
     h->nTileEnt = (int64_t)ents.size(), h->nObEnt = d.nGroups;

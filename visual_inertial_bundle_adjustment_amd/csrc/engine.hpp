@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstddef>
+#include <cstdlib>
 
 namespace viba {
 
@@ -203,6 +204,13 @@ struct Dev {
   LossParams reproj, imu;
   ImuIdx jac;
 };
+
+// Schur tile-product kernel (solver.hip launch_schur; the compact kinds 0 and 3 need the tile entries
+// sorted into runs of identical row masks, which api.hip does at finalize)
+inline int schur_kind() {
+  static const int k = getenv("VIBA_SCHUR") ? atoi(getenv("VIBA_SCHUR")) : 0;
+  return k;
+}
 
 // partitioned factorization: does this handle assemble into tile column `col`?
 __device__ __forceinline__ bool owns_col(const Dev& d, int64_t col) {

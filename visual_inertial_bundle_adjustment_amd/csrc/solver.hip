@@ -460,6 +460,336 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) s
   }
 }
 
+// Schur assembly by target tile, compact form with LDS images (VIBA_SCHUR=3; measured slower, kept for the record:
+// 8.5 ms against 7.1 for schur_tile_kernel on config C -- the compact products of most runs fit one
+// wave's 32 x 32 quadrant, so three of the four waves idle at every batch barrier while the gathers
+// per batch stay the same).  api.hip sorts every tile's landmark entries
+// by their (row mask in tile I, row mask in tile J), so a work item is a sequence of RUNS of landmarks
+// that touch exactly the same tile rows.  Within a run the product is formed in compact coordinates:
+// the c-th panel column of a landmark inside tile I is compact column c (its rows ascend with its
+// columns), so the LDS images hold Y^T densely (K row 3 e + coordinate for landmark e, column c) and
+// the 4 waves' 32 x 32 quadrants of the compact nJ x nI product need only ceil(nJ / 16) x ceil(nI / 16)
+// blocks of v_mfma_f64_16x16x4_f64 per 4 K rows (3 rows per landmark, no padding row).  At the end of a
+// run every lane adds its accumulators into the item's tile accumulator in LDS through the run's
+// compact -> tile row maps (posI / posJ: the rank-th set bit of the mask), distinct positions within a
+// run, so plain LDS read-modify-writes.  Config C: 34M MFMAs instead of the 70M of the tile-coordinate
+// form (16-row masks, one padded k-step per landmark; VIBA_SCHUR_STATS=1 prints the counts).  Batches
+// of up to 10 landmarks (30 of the 32 K rows) never cross a run; rows beyond the batch are zeroed at
+// the operand read, and stale image columns beyond nI / nJ only feed products that are not scattered,
+// so the images are never cleared.  The next batch's gathers are issued into registers before the
+// current batch's MFMAs.  Diagonal tiles: lower compact block pairs only, and rhs -= Y^T z per tile row.
+constexpr int kRB = 10;  // landmarks per batch (30 of kTK = 32 K rows)
+
+struct RunSlots {  // one thread's three fill slots of a batch
+  rec_t yI[3][3], yJ[3][3];
+  double z[3];
+  bool vI[3], vJ[3];
+};
+
+__device__ __forceinline__ void run_gather(const Dev& d, const TileEnt* ents, int b0, int nb, bool diag, int tid,
+                                           RunSlots& S) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int sl = tid + 256 * k, eb = sl >> 6, c = sl & 63;
+    S.vI[k] = S.vJ[k] = false;
+    if (eb >= nb) continue;
+    const TileEnt& en = ents[b0 + eb];
+    if (c < en.nI) {
+      const rec_t* y = d.Y + 3 * ((int64_t)en.colI + c);
+      S.yI[k][0] = y[0], S.yI[k][1] = y[1], S.yI[k][2] = y[2], S.vI[k] = true;
+    }
+    if (!diag && c < en.nJ) {
+      const rec_t* y = d.Y + 3 * ((int64_t)en.colJ + c);
+      S.yJ[k][0] = y[0], S.yJ[k][1] = y[1], S.yJ[k][2] = y[2], S.vJ[k] = true;
+    }
+    if (diag && c < 3) S.z[k] = d.z[3 * (int64_t)en.lm + c];
+  }
+}
+
+__global__ void __launch_bounds__(256) schur_run_kernel(Dev d, double lambda) {
+  __shared__ rec_t Yi[kTK * TS];
+  __shared__ rec_t Yj[kTK * TS];
+  __shared__ double C[TS * TS];  // the item's tile accumulator (column-major like the tile store)
+  __shared__ TileEnt ents[256];
+  __shared__ int16_t runStart[258];
+  __shared__ uint8_t pos[2][2][TS];  // [run parity][I / J][compact index] -> tile row
+  __shared__ double zb[kTK];
+  __shared__ double rq[TS];
+  __shared__ int nRunsS;
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
+  const TileWork wk = d.tileWorks[w];
+  const bool diag = wk.I == wk.J;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  const int cnt = wk.count;
+  if (tid < cnt) ents[tid] = d.tileEnts[wk.start + tid];
+  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
+  if (tid < TS) rq[tid] = 0.0;
+  __syncthreads();
+  if (wave == 0) {  // run starts, in entry order
+    int n = 0;
+    for (int e0 = 0; e0 < cnt; e0 += 64) {
+      const int e = e0 + lane;
+      const bool st = e < cnt && (e == 0 || ents[e].maskI != ents[e - 1].maskI || ents[e].maskJ != ents[e - 1].maskJ);
+      const uint64_t b = __ballot(st);
+      if (st) runStart[n + __popcll(b & ((1ull << lane) - 1))] = (int16_t)e;
+      n += __popcll(b);
+    }
+    if (lane == 0) runStart[n] = (int16_t)cnt, nRunsS = n;
+  }
+  __syncthreads();
+  const int nRuns = nRunsS;
+  hacc4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) acc[a][b] = hacc4_t{0, 0, 0, 0};
+  double racc = 0.0;  // diagonal tiles, wave 0: lane = compact column of the run
+  const rec_t* yj = diag ? Yi : Yj;
+  RunSlots S;
+  int r = 0, b0 = 0;
+  if (nRuns > 0) run_gather(d, ents, 0, min(kRB, runStart[1] - 0), diag, tid, S);
+  while (r < nRuns) {
+    const int e1 = runStart[r + 1];
+    const int nb = min(kRB, e1 - b0);
+    const uint64_t mI = ents[b0].maskI, mJ = diag ? mI : ents[b0].maskJ;
+    const int nI = __popcll(mI), nJ = __popcll(mJ);
+    const int par = r & 1;
+    if (b0 == runStart[r]) {  // first batch of the run: its compact -> tile row maps
+      if (wave == 0 && ((mI >> lane) & 1)) pos[par][0][__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
+      if (wave == 1 && ((mJ >> lane) & 1)) pos[par][1][__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
+    }
+    // fill the images: landmark eb of the batch owns K rows 3 eb .. 3 eb + 2 (odd rows XOR 16)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int sl = tid + 256 * k, eb = sl >> 6, c = sl & 63;
+      if (S.vI[k]) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) Yi[(3 * eb + q) * TS + (c ^ (((3 * eb + q) & 1) << 4))] = S.yI[k][q];
+      }
+      if (S.vJ[k]) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) Yj[(3 * eb + q) * TS + (c ^ (((3 * eb + q) & 1) << 4))] = S.yJ[k][q];
+      }
+      if (diag && c < 3 && eb < nb) zb[3 * eb + c] = S.z[k];
+    }
+    __syncthreads();
+    // next batch's gathers in flight during this batch's products
+    int rn = r, bn = b0 + nb;
+    if (bn >= e1) rn = r + 1, bn = e1;
+    if (rn < nRuns) run_gather(d, ents, bn, min(kRB, runStart[rn + 1] - bn), diag, tid, S);
+    const int rows = 3 * nb, nks = (rows + 3) / 4;
+    // compact blocks of this wave's quadrant: J side rows pb + 16 a < nJ, I side cols qb + 16 b < nI
+    const bool actA0 = pb < nJ, actA1 = pb + 16 < nJ, actB0 = qb < nI, actB1 = qb + 16 < nI;
+    const bool w00 = actA0 && actB0 && !(diag && (pb >> 4) > (qb >> 4));
+    const bool w01 = actA0 && actB1 && !(diag && (pb >> 4) > (qb >> 4) + 1);
+    const bool w10 = actA1 && actB0 && !(diag && (pb >> 4) + 1 > (qb >> 4));
+    const bool w11 = actA1 && actB1 && !(diag && (pb >> 4) + 1 > (qb >> 4) + 1);
+    if (w00 || w01 || w10 || w11) {
+      for (int ks = 0; ks < nks; ks++) {
+        const int kr = 4 * ks + l4;
+        const bool kv = kr < rows;
+        const int sw = (kr & 1) << 4;
+        rec_t av[2], bv[2];
+#pragma unroll
+        for (int a = 0; a < 2; a++) av[a] = kv ? yj[kr * TS + ((pb + a * 16 + l15) ^ sw)] : (rec_t)0;
+#pragma unroll
+        for (int b = 0; b < 2; b++) bv[b] = kv ? Yi[kr * TS + ((qb + b * 16 + l15) ^ sw)] : (rec_t)0;
+        if (w00) acc[0][0] = mfma_h(av[0], bv[0], acc[0][0]);
+        if (w01) acc[0][1] = mfma_h(av[0], bv[1], acc[0][1]);
+        if (w10) acc[1][0] = mfma_h(av[1], bv[0], acc[1][0]);
+        if (w11) acc[1][1] = mfma_h(av[1], bv[1], acc[1][1]);
+      }
+    }
+    if (diag && wave == 0 && lane < nI) {
+      for (int k = 0; k < rows; k++) racc += (double)Yi[k * TS + (lane ^ ((k & 1) << 4))] * zb[k];
+    }
+    if (bn == e1 || rn != r) {
+      // end of the run: add the compact product into the tile accumulator
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 2; b++) {
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int m = pb + 16 * a + kAccL4 * l4 + kAccR * q, n = qb + 16 * b + l15;
+            if (m < nJ && n < nI) C[pos[par][1][m] * TS + pos[par][0][n]] -= (double)acc[a][b][q];
+          }
+          acc[a][b] = hacc4_t{0, 0, 0, 0};
+        }
+      if (diag && wave == 0 && lane < nI) rq[pos[par][0][lane]] -= racc;
+      racc = 0.0;
+    }
+    __syncthreads();  // the images are rewritten by the next batch
+    r = rn, b0 = bn;
+  }
+  // epilogue: the tile accumulator into the tile store
+  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
+  if (wk.kind) {
+    for (int i = tid; i < TS * TS; i += 256)
+      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else {
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
+  }
+  if (diag && tid < TS) {
+    const int64_t row = (int64_t)wk.I * TS + tid;
+    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
+  }
+}
+
+// Schur assembly by target tile, compact runs with register operands (default, VIBA_SCHUR=0).  Same
+// runs as schur_run_kernel, but no images and no barriers: a task is (run, chunk of <= kCh landmarks, compact
+// block row a of the J side); a wave takes every fourth task of its item and accumulates the nI-wide
+// block row over the chunk's dense K (3 rows per landmark), its operands gathered straight from the Y
+// panel (lane l: compact column 16 a + (l & 15) / 16 b + (l & 15), K row 4 ks + (l >> 4)), the next
+// k-step's loads issued before the current MFMAs.  At the end of the task the block row is added into
+// the item's LDS tile accumulator with LDS atomics (tasks of different waves overlap), through
+// wave-private compact -> tile row maps.
+#ifndef VIBA_SCHUR_CH
+#define VIBA_SCHUR_CH 16
+#endif
+#ifndef VIBA_SCHUR_TR
+#define VIBA_SCHUR_TR 2
+#endif
+#ifndef VIBA_SCHUR_GENTS
+#define VIBA_SCHUR_GENTS 0  // 1: read the entries from global memory (no LDS copy)
+#endif
+constexpr int kCh = VIBA_SCHUR_CH;  // landmarks per task
+constexpr int kTR = VIBA_SCHUR_TR;  // compact block rows per task (1 or 2)
+
+__global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
+  __shared__ double C[TS * TS];
+#if VIBA_SCHUR_GENTS
+  const TileEnt* ents = d.tileEnts + d.tileWorks[xcd_block(blockIdx.x, gridDim.x)].start;
+#else
+  __shared__ TileEnt ents[256];
+#endif
+  __shared__ int16_t runStart[258];
+  __shared__ uint8_t posW[4][2][TS];
+  __shared__ double rq[TS];
+  __shared__ int nRunsS;
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
+  const TileWork wk = d.tileWorks[w];
+  const bool diag = wk.I == wk.J;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int cnt = wk.count;
+#if !VIBA_SCHUR_GENTS
+  if (tid < cnt) ents[tid] = d.tileEnts[wk.start + tid];
+#endif
+  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
+  if (tid < TS) rq[tid] = 0.0;
+  __syncthreads();
+  if (wave == 0) {
+    int n = 0;
+    for (int e0 = 0; e0 < cnt; e0 += 64) {
+      const int e = e0 + lane;
+      const bool st = e < cnt && (e == 0 || ents[e].maskI != ents[e - 1].maskI || ents[e].maskJ != ents[e - 1].maskJ);
+      const uint64_t b = __ballot(st);
+      if (st) runStart[n + __popcll(b & ((1ull << lane) - 1))] = (int16_t)e;
+      n += __popcll(b);
+    }
+    if (lane == 0) runStart[n] = (int16_t)cnt, nRunsS = n;
+  }
+  __syncthreads();
+  const int nRuns = nRunsS;
+  uint8_t* posI = posW[wave][0];
+  uint8_t* posJ = posW[wave][1];
+  int task = 0;
+  for (int r = 0; r < nRuns; r++) {
+    const int e0 = runStart[r], e1 = runStart[r + 1];
+    const uint64_t mI = uniform64(ents[e0].maskI), mJ = diag ? mI : uniform64(ents[e0].maskJ);
+    const int nI = __popcll(mI), nJ = __popcll(mJ);
+    const int nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4, nbR = (nbJ + kTR - 1) / kTR;
+    const int nch = (e1 - e0 + kCh - 1) / kCh;
+    const int nTask = nch * nbR;
+    bool mapped = false;
+    for (int t = 0; t < nTask; t++, task++) {
+      if ((task & 3) != wave) continue;
+      if (!mapped) {  // the run's compact -> tile row maps (wave-private)
+        if ((mI >> lane) & 1) posI[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
+        if ((mJ >> lane) & 1) posJ[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        mapped = true;
+      }
+      const int ch = t / nbR, a0 = kTR * (t - ch * nbR);
+      const int c0 = e0 + ch * kCh, nl = min(kCh, e1 - c0), rows = 3 * nl, nks = (rows + 3) >> 2;
+      hacc4_t acc[kTR][4];
+#pragma unroll
+      for (int i = 0; i < kTR; i++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[i][b] = hacc4_t{0, 0, 0, 0};
+      auto ld = [&](int ks, rec_t (&av)[kTR], rec_t (&bv)[4]) {
+        const int kr = 4 * ks + l4;
+        const bool kv = kr < rows;
+        const int e = c0 + (kv ? kr / 3 : 0), q = kv ? kr - 3 * (kr / 3) : 0;
+        const TileEnt& en = ents[e];
+        const int64_t cJ = diag ? en.colI : en.colJ;
+#pragma unroll
+        for (int i = 0; i < kTR; i++) {
+          const int m = 16 * (a0 + i) + l15;
+          av[i] = (kv && m < nJ) ? d.Y[3 * (cJ + m) + q] : (rec_t)0;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int n = 16 * b + l15;
+          bv[b] = (kv && b < nbI && n < nI) ? d.Y[3 * ((int64_t)en.colI + n) + q] : (rec_t)0;
+        }
+      };
+      rec_t av[kTR], bv[4], av2[kTR], bv2[4];
+      ld(0, av, bv);
+      for (int ks = 0; ks < nks; ks++) {
+        if (ks + 1 < nks) ld(ks + 1, av2, bv2);
+#pragma unroll
+        for (int i = 0; i < kTR; i++)
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (a0 + i < nbJ && b < nbI && !(diag && a0 + i > b)) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
+#pragma unroll
+        for (int i = 0; i < kTR; i++) av[i] = av2[i];
+#pragma unroll
+        for (int b = 0; b < 4; b++) bv[b] = bv2[b];
+      }
+#pragma unroll
+      for (int i = 0; i < kTR; i++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          if (a0 + i >= nbJ || b >= nbI || (diag && a0 + i > b)) continue;
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q, n = 16 * b + l15;
+            if (m < nJ && n < nI) atomicAdd(&C[posJ[m] * TS + posI[n]], -(double)acc[i][b][q]);
+          }
+        }
+      if (diag && a0 == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
+        double racc = 0.0;
+        for (int e = c0; e < c0 + nl; e++) {
+          const rec_t* y = d.Y + 3 * ((int64_t)ents[e].colI + lane);
+          const double* zz = d.z + 3 * (int64_t)ents[e].lm;
+          racc += (double)y[0] * zz[0] + (double)y[1] * zz[1] + (double)y[2] * zz[2];
+        }
+        atomicAdd(&rq[posI[lane]], -racc);
+      }
+    }
+    if (mapped) __builtin_amdgcn_wave_barrier();  // the maps are rewritten by this wave's next run
+  }
+  __syncthreads();
+  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
+  if (wk.kind) {
+    for (int i = tid; i < TS * TS; i += 256)
+      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else {
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
+  }
+  if (diag && tid < TS) {
+    const int64_t row = (int64_t)wk.I * TS + tid;
+    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
+  }
+}
+
 // Direct visual terms by observation group (observations sharing their reduced blocks: one rig, one
 // camera).  Per group: H = sum_o J~_o^T J~_o over the 32 columns [pose 6 | extr 6 | intr <= 17 |
 // vel 3] and g = sum_o J~_o^T e~_o, on v_mfma_f64_16x16x4_f64 (K = the group's residual rows, 4 per
@@ -1389,10 +1719,15 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
   if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
-  static const int v2 = getenv("VIBA_SCHUR_V2") ? atoi(getenv("VIBA_SCHUR_V2")) : 0;
+  // VIBA_SCHUR (must match the setting api.hip built the entries under, schur_kind()):
+  //   0 compact runs, register operands (default)   1 tile-coordinate LDS images
+  //   2 tile-coordinate register operands            3 compact runs, LDS images
+  const int kind = schur_kind();
   if (d.nTileWorks) {
-    if (v2) launchK(schur_tile2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else launchK(schur_tile_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    if (kind == 1) launchK(schur_tile_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else if (kind == 2) launchK(schur_tile2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else if (kind == 3) launchK(schur_run_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
   }
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
