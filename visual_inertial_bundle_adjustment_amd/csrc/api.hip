@@ -768,6 +768,18 @@ int doFinalize(vb_handle h) {
   if (h->lmEnd < 0) h->lmBegin = 0, h->lmEnd = nPts;
   if (h->lmBegin < 0 || h->lmEnd > nPts || h->lmBegin > h->lmEnd) return fail(VB_E_ARG, "bad landmark shard range");
   d.lmB = h->lmBegin, d.lmE = h->lmEnd, d.root = h->isRoot ? 1 : 0;
+  {  // landmark lists by panel width (solver.hip landmark_obs_kernel)
+    std::vector<int32_t> small, big;
+    int64_t bigCols = 0;
+    for (int64_t l = h->lmBegin; l < h->lmEnd; l++) {
+      const int64_t nc = (lmY[l + 1] - lmY[l]) / 3;
+      if (nc <= kLmSmallCols) small.push_back((int32_t)l);
+      else big.push_back((int32_t)l), bigCols = std::max(bigCols, nc);
+    }
+    d.nLmSmall = (int64_t)small.size(), d.nLmBig = (int64_t)big.size(), d.lmBigCols = (int32_t)bigCols;
+    small.insert(small.end(), big.begin(), big.end());
+    if (upload(&d.lmList, small)) return VB_E_HIP;
+  }
   d.obB = lmObs[h->lmBegin], d.obE = lmObs[h->lmEnd], d.obFree = lmObs[nPts];
   // constant-point observations of this handle: [fB, fE) (the root's whole tail unless partitioned)
   d.fB = d.obFree, d.fE = h->isRoot ? nObs : d.obFree;
@@ -1498,7 +1510,7 @@ int vb_destroy(vb_handle h) {
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
-                  d.stepPt, d.subRed, d.subPt, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
+                  d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD};

@@ -33,6 +33,8 @@ typedef float rec_t;
 typedef double rec_t;
 #endif
 
+constexpr int kLmSmallCols = 256;  // landmark_obs_kernel's narrow class (Y panel columns)
+
 // planes of the whitened visual Jacobian record
 constexpr int kJe = 0;      // e0, e1
 constexpr int kJpt = 2;     // 2x3 point, row-major
@@ -195,6 +197,11 @@ struct Dev {
   // [obFree, nObs) on the root unless partitioned); the root also owns the reduced-variable step
   // ratios and, unless partitioned, every small factor
   int64_t lmB = 0, lmE = 0, obB = 0, obE = 0, obFree = 0, fB = 0, fE = 0;
+  // this handle's landmarks by Y panel width for landmark_obs_kernel: lmList[0, nLmSmall) have at
+  // most kLmSmallCols panel columns, lmList[nLmSmall, nLmSmall + nLmBig) at most lmBigCols
+  int32_t* lmList = nullptr;
+  int64_t nLmSmall = 0, nLmBig = 0;
+  int32_t lmBigCols = 0;
   int32_t root = 1;
   // partitioned factorization: owner of every tile column (world = ROOT, rank 0), this rank, world
   // (world <= 1: not partitioned, every column is this handle's)

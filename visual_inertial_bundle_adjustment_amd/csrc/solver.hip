@@ -57,10 +57,8 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
-__global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int mode, int64_t lo, int64_t hi) {
+__device__ __forceinline__ void landmark_eliminate(const Dev& d, double lambda, int mode, int64_t l) {
   const int lane = threadIdx.x & 63;
-  const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (l >= hi) return;
   const rec_t* Jt = d.Jt;
   const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
   double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
@@ -122,6 +120,179 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
     const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
     Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
   }
+}
+__global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int mode, int64_t lo, int64_t hi) {
+  const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (l >= hi) return;
+  landmark_eliminate(d, lambda, mode, l);
+}
+
+// Landmark elimination by observation (mode 0, default).  One wave per landmark; each half-wave takes
+// one of the landmark's observations at a time and its 32 lanes the observation's 32 slot columns
+// [pose 6 | extr 6 | intr 17 | vel 3] (record planes 8..71, read once and coalesced, with the point
+// Jacobian and residual of planes 0..7): the column's contribution Jp^T J_x(:, j) goes into the
+// landmark's W panel in LDS at panel column obCol + j with LDS atomics (both halves may hit a shared
+// calibration block), and lane 0 of the half accumulates V and g.  Then the damped 3 x 3 Cholesky,
+// z, and Y = L^-1 W over the panel columns.  No per-block observation lists: every record is read
+// once.  Two launches by panel width (api.hip lmList): landmarks with up to kLmSmallCols columns one
+// per wave with a 24 KB workgroup (6 per CU); the wider ones (long tracks) one per workgroup,
+// landmark_obs_wg_kernel, whose panel is per workgroup.  Measured on config C: 1.04 + 0.72 ms against
+// 2.63 for the per-column landmark_kernel; one 48 KB per-wave class for all ran at 2.9 ms and the
+// per-workgroup kernel for all at 2.1 (occupancy vs. barriers).
+constexpr int kLmBigCols = 2048;  // 3 x 2048 doubles = 48 KB of dynamic LDS per workgroup; wider: per-column path
+
+__global__ void __launch_bounds__(256) landmark_obs_kernel(Dev d, double lambda, int64_t first, int64_t n, int cap) {
+  extern __shared__ double Wl[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t li = (int64_t)blockIdx.x * 4 + wave;
+  if (li >= n) return;
+  const int64_t l = d.lmList[first + li];
+  const rec_t* Jt = d.Jt;
+  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
+  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
+  double* W = Wl + wave * 3 * cap;  // cap: panel columns per wave of this launch
+  for (int i = lane; i < 3 * ncol; i += 64) W[i] = 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int h = lane >> 5, jj = lane & 31;
+  const int s = jj < 6 ? 0 : jj < 12 ? 1 : jj < 29 ? 2 : 3;
+  const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
+  const int pl = slotPlane(s) + j, st = slotStride(s);
+  double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  for (int64_t o = o0 + h; o < o1; o += 2) {
+    const rec_t* r = Jt + o * kJA;
+    const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
+    const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
+    const rec_t* x = jt_plane(Jt, d.nObsPad, o, pl);
+    const double x0 = x[0], x1 = x[st];
+    const int32_t X = d.obRed[o * 4 + s];
+    if (jj == 0) {
+      const double e0 = r[kJe], e1 = r[kJe + 1];
+      g0 += a0 * e0 + b0 * e1, g1 += a1 * e0 + b1 * e1, g2 += a2 * e0 + b2 * e1;
+      v00 += a0 * a0 + b0 * b0, v10 += a1 * a0 + b1 * b0, v20 += a2 * a0 + b2 * b0;
+      v11 += a1 * a1 + b1 * b1, v21 += a2 * a1 + b2 * b1, v22 += a2 * a2 + b2 * b2;
+    }
+    if (X >= 0 && j < d.rvDim[X]) {
+      const int c = d.obCol[o * 4 + s] + j;
+      atomicAdd(&W[3 * c + 0], a0 * x0 + b0 * x1);
+      atomicAdd(&W[3 * c + 1], a1 * x0 + b1 * x1);
+      atomicAdd(&W[3 * c + 2], a2 * x0 + b2 * x1);
+    }
+  }
+  g0 = wave_sum(g0), g1 = wave_sum(g1), g2 = wave_sum(g2);
+  v00 = wave_sum(v00), v10 = wave_sum(v10), v20 = wave_sum(v20);
+  v11 = wave_sum(v11), v21 = wave_sum(v21), v22 = wave_sum(v22);
+  v00 = v00 * (1.0 + lambda) + lambda;
+  v11 = v11 * (1.0 + lambda) + lambda;
+  v22 = v22 * (1.0 + lambda) + lambda;
+  const double l00 = sqrt(v00);
+  const double l10 = v10 / l00, l20 = v20 / l00;
+  const double d11 = v11 - l10 * l10;
+  const double l11 = sqrt(d11);
+  const double l21 = (v21 - l20 * l10) / l11;
+  const double d22 = v22 - l20 * l20 - l21 * l21;
+  const double l22 = sqrt(d22);
+  if (lane == 0) {
+    if (!(v00 > 0) || !(d11 > 0) || !(d22 > 0)) atomicOr(d.err, 2);
+    double* L = d.Vchol + l * 6;
+    L[0] = l00, L[1] = l10, L[2] = l20, L[3] = l11, L[4] = l21, L[5] = l22;
+    const double z0 = g0 / l00, z1 = (g1 - l10 * z0) / l11, z2 = (g2 - l20 * z0 - l21 * z1) / l22;
+    d.z[l * 3] = z0, d.z[l * 3 + 1] = z1, d.z[l * 3 + 2] = z2;
+    d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  rec_t* Y = d.Y + d.lmY[l];
+  for (int64_t c = lane; c < ncol; c += 64) {
+    const double y0 = W[3 * c] / l00;
+    const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
+    const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
+    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
+  }
+}
+
+// the same with one workgroup per landmark (its 8 half-waves share the observations, the W panel is
+// one per workgroup): for the wide class, whose per-wave panels would cap the occupancy
+__global__ void __launch_bounds__(256) landmark_obs_wg_kernel(Dev d, double lambda, int64_t first, int cap) {
+  extern __shared__ double W[];
+  __shared__ double part[4][9];
+  __shared__ double Ls[6];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t l = d.lmList[first + blockIdx.x];
+  const rec_t* Jt = d.Jt;
+  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
+  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
+  for (int i = tid; i < 3 * ncol; i += 256) W[i] = 0.0;
+  __syncthreads();
+  const int h = tid >> 5, jj = lane & 31;
+  const int s = jj < 6 ? 0 : jj < 12 ? 1 : jj < 29 ? 2 : 3;
+  const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
+  const int pl = slotPlane(s) + j, st = slotStride(s);
+  double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // v00 v10 v20 v11 v21 v22 g0 g1 g2
+  for (int64_t o = o0 + h; o < o1; o += 8) {
+    const rec_t* r = Jt + o * kJA;
+    const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
+    const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
+    const rec_t* x = jt_plane(Jt, d.nObsPad, o, pl);
+    const double x0 = x[0], x1 = x[st];
+    const int32_t X = d.obRed[o * 4 + s];
+    if (jj == 0) {
+      const double e0 = r[kJe], e1 = r[kJe + 1];
+      v[6] += a0 * e0 + b0 * e1, v[7] += a1 * e0 + b1 * e1, v[8] += a2 * e0 + b2 * e1;
+      v[0] += a0 * a0 + b0 * b0, v[1] += a1 * a0 + b1 * b0, v[2] += a2 * a0 + b2 * b0;
+      v[3] += a1 * a1 + b1 * b1, v[4] += a2 * a1 + b2 * b1, v[5] += a2 * a2 + b2 * b2;
+    }
+    if (X >= 0 && j < d.rvDim[X]) {
+      const int c = d.obCol[o * 4 + s] + j;
+      atomicAdd(&W[3 * c + 0], a0 * x0 + b0 * x1);
+      atomicAdd(&W[3 * c + 1], a1 * x0 + b1 * x1);
+      atomicAdd(&W[3 * c + 2], a2 * x0 + b2 * x1);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) v[k] = wave_sum(v[k]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 9; k++) part[wave][k] = v[k];
+  __syncthreads();
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 9; k++) v[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+    const double v00 = v[0] * (1.0 + lambda) + lambda, v11 = v[3] * (1.0 + lambda) + lambda;
+    const double v22 = v[5] * (1.0 + lambda) + lambda;
+    const double l00 = sqrt(v00);
+    const double l10 = v[1] / l00, l20 = v[2] / l00;
+    const double d11 = v11 - l10 * l10;
+    const double l11 = sqrt(d11);
+    const double l21 = (v[4] - l20 * l10) / l11;
+    const double d22 = v22 - l20 * l20 - l21 * l21;
+    const double l22 = sqrt(d22);
+    if (!(v00 > 0) || !(d11 > 0) || !(d22 > 0)) atomicOr(d.err, 2);
+    double* L = d.Vchol + l * 6;
+    L[0] = Ls[0] = l00, L[1] = Ls[1] = l10, L[2] = Ls[2] = l20, L[3] = Ls[3] = l11, L[4] = Ls[4] = l21;
+    L[5] = Ls[5] = l22;
+    const double z0 = v[6] / l00, z1 = (v[7] - l10 * z0) / l11, z2 = (v[8] - l20 * z0 - l21 * z1) / l22;
+    d.z[l * 3] = z0, d.z[l * 3 + 1] = z1, d.z[l * 3 + 2] = z2;
+    d.gp[l * 3] = v[6], d.gp[l * 3 + 1] = v[7], d.gp[l * 3 + 2] = v[8];
+  }
+  __syncthreads();
+  const double l00 = Ls[0], l10 = Ls[1], l20 = Ls[2], l11 = Ls[3], l21 = Ls[4], l22 = Ls[5];
+  rec_t* Y = d.Y + d.lmY[l];
+  for (int64_t c = tid; c < ncol; c += 256) {
+    const double y0 = W[3 * c] / l00;
+    const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
+    const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
+    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
+  }
+}
+
+// the wide class when its panels exceed kLmBigCols: landmark_kernel's per-column path
+__global__ void __launch_bounds__(256) landmark_list_kernel(Dev d, double lambda, int64_t first, int64_t n) {
+  const int64_t li = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (li >= n) return;
+  landmark_eliminate(d, lambda, 0, d.lmList[first + li]);
 }
 
 // mode 2: zNew = L^-1 gpNew, one thread per landmark
@@ -1712,8 +1883,22 @@ void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hip
 
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
-  if (mode == 2) launchK(landmark_z_kernel, dim3(blocks(hi - lo, 256)), dim3(256), 0, st, d, lo, hi);
-  else launchK(landmark_kernel, dim3(blocks(hi - lo, 4)), dim3(256), 0, st, d, lambda, mode, lo, hi);
+  static const int v1 = getenv("VIBA_LANDMARK_V1") ? atoi(getenv("VIBA_LANDMARK_V1")) : 0;
+  if (mode == 2) {
+    launchK(landmark_z_kernel, dim3(blocks(hi - lo, 256)), dim3(256), 0, st, d, lo, hi);
+  } else if (mode == 0 && !v1 && lo == d.lmB && hi == d.lmE) {
+    if (d.nLmSmall)
+      launchK(landmark_obs_kernel, dim3(blocks(d.nLmSmall, 4)), dim3(256),
+              (uint32_t)(4 * 3 * kLmSmallCols * sizeof(double)), st, d, lambda, (int64_t)0, d.nLmSmall, kLmSmallCols);
+    if (d.nLmBig && d.lmBigCols <= kLmBigCols)
+      hipLaunchKernelGGL(landmark_obs_wg_kernel, dim3((unsigned)d.nLmBig), dim3(256),
+                         (uint32_t)(3 * d.lmBigCols * sizeof(double)), st, d, lambda, d.nLmSmall, (int)d.lmBigCols);
+    else if (d.nLmBig)
+      hipLaunchKernelGGL(landmark_list_kernel, dim3(blocks(d.nLmBig, 4)), dim3(256), 0, st, d, lambda, d.nLmSmall,
+                         d.nLmBig);
+  } else {
+    launchK(landmark_kernel, dim3(blocks(hi - lo, 4)), dim3(256), 0, st, d, lambda, mode, lo, hi);
+  }
 }
 // S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry)
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
