@@ -823,19 +823,12 @@ __global__ void __launch_bounds__(256) schur_run_kernel(Dev d, double lambda) {
 #ifndef VIBA_SCHUR_TR
 #define VIBA_SCHUR_TR 2
 #endif
-#ifndef VIBA_SCHUR_GENTS
-#define VIBA_SCHUR_GENTS 0  // 1: read the entries from global memory (no LDS copy)
-#endif
 constexpr int kCh = VIBA_SCHUR_CH;  // landmarks per task
 constexpr int kTR = VIBA_SCHUR_TR;  // compact block rows per task (1 or 2)
 
 __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
   __shared__ double C[TS * TS];
-#if VIBA_SCHUR_GENTS
-  const TileEnt* ents = d.tileEnts + d.tileWorks[xcd_block(blockIdx.x, gridDim.x)].start;
-#else
-  __shared__ TileEnt ents[256];
-#endif
+  __shared__ uint32_t ecol[256][2];  // the entries' first panel columns (colI, colJ); the rest from global
   __shared__ int16_t runStart[258];
   __shared__ uint8_t posW[4][2][TS];
   __shared__ double rq[TS];
@@ -846,9 +839,8 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, l4 = lane >> 4;
   const int cnt = wk.count;
-#if !VIBA_SCHUR_GENTS
-  if (tid < cnt) ents[tid] = d.tileEnts[wk.start + tid];
-#endif
+  const TileEnt* ents = d.tileEnts + wk.start;
+  if (tid < cnt) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
   for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
   if (tid < TS) rq[tid] = 0.0;
   __syncthreads();
@@ -897,8 +889,7 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
         const int kr = 4 * ks + l4;
         const bool kv = kr < rows;
         const int e = c0 + (kv ? kr / 3 : 0), q = kv ? kr - 3 * (kr / 3) : 0;
-        const TileEnt& en = ents[e];
-        const int64_t cJ = diag ? en.colI : en.colJ;
+        const int64_t cI = ecol[e][0], cJ = ecol[e][diag ? 0 : 1];
 #pragma unroll
         for (int i = 0; i < kTR; i++) {
           const int m = 16 * (a0 + i) + l15;
@@ -907,7 +898,7 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
 #pragma unroll
         for (int b = 0; b < 4; b++) {
           const int n = 16 * b + l15;
-          bv[b] = (kv && b < nbI && n < nI) ? d.Y[3 * ((int64_t)en.colI + n) + q] : (rec_t)0;
+          bv[b] = (kv && b < nbI && n < nI) ? d.Y[3 * (cI + n) + q] : (rec_t)0;
         }
       };
       rec_t av[kTR], bv[4], av2[kTR], bv2[4];
@@ -938,7 +929,7 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
       if (diag && a0 == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
         double racc = 0.0;
         for (int e = c0; e < c0 + nl; e++) {
-          const rec_t* y = d.Y + 3 * ((int64_t)ents[e].colI + lane);
+          const rec_t* y = d.Y + 3 * ((int64_t)ecol[e][0] + lane);
           const double* zz = d.z + 3 * (int64_t)ents[e].lm;
           racc += (double)y[0] * zz[0] + (double)y[1] * zz[1] + (double)y[2] * zz[2];
         }
