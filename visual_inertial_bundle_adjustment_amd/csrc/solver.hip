@@ -985,20 +985,35 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
   hacc4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
   double g0 = 0.0, g1 = 0.0;
   const rec_t* Jt = d.Jt;
-  for (int64_t ks = wave; ks < nks; ks += 4) {
-    const int64_t e = 2 * ks + (l4 >> 1);
-    rec_t v0 = 0, v1 = 0, er = 0;
-    if (e < n) {
-      const int64_t o = d.grpObs[o0 + e];
-      er = Jt[o * kJA + kJe + r];
-      if (row0 >= 0) v0 = jt_plane(Jt, d.nObsPad, o, p0)[r * s0];
-      if (row1 >= 0) v1 = jt_plane(Jt, d.nObsPad, o, p1)[r * s1];
+  // 4 k-steps per iteration (this wave's ks, ks + 4, ks + 8, ks + 12): their observation indices, then
+  // all their record loads, then the products, so the loads of one iteration are in flight together
+  constexpr int kU = 4;
+  for (int64_t ks0 = wave; ks0 < nks; ks0 += 4 * kU) {
+    int64_t oo[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int64_t e = 2 * (ks0 + 4 * u) + (l4 >> 1);
+      oo[u] = e < n ? d.grpObs[o0 + e] : -1;
     }
-    g0 += (double)v0 * er, g1 += (double)v1 * er;
-    if (mode == 0) {
-      a00 = mfma_h(v0, v0, a00);
-      a10 = mfma_h(v1, v0, a10);
-      a11 = mfma_h(v1, v1, a11);
+    rec_t v0[kU], v1[kU], er[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      v0[u] = v1[u] = er[u] = 0;
+      const int64_t o = oo[u];
+      if (o >= 0) {
+        er[u] = Jt[o * kJA + kJe + r];
+        if (row0 >= 0) v0[u] = jt_plane(Jt, d.nObsPad, o, p0)[r * s0];
+        if (row1 >= 0) v1[u] = jt_plane(Jt, d.nObsPad, o, p1)[r * s1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      g0 += (double)v0[u] * er[u], g1 += (double)v1[u] * er[u];
+      if (mode == 0) {
+        a00 = mfma_h(v0[u], v0[u], a00);
+        a10 = mfma_h(v1[u], v0[u], a10);
+        a11 = mfma_h(v1[u], v1[u], a11);
+      }
     }
   }
   // reduce the 4 waves (and, for g, the 4 lane groups) through LDS
