@@ -772,12 +772,15 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallLaunch L) {
 // block rho' J^T J over the factor's non-constant columns, lane-parallel over the lower-triangle
 // entries, fp64 atomics into the reduced tiles (Optimizer.cpp:136-146 via the factor stores'
 // jacobian accumulation, InertialFactor / PriorFactor / RandomWalkFactor).
-__global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, double* gOut) {
-  __shared__ double Jl[4][kMaxM * kMaxCols];
+// MM: row capacity of the launch (its kinds' residual sizes), so that the per-wave LDS copy of the
+// whitened Jacobian is only as large as needed (IMU factors: 9 rows -> 6 workgroups per CU)
+template <int MM>
+__global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, double* gOut, int64_t s0, int64_t s1) {
+  __shared__ double Jl[4][MM * kMaxCols];
   __shared__ int32_t act[4][kMaxCols][2];  // active column: (staged column, reduced row)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t slot = (int64_t)blockIdx.x * 4 + wave;
-  if (slot >= d.nSmallStage) return;
+  const int64_t slot = s0 + (int64_t)blockIdx.x * 4 + wave;
+  if (slot >= s1) return;
   const int32_t* mt = d.sMeta + slot * kSmallMeta;
   const int m = mt[0], colc = mt[1], nv = mt[2], uoff = mt[3], fk = mt[4];
   const double* Jg = d.sJ + slot * kSmallJ;
@@ -786,17 +789,23 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
   double* J = Jl[wave];
   const double* U = uoff >= 0 ? d.sf[fk].consts + uoff : nullptr;
   for (int j = lane; j < colc; j += 64) {
-    double col[kMaxM];
+    double col[MM];  // statically indexed (registers): every loop over it is unrolled to MM
 #pragma unroll
-    for (int i = 0; i < kMaxM; i++) col[i] = i < m ? Jg[i * kMaxCols + j] : 0.0;
+    for (int i = 0; i < MM; i++) col[i] = i < m ? Jg[i * kMaxCols + j] : 0.0;
     if (U) {
-      for (int i = 0; i < m; i++) {
+#pragma unroll
+      for (int i = 0; i < MM; i++) {
+        if (i >= m) break;
         double s = 0;
-        for (int q = 0; q < m; q++) s += U[i * m + q] * col[q];
+#pragma unroll
+        for (int q = 0; q < MM; q++)
+          if (q < m) s += U[i * m + q] * col[q];
         J[i * kMaxCols + j] = s;
       }
     } else {
-      for (int i = 0; i < m; i++) J[i * kMaxCols + j] = col[i];
+#pragma unroll
+      for (int i = 0; i < MM; i++)
+        if (i < m) J[i * kMaxCols + j] = col[i];
     }
   }
   if (lane == 0) {
@@ -821,7 +830,7 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
   if (mode != 0) return;
   const int P = A * (A + 1) / 2;
   for (int p = lane; p < P; p += 64) {
-    int a = (int)((sqrt(8.0 * p + 1.0) - 1.0) * 0.5);
+    int a = (int)((sqrtf(8.0f * p + 1.0f) - 1.0f) * 0.5f);  // f32 estimate, corrected below
     while (a * (a + 1) / 2 > p) a--;
     while ((a + 1) * (a + 2) / 2 <= p) a++;
     const int b = p - a * (a + 1) / 2;
@@ -1043,8 +1052,17 @@ void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st) {
 
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st) {
   launch_small_eval(d, mode, gOut, st);
-  if (mode != 2 && d.nSmallStage > 0)
-    launchK(small_assemble_kernel, dim3((unsigned)((d.nSmallStage + 3) / 4)), dim3(256), 0, st, d, mode, gOut);
+  if (mode == 2 || d.nSmallStage <= 0) return;
+  // three launches by residual size: IMU kinds 1-3 (9 rows), omega priors (3), the rest (<= 23); the
+  // staging slots run kind by kind
+  const int64_t a = d.sf[1].stage, b = d.sf[4].stage, c = d.sf[5].stage, e = d.nSmallStage;
+  if (b > a)
+    launchK(small_assemble_kernel<9>, dim3((unsigned)((b - a + 3) / 4)), dim3(256), 0, st, d, mode, gOut, a, b);
+  if (c > b)
+    hipLaunchKernelGGL(small_assemble_kernel<3>, dim3((unsigned)((c - b + 3) / 4)), dim3(256), 0, st, d, mode, gOut, b, c);
+  if (e > c)
+    hipLaunchKernelGGL(small_assemble_kernel<kMaxM>, dim3((unsigned)((e - c + 3) / 4)), dim3(256), 0, st, d, mode, gOut,
+                       c, e);
 }
 
 }  // namespace viba
