@@ -269,6 +269,7 @@ struct vb_handle_s {
   bool isRoot = true;
   int partRank = 0, partWorld = 1;  // vb_set_partition (partitioned factorization), else 1
   std::vector<int8_t> colOwner;     // per tile column: owning rank, partWorld = ROOT (rank 0)
+  std::vector<std::pair<int64_t, int64_t>> zeroRuns;  // partitioned: tile runs this rank writes (its + ROOT columns)
   int64_t tileFirst = 0, tileCount = 0, nTileEnt = 0;
   std::vector<int32_t> shardTiles;  // exact tiles of this (non-root) shard's partial system
   int32_t* shardTilesD = nullptr;
@@ -1188,6 +1189,12 @@ int doFinalize(vb_handle h) {
       if (me == 0)
         if (int rc = build(h->sch[1], root, root, root, none)) return rc;
       for (int32_t J = 0; J < nT; J++)
+        if (ownOrRoot(J)) {  // the only tiles this rank writes: cleared per linearize instead of the store
+          const int64_t a = h->colStart[J], b = h->colStart[J + 1];
+          if (!h->zeroRuns.empty() && h->zeroRuns.back().second == a) h->zeroRuns.back().second = b;
+          else h->zeroRuns.push_back({a, b});
+        }
+      for (int32_t J = 0; J < nT; J++)
         if (root(J)) {
           h->rootRows.push_back(J);
           for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) h->rootTiles.push_back(h->colTilesH[c]);
@@ -1713,7 +1720,12 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   if (!h || !h->finalized) return fail(VB_E_STATE, "vb_linearize before vb_finalize");
   Dev& d = h->d;
   HIPCHK(hipEventRecord(h->ev[0], h->st));
-  HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), h->st));
+  if (h->zeroRuns.empty()) {
+    HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), h->st));
+  } else {  // partitioned: colStart runs are tile-store index ranges (tiles stored column by column)
+    for (const auto& r : h->zeroRuns)
+      HIPCHK(hipMemsetAsync(d.tiles + r.first * TS * TS, 0, (size_t)(r.second - r.first) * TS * TS * sizeof(double), h->st));
+  }
   HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
