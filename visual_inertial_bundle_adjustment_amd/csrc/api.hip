@@ -1409,6 +1409,13 @@ int factorReduced(vb_handle h, int which = 0) {
   return 0;
 }
 
+// resident workgroups per CU of the persistent fan-out solves (VIBA_SOLVE_WG_PER_CU; every launched
+// workgroup must be resident at once: the kernels' occupancy allows 3 per CU)
+int solveWgPerCU() {
+  static const int k = getenv("VIBA_SOLVE_WG_PER_CU") ? std::max(1, std::min(3, atoi(getenv("VIBA_SOLVE_WG_PER_CU")))) : 1;
+  return k;
+}
+
 // solves with rhsWork as right-hand side, result in xRed (schedule `which`, phases bit 0 forward,
 // bit 1 backward; a partitioned backward pass takes the ROOT rows of xRed as given)
 int solveReduced(vb_handle h, int which = 0, int phases = 3) {
@@ -1418,7 +1425,8 @@ int solveReduced(vb_handle h, int which = 0, int phases = 3) {
     Dev& d = h->d;
     profBegin(h, KF_FWD);
     launch_solve_fanout(d, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD,
-                        h->rowTilesD, h->rowColD, h->linv, h->rhsWork, h->yvec, d.xRed, h->solveFlags, h->numCUs,
+                        h->rowTilesD, h->rowColD, h->linv, h->rhsWork, h->yvec, d.xRed, h->solveFlags,
+                        h->numCUs * solveWgPerCU(),
                         h->st, phases, S.preReadyD, S.nPreReady);
     profEnd(h, KF_FWD);
     return 0;
