@@ -1728,17 +1728,28 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   if (!h || !h->finalized) return fail(VB_E_STATE, "vb_linearize before vb_finalize");
   Dev& d = h->d;
   HIPCHK(hipEventRecord(h->ev[0], h->st));
-  if (h->zeroRuns.empty()) {
-    HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), h->st));
-  } else {  // partitioned: colStart runs are tile-store index ranges (tiles stored column by column)
-    for (const auto& r : h->zeroRuns)
-      HIPCHK(hipMemsetAsync(d.tiles + r.first * TS * TS, 0, (size_t)(r.second - r.first) * TS * TS * sizeof(double), h->st));
-  }
-  HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  if (h->isRoot || h->partWorld > 1) launch_pad_diag(d, h->padRowsD, h->nPadRows, h->st);
-  forkSmall(h, 0, d.gRed);
+  // the reduced system is cleared and the small factors assembled on the side stream while the visual
+  // factors linearize on the main stream (they write only their records and the cost)
+  const bool side = smallHere(h, 0);
+  hipStream_t zs = side ? h->st2 : h->st;
+  if (side) {
+    HIPCHK(hipEventRecord(h->evFork, h->st));
+    HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
+  }
+  if (h->zeroRuns.empty()) {
+    HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), zs));
+  } else {  // partitioned: colStart runs are tile-store index ranges (tiles stored column by column)
+    for (const auto& r : h->zeroRuns)
+      HIPCHK(hipMemsetAsync(d.tiles + r.first * TS * TS, 0, (size_t)(r.second - r.first) * TS * TS * sizeof(double), zs));
+  }
+  HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), zs));
+  if (h->isRoot || h->partWorld > 1) launch_pad_diag(d, h->padRowsD, h->nPadRows, zs);
+  if (side) {
+    launch_small(d, 0, d.gRed, h->st2);
+    HIPCHK(hipEventRecord(h->evJoin, h->st2));
+  }
   visualLinShard(h, update_cache, dont_retry_failed);
   joinSmall(h);
   HIPCHK(hipEventRecord(h->ev[1], h->st));
