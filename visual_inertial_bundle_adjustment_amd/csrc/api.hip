@@ -958,9 +958,8 @@ int doFinalize(vb_handle h) {
               "1 / 2-3 / 4-7 / 8-15 / 16-63 / 64+: %lld %lld %lld %lld %lld %lld\n", grpTile, (long long)gsz[0],
               (long long)gsz[1], (long long)gsz[2], (long long)gsz[3], (long long)gsz[4], (long long)gsz[5]);
     }
-    // compact Schur kinds: entries of a tile in runs of identical (maskI, maskJ) (solver.hip
-    // schur_run2_kernel / schur_run_kernel), by landmark within a run
-    if (schur_kind() == 0 || schur_kind() == 3)
+    // entries of a tile in runs of identical (maskI, maskJ) (solver.hip schur_run2_kernel), by
+    // landmark within a run
     for (int64_t t = 0; t < nTiles; t++)
       std::sort(ents.begin() + tcnt[t], ents.begin() + tcnt[t + 1], [](const TileEnt& a, const TileEnt& b) {
         if (a.maskI != b.maskI) return a.maskI < b.maskI;

@@ -212,13 +212,6 @@ struct Dev {
   ImuIdx jac;
 };
 
-// Schur tile-product kernel (solver.hip launch_schur; the compact kinds 0 and 3 need the tile entries
-// sorted into runs of identical row masks, which api.hip does at finalize)
-inline int schur_kind() {
-  static const int k = getenv("VIBA_SCHUR") ? atoi(getenv("VIBA_SCHUR")) : 0;
-  return k;
-}
-
 // partitioned factorization: does this handle assemble into tile column `col`?
 __device__ __forceinline__ bool owns_col(const Dev& d, int64_t col) {
   if (d.world <= 1) return true;

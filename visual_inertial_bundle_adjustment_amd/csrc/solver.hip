@@ -315,28 +315,6 @@ __device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
   return d.tiles + (int64_t)ti * TS * TS + (c % TS) * TS + (r % TS);
 }
 
-// Schur assembly by target tile (api.hip builds the work list; engine.hpp TileWork / TileEnt).
-// One workgroup per work item: a 64 x 64 tile (I, J) of the reduced system and up to 256 of its
-// landmark entries (staged in LDS at the start).  Each batch of 8 landmarks is scattered into LDS as
-// K = 32 rows x 64 tile rows: landmark e owns rows 4 e .. 4 e + 2 (its Y = L^-1 W panel rows; row
-// 4 e + 3 stays zero), so one landmark is exactly one k-step of v_mfma_f64_16x16x4_f64 and the update
-// C -= Yi^T Yj is a sum of rank-3 16 x 16 block products.  The fill records, per landmark, which
-// 16-row blocks of tile I and of tile J its columns touch; a k-step's MFMA on block pair (a, b) runs
-// only when both are touched.  The gathers of batch b + 1 (pcRow, Y, z) are issued into registers
-// before batch b's MFMAs, so their latency overlaps the products.  Computed transposed (D = Yj^T Yi)
-// so the MFMA output column (lane & 15) runs along the tile's contiguous row index q; wave w owns the
-// 32 x 32 block (p in 32 (w >> 1) .., q in 32 (w & 1) ..).  Odd K rows are stored with the column
-// XOR 16, so the two 16-lane halves of each ds_read_b64 half-wave (K rows k, k + 1, 512 B apart) hit
-// disjoint banks.  The LDS image is zeroed once; after each batch the filling threads clear exactly
-// the entries they wrote.  A tile split over several items
-// (wk.kind) is updated with fp64 atomics, else by a plain read-modify-write.  Diagonal tiles also
-// emit rhs -= Y^T z.
-#ifndef VIBA_SCHUR_EXPT
-#define VIBA_SCHUR_EXPT 0  // diagnostic builds only: 1 = no MFMA, 2 = no gathers
-#endif
-constexpr int kTK = 32;       // K rows per batch
-constexpr int kTB = kTK / 4;  // landmarks per batch
-
 // XCD-aware block id: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch), so
 // hand each XCD a contiguous range of work (bijective for any grid size)
 __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
@@ -344,473 +322,20 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-struct SchurSlots {  // one thread's two fill slots of a batch, in registers
-  rec_t yI[2][3], yJ[2][3];
-  double z[2];
-  int rowI[2], rowJ[2], eb[2], c[2];
-};
-
-__device__ __forceinline__ void schur_gather(const Dev& d, const TileEnt* ents, int count, int b, bool diag, int64_t rI,
-                                             int64_t rJ, int tid, SchurSlots& S) {
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int sl = tid + 256 * k;
-    const int eb = sl / TS, c = sl - eb * TS, e = b * kTB + eb;
-    S.eb[k] = eb, S.c[k] = c, S.rowI[k] = -1, S.rowJ[k] = -1;
-    if (e >= count) continue;
-    const TileEnt en = ents[e];
-#if VIBA_SCHUR_EXPT == 2  // diagnostic only: no gathers
-    if (c < en.nI) S.rowI[k] = c, S.yI[k][0] = S.yI[k][1] = S.yI[k][2] = 0.0;
-    if (!diag && c < en.nJ) S.rowJ[k] = c, S.yJ[k][0] = S.yJ[k][1] = S.yJ[k][2] = 0.0;
-#else
-    if (c < en.nI) {
-      const int64_t col = (int64_t)en.colI + c;
-      S.rowI[k] = (int)(d.pcRow[col] - rI);
-      const rec_t* y = d.Y + 3 * col;
-      S.yI[k][0] = y[0], S.yI[k][1] = y[1], S.yI[k][2] = y[2];
-    }
-    if (!diag && c < en.nJ) {
-      const int64_t col = (int64_t)en.colJ + c;
-      S.rowJ[k] = (int)(d.pcRow[col] - rJ);
-      const rec_t* y = d.Y + 3 * col;
-      S.yJ[k][0] = y[0], S.yJ[k][1] = y[1], S.yJ[k][2] = y[2];
-    }
-#endif
-    if (diag && c < 3) S.z[k] = d.z[3 * (int64_t)en.lm + c];
-  }
-}
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) schur_tile_kernel(Dev d, double lambda) {
-  __shared__ rec_t Yi[kTK * TS];
-  __shared__ rec_t Yj[kTK * TS];
-  __shared__ double zb[kTK];
-  __shared__ uint32_t msk[kTB];  // bits 0-3: row blocks of tile I, 4-7: of tile J
-  __shared__ TileEnt ents[256];
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
-  const TileWork wk = d.tileWorks[w];
-  const bool diag = wk.I == wk.J;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  const int nb = (wk.count + kTB - 1) / kTB;
-  const int64_t rI = (int64_t)wk.I * TS, rJ = (int64_t)wk.J * TS;
-  if (tid < wk.count) ents[tid] = d.tileEnts[wk.start + tid];
-  for (int i = tid; i < kTK * TS; i += 256) Yi[i] = 0.0, Yj[i] = 0.0;
-  if (tid < kTK) zb[tid] = 0.0;
-  __syncthreads();
-  hacc4_t acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++) acc[a][b] = hacc4_t{0, 0, 0, 0};
-  double racc = 0.0;
-  const rec_t* yj = diag ? Yi : Yj;
-  // row blocks this wave's quadrant reads: k-steps touching none of them are skipped whole; on a
-  // diagonal tile the strictly upper block pairs are never formed (only the lower triangle is used)
-  const uint32_t qmask = (3u << (4 + (pb >> 4))) | (3u << (qb >> 4));
-  SchurSlots S;
-  schur_gather(d, ents, wk.count, 0, diag, rI, rJ, tid, S);
-  for (int b = 0; b < nb; b++) {
-    int posI[2], posJ[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      const int eb = S.eb[k];
-      uint32_t bits = 0;
-      posI[k] = -1, posJ[k] = -1;
-      if (S.rowI[k] >= 0) {
-        const int p = 4 * eb * TS + S.rowI[k];
-        Yi[p] = S.yI[k][0], Yi[(p + TS) ^ 16] = S.yI[k][1], Yi[p + 2 * TS] = S.yI[k][2];
-        posI[k] = p;
-        bits |= 1u << (S.rowI[k] >> 4);
-      }
-      if (S.rowJ[k] >= 0) {
-        const int p = 4 * eb * TS + S.rowJ[k];
-        Yj[p] = S.yJ[k][0], Yj[(p + TS) ^ 16] = S.yJ[k][1], Yj[p + 2 * TS] = S.yJ[k][2];
-        posJ[k] = p;
-        bits |= 16u << (S.rowJ[k] >> 4);
-      }
-      if (diag) bits |= bits << 4;
-      // slot k of every lane of this wave belongs to landmark eb = wave + 4 k: OR the bits over
-      // the wave by ballot and store once (an LDS atomic from 64 lanes on one word serialises)
-      uint32_t wb = 0;
-#pragma unroll
-      for (int i = 0; i < 8; i++) wb |= __ballot((bits >> i) & 1u) ? (1u << i) : 0u;
-      if (lane == 0) msk[eb] = wb;
-      if (diag && S.c[k] < 3 && b * kTB + eb < wk.count) zb[4 * eb + S.c[k]] = S.z[k];
-    }
-    __syncthreads();
-    if (b + 1 < nb) schur_gather(d, ents, wk.count, b + 1, diag, rI, rJ, tid, S);
-#pragma unroll
-    for (int eb = 0; eb < kTB; eb++) {
-      const uint32_t m = msk[eb] & qmask;
-      if (m == 0) continue;
-      const int k0 = 4 * eb;
-      rec_t av[2], bv[2];
-#pragma unroll
-      for (int a = 0; a < 2; a++) av[a] = yj[(k0 + l4) * TS + ((pb + a * 16 + l15) ^ ((l4 & 1) << 4))];
-#pragma unroll
-      for (int bb = 0; bb < 2; bb++) bv[bb] = Yi[(k0 + l4) * TS + ((qb + bb * 16 + l15) ^ ((l4 & 1) << 4))];
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int bb = 0; bb < 2; bb++)
-          if (VIBA_SCHUR_EXPT != 1 && ((m >> (4 + (pb >> 4) + a)) & (m >> ((qb >> 4) + bb)) & 1u) &&
-              !(diag && (pb >> 4) + a > (qb >> 4) + bb))
-            acc[a][bb] = mfma_h(av[a], bv[bb], acc[a][bb]);
-    }
-    if (diag && tid < TS) {
-#pragma unroll 8
-      for (int k = 0; k < kTK; k++) racc += (double)Yi[k * TS + (tid ^ ((k & 1) << 4))] * zb[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      if (posI[k] >= 0) Yi[posI[k]] = 0.0, Yi[(posI[k] + TS) ^ 16] = 0.0, Yi[posI[k] + 2 * TS] = 0.0;
-      if (posJ[k] >= 0) Yj[posJ[k]] = 0.0, Yj[(posJ[k] + TS) ^ 16] = 0.0, Yj[posJ[k] + 2 * TS] = 0.0;
-    }
-    __syncthreads();
-  }
-  double* Cw = d.tiles + (int64_t)wk.tile * TS * TS + (pb + kAccL4 * l4) * TS + qb + l15;
-  if (wk.kind) {
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int bb = 0; bb < 2; bb++)
-#pragma unroll
-        for (int r = 0; r < 4; r++)
-          if (acc[a][bb][r] != 0.0) atomicAdd(Cw + (a * 16 + kAccR * r) * TS + bb * 16, -(double)acc[a][bb][r]);
-  } else {
-    double v[2][2][4];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int bb = 0; bb < 2; bb++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) v[a][bb][r] = Cw[(a * 16 + kAccR * r) * TS + bb * 16];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int bb = 0; bb < 2; bb++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) Cw[(a * 16 + kAccR * r) * TS + bb * 16] = v[a][bb][r] - (double)acc[a][bb][r];
-  }
-  if (diag && tid < TS) {
-    const int64_t row = rI + tid;
-    if (row < d.nRed && racc != 0.0) atomicAdd(d.rhs + row, -racc);
-  }
-}
-
-// Schur assembly, register-operand form (no LDS images, no per-batch barriers).  Same work items and
-// quadrant split as schur_tile_kernel; every k-step is one landmark entry (k = lane >> 4 < 3 its
-// three coordinates), and each lane fetches its MFMA operands straight from the Y panel: row r of
-// the tile is the entry's column popcount(mask & ((1 << r) - 1)) when bit r of the entry's row mask
-// is set (rows of a landmark's run ascend with its columns), else 0.  Loads are unconditional (index
-// clamped) and selected afterwards, so the operands of group g + 1 (4 entries) are in flight while
-// group g runs on the MFMA pipe.  Block pairs an entry does not touch are skipped by scalar tests on
-// the (wave-uniform) masks.
-constexpr int kSG = 4;  // entries per prefetch group
-
-struct SchurOps {
-  double v[kSG][4];  // per entry: J-side rows pb + l15, pb + 16 + l15; I-side rows qb + l15, qb + 16 + l15
-};
-
-__device__ __forceinline__ double schur_opnd(const Dev& d, uint64_t m, uint32_t col, uint64_t bit, int kk, bool kv) {
-  const int c = __popcll(m & (bit - 1));
-  const int64_t idx = min<int64_t>(3 * ((int64_t)col + c) + kk, 3 * d.nYcol - 1);
-  const double y = d.Y[idx];
-  return (kv && (m & bit)) ? y : 0.0;
-}
-
 __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return ((uint64_t)hi << 32) | lo;
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) schur_tile2_kernel(Dev d, double lambda) {
-  __shared__ TileEnt ents[256];
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
-  const TileWork wk = d.tileWorks[w];
-  const bool diag = wk.I == wk.J;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  const int cnt = wk.count;
-  if (tid < cnt) ents[tid] = d.tileEnts[wk.start + tid];
-  __syncthreads();
-  double4_t acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
-  const bool kv = l4 < 3;
-  const int kk = kv ? l4 : 0;
-  const uint64_t bA0 = 1ull << (pb + l15), bA1 = 1ull << (pb + 16 + l15);
-  const uint64_t bB0 = 1ull << (qb + l15), bB1 = 1ull << (qb + 16 + l15);
-  // on a diagonal tile only the lower-triangle block pairs are formed (wave pb 32 / qb 0 idles)
-  const bool skip01 = diag && (pb >> 4) > (qb >> 4) + 1, skip00 = diag && (pb >> 4) > (qb >> 4);
-  const bool skip11 = skip00, skip10 = diag && (pb >> 4) + 1 > (qb >> 4);
-  const int ng = (cnt + kSG - 1) / kSG;
-  auto load = [&](int g, SchurOps& R) {
-#pragma unroll
-    for (int i = 0; i < kSG; i++) {
-      const int e = min(g * kSG + i, cnt - 1);
-      const TileEnt& en = ents[e];
-      const uint64_t mI = en.maskI, mJ = diag ? en.maskI : en.maskJ;
-      const uint32_t cI = en.colI, cJ = diag ? en.colI : en.colJ;
-      R.v[i][0] = schur_opnd(d, mJ, cJ, bA0, kk, kv);
-      R.v[i][1] = schur_opnd(d, mJ, cJ, bA1, kk, kv);
-      R.v[i][2] = schur_opnd(d, mI, cI, bB0, kk, kv);
-      R.v[i][3] = schur_opnd(d, mI, cI, bB1, kk, kv);
-    }
-  };
-  auto comp = [&](int g, const SchurOps& R) {
-#pragma unroll
-    for (int i = 0; i < kSG; i++) {
-      const int e = g * kSG + i;
-      if (e >= cnt) break;
-      const uint64_t mI = uniform64(ents[e].maskI), mJ = diag ? mI : uniform64(ents[e].maskJ);
-      const bool j0 = (mJ >> pb) & 0xffffull, j1 = (mJ >> (pb + 16)) & 0xffffull;
-      const bool i0 = (mI >> qb) & 0xffffull, i1 = (mI >> (qb + 16)) & 0xffffull;
-      if (j0 && i0 && !skip00) acc[0][0] = mfma64(R.v[i][0], R.v[i][2], acc[0][0]);
-      if (j0 && i1 && !skip01) acc[0][1] = mfma64(R.v[i][0], R.v[i][3], acc[0][1]);
-      if (j1 && i0 && !skip10) acc[1][0] = mfma64(R.v[i][1], R.v[i][2], acc[1][0]);
-      if (j1 && i1 && !skip11) acc[1][1] = mfma64(R.v[i][1], R.v[i][3], acc[1][1]);
-    }
-  };
-  if (!(diag && pb > qb)) {
-    SchurOps RA, RB;
-    load(0, RA);
-    for (int g = 0; g < ng; g += 2) {
-      if (g + 1 < ng) load(g + 1, RB);
-      comp(g, RA);
-      if (g + 1 < ng) {
-        if (g + 2 < ng) load(g + 2, RA);
-        comp(g + 1, RB);
-      }
-    }
-  }
-  double* Cw = d.tiles + (int64_t)wk.tile * TS * TS + (pb + l4) * TS + qb + l15;
-  if (!(diag && pb > qb)) {
-    if (wk.kind) {
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int bb = 0; bb < 2; bb++)
-#pragma unroll
-          for (int r = 0; r < 4; r++)
-            if (acc[a][bb][r] != 0.0) atomicAdd(Cw + (a * 16 + 4 * r) * TS + bb * 16, -acc[a][bb][r]);
-    } else {
-      double v[2][2][4];
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int bb = 0; bb < 2; bb++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) v[a][bb][r] = Cw[(a * 16 + 4 * r) * TS + bb * 16];
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int bb = 0; bb < 2; bb++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + bb * 16] = v[a][bb][r] - acc[a][bb][r];
-    }
-  }
-  // diagonal tiles: rhs -= Y^T z (the idle wave: pb 32, qb 0), lane = tile row
-  if (diag && pb > qb) {
-    const uint64_t bit = 1ull << lane;
-    double racc = 0.0;
-    for (int e = 0; e < cnt; e++) {
-      const uint64_t m = ents[e].maskI;
-      if (!(m & bit)) continue;
-      const int64_t col = (int64_t)ents[e].colI + __popcll(m & (bit - 1));
-      const double* zz = d.z + 3 * (int64_t)ents[e].lm;
-      racc += (double)d.Y[3 * col] * zz[0] + (double)d.Y[3 * col + 1] * zz[1] + (double)d.Y[3 * col + 2] * zz[2];
-    }
-    const int64_t row = (int64_t)wk.I * TS + lane;
-    if (row < d.nRed && racc != 0.0) atomicAdd(d.rhs + row, -racc);
-  }
-}
-
-// Schur assembly by target tile, compact form with LDS images (VIBA_SCHUR=3; measured slower, kept for the record:
-// 8.5 ms against 7.1 for schur_tile_kernel on config C -- the compact products of most runs fit one
-// wave's 32 x 32 quadrant, so three of the four waves idle at every batch barrier while the gathers
-// per batch stay the same).  api.hip sorts every tile's landmark entries
-// by their (row mask in tile I, row mask in tile J), so a work item is a sequence of RUNS of landmarks
-// that touch exactly the same tile rows.  Within a run the product is formed in compact coordinates:
-// the c-th panel column of a landmark inside tile I is compact column c (its rows ascend with its
-// columns), so the LDS images hold Y^T densely (K row 3 e + coordinate for landmark e, column c) and
-// the 4 waves' 32 x 32 quadrants of the compact nJ x nI product need only ceil(nJ / 16) x ceil(nI / 16)
-// blocks of v_mfma_f64_16x16x4_f64 per 4 K rows (3 rows per landmark, no padding row).  At the end of a
-// run every lane adds its accumulators into the item's tile accumulator in LDS through the run's
-// compact -> tile row maps (posI / posJ: the rank-th set bit of the mask), distinct positions within a
-// run, so plain LDS read-modify-writes.  Config C: 34M MFMAs instead of the 70M of the tile-coordinate
-// form (16-row masks, one padded k-step per landmark; VIBA_SCHUR_STATS=1 prints the counts).  Batches
-// of up to 10 landmarks (30 of the 32 K rows) never cross a run; rows beyond the batch are zeroed at
-// the operand read, and stale image columns beyond nI / nJ only feed products that are not scattered,
-// so the images are never cleared.  The next batch's gathers are issued into registers before the
-// current batch's MFMAs.  Diagonal tiles: lower compact block pairs only, and rhs -= Y^T z per tile row.
-constexpr int kRB = 10;  // landmarks per batch (30 of kTK = 32 K rows)
-
-struct RunSlots {  // one thread's three fill slots of a batch
-  rec_t yI[3][3], yJ[3][3];
-  double z[3];
-  bool vI[3], vJ[3];
-};
-
-__device__ __forceinline__ void run_gather(const Dev& d, const TileEnt* ents, int b0, int nb, bool diag, int tid,
-                                           RunSlots& S) {
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    const int sl = tid + 256 * k, eb = sl >> 6, c = sl & 63;
-    S.vI[k] = S.vJ[k] = false;
-    if (eb >= nb) continue;
-    const TileEnt& en = ents[b0 + eb];
-    if (c < en.nI) {
-      const rec_t* y = d.Y + 3 * ((int64_t)en.colI + c);
-      S.yI[k][0] = y[0], S.yI[k][1] = y[1], S.yI[k][2] = y[2], S.vI[k] = true;
-    }
-    if (!diag && c < en.nJ) {
-      const rec_t* y = d.Y + 3 * ((int64_t)en.colJ + c);
-      S.yJ[k][0] = y[0], S.yJ[k][1] = y[1], S.yJ[k][2] = y[2], S.vJ[k] = true;
-    }
-    if (diag && c < 3) S.z[k] = d.z[3 * (int64_t)en.lm + c];
-  }
-}
-
-__global__ void __launch_bounds__(256) schur_run_kernel(Dev d, double lambda) {
-  __shared__ rec_t Yi[kTK * TS];
-  __shared__ rec_t Yj[kTK * TS];
-  __shared__ double C[TS * TS];  // the item's tile accumulator (column-major like the tile store)
-  __shared__ TileEnt ents[256];
-  __shared__ int16_t runStart[258];
-  __shared__ uint8_t pos[2][2][TS];  // [run parity][I / J][compact index] -> tile row
-  __shared__ double zb[kTK];
-  __shared__ double rq[TS];
-  __shared__ int nRunsS;
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
-  const TileWork wk = d.tileWorks[w];
-  const bool diag = wk.I == wk.J;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  const int cnt = wk.count;
-  if (tid < cnt) ents[tid] = d.tileEnts[wk.start + tid];
-  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
-  if (tid < TS) rq[tid] = 0.0;
-  __syncthreads();
-  if (wave == 0) {  // run starts, in entry order
-    int n = 0;
-    for (int e0 = 0; e0 < cnt; e0 += 64) {
-      const int e = e0 + lane;
-      const bool st = e < cnt && (e == 0 || ents[e].maskI != ents[e - 1].maskI || ents[e].maskJ != ents[e - 1].maskJ);
-      const uint64_t b = __ballot(st);
-      if (st) runStart[n + __popcll(b & ((1ull << lane) - 1))] = (int16_t)e;
-      n += __popcll(b);
-    }
-    if (lane == 0) runStart[n] = (int16_t)cnt, nRunsS = n;
-  }
-  __syncthreads();
-  const int nRuns = nRunsS;
-  hacc4_t acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++) acc[a][b] = hacc4_t{0, 0, 0, 0};
-  double racc = 0.0;  // diagonal tiles, wave 0: lane = compact column of the run
-  const rec_t* yj = diag ? Yi : Yj;
-  RunSlots S;
-  int r = 0, b0 = 0;
-  if (nRuns > 0) run_gather(d, ents, 0, min(kRB, runStart[1] - 0), diag, tid, S);
-  while (r < nRuns) {
-    const int e1 = runStart[r + 1];
-    const int nb = min(kRB, e1 - b0);
-    const uint64_t mI = ents[b0].maskI, mJ = diag ? mI : ents[b0].maskJ;
-    const int nI = __popcll(mI), nJ = __popcll(mJ);
-    const int par = r & 1;
-    if (b0 == runStart[r]) {  // first batch of the run: its compact -> tile row maps
-      if (wave == 0 && ((mI >> lane) & 1)) pos[par][0][__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
-      if (wave == 1 && ((mJ >> lane) & 1)) pos[par][1][__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
-    }
-    // fill the images: landmark eb of the batch owns K rows 3 eb .. 3 eb + 2 (odd rows XOR 16)
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const int sl = tid + 256 * k, eb = sl >> 6, c = sl & 63;
-      if (S.vI[k]) {
-#pragma unroll
-        for (int q = 0; q < 3; q++) Yi[(3 * eb + q) * TS + (c ^ (((3 * eb + q) & 1) << 4))] = S.yI[k][q];
-      }
-      if (S.vJ[k]) {
-#pragma unroll
-        for (int q = 0; q < 3; q++) Yj[(3 * eb + q) * TS + (c ^ (((3 * eb + q) & 1) << 4))] = S.yJ[k][q];
-      }
-      if (diag && c < 3 && eb < nb) zb[3 * eb + c] = S.z[k];
-    }
-    __syncthreads();
-    // next batch's gathers in flight during this batch's products
-    int rn = r, bn = b0 + nb;
-    if (bn >= e1) rn = r + 1, bn = e1;
-    if (rn < nRuns) run_gather(d, ents, bn, min(kRB, runStart[rn + 1] - bn), diag, tid, S);
-    const int rows = 3 * nb, nks = (rows + 3) / 4;
-    // compact blocks of this wave's quadrant: J side rows pb + 16 a < nJ, I side cols qb + 16 b < nI
-    const bool actA0 = pb < nJ, actA1 = pb + 16 < nJ, actB0 = qb < nI, actB1 = qb + 16 < nI;
-    const bool w00 = actA0 && actB0 && !(diag && (pb >> 4) > (qb >> 4));
-    const bool w01 = actA0 && actB1 && !(diag && (pb >> 4) > (qb >> 4) + 1);
-    const bool w10 = actA1 && actB0 && !(diag && (pb >> 4) + 1 > (qb >> 4));
-    const bool w11 = actA1 && actB1 && !(diag && (pb >> 4) + 1 > (qb >> 4) + 1);
-    if (w00 || w01 || w10 || w11) {
-      for (int ks = 0; ks < nks; ks++) {
-        const int kr = 4 * ks + l4;
-        const bool kv = kr < rows;
-        const int sw = (kr & 1) << 4;
-        rec_t av[2], bv[2];
-#pragma unroll
-        for (int a = 0; a < 2; a++) av[a] = kv ? yj[kr * TS + ((pb + a * 16 + l15) ^ sw)] : (rec_t)0;
-#pragma unroll
-        for (int b = 0; b < 2; b++) bv[b] = kv ? Yi[kr * TS + ((qb + b * 16 + l15) ^ sw)] : (rec_t)0;
-        if (w00) acc[0][0] = mfma_h(av[0], bv[0], acc[0][0]);
-        if (w01) acc[0][1] = mfma_h(av[0], bv[1], acc[0][1]);
-        if (w10) acc[1][0] = mfma_h(av[1], bv[0], acc[1][0]);
-        if (w11) acc[1][1] = mfma_h(av[1], bv[1], acc[1][1]);
-      }
-    }
-    if (diag && wave == 0 && lane < nI) {
-      for (int k = 0; k < rows; k++) racc += (double)Yi[k * TS + (lane ^ ((k & 1) << 4))] * zb[k];
-    }
-    if (bn == e1 || rn != r) {
-      // end of the run: add the compact product into the tile accumulator
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 2; b++) {
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const int m = pb + 16 * a + kAccL4 * l4 + kAccR * q, n = qb + 16 * b + l15;
-            if (m < nJ && n < nI) C[pos[par][1][m] * TS + pos[par][0][n]] -= (double)acc[a][b][q];
-          }
-          acc[a][b] = hacc4_t{0, 0, 0, 0};
-        }
-      if (diag && wave == 0 && lane < nI) rq[pos[par][0][lane]] -= racc;
-      racc = 0.0;
-    }
-    __syncthreads();  // the images are rewritten by the next batch
-    r = rn, b0 = bn;
-  }
-  // epilogue: the tile accumulator into the tile store
-  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind) {
-    for (int i = tid; i < TS * TS; i += 256)
-      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
-  } else {
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
-  }
-  if (diag && tid < TS) {
-    const int64_t row = (int64_t)wk.I * TS + tid;
-    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
-  }
-}
-
-// Schur assembly by target tile, compact runs with register operands (default, VIBA_SCHUR=0).  Same
-// runs as schur_run_kernel, but no images and no barriers: a task is (run, chunk of <= kCh landmarks, compact
+// Schur assembly by target tile (api.hip builds the work list; engine.hpp TileWork / TileEnt), in
+// compact runs with register operands.  api.hip sorts every tile's landmark entries by their (row mask
+// in tile I, row mask in tile J): a work item is a sequence of RUNS of landmarks touching exactly the
+// same tile rows.  Within a run the c-th panel column of a landmark inside tile I is compact column c
+// (its rows ascend with its columns), K is dense (3 rows per landmark), and the compact nJ x nI product
+// needs only ceil(nJ / 16) x ceil(nI / 16) blocks of v_mfma_f64_16x16x4_f64 per 4 K rows: 34M MFMAs
+// on config C against 70M for the tile-coordinate form (16-row masks, one padded k-step per landmark;
+// VIBA_SCHUR_STATS=1 prints the counts; the tile-coordinate and LDS-image forms are in the history,
+// DESIGN.md §8).  No images and no barriers: a task is (run, chunk of <= kCh landmarks, compact
 // block row a of the J side); a wave takes every fourth task of its item and accumulates the nI-wide
 // block row over the chunk's dense K (3 rows per landmark), its operands gathered straight from the Y
 // panel (lane l: compact column 16 a + (l & 15) / 16 b + (l & 15), K row 4 ks + (l >> 4)), the next
@@ -1060,7 +585,7 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
   }
 }
 
-// damping of the small-factor part of the diagonal (visual part: schur_tile_kernel) and the
+// damping of the small-factor part of the diagonal (visual part: obs_group_kernel) and the
 // identity term (Optimizer.cpp:136-146 addDamping: H_ii += lambda * H_ii + lambda)
 __global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1910,16 +1435,7 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
   if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
-  // VIBA_SCHUR (must match the setting api.hip built the entries under, schur_kind()):
-  //   0 compact runs, register operands (default)   1 tile-coordinate LDS images
-  //   2 tile-coordinate register operands            3 compact runs, LDS images
-  const int kind = schur_kind();
-  if (d.nTileWorks) {
-    if (kind == 1) launchK(schur_tile_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else if (kind == 2) launchK(schur_tile2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else if (kind == 3) launchK(schur_run_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-  }
+  if (d.nTileWorks) launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
