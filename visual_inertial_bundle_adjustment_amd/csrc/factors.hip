@@ -100,7 +100,10 @@ __device__ bool vis_eval(const double* obsC, v3 X, const se3& Tbw, const se3& Tc
     const int n = (int)cam[1];
 #pragma unroll
     for (int j = 0; j < 17; j++) {
-      const double a0 = j < n ? Jp[j] : 0.0, a1 = j < n ? Jp[15 + j] : 0.0;
+      // n <= 15 projection parameters: columns 15, 16 (readout, offset) are never read from Jp, which
+      // keeps every Jp index static and in bounds (a possibly-out-of-bounds select spilled Jp to scratch)
+      const bool in = j < 15 && j < n;
+      const double a0 = in ? Jp[j < 15 ? j : 0] : 0.0, a1 = in ? Jp[15 + (j < 15 ? j : 0)] : 0.0;
       o.Jintr[j] = s00 * a0 + s01 * a1;
       o.Jintr[17 + j] = s10 * a0 + s11 * a1;
     }
@@ -194,18 +197,21 @@ __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se
 // LDS per wave and written as full lines of the Jt regions (A: planes 0..31, B: 32..71): a wave's 64
 // records are one contiguous span of each region, so every 16 B store of the copy loop lands in a
 // line the wave writes completely (per-lane 576 B record stores wrote partial lines, read for
-// ownership: 2.5x the algorithmic HBM traffic).  LDS record strides 33 / 41 doubles are odd, so the
-// per-lane ds_write_b64 of one plane hits 32 distinct banks.
+// ownership: 2.5x the algorithmic HBM traffic).  Region A is staged at an odd record stride (33
+// doubles: the per-lane ds_write_b64 of one plane hits 32 distinct banks); region B at kJB = 40, so a
+// two-wave block takes exactly 40 KB and four blocks (the VGPR limit, 2 waves per SIMD) fit a CU's
+// 160 KB -- at 41 only three did.  Its per-lane plane writes then conflict 8-way, a few hundred LDS
+// cycles against the evaluation's tens of thousands.
 typedef double double2_t __attribute__((ext_vector_type(2)));
 typedef float float2_t __attribute__((ext_vector_type(2)));
 // two adjacent record planes, rounded to the record type
 __device__ __forceinline__ void store_planes(double* p, double a, double b) { *(double2_t*)p = double2_t{a, b}; }
 __device__ __forceinline__ void store_planes(float* p, double a, double b) { *(float2_t*)p = float2_t{(float)a, (float)b}; }
-constexpr int kVisBlock = 128;  // two waves, 2 x 21 KB of staging
+constexpr int kVisBlock = 128;  // two waves, 2 x 20 KB of staging
 
 __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int updateCache, int dontRetry, int64_t lo,
                                                                int64_t hi) {
-  __shared__ double stage[kVisBlock / 64][64 * (kJB + 1)];
+  __shared__ double stage[kVisBlock / 64][64 * kJB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t ob = lo + (int64_t)blockIdx.x * kVisBlock + wave * 64;  // the wave's first record
   const int64_t o = ob + lane;
@@ -213,7 +219,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   double* S = stage[wave];
   double acc[1] = {0.0};
   VisOut v;
-  v.Jintr = S + lane * (kJB + 1);  // region-B position of the record (intrinsics are planes 32..65)
+  v.Jintr = S + lane * kJB;  // region-B position of the record (intrinsics are planes 32..65)
   bool ok = false;
   double w = 0.0;
   if (o < hi) {
@@ -255,7 +261,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   }
   // region B (intrinsics already in place from the evaluation): scale by w, velocity, copy out
   if (lane < nrec) {
-    double* r = S + lane * (kJB + 1);
+    double* r = S + lane * kJB;
 #pragma unroll
     for (int i = 0; i < 34; i++) r[i] = ok ? w * r[i] : 0.0;
 #pragma unroll
@@ -268,7 +274,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
     rec_t* dst = d.Jt + d.nObsPad * kJA + ob * kJB;
     for (int q = lane; q < nrec * (kJB / 2); q += 64) {
       const int r = q / (kJB / 2), c = 2 * (q % (kJB / 2));
-      const double* src = S + r * (kJB + 1) + c;
+      const double* src = S + r * kJB + c;
       store_planes(dst + r * kJB + c, src[0], src[1]);
     }
   }
@@ -298,7 +304,11 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
       store_planes(dst + r * kJA + c, src[0], src[1]);
     }
   }
-  block_sum_atomic<1>(acc, d.red + 0);
+  // wave sum, one atomic per wave (no LDS: the staging owns all of it)
+  double x = acc[0];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+  if (lane == 0 && x != 0.0) atomicAdd(d.red + 0, x);
 }
 
 // cost pass: red[1] += cost, red[2..4] += stats (numTotal, numInvalid, numPrevInvalid)
