@@ -26,7 +26,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # kernel families of vb_profile_kernel
-KF_VISUAL_LIN, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACKSUB, KF_COST = range(9)
+KF_VISUAL_LIN, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACKSUB, KF_COST, KF_SMALL, KF_TRSM, \
+    KF_SYMV = range(12)
+SOLVERS = {"direct": 0, "pcg-trivial": 1, "pcg-jacobi": 2, "pcg-gauss-seidel": 3}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix peak (spec)
 
@@ -126,7 +128,14 @@ def main():
     ap.add_argument("--rs-tables", choices=("device", "host"), default="device",
                     help="device: rebuild the rolling-shutter tables from the IMU stream at the start of every "
                          "iteration (ark_vi_ba's preStepCallback); host: fixed precomputed tables")
+    ap.add_argument("--solver", choices=tuple(SOLVERS), default="direct",
+                    help="reduced-system solver (Optimizer::Settings solverType): the tile Cholesky, or PCG with "
+                         "the identity / block-Jacobi / block-Gauss-Seidel preconditioner")
+    ap.add_argument("--pcg-iterations", type=int, default=40, help="pcgMaxIterations (Optimizer.h:44)")
+    ap.add_argument("--pcg-residual", type=float, default=1e-10, help="pcgDesiredResidual (Optimizer.h:45)")
     args = ap.parse_args()
+    if args.solver != "direct" and args.profile_family == KF_GEMM:
+        args.profile_family = KF_SYMV  # no fan-in without the factorization: the PCG product instead
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -148,6 +157,7 @@ def main():
         log(f"[bench] mixed vs fp64, first LM step: {tolerance}")
     e = HipEngine(imu_calib_options=p.imu_calib_options, device=local, precision=args.precision)
     synth.load_into(e, p, rs_device=args.rs_tables == "device")
+    e.set_solver(SOLVERS[args.solver], args.pcg_iterations, args.pcg_residual)
     st = e.problem_stats()
     log(f"[bench] finalize {time.perf_counter() - t:.1f}s; reduced order {st[3]}, tiles {st[5]} "
         f"({st[4]} tile columns, {st[10]} levels), gemm pairs/factorization {st[6]}, Schur entries: landmark-tile {st[8]}, obs-pair {st[9]}")
@@ -196,6 +206,14 @@ def main():
                 "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
                           "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
                 "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches}
+    elif args.profile_family == KF_SYMV:
+        # every stored tile of S once (32 KB) + x and y rows (1 KB) per launch
+        b = st[5] * (64 * 64 * 8 + 2 * 64 * 8)
+        achieved = b / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("tile_symv_kernel"),
+                "kernel": "tile_symv_kernel (PCG product y += S x over the stored lower tiles)",
+                "bytes_per_launch": b, "avg_launch_ms": avg_ms, "launches": launches}
     else:
         b = visual_bytes_per_launch(p, st[0])
         achieved = b / (avg_ms * 1e-3) / 1e9
@@ -215,6 +233,12 @@ def main():
                      "vs_fp64": tolerance}
     else:
         out_extra = {}
+    if args.solver != "direct":
+        it, res = e.pcg_stats()
+        out_extra["solver"] = {"type": args.solver, "max_iterations": args.pcg_iterations,
+                               "desired_residual": args.pcg_residual, "last_iterations": it,
+                               "last_relative_residual": res}
+        log(f"[bench] last PCG solve: {it} iterations, relative residual {res:.3g}")
     out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
            "unit": "LM iterations/s", "n_gpus": 1, "steps": iters, "warmup": args.warmup,
            "ms_per_step": ms, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,

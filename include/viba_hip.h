@@ -263,6 +263,22 @@ int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red);
 /* sub-step: solve with the gradient computed by vb_gradient_dot_step using the existing factor,
  * negate, and store as the sub-step (Optimizer.cpp:958-972) */
 int vb_solve_with_new_gradient(vb_handle h);
+/* Reduced-system solver (Optimizer::Settings solverType / pcgMaxIterations / pcgDesiredResidual,
+ * Optimizer.h:31-45; Optimizer.cpp:211-331).  VB_SOLVER_DIRECT is the tile Cholesky.  The PCG types
+ * run the reference's PCG (PCG.cpp:15-104) on the Schur-reduced system after the point elimination,
+ * with the preconditioners of Preconditioner.h: identity, block Jacobi over the parameter blocks, and
+ * block Gauss-Seidel (the pseudo-factor -- diagonal blocks factored, off-diagonal blocks scaled, no
+ * updates -- here over the 64 x 64 tiles of this library's reduced ordering, as BaSpaCho's is over
+ * its supernodes).  The lower-precision-factor preconditioner is not built (VB_E_UNSUPPORTED).  Single
+ * handle only: VB_E_UNSUPPORTED on a landmark shard or a partitioned rank.  Any time after vb_create. */
+#define VB_SOLVER_DIRECT 0
+#define VB_SOLVER_PCG_TRIVIAL 1
+#define VB_SOLVER_PCG_JACOBI 2
+#define VB_SOLVER_PCG_GAUSS_SEIDEL 3
+#define VB_SOLVER_PCG_LOWER_PREC 4
+int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double pcg_desired_residual);
+/* iterations and relative residual of the last PCG solve (PCG::Result) */
+int vb_pcg_stats(vb_handle h, int32_t* iterations, double* relative_residual);
 /* step *= factor (in place) */
 int vb_scale_step(vb_handle h, double factor);
 /* applyStep(step) or applyStep(substep) (which = 0 / 1); ratios = {Linf, L2, L1} */

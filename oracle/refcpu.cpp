@@ -109,6 +109,13 @@ struct Problem {
   std::vector<double> cache;      // ResultCache per visual factor
   // factorization state
   std::vector<double> L;          // skyline factor
+  // reduced solver (Optimizer.h:31-45): 0 direct, 1 PCG trivial, 2 PCG block Jacobi
+  int solverType = 0, pcgMaxIt = 40;
+  double pcgTol = 1e-10;
+  int pcgIters = 0;
+  double pcgRel = 0.0;
+  std::vector<double> jacL;       // PCG Jacobi: LLT of every reduced parameter block (d x d, column-major)
+  std::vector<int64_t> jacOff;
   std::vector<double> Vchol;      // per point lower Cholesky (9 doubles)
   std::vector<double> step, substep, gradNew;
   // landmark shard (multi-device controller test): points [lmB, lmE) of the elimination range;
@@ -605,6 +612,95 @@ double computeCost(Problem& P, bool comparable, int64_t* stats) {
   return cost;
 }
 
+// ------------------------------------------------------------------ PCG (Optimizer.cpp:232-331)
+// Eigen::LLT in place (lower), no pivoting; the upper part is left as is
+void llt(Mat& B) {
+  const int n = B.r;
+  for (int j = 0; j < n; j++) {
+    double d = B(j, j);
+    for (int k = 0; k < j; k++) d -= B(j, k) * B(j, k);
+    B(j, j) = std::sqrt(d);
+    for (int i = j + 1; i < n; i++) {
+      double v = B(i, j);
+      for (int k = 0; k < j; k++) v -= B(i, k) * B(j, k);
+      B(i, j) = v / B(j, j);
+    }
+  }
+}
+
+// y = S x over the skyline lower storage of the damped Schur complement (solver.addMvFrom)
+void skylineSymv(const Problem& P, const std::vector<double>& x, std::vector<double>& y) {
+  y.assign(P.nRed, 0.0);
+  for (int64_t i = 0; i < P.nRed; i++) {
+    const int64_t fi = P.rowFirst[i];
+    const double* Si = &P.L[P.rowOff[i]];
+    double s = Si[i - fi] * x[i];
+    for (int64_t k = fi; k < i; k++) s += Si[k - fi] * x[k], y[k] += Si[k - fi] * x[i];
+    y[i] += s;
+  }
+}
+
+// Preconditioner::operator(): IdentityPrecond (Preconditioner.h:27-48) or BlockJacobiPrecond
+// (:50-112, per parameter block: L y = r, L^T z = y)
+void precond(const Problem& P, const std::vector<double>& r, std::vector<double>& z) {
+  z = r;
+  if (P.solverType != 2) return;
+  const int64_t nRP = (int64_t)P.redStart.size() - 1;
+  for (int64_t rp = 0; rp < nRP; rp++) {
+    const int64_t o = P.redStart[rp];
+    const int n = (int)(P.redStart[rp + 1] - o);
+    const double* L = &P.jacL[P.jacOff[rp]];  // column-major: L(i, k) = L[k * n + i]
+    double* t = &z[o];
+    for (int i = 0; i < n; i++) {
+      double v = t[i];
+      for (int k = 0; k < i; k++) v -= L[k * n + i] * t[k];
+      t[i] = v / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+      double v = t[i];
+      for (int k = i + 1; k < n; k++) v -= L[i * n + k] * t[k];
+      t[i] = v / L[i * n + i];
+    }
+  }
+}
+
+double vdot(const std::vector<double>& a, const std::vector<double>& b) {
+  double s = 0;
+  for (size_t i = 0; i < a.size(); i++) s += a[i] * b[i];
+  return s;
+}
+
+// PCG::solve (PCG.cpp:15-104), x_0 = 0; b is replaced by x
+void pcgSolve(Problem& P, std::vector<double>& b) {
+  const size_t n = b.size();
+  std::vector<double> x(n, 0.0), r = b, z, p, Ap;
+  precond(P, r, z);
+  p = z;
+  const double r0 = std::sqrt(vdot(r, r));
+  double zr = vdot(z, r), rel = 0.0;
+  for (int k = 0;; k++) {
+    skylineSymv(P, p, Ap);
+    const double alpha = zr / vdot(p, Ap);
+    for (size_t i = 0; i < n; i++) x[i] += p[i] * alpha, r[i] -= Ap[i] * alpha;
+    rel = std::sqrt(vdot(r, r)) / r0;
+    if (rel < P.pcgTol || k + 1 >= P.pcgMaxIt) {
+      P.pcgIters = k + 1, P.pcgRel = rel;
+      break;
+    }
+    precond(P, r, z);
+    const double zr1 = vdot(z, r), beta = zr1 / zr;
+    for (size_t i = 0; i < n; i++) p[i] = z[i] + p[i] * beta;
+    zr = zr1;
+  }
+  b = x;
+}
+
+bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<double>& rhs,
+                    std::vector<double>& x);
+bool solveOnly(Problem& P, const std::vector<double>& rhs, std::vector<double>& x) {
+  return factorAndSolve(P, 0.0, false, rhs, x);
+}
+
 // ------------------------------------------------------------------ direct solve
 // addDamping (Optimizer.cpp:136-146) + Schur elimination of points + skyline Cholesky + solve.
 // Returns false on numeric breakdown.
@@ -654,6 +750,22 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
             }
         }
     }
+    if (P.solverType != 0) {  // PCG: keep S (in P.L) unfactored; BlockJacobiPrecond::init
+      P.jacOff.assign(1, 0);
+      P.jacL.clear();
+      const int64_t nRP = (int64_t)P.redStart.size() - 1;
+      for (int64_t rp = 0; rp < nRP; rp++) {
+        const int64_t o = P.redStart[rp];
+        const int n = (int)(P.redStart[rp + 1] - o);
+        Mat B(n, n);
+        for (int i = 0; i < n; i++)
+          for (int j = 0; j <= i; j++) B(i, j) = P.rowFirst[o + i] <= o + j ? P.L[redElem(P, o + i, o + j)] : 0.0;
+        if (P.solverType == 2) llt(B);
+        for (int i = 0; i < n * n; i++) P.jacL.push_back(B.a[i]);
+        P.jacOff.push_back((int64_t)P.jacL.size());
+      }
+      return solveOnly(P, rhs, x);
+    }
     // skyline Cholesky (row-oriented)
     for (int64_t i = 0; i < P.nRed; i++) {
       const int64_t fi = P.rowFirst[i];
@@ -698,6 +810,9 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
       }
     }
   }
+  if (P.solverType != 0) {
+    pcgSolve(P, r);
+  } else {
   // forward / backward with the skyline factor
   for (int64_t i = 0; i < P.nRed; i++) {
     const int64_t fi = P.rowFirst[i];
@@ -711,6 +826,7 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
     const double* Li = &P.L[P.rowOff[i]];
     r[i] /= Li[i - fi];
     for (int64_t k = fi; k < i; k++) r[k] -= Li[k - fi] * r[i];
+  }
   }
   x.assign(P.order, 0.0);
   for (int64_t p = nPts; p < (int64_t)P.params.size(); p++) {
@@ -987,6 +1103,30 @@ int ref_gradient_dot_step(void* h, int dontRetry, double* backRed) {
   double d = 0;
   for (int64_t i = 0; i < P.order; i++) d += P.gradNew[i] * P.step[i];
   *backRed = -0.5 * d;
+  return 0;
+}
+
+int ref_set_solver(void* h, int type, int maxIt, double tol) {
+  Problem& P = *(Problem*)h;
+  if (type < 0 || type > 4) {
+    g_err = "unknown solver type";
+    return -1;
+  }
+  if (type == 3 || type == 4) {  // the tile Gauss-Seidel pseudo-factor / fp32 factor: GPU-side only
+    g_err = "oracle: PCG with the Gauss-Seidel or lower-precision preconditioner is not restated";
+    return -6;
+  }
+  if (maxIt < 1) {
+    g_err = "pcg_max_iterations must be >= 1";
+    return -1;
+  }
+  P.solverType = type, P.pcgMaxIt = maxIt, P.pcgTol = tol;
+  return 0;
+}
+int ref_pcg_stats(void* h, int32_t* iters, double* rel) {
+  Problem& P = *(Problem*)h;
+  if (iters) *iters = P.pcgIters;
+  if (rel) *rel = P.pcgRel;
   return 0;
 }
 

@@ -33,6 +33,10 @@ void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
                  hipStream_t st);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
+void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
+                      double* y, hipStream_t st);
+void launch_jacobi_init(const Dev& d, double* jac, hipStream_t st);
+void launch_jacobi_apply(const Dev& d, const double* jac, const double* r, double* z, hipStream_t st);
 void launch_tile_gather(const Dev& d, const int32_t* tiles, int64_t n, double* out, hipStream_t st);
 void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, const double* in, hipStream_t st);
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st);
@@ -266,6 +270,7 @@ struct vb_handle_s {
   double *dinv = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
+  bool sharded = false;  // vb_set_landmark_shard called
   bool isRoot = true;
   int partRank = 0, partWorld = 1;  // vb_set_partition (partitioned factorization), else 1
   std::vector<int8_t> colOwner;     // per tile column: owning rank, partWorld = ROOT (rank 0)
@@ -274,6 +279,15 @@ struct vb_handle_s {
   std::vector<int32_t> shardTiles;  // exact tiles of this (non-root) shard's partial system
   int32_t* shardTilesD = nullptr;
   double* shardPack = nullptr;      // packed copy of those tiles (vb_pack_shard_tiles)
+  // iterative reduced solve (vb_set_solver; pcg.hip): S x = rhsWork by PCG over the unfactored tiles
+  int solverType = VB_SOLVER_DIRECT, pcgMaxIt = 40;  // Optimizer.h:43-45 defaults
+  double pcgTol = 1e-10;
+  int32_t pcgIters = 0;
+  double pcgRelRes = 0.0;
+  int32_t *symvTilesD = nullptr, *symvRCD = nullptr;  // every stored tile and its (row, column) tile
+  int64_t nSymv = 0;
+  double *pcgR = nullptr, *pcgZ = nullptr, *pcgP = nullptr, *pcgAp = nullptr, *pcgB = nullptr;
+  double *jacL = nullptr, *tilesGS = nullptr;  // Jacobi block factors / Gauss-Seidel pseudo-factor
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
   hipGraphExec_t solveGraph = nullptr;
   bool useGraphs = true;
@@ -297,7 +311,7 @@ namespace {
 
 // kernel families for vb_profile_kernel
 enum { KF_VISUAL_LIN = 0, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACKSUB, KF_VISUAL_COST,
-       KF_SMALL, KF_TRSM, KF_COUNT };
+       KF_SMALL, KF_TRSM, KF_SYMV, KF_COUNT };
 
 inline void profBegin(vb_handle h, int fam) {
   if (h->profFamily != fam) return;
@@ -1458,6 +1472,121 @@ void backSubstitute(vb_handle h, int which) {
   launch_axpby((which ? d.subPt : d.stepPt) + p0, d.xp + p0, -1.0, 0.0, np, h->st);
 }
 
+// ---------------------------------------------------------------- iterative reduced solve
+// (Optimizer.cpp:232-331; pcg.hip)
+bool pcgMode(vb_handle h) { return h->solverType != VB_SOLVER_DIRECT; }
+
+// device buffers of the PCG path, on first use: the tile list of S x, the five vectors, and the
+// preconditioner storage of the selected type
+int pcgPrepare(vb_handle h) {
+  Dev& d = h->d;
+  if (h->partWorld > 1 || h->sharded)
+    return fail(VB_E_UNSUPPORTED, "the PCG solvers run on a single handle (no landmark shards, no partition)");
+  const int64_t nPad = (int64_t)d.nT * TS;
+  if (!h->symvTilesD) {
+    std::vector<int32_t> tl, rc;
+    for (int32_t J = 0; J < d.nT; J++)
+      for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++)
+        tl.push_back(h->colTilesH[c]), rc.push_back(h->colRowsH[c]), rc.push_back(J);
+    h->nSymv = (int64_t)tl.size();
+    if (upload(&h->symvTilesD, tl) || upload(&h->symvRCD, rc) || alloc0(&h->pcgR, nPad) || alloc0(&h->pcgZ, nPad) ||
+        alloc0(&h->pcgP, nPad) || alloc0(&h->pcgAp, nPad) || alloc0(&h->pcgB, nPad))
+      return VB_E_HIP;
+  }
+  if (h->solverType == VB_SOLVER_PCG_JACOBI && !h->jacL && alloc0(&h->jacL, nPad * 32)) return VB_E_HIP;
+  if (h->solverType == VB_SOLVER_PCG_GAUSS_SEIDEL && !h->tilesGS && alloc0(&h->tilesGS, d.nTiles * TS * TS))
+    return VB_E_HIP;
+  return 0;
+}
+
+// Preconditioner::init on the assembled (damped) S
+int precondInit(vb_handle h) {
+  Dev& d = h->d;
+  if (int rc = pcgPrepare(h)) return rc;
+  if (h->solverType == VB_SOLVER_PCG_JACOBI) {
+    launch_jacobi_init(d, h->jacL, h->st);
+  } else if (h->solverType == VB_SOLVER_PCG_GAUSS_SEIDEL) {
+    // pseudo-factor (BaSpaCho pseudoFactorFrom, Preconditioner.h:125-133): every diagonal tile
+    // factored, every off-diagonal tile times L_JJ^-T, no Schur updates -- so all columns at once
+    HIPCHK(hipMemcpyAsync(h->tilesGS, d.tiles, (size_t)d.nTiles * TS * TS * sizeof(double), hipMemcpyDeviceToDevice,
+                          h->st));
+    Dev g = d;
+    g.tiles = h->tilesGS;
+    const Sched& S = h->sch[0];
+    launch_potrf(g, S.potrfTileD, S.potrfColD, (int)S.lvP[S.nLevels], h->dinv, h->st);
+    launch_trsm(g, S.trsmDiagD, S.trsmTargetD, S.trsmColD, (int)S.lvT[S.nLevels], h->dinv, h->st);
+    launch_diag_inverse(g, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
+  }
+  return 0;
+}
+
+// z = M^-1 r (Preconditioner::operator())
+void precondApply(vb_handle h, const double* r, double* z) {
+  Dev& d = h->d;
+  const size_t bytes = (size_t)d.nT * TS * sizeof(double);
+  if (h->solverType == VB_SOLVER_PCG_GAUSS_SEIDEL) {
+    (void)hipMemcpyAsync(h->pcgB, r, bytes, hipMemcpyDeviceToDevice, h->st);
+    Dev g = d;
+    g.tiles = h->tilesGS;
+    const Sched& S = h->sch[0];
+    launch_solve_fanout(g, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD, h->rowTilesD,
+                        h->rowColD, h->linv, h->pcgB, h->yvec, z, h->solveFlags, h->numCUs * solveWgPerCU(), h->st, 3,
+                        nullptr, 0);
+    return;
+  }
+  (void)hipMemcpyAsync(z, r, bytes, hipMemcpyDeviceToDevice, h->st);
+  if (h->solverType == VB_SOLVER_PCG_JACOBI) launch_jacobi_apply(d, h->jacL, r, z, h->st);
+}
+
+// PCG::solve (PCG.cpp:15-104): S x = rhsWork -> xRed, x_0 = 0; stops when |r_k+1| / |r_0| is below
+// pcgDesiredResidual or after pcgMaxIterations products
+int pcgSolve(vb_handle h) {
+  Dev& d = h->d;
+  const int64_t n = (int64_t)d.nT * TS;
+  const size_t bytes = (size_t)n * sizeof(double);
+  double* x = d.xRed;
+  double *r = h->pcgR, *z = h->pcgZ, *p = h->pcgP, *Ap = h->pcgAp;
+  HIPCHK(hipMemsetAsync(x, 0, bytes, h->st));
+  HIPCHK(hipMemcpyAsync(r, h->rhsWork, bytes, hipMemcpyDeviceToDevice, h->st));
+  precondApply(h, r, z);
+  HIPCHK(hipMemcpyAsync(p, z, bytes, hipMemcpyDeviceToDevice, h->st));
+  HIPCHK(hipMemsetAsync(d.red + 32, 0, 4 * sizeof(double), h->st));
+  launch_dot(r, r, n, d.red + 32, h->st);
+  launch_dot(z, r, n, d.red + 33, h->st);
+  double s2[2];
+  if (int rc = readRed(h, s2, 32, 2)) return rc;
+  const double r0 = std::sqrt(s2[0]);
+  double zr = s2[1], rel = 0.0;
+  for (int k = 0;; k++) {
+    HIPCHK(hipMemsetAsync(Ap, 0, bytes, h->st));
+    profBegin(h, KF_SYMV);
+    launch_tile_symv(d.tiles, h->symvTilesD, h->symvRCD, h->nSymv, p, Ap, h->st);
+    profEnd(h, KF_SYMV);
+    HIPCHK(hipMemsetAsync(d.red + 32, 0, 3 * sizeof(double), h->st));
+    launch_dot(p, Ap, n, d.red + 32, h->st);
+    double pAp = 0;
+    if (int rc = readRed(h, &pAp, 32, 1)) return rc;
+    const double alpha = zr / pAp;
+    launch_axpby(x, p, alpha, 1.0, n, h->st);
+    launch_axpby(r, Ap, -alpha, 1.0, n, h->st);
+    launch_dot(r, r, n, d.red + 33, h->st);
+    double rn2 = 0;
+    if (int rc = readRed(h, &rn2, 33, 1)) return rc;
+    rel = std::sqrt(rn2) / r0;
+    if (rel < h->pcgTol || k + 1 >= h->pcgMaxIt) {
+      h->pcgIters = k + 1, h->pcgRelRes = rel;
+      return checkErr(h);
+    }
+    precondApply(h, r, z);
+    launch_dot(z, r, n, d.red + 34, h->st);
+    double zr1 = 0;
+    if (int rc = readRed(h, &zr1, 34, 1)) return rc;
+    const double beta = zr1 / zr;
+    launch_axpby(p, z, 1.0, beta, n, h->st);
+    zr = zr1;
+  }
+}
+
 double elapsed(hipEvent_t a, hipEvent_t b) {
   float ms = 0;
   hipEventElapsedTime(&ms, a, b);
@@ -1527,7 +1656,8 @@ int vb_destroy(vb_handle h) {
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
-                  h->rhsWork, h->linv, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD};
+                  h->rhsWork, h->linv, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
+                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int k = 0; k < 9; k++) {
@@ -1719,7 +1849,7 @@ int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_
   if (!h) return fail(VB_E_ARG, "null handle");
   if (h->finalized) return fail(VB_E_STATE, "vb_set_landmark_shard must precede vb_finalize");
   if (lm_begin < 0 || lm_begin > lm_end) return fail(VB_E_ARG, "bad landmark range");
-  h->lmBegin = lm_begin, h->lmEnd = lm_end, h->isRoot = is_root != 0;
+  h->lmBegin = lm_begin, h->lmEnd = lm_end, h->isRoot = is_root != 0, h->sharded = true;
   return 0;
 }
 
@@ -1775,10 +1905,18 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
     launch_schur(d, lambda, (h->isRoot || h->partWorld > 1) ? 1 : 0, h->st);
     profEnd(h, KF_SCHUR);
   HIPCHK(hipEventRecord(h->ev[3], h->st));
-  if (int rc = factorReduced(h)) return rc;
+  if (pcgMode(h)) {
+    if (int rc = precondInit(h)) return rc;
+  } else if (int rc = factorReduced(h)) {
+    return rc;
+  }
   HIPCHK(hipEventRecord(h->ev[4], h->st));
   HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  if (int rc = solveReduced(h)) return rc;
+  if (pcgMode(h)) {
+    if (int rc = pcgSolve(h)) return rc;
+  } else if (int rc = solveReduced(h)) {
+    return rc;
+  }
   backSubstitute(h, 0);
   HIPCHK(hipEventRecord(h->ev[5], h->st));
   double dotv = 0;
@@ -1819,10 +1957,32 @@ int vb_solve_with_new_gradient(vb_handle h) {
   launch_landmark(d, 0.0, 2, d.lmB, d.lmE, h->st);
   launch_reduced_grad(d, 1, h->st);
   HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  if (int rc = solveReduced(h)) return rc;
+  if (pcgMode(h)) {
+    if (int rc = pcgSolve(h)) return rc;
+  } else if (int rc = solveReduced(h)) {
+    return rc;
+  }
   backSubstitute(h, 1);
   HIPCHK(hipStreamSynchronize(h->st));
   return checkErr(h);
+}
+
+int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double pcg_desired_residual) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  if (solver_type < VB_SOLVER_DIRECT || solver_type > VB_SOLVER_PCG_LOWER_PREC) return fail(VB_E_ARG, "unknown solver type");
+  if (solver_type == VB_SOLVER_PCG_LOWER_PREC)
+    return fail(VB_E_UNSUPPORTED, "LowerPrecSolvePrecond is not built (use VB_SOLVER_PCG_GAUSS_SEIDEL or the direct solver)");
+  if (solver_type != VB_SOLVER_DIRECT && (h->partWorld > 1 || h->sharded))
+    return fail(VB_E_UNSUPPORTED, "the PCG solvers run on a single handle (no landmark shards, no partition)");
+  if (pcg_max_iterations < 1) return fail(VB_E_ARG, "pcg_max_iterations must be >= 1");
+  h->solverType = solver_type, h->pcgMaxIt = pcg_max_iterations, h->pcgTol = pcg_desired_residual;
+  return 0;
+}
+int vb_pcg_stats(vb_handle h, int32_t* iterations, double* relative_residual) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  if (iterations) *iterations = h->pcgIters;
+  if (relative_residual) *relative_residual = h->pcgRelRes;
+  return 0;
 }
 
 int vb_scale_step(vb_handle h, double f) {

@@ -199,6 +199,19 @@ class CEngineBase:
     def solve_with_new_gradient(self):
         self._check(self._fn("solve_with_new_gradient", [])(self.h))
 
+    # ---------------------------------------------------------------- reduced solver
+    def set_solver(self, solver_type: int, pcg_max_iterations: int = 40, pcg_desired_residual: float = 1e-10):
+        """Optimizer::Settings solverType / pcgMaxIterations / pcgDesiredResidual (Optimizer.h:31-45):
+        SOLVER_DIRECT, SOLVER_PCG_TRIVIAL, SOLVER_PCG_JACOBI, SOLVER_PCG_GAUSS_SEIDEL."""
+        self._check(self._fn("set_solver", [C.c_int, C.c_int, C.c_double])(
+            self.h, int(solver_type), int(pcg_max_iterations), float(pcg_desired_residual)))
+
+    def pcg_stats(self):
+        """(iterations, relative residual) of the last PCG solve (PCG::Result)."""
+        it, rel = C.c_int32(), C.c_double()
+        self._check(self._fn("pcg_stats", [C.POINTER(C.c_int32), _dp])(self.h, C.byref(it), C.byref(rel)))
+        return it.value, rel.value
+
     def scale_step(self, f: float):
         self._check(self._fn("scale_step", [C.c_double])(self.h, f))
 

@@ -32,3 +32,6 @@ def factor_num_vars(kind: int) -> int:
 
 def factor_num_consts(kind: int) -> int:
     return _NUM_CONSTS[kind]
+
+# reduced-system solvers (include/viba_hip.h VB_SOLVER_*; Optimizer.h:31-37 SolverType)
+SOLVER_DIRECT, SOLVER_PCG_TRIVIAL, SOLVER_PCG_JACOBI, SOLVER_PCG_GAUSS_SEIDEL, SOLVER_PCG_LOWER_PREC = range(5)
