@@ -37,6 +37,9 @@ void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_
                       double* y, hipStream_t st);
 void launch_jacobi_init(const Dev& d, double* jac, hipStream_t st);
 void launch_jacobi_apply(const Dev& d, const double* jac, const double* r, double* z, hipStream_t st);
+void launch_pcg_xr(double* x, double* r, const double* p, const double* Ap, const double* red, int zr, int pAp,
+                   int64_t n, double* rn2, hipStream_t st);
+void launch_pcg_p(double* p, const double* z, const double* red, int zrNew, int zr, int64_t n, hipStream_t st);
 void launch_tile_gather(const Dev& d, const int32_t* tiles, int64_t n, double* out, hipStream_t st);
 void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, const double* in, hipStream_t st);
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st);
@@ -247,6 +250,7 @@ struct vb_handle_s {
   int64_t nParams = 0, order = 0, nLmObs = 0, nLmEnt = 0, nObEnt = 0, nRedReal = 0, nParts = 0, nPadRows = 0;
   int64_t* padRowsD = nullptr;  // reduced rows that belong to no variable (tile alignment of parts)
   std::vector<int64_t> colStart;   // per tile column into colTilesH / colRowsH
+  std::vector<uint8_t> tileFill;   // per tile: 1 = created by the symbolic factorization (zero in S)
   std::vector<int32_t> colTilesH, colRowsH;
   // tile-Cholesky schedules: sch[0] the whole factorization (or, partitioned, this rank's subtree
   // plus its partial fan-in into the ROOT targets), sch[1] the ROOT separators (partitioned, rank 0)
@@ -284,7 +288,7 @@ struct vb_handle_s {
   double pcgTol = 1e-10;
   int32_t pcgIters = 0;
   double pcgRelRes = 0.0;
-  int32_t *symvTilesD = nullptr, *symvRCD = nullptr;  // every stored tile and its (row, column) tile
+  int32_t *symvTilesD = nullptr, *symvRCD = nullptr;  // the tiles of S (no fill) and their (row, column)
   int64_t nSymv = 0;
   double *pcgR = nullptr, *pcgZ = nullptr, *pcgP = nullptr, *pcgAp = nullptr, *pcgB = nullptr;
   double *jacL = nullptr, *tilesGS = nullptr;  // Jacobi block factors / Gauss-Seidel pseudo-factor
@@ -862,9 +866,13 @@ int doFinalize(vb_handle h) {
     for (int32_t I = J + 1; I < nT; I++)
       if (pat[(size_t)I * nT + J]) rows.push_back(I);
     for (size_t a = 0; a < rows.size(); a++)
-      for (size_t b = 0; b <= a; b++) pat[(size_t)rows[a] * nT + rows[b]] = 1;
+      for (size_t b = 0; b <= a; b++) {
+        uint8_t& q = pat[(size_t)rows[a] * nT + rows[b]];
+        q = q ? q : 2;  // 2: fill (zero in S; the PCG product skips it)
+      }
   }
   std::vector<int32_t> tileIdx((size_t)nT * nT, -1);
+  h->tileFill.clear();
   h->colStart.assign(nT + 1, 0);
   h->colTilesH.clear(), h->colRowsH.clear();
   int64_t nTiles = 0;
@@ -872,6 +880,7 @@ int doFinalize(vb_handle h) {
     for (int32_t I = J; I < nT; I++)
       if (I == J || pat[(size_t)I * nT + J]) {
         tileIdx[(size_t)I * nT + J] = (int32_t)nTiles;
+        h->tileFill.push_back(I != J && pat[(size_t)I * nT + J] == 2 ? 1 : 0);
         h->colTilesH.push_back((int32_t)nTiles++);
         h->colRowsH.push_back(I);
       }
@@ -1487,7 +1496,7 @@ int pcgPrepare(vb_handle h) {
     std::vector<int32_t> tl, rc;
     for (int32_t J = 0; J < d.nT; J++)
       for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++)
-        tl.push_back(h->colTilesH[c]), rc.push_back(h->colRowsH[c]), rc.push_back(J);
+        if (!h->tileFill[h->colTilesH[c]]) tl.push_back(h->colTilesH[c]), rc.push_back(h->colRowsH[c]), rc.push_back(J);
     h->nSymv = (int64_t)tl.size();
     if (upload(&h->symvTilesD, tl) || upload(&h->symvRCD, rc) || alloc0(&h->pcgR, nPad) || alloc0(&h->pcgZ, nPad) ||
         alloc0(&h->pcgP, nPad) || alloc0(&h->pcgAp, nPad) || alloc0(&h->pcgB, nPad))
@@ -1539,7 +1548,10 @@ void precondApply(vb_handle h, const double* r, double* z) {
 }
 
 // PCG::solve (PCG.cpp:15-104): S x = rhsWork -> xRed, x_0 = 0; stops when |r_k+1| / |r_0| is below
-// pcgDesiredResidual or after pcgMaxIterations products
+// pcgDesiredResidual or after pcgMaxIterations products.  alpha and beta are formed on the device
+// (red[32] = p.Ap, red[33] = r.r, red[36 + (k & 1)] = z.r of iteration k); the host reads r.r once per
+// iteration.  z = M^-1 r of the last iteration is computed before that test, so it is one
+// preconditioner application the reference does not make (it changes nothing returned).
 int pcgSolve(vb_handle h) {
   Dev& d = h->d;
   const int64_t n = (int64_t)d.nT * TS;
@@ -1550,40 +1562,32 @@ int pcgSolve(vb_handle h) {
   HIPCHK(hipMemcpyAsync(r, h->rhsWork, bytes, hipMemcpyDeviceToDevice, h->st));
   precondApply(h, r, z);
   HIPCHK(hipMemcpyAsync(p, z, bytes, hipMemcpyDeviceToDevice, h->st));
-  HIPCHK(hipMemsetAsync(d.red + 32, 0, 4 * sizeof(double), h->st));
-  launch_dot(r, r, n, d.red + 32, h->st);
-  launch_dot(z, r, n, d.red + 33, h->st);
-  double s2[2];
-  if (int rc = readRed(h, s2, 32, 2)) return rc;
-  const double r0 = std::sqrt(s2[0]);
-  double zr = s2[1], rel = 0.0;
+  HIPCHK(hipMemsetAsync(d.red + 32, 0, 6 * sizeof(double), h->st));
+  launch_dot(r, r, n, d.red + 33, h->st);
+  launch_dot(z, r, n, d.red + 36, h->st);
+  double r02 = 0;
+  if (int rc = readRed(h, &r02, 33, 1)) return rc;
+  const double r0 = std::sqrt(r02);
   for (int k = 0;; k++) {
+    const int zr = 36 + (k & 1), zrNew = 36 + ((k + 1) & 1);
     HIPCHK(hipMemsetAsync(Ap, 0, bytes, h->st));
     profBegin(h, KF_SYMV);
     launch_tile_symv(d.tiles, h->symvTilesD, h->symvRCD, h->nSymv, p, Ap, h->st);
     profEnd(h, KF_SYMV);
-    HIPCHK(hipMemsetAsync(d.red + 32, 0, 3 * sizeof(double), h->st));
+    HIPCHK(hipMemsetAsync(d.red + 32, 0, 2 * sizeof(double), h->st));
+    HIPCHK(hipMemsetAsync(d.red + zrNew, 0, sizeof(double), h->st));
     launch_dot(p, Ap, n, d.red + 32, h->st);
-    double pAp = 0;
-    if (int rc = readRed(h, &pAp, 32, 1)) return rc;
-    const double alpha = zr / pAp;
-    launch_axpby(x, p, alpha, 1.0, n, h->st);
-    launch_axpby(r, Ap, -alpha, 1.0, n, h->st);
-    launch_dot(r, r, n, d.red + 33, h->st);
+    launch_pcg_xr(x, r, p, Ap, d.red, zr, 32, n, d.red + 33, h->st);
+    precondApply(h, r, z);
+    launch_dot(z, r, n, d.red + zrNew, h->st);
     double rn2 = 0;
     if (int rc = readRed(h, &rn2, 33, 1)) return rc;
-    rel = std::sqrt(rn2) / r0;
+    const double rel = std::sqrt(rn2) / r0;
     if (rel < h->pcgTol || k + 1 >= h->pcgMaxIt) {
       h->pcgIters = k + 1, h->pcgRelRes = rel;
       return checkErr(h);
     }
-    precondApply(h, r, z);
-    launch_dot(z, r, n, d.red + 34, h->st);
-    double zr1 = 0;
-    if (int rc = readRed(h, &zr1, 34, 1)) return rc;
-    const double beta = zr1 / zr;
-    launch_axpby(p, z, 1.0, beta, n, h->st);
-    zr = zr1;
+    launch_pcg_p(p, z, d.red, zrNew, zr, n, h->st);
   }
 }
 

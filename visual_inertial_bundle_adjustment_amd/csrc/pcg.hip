@@ -5,25 +5,26 @@
 // (api.hip: the pseudo-factor of the tile store, potrf + trsm without updates, applied by the
 // fan-out triangular solves).  This file holds the two kernels the direct path has no use for:
 //
-//   tile_symv_kernel   y += S x over the stored lower tiles of S (one wave per tile; HBM-bound:
-//                      32 KB of tile per 2 x 8 KFLOP).  Lane r holds row r of the tile's 64 columns
-//                      in registers: the product A x_J is lane-local; A^T x_I is a transpose-reduce
-//                      across the wave (6 butterfly steps, 63 exchanges), so no LDS and no second
-//                      read of the tile.  Diagonal tiles use their lower triangle only.
+//   tile_symv_kernel   y += S x over the lower tiles of S, fill tiles skipped (one wave per tile;
+//                      HBM-bound: 32 KB of tile per 2 x 8 KFLOP).  Lane r holds row r of half the
+//                      tile's columns in registers: the product A x_J is lane-local; A^T x_I is a
+//                      transpose-reduce across the wave, so no LDS and no second read of the tile.
+//                      Diagonal tiles use their lower triangle only.
 //   jacobi_*_kernel    BlockJacobiPrecond::init / operator() (Preconditioner.h:62-112): the LLT of
 //                      every reduced variable's diagonal block (<= 32 x 32; one wave per variable,
 //                      lane = row, the block in LDS), then z = L^-T L^-1 r per block.
 #include "device_math.hpp"
 #include "engine.hpp"
+#include <algorithm>
 
 namespace viba {
 namespace {
 constexpr int kT = 64;
 
-// one step of the transpose-reduce: lanes with bit `W` of the lane id set keep the upper half of
-// their W * 2 partial columns, the others the lower half; each adds its partner's copy
-template <int W>
-__device__ __forceinline__ void treduce_step(double (&v)[64], int lane) {
+// one step of the transpose-reduce over N partial columns per lane: lanes with bit W of the lane id
+// set keep the upper half of their 2 W values, the others the lower half; each adds its partner's copy
+template <int W, int N>
+__device__ __forceinline__ void treduce_step(double (&v)[N], int lane) {
   const bool up = (lane & W) != 0;
 #pragma unroll
   for (int j = 0; j < W; j++) {
@@ -32,8 +33,19 @@ __device__ __forceinline__ void treduce_step(double (&v)[64], int lane) {
     v[j] = keep + __shfl_xor(send, W, 64);
   }
 }
+
+__device__ __forceinline__ double bcast(double v, int l) {
+  const int64_t b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
 }  // namespace
 
+// One wave per stored tile, the tile in two 32-column halves (64 VGPRs of tile per lane: two waves per
+// SIMD).  Per half: A(:, h) x_J(h) lane-local (x broadcast by readlane), and A(:, h)^T x_I by the
+// transpose-reduce: 5 butterfly steps leave lane l with column h0 + (l & 31) summed over the lanes
+// l' = l (mod 32), one more exchange with lane l ^ 32 completes it.
 __global__ void __launch_bounds__(256) tile_symv_kernel(const double* tiles, const int32_t* tileList,
                                                         const int32_t* tileRC, int64_t n, const double* x,
                                                         double* y) {
@@ -42,37 +54,34 @@ __global__ void __launch_bounds__(256) tile_symv_kernel(const double* tiles, con
   if (t >= n) return;
   const int64_t I = tileRC[2 * t], J = tileRC[2 * t + 1];
   const double* A = tiles + (int64_t)tileList[t] * kT * kT;
-  double v[64];
-#pragma unroll
-  for (int c = 0; c < 64; c++) v[c] = A[c * kT + lane];  // A(lane, c): column-major tile
   const bool diag = I == J;
-  if (diag) {  // lower triangle (c <= lane) only
+  const double xj = x[J * kT + lane], xi = x[I * kT + lane];
+  double yr = 0.0, yc = 0.0;
 #pragma unroll
-    for (int c = 0; c < 64; c++) v[c] = c <= lane ? v[c] : 0.0;
+  for (int h = 0; h < 2; h++) {
+    double v[32];
+#pragma unroll
+    for (int c = 0; c < 32; c++) v[c] = A[(32 * h + c) * kT + lane];  // A(lane, 32 h + c)
+#pragma unroll
+    for (int c = 0; c < 32; c++) {
+      const int col = 32 * h + c;
+      if (diag) v[c] = col <= lane ? v[c] : 0.0;  // lower triangle only
+      yr += v[c] * bcast(xj, col);
+      v[c] = (diag && col == lane) ? 0.0 : v[c] * xi;  // strict lower part for the transposed product
+    }
+    treduce_step<16>(v, lane);
+    treduce_step<8>(v, lane);
+    treduce_step<4>(v, lane);
+    treduce_step<2>(v, lane);
+    treduce_step<1>(v, lane);
+    const double full = v[0] + __shfl_xor(v[0], 32, 64);  // column 32 h + (lane & 31)
+    if ((lane >> 5) == h) yc = full;
   }
-  // A x_J (lane r: row r)
-  const double xj = x[J * kT + lane];
-  double yr = 0.0;
-#pragma unroll
-  for (int c = 0; c < 64; c++) {
-    const double xc = __shfl(xj, c, 64);
-    yr += v[c] * xc;
-  }
-  // A^T x_I (lane c: column c), strict lower part on diagonal tiles
-  const double xi = x[I * kT + lane];
-#pragma unroll
-  for (int c = 0; c < 64; c++) v[c] = (diag && c == lane) ? 0.0 : v[c] * xi;
-  treduce_step<32>(v, lane);
-  treduce_step<16>(v, lane);
-  treduce_step<8>(v, lane);
-  treduce_step<4>(v, lane);
-  treduce_step<2>(v, lane);
-  treduce_step<1>(v, lane);
   if (diag) {
-    atomicAdd(y + I * kT + lane, yr + v[0]);
+    atomicAdd(y + I * kT + lane, yr + yc);
   } else {
     atomicAdd(y + I * kT + lane, yr);
-    atomicAdd(y + J * kT + lane, v[0]);
+    atomicAdd(y + J * kT + lane, yc);
   }
 }
 
@@ -151,6 +160,41 @@ __global__ void __launch_bounds__(256) jacobi_apply_kernel(Dev d, const double* 
   if (lane < n) z[off + lane] = t;
 }
 
+// PCG vector steps with the scalars kept on the device (red: alpha = red[zr] / red[pAp], beta =
+// red[zrNew] / red[zr]), so an iteration syncs with the host once, for the convergence test
+__global__ void __launch_bounds__(256) pcg_xr_kernel(double* x, double* r, const double* p, const double* Ap,
+                                                     const double* red, int zr, int pAp, int64_t n, double* rn2) {
+  const double alpha = red[zr] / red[pAp];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    x[i] += p[i] * alpha;
+    const double ri = r[i] - Ap[i] * alpha;
+    r[i] = ri;
+    s += ri * ri;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+  __shared__ double sh[4];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(rn2, sh[0] + sh[1] + sh[2] + sh[3]);
+}
+__global__ void __launch_bounds__(256) pcg_p_kernel(double* p, const double* z, const double* red, int zrNew, int zr,
+                                                    int64_t n) {
+  const double beta = red[zrNew] / red[zr];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = z[i] + p[i] * beta;
+}
+
+void launch_pcg_xr(double* x, double* r, const double* p, const double* Ap, const double* red, int zr, int pAp,
+                   int64_t n, double* rn2, hipStream_t st) {
+  launchK(pcg_xr_kernel, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, x, r, p, Ap, red,
+          zr, pAp, n, rn2);
+}
+void launch_pcg_p(double* p, const double* z, const double* red, int zrNew, int zr, int64_t n, hipStream_t st) {
+  launchK(pcg_p_kernel, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, p, z, red, zrNew, zr,
+          n);
+}
 void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
                       double* y, hipStream_t st) {
   if (n > 0) launchK(tile_symv_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, tiles, tileList, tileRC, n, x, y);
