@@ -207,12 +207,12 @@ def main():
                           "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
                 "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches}
     elif args.profile_family == KF_SYMV:
-        # every stored tile of S once (32 KB) + x and y rows (1 KB) per launch
-        b = st[5] * (64 * 64 * 8 + 2 * 64 * 8)
+        # every tile of S (stored tiles less the symbolic fill) once (32 KB) + x and y rows (1 KB) per launch
+        b = st[11] * (64 * 64 * 8 + 2 * 64 * 8)
         achieved = b / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("tile_symv_kernel"),
-                "kernel": "tile_symv_kernel (PCG product y += S x over the stored lower tiles)",
+                "kernel": "tile_symv_kernel (PCG product y += S x over the lower tiles of S, fill skipped)",
                 "bytes_per_launch": b, "avg_launch_ms": avg_ms, "launches": launches}
     else:
         b = visual_bytes_per_launch(p, st[0])

@@ -385,7 +385,7 @@ int vb_profile_kernel(vb_handle h, int family);
 int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
 /* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs (per factorization),
  *  nSmallFactors, Schur landmark-pair entries, Schur observation-pair entries,
- *  update launches per factorization, trsm launches per factorization] */
+ *  fan-in launches per factorization, tiles of S without the symbolic fill] */
 int vb_problem_stats(vb_handle h, int64_t* out12);
 /* tuning aid: average kernel time [us] of one factorization kernel on scratch tiles
  * (which: 0 potrf, 1 trsm, 2 update + fused next-diagonal potrf, 3 update) */

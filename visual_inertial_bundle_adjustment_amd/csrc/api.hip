@@ -2142,9 +2142,11 @@ int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
   out[7] = sm;
   // Schur work-list sizes: landmark-pair entries, observation-pair entries
   out[8] = h->nTileEnt, out[9] = h->nObEnt;
-  // levels of the tile Cholesky (update / trsm launches per factorization), pairs per factorization
-  const int64_t nu = h->nLevels, nt = h->nLevels;
-  out[10] = nu, out[11] = nt;
+  // levels of the tile Cholesky (fan-in launches per factorization); tiles of S itself (the stored
+  // tiles less the symbolic fill: what the PCG product reads)
+  int64_t nS = 0;
+  for (uint8_t f : h->tileFill) nS += f ? 0 : 1;
+  out[10] = h->nLevels, out[11] = nS;
   return 0;
 }
 
