@@ -34,12 +34,14 @@ void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const
                  hipStream_t st);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
-                      double* y, hipStream_t st);
+                      double* y, const double* stop, hipStream_t st);
 void launch_jacobi_init(const Dev& d, double* jac, hipStream_t st);
 void launch_jacobi_apply(const Dev& d, const double* jac, const double* r, double* z, hipStream_t st);
 void launch_pcg_xr(double* x, double* r, const double* p, const double* Ap, const double* red, int zr, int pAp,
                    int64_t n, double* rn2, hipStream_t st);
-void launch_pcg_p(double* p, const double* z, const double* red, int zrNew, int zr, int64_t n, hipStream_t st);
+void launch_pcg_p(double* p, double* Ap, const double* z, const double* red, int zrNew, int zr, int64_t n,
+                  hipStream_t st);
+void launch_pcg_check(double* red, double r0, double tol, int k, int maxIt, int zrNew, hipStream_t st);
 void launch_tile_gather(const Dev& d, const int32_t* tiles, int64_t n, double* out, hipStream_t st);
 void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, const double* in, hipStream_t st);
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st);
@@ -1548,46 +1550,52 @@ void precondApply(vb_handle h, const double* r, double* z) {
 }
 
 // PCG::solve (PCG.cpp:15-104): S x = rhsWork -> xRed, x_0 = 0; stops when |r_k+1| / |r_0| is below
-// pcgDesiredResidual or after pcgMaxIterations products.  alpha and beta are formed on the device
-// (red[32] = p.Ap, red[33] = r.r, red[36 + (k & 1)] = z.r of iteration k); the host reads r.r once per
-// iteration.  z = M^-1 r of the last iteration is computed before that test, so it is one
-// preconditioner application the reference does not make (it changes nothing returned).
+// pcgDesiredResidual or after pcgMaxIterations products.  alpha, beta and the stop test live on the
+// device (red[32] = p.Ap, red[33] = r.r, red[36 + (k & 1)] = z.r of iteration k, red[40..42] the stop
+// slot, pcg.hip); the host queues kPcgBatch iterations between reads of the stop slot.  Iterations
+// queued after the stop leave x, r and p alone (their products and dots are skipped or discarded).
+// z = M^-1 r of the last iteration is computed before the test, one preconditioner application the
+// reference does not make (it changes nothing returned).  The Gauss-Seidel preconditioner (two
+// fan-out triangular solves) costs more than a host read, so it reads every iteration.
 int pcgSolve(vb_handle h) {
   Dev& d = h->d;
   const int64_t n = (int64_t)d.nT * TS;
   const size_t bytes = (size_t)n * sizeof(double);
   double* x = d.xRed;
   double *r = h->pcgR, *z = h->pcgZ, *p = h->pcgP, *Ap = h->pcgAp;
+  const int batch = h->solverType == VB_SOLVER_PCG_GAUSS_SEIDEL ? 1 : 8;
   HIPCHK(hipMemsetAsync(x, 0, bytes, h->st));
+  HIPCHK(hipMemsetAsync(Ap, 0, bytes, h->st));
   HIPCHK(hipMemcpyAsync(r, h->rhsWork, bytes, hipMemcpyDeviceToDevice, h->st));
   precondApply(h, r, z);
   HIPCHK(hipMemcpyAsync(p, z, bytes, hipMemcpyDeviceToDevice, h->st));
-  HIPCHK(hipMemsetAsync(d.red + 32, 0, 6 * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.red + 32, 0, 12 * sizeof(double), h->st));
   launch_dot(r, r, n, d.red + 33, h->st);
   launch_dot(z, r, n, d.red + 36, h->st);
   double r02 = 0;
   if (int rc = readRed(h, &r02, 33, 1)) return rc;
   const double r0 = std::sqrt(r02);
+  HIPCHK(hipMemsetAsync(d.red + 33, 0, sizeof(double), h->st));
   for (int k = 0;; k++) {
     const int zr = 36 + (k & 1), zrNew = 36 + ((k + 1) & 1);
-    HIPCHK(hipMemsetAsync(Ap, 0, bytes, h->st));
     profBegin(h, KF_SYMV);
-    launch_tile_symv(d.tiles, h->symvTilesD, h->symvRCD, h->nSymv, p, Ap, h->st);
+    launch_tile_symv(d.tiles, h->symvTilesD, h->symvRCD, h->nSymv, p, Ap, d.red + 40, h->st);
     profEnd(h, KF_SYMV);
-    HIPCHK(hipMemsetAsync(d.red + 32, 0, 2 * sizeof(double), h->st));
-    HIPCHK(hipMemsetAsync(d.red + zrNew, 0, sizeof(double), h->st));
     launch_dot(p, Ap, n, d.red + 32, h->st);
     launch_pcg_xr(x, r, p, Ap, d.red, zr, 32, n, d.red + 33, h->st);
+    launch_pcg_check(d.red, r0, h->pcgTol, k, h->pcgMaxIt, zrNew, h->st);
     precondApply(h, r, z);
     launch_dot(z, r, n, d.red + zrNew, h->st);
-    double rn2 = 0;
-    if (int rc = readRed(h, &rn2, 33, 1)) return rc;
-    const double rel = std::sqrt(rn2) / r0;
-    if (rel < h->pcgTol || k + 1 >= h->pcgMaxIt) {
-      h->pcgIters = k + 1, h->pcgRelRes = rel;
-      return checkErr(h);
+    launch_pcg_p(p, Ap, z, d.red, zrNew, zr, n, h->st);
+    if ((k + 1) % batch == 0 || k + 1 >= h->pcgMaxIt) {
+      double stop[3];
+      if (int rc = readRed(h, stop, 40, 3)) return rc;
+      if (stop[0] != 0.0) {
+        h->pcgIters = (int32_t)stop[1], h->pcgRelRes = stop[2];
+        return checkErr(h);
+      }
+      if (k + 1 >= h->pcgMaxIt) return fail(VB_E_HIP, "PCG: no stop after pcgMaxIterations");
     }
-    launch_pcg_p(p, z, d.red, zrNew, zr, n, h->st);
   }
 }
 

@@ -48,7 +48,8 @@ __device__ __forceinline__ double bcast(double v, int l) {
 // l' = l (mod 32), one more exchange with lane l ^ 32 completes it.
 __global__ void __launch_bounds__(256) tile_symv_kernel(const double* tiles, const int32_t* tileList,
                                                         const int32_t* tileRC, int64_t n, const double* x,
-                                                        double* y) {
+                                                        double* y, const double* stop) {
+  if (stop && *stop != 0.0) return;  // PCG converged: the remaining iterations of the batch are no-ops
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (t >= n) return;
@@ -161,9 +162,13 @@ __global__ void __launch_bounds__(256) jacobi_apply_kernel(Dev d, const double* 
 }
 
 // PCG vector steps with the scalars kept on the device (red: alpha = red[zr] / red[pAp], beta =
-// red[zrNew] / red[zr]), so an iteration syncs with the host once, for the convergence test
+// red[zrNew] / red[zr]) and the stop test too (pcg_check_kernel: red[kStop] = 1 once converged or
+// capped, red[kStop + 1] = iterations, red[kStop + 2] = |r| / |r0|), so the host queues a batch of
+// iterations and reads the stop slot once per batch.  x, r and p change only while red[kStop] == 0.
+constexpr int kStop = 40;
 __global__ void __launch_bounds__(256) pcg_xr_kernel(double* x, double* r, const double* p, const double* Ap,
                                                      const double* red, int zr, int pAp, int64_t n, double* rn2) {
+  if (red[kStop] != 0.0) return;
   const double alpha = red[zr] / red[pAp];
   double s = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -179,11 +184,26 @@ __global__ void __launch_bounds__(256) pcg_xr_kernel(double* x, double* r, const
   __syncthreads();
   if (threadIdx.x == 0) atomicAdd(rn2, sh[0] + sh[1] + sh[2] + sh[3]);
 }
-__global__ void __launch_bounds__(256) pcg_p_kernel(double* p, const double* z, const double* red, int zrNew, int zr,
-                                                    int64_t n) {
+// p = z + beta p, and Ap cleared for the next product
+__global__ void __launch_bounds__(256) pcg_p_kernel(double* p, double* Ap, const double* z, const double* red, int zrNew,
+                                                    int zr, int64_t n) {
+  if (red[kStop] != 0.0) return;
   const double beta = red[zrNew] / red[zr];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     p[i] = z[i] + p[i] * beta;
+    Ap[i] = 0.0;
+  }
+}
+// PCG.cpp:67-73 after iteration k: stop when |r_k+1| / |r_0| < tol or k + 1 == maxIterations.  Then
+// clears the accumulators of the next iteration: p.Ap, r.r, and the z.r slot iteration k fills
+// (its last reader was iteration k - 1's p update)
+__global__ void pcg_check_kernel(double* red, double r0, double tol, int k, int maxIt, int zrNew) {
+  if (threadIdx.x != 0) return;
+  if (red[kStop] == 0.0) {
+    const double rel = sqrt(red[33]) / r0;
+    if (rel < tol || k + 1 >= maxIt) red[kStop] = 1.0, red[kStop + 1] = k + 1, red[kStop + 2] = rel;
+  }
+  red[32] = 0.0, red[33] = 0.0, red[zrNew] = 0.0;
 }
 
 void launch_pcg_xr(double* x, double* r, const double* p, const double* Ap, const double* red, int zr, int pAp,
@@ -191,13 +211,18 @@ void launch_pcg_xr(double* x, double* r, const double* p, const double* Ap, cons
   launchK(pcg_xr_kernel, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, x, r, p, Ap, red,
           zr, pAp, n, rn2);
 }
-void launch_pcg_p(double* p, const double* z, const double* red, int zrNew, int zr, int64_t n, hipStream_t st) {
-  launchK(pcg_p_kernel, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, p, z, red, zrNew, zr,
-          n);
+void launch_pcg_p(double* p, double* Ap, const double* z, const double* red, int zrNew, int zr, int64_t n,
+                  hipStream_t st) {
+  launchK(pcg_p_kernel, dim3((unsigned)std::min<int64_t>(1024, (n + 255) / 256)), dim3(256), 0, st, p, Ap, z, red,
+          zrNew, zr, n);
+}
+void launch_pcg_check(double* red, double r0, double tol, int k, int maxIt, int zrNew, hipStream_t st) {
+  launchK(pcg_check_kernel, dim3(1), dim3(64), 0, st, red, r0, tol, k, maxIt, zrNew);
 }
 void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
-                      double* y, hipStream_t st) {
-  if (n > 0) launchK(tile_symv_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, tiles, tileList, tileRC, n, x, y);
+                      double* y, const double* stop, hipStream_t st) {
+  if (n > 0)
+    launchK(tile_symv_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, tiles, tileList, tileRC, n, x, y, stop);
 }
 void launch_jacobi_init(const Dev& d, double* jac, hipStream_t st) {
   if (d.nRV > 0) launchK(jacobi_init_kernel, dim3((unsigned)((d.nRV + 3) / 4)), dim3(256), 0, st, d, jac);
