@@ -1272,6 +1272,21 @@ int doFinalize(vb_handle h) {
   if (upload(&d.rvKind, h->rvKind) || upload(&d.rvHandle, h->rvHandle) || upload(&d.rvDim, h->rvDim) ||
       upload(&d.rvOff, h->rvOff) || upload(&d.rvRowEnd, rowEnd))
     return VB_E_HIP;
+  // visual_cost_kernel's order: the observations of each range the kernels run over ([obB, obE),
+  // [fB, fE) and the gaps between them), stably partitioned into global-shutter then rolling-shutter,
+  // so a wave takes one of the two evaluation paths instead of both
+  std::vector<int32_t> costOrder(nObs);
+  {
+    std::vector<int64_t> cuts = {0, d.obB, d.obE, d.fB, d.fE, nObs};
+    std::sort(cuts.begin(), cuts.end());
+    for (size_t c = 0; c + 1 < cuts.size(); c++) {
+      int64_t w = cuts[c];
+      for (int pass = 0; pass < 2; pass++)
+        for (int64_t i = cuts[c]; i < cuts[c + 1]; i++)
+          if ((obRS[i] >= 0) == (pass == 1)) costOrder[w++] = (int32_t)i;
+    }
+  }
+  if (upload(&d.obCostOrder, costOrder)) return VB_E_HIP;
   if (upload(&d.obPose, obPose) || upload(&d.obExtr, obExtr) || upload(&d.obIntr, obIntr) ||
       upload(&d.obVel, obVel) || upload(&d.obRS, obRS) || upload(&d.obPt, obPt) || upload(&d.obRed, obRed) ||
       upload(&d.obCol, obCol) || upload(&d.obC, obC))
@@ -1661,7 +1676,7 @@ int vb_destroy(vb_handle h) {
   hipSetDevice(h->cfg.device);
   hipStreamSynchronize(h->st);
   Dev& d = h->d;
-  void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obPose, d.obExtr, d.obIntr, d.obVel,
+  void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,

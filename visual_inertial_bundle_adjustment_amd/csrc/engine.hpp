@@ -119,6 +119,7 @@ struct Dev {
   int32_t *obPose = nullptr, *obExtr = nullptr, *obIntr = nullptr, *obVel = nullptr,
           *obRS = nullptr, *obPt = nullptr;
   int32_t* obRed = nullptr;  // 4 per obs
+  int32_t* obCostOrder = nullptr;  // visual_cost_kernel's order: per observation range, global shutter first
   int32_t* obCol = nullptr;  // 4 per obs (column offset in the landmark's Y panel, -1)
   double* obC = nullptr;     // 6 per obs
   double* cache = nullptr;   // ResultCache per obs

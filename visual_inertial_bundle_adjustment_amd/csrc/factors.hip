@@ -194,10 +194,11 @@ __device__ bool rs_eval(const Dev& d, const double* obsC, int rs, v3 X, const se
 
 // ------------------------------------------------------------------ visual kernels
 // Linearization of the visual factors, one observation per lane.  The whitened record is staged in
-// LDS per wave and written as full lines of the Jt regions (A: planes 0..31, B: 32..71): a wave's 64
-// records are one contiguous span of each region, so every 16 B store of the copy loop lands in a
-// line the wave writes completely (per-lane 576 B record stores wrote partial lines, read for
-// ownership: 2.5x the algorithmic HBM traffic).  Region A is staged at an odd record stride (33
+// LDS per wave and copied out record by record with 16 B lane stores (A: planes 0..31, B: 32..71), so
+// a record's lines are written whole (per-lane 576 B record stores wrote partial lines, read for
+// ownership: 2.5x the algorithmic HBM traffic).  Lanes take the observations in obCostOrder (each
+// range global shutter first), so a wave runs one of the two evaluation paths; the order leaves only
+// the record's position, which stays the observation's own slot.  Region A is staged at an odd record stride (33
 // doubles: the per-lane ds_write_b64 of one plane hits 32 distinct banks); region B at kJB = 40, so a
 // two-wave block takes exactly 40 KB and four blocks (the VGPR limit, 2 waves per SIMD) fit a CU's
 // 160 KB -- at 41 only three did.  Its per-lane plane writes then conflict 8-way, a few hundred LDS
@@ -213,16 +214,18 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
                                                                int64_t hi) {
   __shared__ double stage[kVisBlock / 64][64 * kJB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t ob = lo + (int64_t)blockIdx.x * kVisBlock + wave * 64;  // the wave's first record
-  const int64_t o = ob + lane;
+  const int64_t ob = lo + (int64_t)blockIdx.x * kVisBlock + wave * 64;  // the wave's first position
   const int nrec = (int)max<int64_t>(0, min<int64_t>(64, hi - ob));
+  // the observation of this lane: the range in obCostOrder (global shutter first), so a wave takes one
+  // evaluation path; its record still goes to the observation's own slot
+  const int32_t o = lane < nrec ? d.obCostOrder[ob + lane] : 0;
   double* S = stage[wave];
   double acc[1] = {0.0};
   VisOut v;
   v.Jintr = S + lane * kJB;  // region-B position of the record (intrinsics are planes 32..65)
   bool ok = false;
   double w = 0.0;
-  if (o < hi) {
+  if (lane < nrec) {
     ok = true;
     bool oor = false;
     const double c0 = d.cache[o];
@@ -271,11 +274,13 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   {
-    rec_t* dst = d.Jt + d.nObsPad * kJA + ob * kJB;
-    for (int q = lane; q < nrec * (kJB / 2); q += 64) {
-      const int r = q / (kJB / 2), c = 2 * (q % (kJB / 2));
-      const double* src = S + r * kJB + c;
-      store_planes(dst + r * kJB + c, src[0], src[1]);
+    // wave-uniform trip count: the shuffle must read o from an active lane
+    rec_t* dst = d.Jt + d.nObsPad * kJA;
+    const int nq = nrec * (kJB / 2);
+    for (int q0 = 0; q0 < nq; q0 += 64) {
+      const int q = q0 + lane, r = min(q / (kJB / 2), 63), c = 2 * (q % (kJB / 2));
+      const int64_t orec = __shfl(o, r, 64);
+      if (q < nq) store_planes(dst + orec * kJB + c, S[r * kJB + c], S[r * kJB + c + 1]);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -297,11 +302,11 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   {
-    rec_t* dst = d.Jt + ob * kJA;
-    for (int q = lane; q < nrec * (kJA / 2); q += 64) {
-      const int r = q / (kJA / 2), c = 2 * (q % (kJA / 2));
-      const double* src = S + r * (kJA + 1) + c;
-      store_planes(dst + r * kJA + c, src[0], src[1]);
+    const int nq = nrec * (kJA / 2);
+    for (int q0 = 0; q0 < nq; q0 += 64) {
+      const int q = q0 + lane, r = min(q / (kJA / 2), 63), c = 2 * (q % (kJA / 2));
+      const int64_t orec = __shfl(o, r, 64);
+      if (q < nq) store_planes(d.Jt + orec * kJA + c, S[r * (kJA + 1) + c], S[r * (kJA + 1) + c + 1]);
     }
   }
   // wave sum, one atomic per wave (no LDS: the staging owns all of it)
@@ -313,9 +318,10 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
 
 // cost pass: red[1] += cost, red[2..4] += stats (numTotal, numInvalid, numPrevInvalid)
 __global__ void __launch_bounds__(256) visual_cost_kernel(Dev d, int comparable, int64_t lo, int64_t hi) {
-  const int64_t o = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  if (o < hi) {
+  if (i < hi) {
+    const int64_t o = d.obCostOrder[i];  // a permutation of [lo, hi): global shutter first
     VisOut v;
     v.Jintr = nullptr;
     bool oor = false, ok;
