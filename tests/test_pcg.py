@@ -12,7 +12,8 @@ GPU (through the C-ABI, -m gpu):
     being unknowable here) through its size-independent property: converged, it reproduces the direct
     step, in fewer iterations than block Jacobi;
   - a full optimize with PCG Jacobi (40 iterations, as the reference's default) takes the oracle's
-    LM trajectory: same iteration count, final cost within 1e-7 relative.
+    LM trajectory: same iteration count, final cost within 1e-7 relative;
+  - the device stop test (iterations queued 8 at a time) stops at the oracle's iteration count.
 """
 from __future__ import annotations
 
@@ -148,3 +149,25 @@ def test_gpu_set_solver_errors():
     with pytest.raises(Exception):
         g.set_solver(7)
     g.set_solver(SOLVER_DIRECT)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tol", [1e-6, 1e-9])
+def test_gpu_pcg_stop_inside_a_batch_matches_oracle(tol):
+    """The device stop test (pcg_check_kernel) with iterations queued 8 at a time: a solve that
+    converges inside a batch reports the oracle's iteration count, and the queued iterations after
+    the stop leave the step unchanged."""
+    out = []
+    for cls in (hip(), RefEngine):
+        e, _ = make(cls, "A")
+        e.set_solver(SOLVER_PCG_JACOBI, 4000, tol)
+        m, st = steps(e, LAM)
+        out.append((e.pcg_stats(), m, st))
+    (itg, resg), mg, sg = out[0]
+    (itr, resr), mr, sr = out[1]
+    assert itg == itr and resg < tol
+    assert abs(resg - resr) <= 1e-6 * resr
+    assert abs(mg - mr) <= 1e-9 * abs(mr)
+    for k in range(NUM_VAR_KINDS - 1):
+        if sr[k].size:
+            assert rel(sg[k], sr[k]) < 1e-8, VAR_NAMES[k]
