@@ -277,6 +277,10 @@ int vb_solve_with_new_gradient(vb_handle h);
 #define VB_SOLVER_PCG_GAUSS_SEIDEL 3
 #define VB_SOLVER_PCG_LOWER_PREC 4
 int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double pcg_desired_residual);
+/* test fault injection: in iteration `iteration` (0-based, -1 = off) of the next vb_optimize calls the
+ * model cost reduction is negated, which takes the reference's "quadratic model failing numerically"
+ * branch (Optimizer.cpp:835-854: damping *= dampingAdjustOnFail, the step is kept) */
+int vb_debug_negate_model_reduction(vb_handle h, int iteration);
 /* iterations and relative residual of the last PCG solve (PCG::Result) */
 int vb_pcg_stats(vb_handle h, int32_t* iterations, double* relative_residual);
 /* step *= factor (in place) */

@@ -17,9 +17,49 @@
 namespace refcpu {
 
 // ------------------------------------------------------------------ dense column-major matrix
+// storage with an inline buffer (the factor Jacobians and their Gauss-Newton blocks fit it), so the
+// per-factor arithmetic does not go through the heap, as the reference's fixed-size Eigen types
+// don't; larger matrices spill to the heap
+class MatStore {
+ public:
+  static constexpr size_t kInline = 320;
+  MatStore() {}
+  MatStore(size_t n, double v) { resize(n, v); }
+  MatStore(const MatStore& o) { copyFrom(o); }
+  MatStore& operator=(const MatStore& o) {
+    if (this != &o) copyFrom(o);
+    return *this;
+  }
+  size_t size() const { return n_; }
+  double* data() { return p_; }
+  const double* data() const { return p_; }
+  double& operator[](size_t i) { return p_[i]; }
+  double operator[](size_t i) const { return p_[i]; }
+  double* begin() { return p_; }
+  double* end() { return p_ + n_; }
+  const double* begin() const { return p_; }
+  const double* end() const { return p_ + n_; }
+
+ private:
+  void resize(size_t n, double v) {
+    n_ = n;
+    if (n > kInline) heap_.assign(n, v), p_ = heap_.data();
+    else p_ = buf_, std::fill(buf_, buf_ + n, v);
+  }
+  void copyFrom(const MatStore& o) {
+    n_ = o.n_;
+    if (n_ > kInline) heap_.assign(o.p_, o.p_ + n_), p_ = heap_.data();
+    else p_ = buf_, std::copy(o.p_, o.p_ + n_, buf_);
+  }
+  size_t n_ = 0;
+  double* p_ = buf_;
+  double buf_[kInline];
+  std::vector<double> heap_;
+};
+
 struct Mat {
   int r = 0, c = 0;
-  std::vector<double> a;
+  MatStore a;
   Mat() {}
   Mat(int r_, int c_) : r(r_), c(c_), a((size_t)r_ * c_, 0.0) {}
   double& operator()(int i, int j) { return a[(size_t)j * r + i]; }

@@ -16,10 +16,18 @@
 //   factor functors                                          viba/problem/*Factor.cpp (ref_factors.hpp)
 // The sparse direct solve of BaSpaCho (absent, un-vendored) is restated as: exact Schur
 // elimination of the point range (3x3 Cholesky per point, as BaSpaCho's "sparse elimination"
-// of elimRanges {0, nPts}) followed by an envelope (skyline) Cholesky of the reduced system.
+// of elimRanges {0, nPts}) followed by a blocked envelope Cholesky of the reduced system.
+// Threads: 1 by default (the deterministic restatement the parity tests and golden fixtures use);
+// ref_set_threads(n) runs the factor loops, the point elimination and the block Cholesky on n
+// OpenMP threads (the reference's numThreads = 8 default, Optimizer.h:42) for the timed CPU baseline.
+#include <omp.h>
 #include <algorithm>
+#include <array>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstring>
+#include <exception>
 #include <map>
 #include <numeric>
 #include <string>
@@ -96,21 +104,32 @@ struct Problem {
   std::vector<int64_t> redPos;    // param -> position in reduced order (params >= nPts)
   std::vector<int64_t> redStart;  // reduced param -> row offset (in reduced order)
   std::vector<int64_t> rowFirst;  // envelope first column per reduced row
-  std::vector<int64_t> rowOff;    // offset of row i's first stored element
   int64_t nRed = 0;               // reduced dims
-  std::vector<double> Hred;       // skyline storage (lower, by rows)
+  // block-envelope storage of the lower reduced system: block rows of kB rows; block row i keeps the
+  // kB x kB row-major blocks of block columns [bFirst[i], i] (the envelope of its rows, which the
+  // Cholesky factor keeps), block (i, j) at block offset bOff[i] + j - bFirst[i]; rows past nRed of
+  // the last block row are identity padding
+  int64_t nb = 0;
+  std::vector<int64_t> bFirst, bOff;
+  std::vector<std::vector<int64_t>> colRows;  // block column k -> block rows i > k with bFirst[i] <= k
+  std::vector<std::vector<int64_t>> rowPts;   // block row -> points whose coupled rows meet it (ascending)
+  std::vector<double> Hred;       // block-envelope storage (lower), assembled Hessian
+  int threads = 1;                // OpenMP threads (1: the deterministic single-thread restatement)
+  double phaseMs[8] = {0};        // last iteration: linearize, schur, factor, solve, step, cost, total, rs
   std::vector<double> Vpt;        // point diag blocks 3x3 (nPts*9)
   // point -> coupled reduced params (sorted) and W block offsets
   std::vector<int64_t> ptCoupStart;
   std::vector<int64_t> ptCoupParam;
   std::vector<int64_t> ptCoupOff;
   std::vector<double> W;          // blocks 3 x d (col-major) per (point, reduced param)
+  std::vector<double> Yp;         // Y = L_V^-1 W per (point, reduced param), W's layout (last factor)
   std::vector<double> grad;       // full gradient (param order)
   std::vector<double> cache;      // ResultCache per visual factor
   // factorization state
   std::vector<double> L;          // skyline factor
   // reduced solver (Optimizer.h:31-45): 0 direct, 1 PCG trivial, 2 PCG block Jacobi
   int solverType = 0, pcgMaxIt = 40;
+  int faultNegModelRedIt = -1;  // ref_debug_negate_model_reduction
   double pcgTol = 1e-10;
   int pcgIters = 0;
   double pcgRel = 0.0;
@@ -340,8 +359,19 @@ double squaredError(const EvalOut& o) {
 }
 
 // ------------------------------------------------------------------ registration / structure
+constexpr int kB = 64;  // block size of the block-envelope storage
+inline int64_t blkIdx(const Problem& P, int64_t ib, int64_t jb) { return P.bOff[ib] + jb - P.bFirst[ib]; }
 int64_t redElem(const Problem& P, int64_t i, int64_t j) {  // reduced (row, col), row >= col
-  return P.rowOff[i] + (j - P.rowFirst[i]);
+  return (blkIdx(P, i / kB, j / kB) * kB + (i % kB)) * kB + (j % kB);
+}
+// x += v, atomically when the caller runs several threads (the role of LockedSharedOps, AtomicOps.h:80-112)
+inline void addTo(const Problem& P, double& x, double v) {
+  if (P.threads > 1) {
+#pragma omp atomic
+    x += v;
+  } else {
+    x += v;
+  }
 }
 
 void finalize(Problem& P) {
@@ -458,15 +488,34 @@ void finalize(Problem& P) {
     P.ptCoupStart[pt + 1] = (int64_t)P.ptCoupParam.size();
   }
   P.W.assign(woff, 0.0);
+  P.Yp.assign(woff, 0.0);
   // rows
   P.rowFirst.assign(P.nRed, 0);
-  P.rowOff.assign(P.nRed + 1, 0);
   for (size_t i = 0; i < red.size(); i++) {
     int64_t fc = P.redStart[firstBlk[i]];
     for (int64_t r = P.redStart[i]; r < P.redStart[i + 1]; r++) P.rowFirst[r] = fc;
   }
-  for (int64_t r = 0; r < P.nRed; r++) P.rowOff[r + 1] = P.rowOff[r] + (r - P.rowFirst[r] + 1);
-  P.Hred.assign(P.rowOff[P.nRed], 0.0);
+  // block envelope: the first block column of a block row is that of its widest row
+  P.nb = (P.nRed + kB - 1) / kB;
+  P.bFirst.assign(P.nb, 0);
+  P.bOff.assign(P.nb + 1, 0);
+  for (int64_t ib = 0; ib < P.nb; ib++) {
+    int64_t f = ib;
+    for (int64_t r = ib * kB; r < std::min(P.nRed, (ib + 1) * kB); r++) f = std::min(f, P.rowFirst[r] / kB);
+    P.bFirst[ib] = f;
+    P.bOff[ib + 1] = P.bOff[ib] + (ib - f + 1);
+  }
+  P.colRows.assign(P.nb, {});
+  for (int64_t ib = 0; ib < P.nb; ib++)
+    for (int64_t k = P.bFirst[ib]; k < ib; k++) P.colRows[k].push_back(ib);
+  P.rowPts.assign(P.nb, {});
+  for (int64_t pt = 0; pt < P.nPts; pt++)
+    for (int64_t q = P.ptCoupStart[pt]; q < P.ptCoupStart[pt + 1]; q++) {
+      const int64_t rp = P.ptCoupParam[q];
+      for (int64_t ib = P.redStart[rp] / kB; ib <= (P.redStart[rp + 1] - 1) / kB; ib++)
+        if (P.rowPts[ib].empty() || P.rowPts[ib].back() != pt) P.rowPts[ib].push_back(pt);
+    }
+  P.Hred.assign((size_t)P.bOff[P.nb] * kB * kB, 0.0);
   P.Vpt.assign(P.nPts * 9, 0.0);
   P.grad.assign(P.order, 0.0);
   P.cache.assign(P.fvars[0].size() / 5, 0.0);
@@ -481,7 +530,7 @@ void addHessBlock(Problem& P, int64_t pa, int64_t pb, const Mat& B) {
   const bool aPt = pa < P.nPts, bPt = pb < P.nPts;
   if (aPt && bPt) {  // point diagonal (only a == b possible)
     for (int i = 0; i < 3; i++)
-      for (int j = 0; j < 3; j++) P.Vpt[pa * 9 + j * 3 + i] += B(i, j);
+      for (int j = 0; j < 3; j++) addTo(P, P.Vpt[pa * 9 + j * 3 + i], B(i, j));
     return;
   }
   if (aPt || bPt) {  // point-reduced coupling: store W = H_{pt, red} (3 x d)
@@ -493,7 +542,7 @@ void addHessBlock(Problem& P, int64_t pa, int64_t pb, const Mat& B) {
     double* w = &P.W[P.ptCoupOff[q]];
     const int d = aPt ? B.c : B.r;
     for (int j = 0; j < d; j++)
-      for (int i = 0; i < 3; i++) w[j * 3 + i] += aPt ? B(i, j) : B(j, i);
+      for (int i = 0; i < 3; i++) addTo(P, w[j * 3 + i], aPt ? B(i, j) : B(j, i));
     return;
   }
   const int64_t ra = P.redStart[P.redPos[pa]], rb = P.redStart[P.redPos[pb]];
@@ -504,7 +553,7 @@ void addHessBlock(Problem& P, int64_t pa, int64_t pb, const Mat& B) {
         if (pa == pb) continue;  // diagonal block: upper half implied
         std::swap(r, c);
       }
-      P.Hred[redElem(P, r, c)] += B(i, j);
+      addTo(P, P.Hred[redElem(P, r, c)], B(i, j));
     }
 }
 
@@ -540,7 +589,7 @@ double singleGradHess(Problem& P, int fk, int64_t k, double* g, bool hess, bool 
     A[s] = o.P.r ? mul(o.P, o.fe.J[s]) : o.fe.J[s];
     A[s] = scale(A[s], drho);
     Mat gs = tmul(A[s], e);  // iAdjJac^T e
-    for (int i = 0; i < gs.r; i++) g[P.pstart[pi[s]] + i] += gs(i, 0);
+    for (int i = 0; i < gs.r; i++) addTo(P, g[P.pstart[pi[s]] + i], gs(i, 0));
     if (hess) {
       for (int t = 0; t < s; t++) {
         if (!wants[t]) continue;
@@ -563,53 +612,83 @@ bool inShard(const Problem& P, int fk, int64_t k) {
   return pi >= P.lmB && pi < (P.lmE < 0 ? P.nPts : P.lmE);
 }
 
+// the factor loop of FactorStore::computeGradHess / computeCost (Factor.h:704-734, 664-701): serial, or
+// an OpenMP loop over chunks (the dispenso parallel_for of Factor.h:714-724) with per-thread partial
+// sums; the first exception of any thread (rolling-shutter lookups throw) is rethrown after the loop
+// f(k, acc) adds into acc[0..3]; the per-thread accumulators are summed in thread order at the end
+template <class F>
+void factorLoop(const Problem& P, int64_t n, double acc[4], F&& f) {
+  if (P.threads <= 1) {
+    for (int64_t k = 0; k < n; k++) f(k, acc);
+    return;
+  }
+  std::exception_ptr err;
+  std::vector<std::array<double, 4>> part(P.threads, std::array<double, 4>{0, 0, 0, 0});
+#pragma omp parallel num_threads(P.threads)
+  {
+    double* a = part[omp_get_thread_num()].data();
+#pragma omp for schedule(dynamic, 256)
+    for (int64_t k = 0; k < n; k++) {
+      try {
+        f(k, a);
+      } catch (...) {
+#pragma omp critical(refcpu_err)
+        if (!err) err = std::current_exception();
+      }
+    }
+  }
+  if (err) std::rethrow_exception(err);
+  for (const auto& a : part)
+    for (int i = 0; i < 4; i++) acc[i] += a[i];
+}
+
 double computeGradHess(Problem& P, double* g, bool hess, bool updateCache, bool dontRetry) {
   if (hess) {
     std::fill(P.Hred.begin(), P.Hred.end(), 0.0);
     std::fill(P.Vpt.begin(), P.Vpt.end(), 0.0);
     std::fill(P.W.begin(), P.W.end(), 0.0);
   }
-  double cost = 0;
+  double acc[4] = {0, 0, 0, 0};
   for (int fk = 0; fk < 14; fk++) {
     const int64_t n = (int64_t)P.fvars[fk].size() / kNumVars[fk];
-    for (int64_t k = 0; k < n; k++)
-      if (inShard(P, fk, k)) cost += singleGradHess(P, fk, k, g, hess, updateCache, dontRetry);
+    factorLoop(P, n, acc, [&](int64_t k, double* a) {
+      if (inShard(P, fk, k)) a[0] += singleGradHess(P, fk, k, g, hess, updateCache, dontRetry);
+    });
   }
-  return cost;
+  return acc[0];
 }
 
 // computeSingleCost (Factor.h:390-417) summed as computeCost (Factor.h:664-701)
 double computeCost(Problem& P, bool comparable, int64_t* stats) {
-  double cost = 0;
-  int64_t nTot = 0, nInv = 0, nPrevInv = 0;
+  double acc[4] = {0, 0, 0, 0};  // cost, numTotal, numInvalid, numPrevInvalid
   for (int fk = 0; fk < 14; fk++) {
     const int nv = kNumVars[fk];
     const int64_t n = (int64_t)P.fvars[fk].size() / nv;
-    bool wants[10] = {false};
-    for (int64_t k = 0; k < n; k++) {
-      if (!inShard(P, fk, k)) continue;
-      nTot++;
+    factorLoop(P, n, acc, [&](int64_t k, double* a) {
+      if (!inShard(P, fk, k)) return;
+      a[1] += 1.0;
+      bool wants[10] = {false};
       EvalOut o = evalFactor(P, fk, k, wants);
       if (fk == 0) {
         const double prev = P.cache[k];
         const bool prevInvalid = prev < 0.0;
-        nInv += o.fe.ok ? 0 : 1;
-        nPrevInv += prevInvalid ? 1 : 0;
+        a[2] += o.fe.ok ? 0.0 : 1.0;
+        a[3] += prevInvalid ? 1.0 : 0.0;
         if (comparable) {
-          if (prevInvalid) continue;
+          if (prevInvalid) return;
           if (!o.fe.ok) {
-            cost += prev;
-            continue;
+            a[0] += prev;
+            return;
           }
         }
-        if (!o.fe.ok) continue;
+        if (!o.fe.ok) return;
       }
       const double s2 = squaredError(o);
-      cost += (o.loss ? o.loss->val(s2) : s2) * 0.5;
-    }
+      a[0] += (o.loss ? o.loss->val(s2) : s2) * 0.5;
+    });
   }
-  if (stats) stats[0] = nTot, stats[1] = nInv, stats[2] = nPrevInv;
-  return cost;
+  if (stats) stats[0] = (int64_t)acc[1], stats[1] = (int64_t)acc[2], stats[2] = (int64_t)acc[3];
+  return acc[0];
 }
 
 // ------------------------------------------------------------------ PCG (Optimizer.cpp:232-331)
@@ -628,16 +707,160 @@ void llt(Mat& B) {
   }
 }
 
-// y = S x over the skyline lower storage of the damped Schur complement (solver.addMvFrom)
-void skylineSymv(const Problem& P, const std::vector<double>& x, std::vector<double>& y) {
-  y.assign(P.nRed, 0.0);
-  for (int64_t i = 0; i < P.nRed; i++) {
-    const int64_t fi = P.rowFirst[i];
-    const double* Si = &P.L[P.rowOff[i]];
-    double s = Si[i - fi] * x[i];
-    for (int64_t k = fi; k < i; k++) s += Si[k - fi] * x[k], y[k] += Si[k - fi] * x[i];
-    y[i] += s;
+// ------------------------------------------------------------------ block-envelope dense kernels
+// (the supernodal Cholesky of BaSpaCho, Optimizer.cpp:200-231, restated as a right-looking blocked
+// Cholesky over the envelope; kB x kB row-major blocks, diagonal blocks hold their lower triangle)
+typedef double v4d __attribute__((vector_size(32)));
+inline v4d ld4(const double* p) {
+  v4d v;
+  std::memcpy(&v, p, sizeof(v));
+  return v;
+}
+inline void st4(double* p, v4d v) { std::memcpy(p, &v, sizeof(v)); }
+
+// C -= A B^T
+void gemmNT(double* __restrict C, const double* __restrict A, const double* __restrict B) {
+  alignas(64) double Bt[kB * kB];
+  for (int j = 0; j < kB; j++)
+    for (int k = 0; k < kB; k++) Bt[k * kB + j] = B[j * kB + k];
+  for (int i = 0; i < kB; i += 4)
+    for (int j0 = 0; j0 < kB; j0 += 16) {
+      v4d c[4][4];
+      for (int r = 0; r < 4; r++)
+        for (int q = 0; q < 4; q++) c[r][q] = ld4(C + (i + r) * kB + j0 + 4 * q);
+      for (int k = 0; k < kB; k++) {
+        v4d b[4];
+        for (int q = 0; q < 4; q++) b[q] = ld4(Bt + k * kB + j0 + 4 * q);
+        for (int r = 0; r < 4; r++) {
+          const double a = A[(i + r) * kB + k];
+          const v4d av = {a, a, a, a};
+          for (int q = 0; q < 4; q++) c[r][q] -= av * b[q];
+        }
+      }
+      for (int r = 0; r < 4; r++)
+        for (int q = 0; q < 4; q++) st4(C + (i + r) * kB + j0 + 4 * q, c[r][q]);
+    }
+}
+// in-place lower Cholesky of a diagonal block (left-looking, row dot products)
+bool potrfBlk(double* A) {
+  for (int j = 0; j < kB; j++) {
+    double* Aj = A + j * kB;
+    double d = Aj[j];
+    for (int k = 0; k < j; k++) d -= Aj[k] * Aj[k];
+    if (!(d > 0)) return false;
+    const double l = std::sqrt(d);
+    Aj[j] = l;
+    for (int i = j + 1; i < kB; i++) {
+      double* Ai = A + i * kB;
+      double v = Ai[j];
+      for (int k = 0; k < j; k++) v -= Ai[k] * Aj[k];
+      Ai[j] = v / l;
+    }
   }
+  return true;
+}
+// X = A L^-T (L lower, from potrfBlk)
+void trsmBlk(double* A, const double* L) {
+  for (int r = 0; r < kB; r++) {
+    double* x = A + r * kB;
+    for (int j = 0; j < kB; j++) {
+      const double* Lj = L + j * kB;
+      double v = x[j];
+      for (int m = 0; m < j; m++) v -= x[m] * Lj[m];
+      x[j] = v / Lj[j];
+    }
+  }
+}
+inline double* blkPtr(const Problem& P, std::vector<double>& S, int64_t ib, int64_t jb) {
+  return &S[(size_t)blkIdx(P, ib, jb) * kB * kB];
+}
+inline const double* blkPtr(const Problem& P, const std::vector<double>& S, int64_t ib, int64_t jb) {
+  return &S[(size_t)blkIdx(P, ib, jb) * kB * kB];
+}
+// identity rows of the last block row's padding
+void padIdentity(const Problem& P, std::vector<double>& S) {
+  for (int64_t r = P.nRed; r < P.nb * kB; r++) S[redElem(P, r, r)] = 1.0;
+}
+// right-looking blocked Cholesky: for every block column k, L_kk = chol(A_kk), L_ik = A_ik L_kk^-T for
+// the block rows below inside the envelope, then A_ij -= L_ik L_jk^T over their pairs (parallel over
+// blocks; every block is updated in ascending k, so the result does not depend on the thread count)
+bool beFactor(const Problem& P, std::vector<double>& S) {
+  for (int64_t k = 0; k < P.nb; k++) {
+    double* Lkk = blkPtr(P, S, k, k);
+    if (!potrfBlk(Lkk)) return false;
+    const std::vector<int64_t>& rows = P.colRows[k];
+    const int64_t nr = (int64_t)rows.size();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(P.threads) if (P.threads > 1 && nr > 1)
+    for (int64_t a = 0; a < nr; a++) trsmBlk(blkPtr(P, S, rows[a], k), Lkk);
+    const int64_t np = nr * (nr + 1) / 2;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(P.threads) if (P.threads > 1 && np > 1)
+    for (int64_t t = 0; t < np; t++) {
+      int64_t a = (int64_t)((std::sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+      while (a * (a + 1) / 2 > t) a--;
+      while ((a + 1) * (a + 2) / 2 <= t) a++;
+      const int64_t b = t - a * (a + 1) / 2;
+      gemmNT(blkPtr(P, S, rows[a], rows[b]), blkPtr(P, S, rows[a], k), blkPtr(P, S, rows[b], k));
+    }
+  }
+  return true;
+}
+// L L^T x = r in place (r padded to nb * kB)
+void beSolve(const Problem& P, const std::vector<double>& L, std::vector<double>& r) {
+  for (int64_t ib = 0; ib < P.nb; ib++) {
+    double* ri = &r[ib * kB];
+    for (int64_t jb = P.bFirst[ib]; jb < ib; jb++) {
+      const double* B = blkPtr(P, L, ib, jb);
+      const double* xj = &r[jb * kB];
+      for (int i = 0; i < kB; i++) {
+        double s = 0.0;
+        for (int c = 0; c < kB; c++) s += B[i * kB + c] * xj[c];
+        ri[i] -= s;
+      }
+    }
+    const double* D = blkPtr(P, L, ib, ib);
+    for (int i = 0; i < kB; i++) {
+      double s = ri[i];
+      for (int c = 0; c < i; c++) s -= D[i * kB + c] * ri[c];
+      ri[i] = s / D[i * kB + i];
+    }
+  }
+  for (int64_t ib = P.nb - 1; ib >= 0; ib--) {
+    double* xi = &r[ib * kB];
+    const double* D = blkPtr(P, L, ib, ib);
+    for (int i = kB - 1; i >= 0; i--) {
+      xi[i] /= D[i * kB + i];
+      for (int c = 0; c < i; c++) xi[c] -= D[i * kB + c] * xi[i];
+    }
+    for (int64_t jb = P.bFirst[ib]; jb < ib; jb++) {
+      const double* B = blkPtr(P, L, ib, jb);
+      double* yj = &r[jb * kB];
+      for (int i = 0; i < kB; i++)
+        for (int c = 0; c < kB; c++) yj[c] -= B[i * kB + c] * xi[i];
+    }
+  }
+}
+// y = S x over the lower block-envelope storage of the damped Schur complement (solver.addMvFrom);
+// x, y of size nRed
+void skylineSymv(const Problem& P, const std::vector<double>& x, std::vector<double>& y) {
+  std::vector<double> xp(P.nb * kB, 0.0), yp(P.nb * kB, 0.0);
+  std::copy(x.begin(), x.end(), xp.begin());
+  for (int64_t ib = 0; ib < P.nb; ib++) {
+    const double* xi = &xp[ib * kB];
+    double* yi = &yp[ib * kB];
+    for (int64_t jb = P.bFirst[ib]; jb < ib; jb++) {
+      const double* B = blkPtr(P, P.L, ib, jb);
+      const double* xj = &xp[jb * kB];
+      double* yj = &yp[jb * kB];
+      for (int i = 0; i < kB; i++)
+        for (int c = 0; c < kB; c++) yi[i] += B[i * kB + c] * xj[c], yj[c] += B[i * kB + c] * xi[i];
+    }
+    const double* D = blkPtr(P, P.L, ib, ib);
+    for (int i = 0; i < kB; i++) {
+      yi[i] += D[i * kB + i] * xi[i];
+      for (int c = 0; c < i; c++) yi[i] += D[i * kB + c] * xi[c], yi[c] += D[i * kB + c] * xi[i];
+    }
+  }
+  y.assign(yp.begin(), yp.begin() + P.nRed);
 }
 
 // Preconditioner::operator(): IdentityPrecond (Preconditioner.h:27-48) or BlockJacobiPrecond
@@ -707,6 +930,8 @@ bool solveOnly(Problem& P, const std::vector<double>& rhs, std::vector<double>& 
 bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<double>& rhs,
                     std::vector<double>& x) {
   const int64_t nPts = P.nPts;
+  using Clock = std::chrono::steady_clock;
+  auto t0 = Clock::now();
   if (doFactor) {
     P.L = P.Hred;
     // damping on the reduced diagonal
@@ -714,42 +939,61 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
       double& d = P.L[redElem(P, r, r)];
       d = d * (1.0 + lambda) + lambda;
     }
+    padIdentity(P, P.L);
+    // per point: damped 3 x 3 Cholesky of V and Y = L^-1 W for each coupled block (BaSpaCho's sparse
+    // elimination of the point range)
     P.Vchol.assign(nPts * 9, 0.0);
+    bool ok = true;
+#pragma omp parallel for schedule(dynamic, 256) num_threads(P.threads) if (P.threads > 1)
     for (int64_t pt = 0; pt < nPts; pt++) {
       Mat V(3, 3);
       for (int i = 0; i < 9; i++) V.a[i] = P.Vpt[pt * 9 + i];
       for (int i = 0; i < 3; i++) V(i, i) = V(i, i) * (1.0 + lambda) + lambda;
-      if (!cholesky(V)) return false;
+      if (!cholesky(V)) {
+        ok = false;
+        continue;
+      }
       for (int i = 0; i < 9; i++) P.Vchol[pt * 9 + i] = V.a[i];
-      // Y = L^-1 W for each coupled block, then S -= Y_a^T Y_b
-      const int64_t s = P.ptCoupStart[pt], e = P.ptCoupStart[pt + 1];
-      std::vector<Mat> Y;
-      for (int64_t q = s; q < e; q++) {
+      for (int64_t q = P.ptCoupStart[pt]; q < P.ptCoupStart[pt + 1]; q++) {
         const int64_t rp = P.ptCoupParam[q];
         const int d = (int)(P.redStart[rp + 1] - P.redStart[rp]);
-        Mat Wb(3, d);
-        for (int i = 0; i < 3 * d; i++) Wb.a[i] = P.W[P.ptCoupOff[q] + i];
+        const double* w = &P.W[P.ptCoupOff[q]];
+        double* y = &P.Yp[P.ptCoupOff[q]];
         for (int j = 0; j < d; j++) {  // forward solve L y = w
-          double y0 = Wb(0, j) / V(0, 0);
-          double y1 = (Wb(1, j) - V(1, 0) * y0) / V(1, 1);
-          double y2 = (Wb(2, j) - V(2, 0) * y0 - V(2, 1) * y1) / V(2, 2);
-          Wb(0, j) = y0, Wb(1, j) = y1, Wb(2, j) = y2;
+          const double y0 = w[3 * j] / V(0, 0);
+          const double y1 = (w[3 * j + 1] - V(1, 0) * y0) / V(1, 1);
+          const double y2 = (w[3 * j + 2] - V(2, 0) * y0 - V(2, 1) * y1) / V(2, 2);
+          y[3 * j] = y0, y[3 * j + 1] = y1, y[3 * j + 2] = y2;
         }
-        Y.push_back(Wb);
       }
-      for (int64_t a = s; a < e; a++)
-        for (int64_t b = s; b <= a; b++) {
-          const Mat& Ya = Y[a - s];
-          const Mat& Yb = Y[b - s];
-          const int64_t ra = P.redStart[P.ptCoupParam[a]], rb = P.redStart[P.ptCoupParam[b]];
-          for (int i = 0; i < Ya.c; i++)
-            for (int j = 0; j < Yb.c; j++) {
-              if (a == b && j > i) continue;
-              const double v = Ya(0, i) * Yb(0, j) + Ya(1, i) * Yb(1, j) + Ya(2, i) * Yb(2, j);
-              P.L[redElem(P, ra + i, rb + j)] -= v;
-            }
-        }
     }
+    if (!ok) return false;
+    // S -= sum_points Y_a^T Y_b, lower part, by block row (a block row is written by one thread, its
+    // points in ascending order: the serial order of every element)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(P.threads) if (P.threads > 1)
+    for (int64_t ib = 0; ib < P.nb; ib++) {
+      const int64_t rowLo = ib * kB, rowHi = std::min(P.nRed, rowLo + kB);
+      for (int64_t pt : P.rowPts[ib]) {
+        const int64_t s = P.ptCoupStart[pt], e = P.ptCoupStart[pt + 1];
+        for (int64_t a = s; a < e; a++) {
+          const int64_t ra = P.redStart[P.ptCoupParam[a]], da = P.redStart[P.ptCoupParam[a] + 1] - ra;
+          const int64_t r0 = std::max(ra, rowLo), r1 = std::min(ra + da, rowHi);
+          for (int64_t row = r0; row < r1; row++) {
+            const int64_t i = row - ra;
+            const double* ya = &P.Yp[P.ptCoupOff[a] + 3 * i];
+            for (int64_t b = s; b <= a; b++) {
+              const int64_t rb = P.redStart[P.ptCoupParam[b]];
+              const int64_t jn = b == a ? i + 1 : P.redStart[P.ptCoupParam[b] + 1] - rb;
+              const double* yb = &P.Yp[P.ptCoupOff[b]];
+              for (int64_t j = 0; j < jn; j++)
+                P.L[redElem(P, row, rb + j)] -= ya[0] * yb[3 * j] + ya[1] * yb[3 * j + 1] + ya[2] * yb[3 * j + 2];
+            }
+          }
+        }
+      }
+    }
+    P.phaseMs[1] = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+    t0 = Clock::now();
     if (P.solverType != 0) {  // PCG: keep S (in P.L) unfactored; BlockJacobiPrecond::init
       P.jacOff.assign(1, 0);
       P.jacL.clear();
@@ -764,69 +1008,49 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
         for (int i = 0; i < n * n; i++) P.jacL.push_back(B.a[i]);
         P.jacOff.push_back((int64_t)P.jacL.size());
       }
+      P.phaseMs[2] = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
       return solveOnly(P, rhs, x);
     }
-    // skyline Cholesky (row-oriented)
-    for (int64_t i = 0; i < P.nRed; i++) {
-      const int64_t fi = P.rowFirst[i];
-      double* Li = &P.L[P.rowOff[i]];
-      for (int64_t j = fi; j < i; j++) {
-        const int64_t fj = P.rowFirst[j];
-        const double* Lj = &P.L[P.rowOff[j]];
-        const int64_t k0 = std::max(fi, fj);
-        double s = Li[j - fi];
-        for (int64_t k = k0; k < j; k++) s -= Li[k - fi] * Lj[k - fj];
-        Li[j - fi] = s / Lj[j - fj];
-      }
-      double d = Li[i - fi];
-      for (int64_t k = fi; k < i; k++) d -= Li[k - fi] * Li[k - fi];
-      if (!(d > 0)) return false;
-      Li[i - fi] = std::sqrt(d);
-    }
+    if (!beFactor(P, P.L)) return false;
+    P.phaseMs[2] = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
   }
-  // ---- solve: reduced rhs
-  std::vector<double> r(P.nRed, 0.0);
+  t0 = Clock::now();
+  // ---- solve: reduced rhs r = g_red - sum_points Y^T z, z = L_V^-1 g_p
+  std::vector<double> r(P.nb * kB, 0.0);
   for (int64_t p = nPts; p < (int64_t)P.params.size(); p++) {
     const int64_t ro = P.redStart[P.redPos[p]];
     for (int i = 0; i < P.pdim[p]; i++) r[ro + i] = rhs[P.pstart[p] + i];
   }
   std::vector<double> z(nPts * 3);
+#pragma omp parallel for schedule(static) num_threads(P.threads) if (P.threads > 1)
   for (int64_t pt = 0; pt < nPts; pt++) {
     const double* V = &P.Vchol[pt * 9];
     const double* g = &rhs[P.pstart[pt]];
-    double z0 = g[0] / V[0];
-    double z1 = (g[1] - V[1] * z0) / V[4];
-    double z2 = (g[2] - V[2] * z0 - V[5] * z1) / V[8];
+    const double z0 = g[0] / V[0];
+    const double z1 = (g[1] - V[1] * z0) / V[4];
+    const double z2 = (g[2] - V[2] * z0 - V[5] * z1) / V[8];
     z[pt * 3] = z0, z[pt * 3 + 1] = z1, z[pt * 3 + 2] = z2;
-    for (int64_t q = P.ptCoupStart[pt]; q < P.ptCoupStart[pt + 1]; q++) {
-      const int64_t rp = P.ptCoupParam[q];
-      const int d = (int)(P.redStart[rp + 1] - P.redStart[rp]);
-      const double* w = &P.W[P.ptCoupOff[q]];
-      for (int j = 0; j < d; j++) {  // Y_j = L^-1 w_j
-        double y0 = w[j * 3] / V[0];
-        double y1 = (w[j * 3 + 1] - V[1] * y0) / V[4];
-        double y2 = (w[j * 3 + 2] - V[2] * y0 - V[5] * y1) / V[8];
-        r[P.redStart[rp] + j] -= y0 * z0 + y1 * z1 + y2 * z2;
+  }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(P.threads) if (P.threads > 1)
+  for (int64_t ib = 0; ib < P.nb; ib++) {
+    const int64_t rowLo = ib * kB, rowHi = std::min(P.nRed, rowLo + kB);
+    for (int64_t pt : P.rowPts[ib]) {
+      const double z0 = z[pt * 3], z1 = z[pt * 3 + 1], z2 = z[pt * 3 + 2];
+      for (int64_t q = P.ptCoupStart[pt]; q < P.ptCoupStart[pt + 1]; q++) {
+        const int64_t ra = P.redStart[P.ptCoupParam[q]], rEnd = P.redStart[P.ptCoupParam[q] + 1];
+        const double* y = &P.Yp[P.ptCoupOff[q]];
+        for (int64_t row = std::max(ra, rowLo); row < std::min(rEnd, rowHi); row++) {
+          const int64_t j = row - ra;
+          r[row] -= y[3 * j] * z0 + y[3 * j + 1] * z1 + y[3 * j + 2] * z2;
+        }
       }
     }
   }
   if (P.solverType != 0) {
+    r.resize(P.nRed);
     pcgSolve(P, r);
   } else {
-  // forward / backward with the skyline factor
-  for (int64_t i = 0; i < P.nRed; i++) {
-    const int64_t fi = P.rowFirst[i];
-    const double* Li = &P.L[P.rowOff[i]];
-    double s = r[i];
-    for (int64_t k = fi; k < i; k++) s -= Li[k - fi] * r[k];
-    r[i] = s / Li[i - fi];
-  }
-  for (int64_t i = P.nRed - 1; i >= 0; i--) {
-    const int64_t fi = P.rowFirst[i];
-    const double* Li = &P.L[P.rowOff[i]];
-    r[i] /= Li[i - fi];
-    for (int64_t k = fi; k < i; k++) r[k] -= Li[k - fi] * r[i];
-  }
+    beSolve(P, P.L, r);  // forward / backward with the block factor
   }
   x.assign(P.order, 0.0);
   for (int64_t p = nPts; p < (int64_t)P.params.size(); p++) {
@@ -834,19 +1058,17 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
     for (int i = 0; i < P.pdim[p]; i++) x[P.pstart[p] + i] = r[ro + i];
   }
   // back-substitute points: x_p = L^-T (z - Y xc)
+#pragma omp parallel for schedule(static) num_threads(P.threads) if (P.threads > 1)
   for (int64_t pt = 0; pt < nPts; pt++) {
     const double* V = &P.Vchol[pt * 9];
     double t0 = z[pt * 3], t1 = z[pt * 3 + 1], t2 = z[pt * 3 + 2];
     for (int64_t q = P.ptCoupStart[pt]; q < P.ptCoupStart[pt + 1]; q++) {
       const int64_t rp = P.ptCoupParam[q];
       const int d = (int)(P.redStart[rp + 1] - P.redStart[rp]);
-      const double* w = &P.W[P.ptCoupOff[q]];
+      const double* y = &P.Yp[P.ptCoupOff[q]];
       for (int j = 0; j < d; j++) {
-        double y0 = w[j * 3] / V[0];
-        double y1 = (w[j * 3 + 1] - V[1] * y0) / V[4];
-        double y2 = (w[j * 3 + 2] - V[2] * y0 - V[5] * y1) / V[8];
         const double xv = r[P.redStart[rp] + j];
-        t0 -= y0 * xv, t1 -= y1 * xv, t2 -= y2 * xv;
+        t0 -= y[3 * j] * xv, t1 -= y[3 * j + 1] * xv, t2 -= y[3 * j + 2] * xv;
       }
     }
     const double x2 = t2 / V[8];
@@ -854,6 +1076,7 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
     const double x0 = (t0 - V[1] * x1 - V[2] * x2) / V[0];
     x[P.pstart[pt]] = x0, x[P.pstart[pt] + 1] = x1, x[P.pstart[pt] + 2] = x2;
   }
+  P.phaseMs[3] = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
   return true;
 }
 
@@ -1065,8 +1288,24 @@ int64_t ref_reduced_order(void* h) { return ((Problem*)h)->nRed; }
 int64_t ref_total_order(void* h) { return ((Problem*)h)->order; }
 int64_t ref_num_params(void* h) { return (int64_t)((Problem*)h)->params.size(); }
 
+static double msSince(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+// OpenMP threads of the factor loops, the point elimination and the block Cholesky (1 = deterministic)
+int ref_set_threads(void* h, int n) {
+  ((Problem*)h)->threads = std::max(1, n);
+  return 0;
+}
+// last-iteration phase times [ms]: linearize, schur (point elimination), factor, solve, step, cost,
+// total (ref_optimize iteration), rolling-shutter rebuild
+int ref_phase_times(void* h, double* out8) {
+  std::copy(((Problem*)h)->phaseMs, ((Problem*)h)->phaseMs + 8, out8);
+  return 0;
+}
+
 int ref_linearize(void* h, int updateCache, int dontRetry, double* cost) {
   Problem& P = *(Problem*)h;
+  const auto t0 = std::chrono::steady_clock::now();
   try {
     std::fill(P.grad.begin(), P.grad.end(), 0.0);
     *cost = computeGradHess(P, P.grad.data(), true, updateCache, dontRetry);
@@ -1074,6 +1313,7 @@ int ref_linearize(void* h, int updateCache, int dontRetry, double* cost) {
     g_err = e.what();
     return -5;
   }
+  P.phaseMs[0] = msSince(t0);
   return 0;
 }
 
@@ -1123,6 +1363,10 @@ int ref_set_solver(void* h, int type, int maxIt, double tol) {
   P.solverType = type, P.pcgMaxIt = maxIt, P.pcgTol = tol;
   return 0;
 }
+int ref_debug_negate_model_reduction(void* h, int iteration) {
+  ((Problem*)h)->faultNegModelRedIt = iteration;
+  return 0;
+}
 int ref_pcg_stats(void* h, int32_t* iters, double* rel) {
   Problem& P = *(Problem*)h;
   if (iters) *iters = P.pcgIters;
@@ -1146,18 +1390,22 @@ int ref_scale_step(void* h, double f) {
 
 int ref_apply_step(void* h, int which, double ratios[3]) {
   Problem& P = *(Problem*)h;
+  const auto t0 = std::chrono::steady_clock::now();
   applyStep(P, which ? P.substep : P.step, ratios);
+  P.phaseMs[4] = msSince(t0);
   return 0;
 }
 
 int ref_cost(void* h, int comparable, double* cost, int64_t* stats) {
   Problem& P = *(Problem*)h;
+  const auto t0 = std::chrono::steady_clock::now();
   try {
     *cost = computeCost(P, comparable, stats);
   } catch (std::range_error& e) {
     g_err = e.what();
     return -5;
   }
+  P.phaseMs[5] = msSince(t0);
   return 0;
 }
 
@@ -1224,7 +1472,9 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
   };
   int rc;
   while (true) {
+    const auto tIt = std::chrono::steady_clock::now();
     if (!P.rsMid.empty() && (rc = ref_update_rs_tables(h))) return rc;  // ark_vi_ba's preStepCallback
+    P.phaseMs[7] = msSince(tIt);
     if (pre) pre(it, user);
     double prevCost;
     if ((rc = ref_linearize(h, 1, dontRetry, &prevCost))) return rc;
@@ -1232,6 +1482,7 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
     if (it == 0) initialCost = prevCost;
     double modelRed;
     if ((rc = ref_damp_factor_solve(h, damping, &modelRed))) return rc;
+    if (it == P.faultNegModelRedIt) modelRed = -modelRed;  // test fault injection
     if (modelRed < 0) {  // :835-854 (the `continue` leaves the do-while: old step is kept; the
       damping *= s->dFail;  // re-linearization at the same point only refreshes identical caches)
     }
@@ -1316,6 +1567,7 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
       }
       finalCost = newCost;
     }
+    P.phaseMs[6] = msSince(tIt);
     it++;
     if (log && s->verbose) {
       snprintf(buf, sizeof(buf), "it %d cost %.12g -> %.12g lambda %.3g", it, prevCost, newCost,
@@ -1660,38 +1912,12 @@ void shardRhs(Problem& P, const std::vector<double>& g, std::vector<double>& zOu
     }
   }
 }
-bool skylineFactor(Problem& P) {
-  for (int64_t i = 0; i < P.nRed; i++) {
-    const int64_t fi = P.rowFirst[i];
-    double* Li = &P.L[P.rowOff[i]];
-    for (int64_t j = fi; j < i; j++) {
-      const int64_t fj = P.rowFirst[j];
-      const double* Lj = &P.L[P.rowOff[j]];
-      double s = Li[j - fi];
-      for (int64_t k = std::max(fi, fj); k < j; k++) s -= Li[k - fi] * Lj[k - fj];
-      Li[j - fi] = s / Lj[j - fj];
-    }
-    double d = Li[i - fi];
-    for (int64_t k = fi; k < i; k++) d -= Li[k - fi] * Li[k - fi];
-    if (!(d > 0)) return false;
-    Li[i - fi] = std::sqrt(d);
-  }
-  return true;
-}
-void skylineSolve(const Problem& P, std::vector<double>& r) {
-  for (int64_t i = 0; i < P.nRed; i++) {
-    const int64_t fi = P.rowFirst[i];
-    const double* Li = &P.L[P.rowOff[i]];
-    double s = r[i];
-    for (int64_t k = fi; k < i; k++) s -= Li[k - fi] * r[k];
-    r[i] = s / Li[i - fi];
-  }
-  for (int64_t i = P.nRed - 1; i >= 0; i--) {
-    const int64_t fi = P.rowFirst[i];
-    const double* Li = &P.L[P.rowOff[i]];
-    r[i] /= Li[i - fi];
-    for (int64_t k = fi; k < i; k++) r[k] -= Li[k - fi] * r[i];
-  }
+// the reduced solve on the partial buffers: rRed has nRed entries, the factor its padded form
+void shardSolve(const Problem& P, std::vector<double>& r) {
+  std::vector<double> rp(P.nb * kB, 0.0);
+  std::copy(r.begin(), r.end(), rp.begin());
+  beSolve(P, P.L, rp);
+  std::copy(rp.begin(), rp.begin() + P.nRed, r.begin());
 }
 }  // namespace
 
@@ -1714,6 +1940,7 @@ int ref_assemble_reduced(void* h, double lambda) {
     double& d = P.L[redElem(P, r, r)];
     d = d * (1.0 + lambda) + (P.root ? lambda : 0.0);
   }
+  if (P.root) padIdentity(P, P.L);  // the partial systems are summed on the root
   P.Vchol.assign(P.nPts * 9, 0.0);
   int64_t b, e;
   shardRange(P, b, e);
@@ -1760,16 +1987,16 @@ int ref_shard_tile_range(void* h, int64_t* first, int64_t* num) {  // whole skyl
 }
 int ref_factor_solve_reduced(void* h) {
   Problem& P = *(Problem*)h;
-  if (!skylineFactor(P)) {
+  if (!beFactor(P, P.L)) {
     g_err = "cholesky breakdown";
     return -4;
   }
-  skylineSolve(P, P.rRed);
+  shardSolve(P, P.rRed);
   return 0;
 }
 int ref_solve_reduced(void* h) {
   Problem& P = *(Problem*)h;
-  skylineSolve(P, P.rRed);
+  shardSolve(P, P.rRed);
   return 0;
 }
 // x_red (in rRed) -> step (which 0) / sub-step (which 1) of the reduced parameters and the shard's

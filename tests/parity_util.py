@@ -39,6 +39,61 @@ def make(engine_cls, which="A", **kw):
     return e, p
 
 
+def oracle_threads() -> int:
+    """Threads for the oracle on the full-size parity cases (its results do not depend on the count
+    beyond summation-order round-off: the factor loops sum per-thread partials); the GPU box's CPU share
+    is OMP_NUM_THREADS (16)."""
+    import os
+    n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", n) or n), 16))
+
+
+# ------------------------------------------------------------------ failing factors
+def _quat_rot(q, v):
+    """rotate v (n, 3) by unit quaternions q (n, 4) [x, y, z, w] (Sophus / Eigen convention)."""
+    u, w = q[:, :3], q[:, 3:4]
+    t = 2.0 * np.cross(u, v)
+    return v + w * t + np.cross(u, t)
+
+
+def _se3_inv_apply(T, x):
+    """T^-1 x for SE3 rows T (n, 7) = [qx, qy, qz, qw, tx, ty, tz]."""
+    q = T[:, :4].copy()
+    q[:, :3] *= -1.0
+    return _quat_rot(q, x - T[:, 4:7])
+
+
+def make_failing(p, n_behind=30, n_edge=60, edge_depth=2e-4, seed=11):
+    """Put landmarks where VisualFactor fails (CameraModelParam.h:49-51: p_c.z < 1e-6 -> nullopt), so the
+    failure semantics of Factor.h:390-417,555-583 are exercised:
+      - n_behind landmarks 0.5 m behind the camera of one of their global-shutter observations: those
+        observations (and neighbouring ones of the moving camera) fail at x0, so the cached cost is -1
+        (ResultCache) and the comparable cost skips them (numPrevInvalid);
+      - n_edge landmarks `edge_depth` in front of the camera of one observation: valid at x0, but the pose
+        update of the step moves many of them behind the camera, so the comparable cost uses their
+        cached cost and CostStats.numInvalid counts them.
+    Modifies p in place (variables only; ground truth untouched) and returns the chosen landmarks."""
+    rng = np.random.default_rng(seed)
+    fv, iv = p.fvars[0], p.fivals[0]
+    gs = np.flatnonzero(iv < 0)
+    pts_gs = np.unique(fv[gs, 0])
+    pick = rng.choice(pts_gs, size=n_behind + n_edge, replace=False)
+    first = {}
+    for o in gs:
+        first.setdefault(int(fv[o, 0]), int(o))
+    obs = np.array([first[int(l)] for l in pick])
+    pose = p.vars[1][fv[obs, 1]]
+    extr = p.vars[5][fv[obs, 2]]
+    q = np.zeros((len(pick), 3))
+    q[:n_behind] = [0.05, -0.05, -0.5]
+    q[n_behind:, :2] = rng.uniform(-0.05, 0.05, size=(n_edge, 2))
+    q[n_behind:, 2] = edge_depth
+    # p_c = T_cb (T_bw X)  =>  X = T_bw^-1 (T_cb^-1 p_c)
+    X = _se3_inv_apply(pose, _se3_inv_apply(extr, q))
+    p.vars[0][pick] = X
+    return pick
+
+
 # ------------------------------------------------------------------ spring chain KAT
 SPRING_X0 = (-2.0, -1.0, 0.0, 0.5, 1.5, 2.5)
 

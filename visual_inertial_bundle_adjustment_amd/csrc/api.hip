@@ -287,6 +287,7 @@ struct vb_handle_s {
   double* shardPack = nullptr;      // packed copy of those tiles (vb_pack_shard_tiles)
   // iterative reduced solve (vb_set_solver; pcg.hip): S x = rhsWork by PCG over the unfactored tiles
   int solverType = VB_SOLVER_DIRECT, pcgMaxIt = 40;  // Optimizer.h:43-45 defaults
+  int faultNegModelRedIt = -1;  // vb_debug_negate_model_reduction (test fault injection)
   double pcgTol = 1e-10;
   int32_t pcgIters = 0;
   double pcgRelRes = 0.0;
@@ -1547,21 +1548,22 @@ int precondInit(vb_handle h) {
 }
 
 // z = M^-1 r (Preconditioner::operator())
-void precondApply(vb_handle h, const double* r, double* z) {
+int precondApply(vb_handle h, const double* r, double* z) {
   Dev& d = h->d;
   const size_t bytes = (size_t)d.nT * TS * sizeof(double);
   if (h->solverType == VB_SOLVER_PCG_GAUSS_SEIDEL) {
-    (void)hipMemcpyAsync(h->pcgB, r, bytes, hipMemcpyDeviceToDevice, h->st);
+    HIPCHK(hipMemcpyAsync(h->pcgB, r, bytes, hipMemcpyDeviceToDevice, h->st));
     Dev g = d;
     g.tiles = h->tilesGS;
     const Sched& S = h->sch[0];
     launch_solve_fanout(g, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD, h->rowTilesD,
                         h->rowColD, h->linv, h->pcgB, h->yvec, z, h->solveFlags, h->numCUs * solveWgPerCU(), h->st, 3,
                         nullptr, 0);
-    return;
+    return 0;
   }
-  (void)hipMemcpyAsync(z, r, bytes, hipMemcpyDeviceToDevice, h->st);
+  HIPCHK(hipMemcpyAsync(z, r, bytes, hipMemcpyDeviceToDevice, h->st));
   if (h->solverType == VB_SOLVER_PCG_JACOBI) launch_jacobi_apply(d, h->jacL, r, z, h->st);
+  return 0;
 }
 
 // PCG::solve (PCG.cpp:15-104): S x = rhsWork -> xRed, x_0 = 0; stops when |r_k+1| / |r_0| is below
@@ -1582,7 +1584,7 @@ int pcgSolve(vb_handle h) {
   HIPCHK(hipMemsetAsync(x, 0, bytes, h->st));
   HIPCHK(hipMemsetAsync(Ap, 0, bytes, h->st));
   HIPCHK(hipMemcpyAsync(r, h->rhsWork, bytes, hipMemcpyDeviceToDevice, h->st));
-  precondApply(h, r, z);
+  if (int rc = precondApply(h, r, z)) return rc;
   HIPCHK(hipMemcpyAsync(p, z, bytes, hipMemcpyDeviceToDevice, h->st));
   HIPCHK(hipMemsetAsync(d.red + 32, 0, 12 * sizeof(double), h->st));
   launch_dot(r, r, n, d.red + 33, h->st);
@@ -1599,7 +1601,7 @@ int pcgSolve(vb_handle h) {
     launch_dot(p, Ap, n, d.red + 32, h->st);
     launch_pcg_xr(x, r, p, Ap, d.red, zr, 32, n, d.red + 33, h->st);
     launch_pcg_check(d.red, r0, h->pcgTol, k, h->pcgMaxIt, zrNew, h->st);
-    precondApply(h, r, z);
+    if (int rc = precondApply(h, r, z)) return rc;
     launch_dot(z, r, n, d.red + zrNew, h->st);
     launch_pcg_p(p, Ap, z, d.red, zrNew, zr, n, h->st);
     if ((k + 1) % batch == 0 || k + 1 >= h->pcgMaxIt) {
@@ -2005,6 +2007,11 @@ int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double p
   h->solverType = solver_type, h->pcgMaxIt = pcg_max_iterations, h->pcgTol = pcg_desired_residual;
   return 0;
 }
+int vb_debug_negate_model_reduction(vb_handle h, int iteration) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  h->faultNegModelRedIt = iteration;
+  return 0;
+}
 int vb_pcg_stats(vb_handle h, int32_t* iterations, double* relative_residual) {
   if (!h) return fail(VB_E_ARG, "null handle");
   if (iterations) *iterations = h->pcgIters;
@@ -2210,10 +2217,14 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     if (it == 0) initialCost = prevCost;
     double modelRed;
     if ((rc = vb_damp_factor_solve(h, damping, &modelRed))) return rc;
+    if (it == h->faultNegModelRedIt) modelRed = -modelRed;  // test fault injection
     if (modelRed < 0) {
-      // Optimizer.cpp:835-854: the reference re-linearizes into `hess` (same point, same cached
-      // costs) and raises the damping, keeping the old step; re-linearizing would only discard the
-      // factor a later sub-step solve reuses, so only the damping update is mirrored.
+      // Optimizer.cpp:835-854: the reference re-linearizes into `hess` at the same point (the caches
+      // and the gradient it recomputes are the ones it has) and raises the damping, keeping the old
+      // step.  Its re-linearization also overwrites the factor in `hess`, so a later sub-step solve
+      // of that iteration runs BaSpaCho's triangular solves on an unfactored matrix; that value is
+      // defined by BaSpaCho's storage layout and is not reproduced: here the sub-step uses the
+      // factor (tests/test_parity_configs.py forces this branch).
       damping *= s.damping_adjust_on_fail;
     }
     if ((rc = vb_backup(h))) return rc;
@@ -2233,8 +2244,7 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
       double sf = backRed > 0 ? modelRed / (modelRed + backRed) : s.step_factor_decrease;
       for (int i = 0; i < s.max_step_factor_attempts; i++) {
         applied *= sf;
-        vb_scale_step(h, sf);
-        vb_restore(h);
+        if ((rc = vb_scale_step(h, sf)) || (rc = vb_restore(h))) return rc;
         double rr[3];
         if ((rc = vb_apply_step(h, 0, rr))) return rc;
         vb_cost_stats stF;
@@ -2273,7 +2283,7 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     if (newCost > prevCost || !okRate) {
       if (lastTroubled != it - 1) troubledStartDamping = damping, troubledStart = it;
       damping *= s.damping_adjust_on_fail;
-      vb_restore(h);
+      if ((rc = vb_restore(h))) return rc;
       if (damping > s.damping_max) break;
       lastTroubled = it;
     } else {

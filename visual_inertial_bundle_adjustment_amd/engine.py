@@ -206,6 +206,11 @@ class CEngineBase:
         self._check(self._fn("set_solver", [C.c_int, C.c_int, C.c_double])(
             self.h, int(solver_type), int(pcg_max_iterations), float(pcg_desired_residual)))
 
+    def debug_negate_model_reduction(self, iteration: int):
+        """Test fault injection: negate the model cost reduction in LM iteration `iteration` of the next
+        optimize (Optimizer.cpp:835-854 branch); -1 disables."""
+        self._check(self._fn("debug_negate_model_reduction", [C.c_int])(self.h, int(iteration)))
+
     def pcg_stats(self):
         """(iterations, relative residual) of the last PCG solve (PCG::Result)."""
         it, rel = C.c_int32(), C.c_double()
