@@ -277,6 +277,12 @@ int vb_solve_with_new_gradient(vb_handle h);
 #define VB_SOLVER_PCG_GAUSS_SEIDEL 3
 #define VB_SOLVER_PCG_LOWER_PREC 4
 int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double pcg_desired_residual);
+/* the reduced ordering of this handle (no reference counterpart: BaSpaCho's own ordering is internal):
+ * reduced variable i = (kinds[i], handles[i]) occupies rows [offsets[i], offsets[i] + tangent dim) of the
+ * padded order of padded_order rows, cut into 64 x 64 tiles; the block Gauss-Seidel preconditioner's
+ * blocks are these tiles.  Any pointer may be NULL (n alone queries the count).  After vb_finalize. */
+int vb_reduced_layout(vb_handle h, int32_t* kinds, int32_t* handles, int64_t* offsets, int64_t* n,
+                      int64_t* padded_order);
 /* test fault injection: in iteration `iteration` (0-based, -1 = off) of the next vb_optimize calls the
  * model cost reduction is negated, which takes the reference's "quadratic model failing numerically"
  * branch (Optimizer.cpp:835-854: damping *= dampingAdjustOnFail, the step is kept) */

@@ -30,6 +30,7 @@
 #include <exception>
 #include <map>
 #include <numeric>
+#include <random>
 #include <string>
 #include <unordered_map>
 #include "ref_factors.hpp"
@@ -130,6 +131,14 @@ struct Problem {
   // reduced solver (Optimizer.h:31-45): 0 direct, 1 PCG trivial, 2 PCG block Jacobi
   int solverType = 0, pcgMaxIt = 40;
   int faultNegModelRedIt = -1;  // ref_debug_negate_model_reduction
+  // BlockGaussSeidelPrecond (Preconditioner.h:117-160) over a block order: reduced row -> row of the
+  // block order (default: this oracle's reduced order; ref_set_block_layout: another engine's padded
+  // tile order, so its Gauss-Seidel blocks can be restated); tiles of the pseudo-factor by tile row
+  std::vector<int64_t> gsPos;
+  int64_t gsN = 0;
+  std::vector<std::vector<std::pair<int64_t, size_t>>> gsRow;  // tile row I -> (J, offset), J <= I ascending
+  std::vector<double> gsTiles;
+  std::vector<float> lpL;  // LowerPrecSolvePrecond (Preconditioner.h:166-246): fp32 factor of S
   double pcgTol = 1e-10;
   int pcgIters = 0;
   double pcgRel = 0.0;
@@ -741,18 +750,28 @@ void gemmNT(double* __restrict C, const double* __restrict A, const double* __re
         for (int q = 0; q < 4; q++) st4(C + (i + r) * kB + j0 + 4 * q, c[r][q]);
     }
 }
+// C -= A B^T in fp32 (the lower-precision preconditioner's factor, Preconditioner.h:166-246)
+void gemmNT(float* __restrict C, const float* __restrict A, const float* __restrict B) {
+  for (int i = 0; i < kB; i++)
+    for (int j = 0; j < kB; j++) {
+      float s = 0.0f;
+      for (int k = 0; k < kB; k++) s += A[i * kB + k] * B[j * kB + k];
+      C[i * kB + j] -= s;
+    }
+}
 // in-place lower Cholesky of a diagonal block (left-looking, row dot products)
-bool potrfBlk(double* A) {
+template <typename T>
+bool potrfBlk(T* A) {
   for (int j = 0; j < kB; j++) {
-    double* Aj = A + j * kB;
-    double d = Aj[j];
+    T* Aj = A + j * kB;
+    T d = Aj[j];
     for (int k = 0; k < j; k++) d -= Aj[k] * Aj[k];
     if (!(d > 0)) return false;
-    const double l = std::sqrt(d);
+    const T l = std::sqrt(d);
     Aj[j] = l;
     for (int i = j + 1; i < kB; i++) {
-      double* Ai = A + i * kB;
-      double v = Ai[j];
+      T* Ai = A + i * kB;
+      T v = Ai[j];
       for (int k = 0; k < j; k++) v -= Ai[k] * Aj[k];
       Ai[j] = v / l;
     }
@@ -760,21 +779,24 @@ bool potrfBlk(double* A) {
   return true;
 }
 // X = A L^-T (L lower, from potrfBlk)
-void trsmBlk(double* A, const double* L) {
+template <typename T>
+void trsmBlk(T* A, const T* L) {
   for (int r = 0; r < kB; r++) {
-    double* x = A + r * kB;
+    T* x = A + r * kB;
     for (int j = 0; j < kB; j++) {
-      const double* Lj = L + j * kB;
-      double v = x[j];
+      const T* Lj = L + j * kB;
+      T v = x[j];
       for (int m = 0; m < j; m++) v -= x[m] * Lj[m];
       x[j] = v / Lj[j];
     }
   }
 }
-inline double* blkPtr(const Problem& P, std::vector<double>& S, int64_t ib, int64_t jb) {
+template <typename T>
+inline T* blkPtr(const Problem& P, std::vector<T>& S, int64_t ib, int64_t jb) {
   return &S[(size_t)blkIdx(P, ib, jb) * kB * kB];
 }
-inline const double* blkPtr(const Problem& P, const std::vector<double>& S, int64_t ib, int64_t jb) {
+template <typename T>
+inline const T* blkPtr(const Problem& P, const std::vector<T>& S, int64_t ib, int64_t jb) {
   return &S[(size_t)blkIdx(P, ib, jb) * kB * kB];
 }
 // identity rows of the last block row's padding
@@ -784,9 +806,10 @@ void padIdentity(const Problem& P, std::vector<double>& S) {
 // right-looking blocked Cholesky: for every block column k, L_kk = chol(A_kk), L_ik = A_ik L_kk^-T for
 // the block rows below inside the envelope, then A_ij -= L_ik L_jk^T over their pairs (parallel over
 // blocks; every block is updated in ascending k, so the result does not depend on the thread count)
-bool beFactor(const Problem& P, std::vector<double>& S) {
+template <typename T>
+bool beFactor(const Problem& P, std::vector<T>& S) {
   for (int64_t k = 0; k < P.nb; k++) {
-    double* Lkk = blkPtr(P, S, k, k);
+    T* Lkk = blkPtr(P, S, k, k);
     if (!potrfBlk(Lkk)) return false;
     const std::vector<int64_t>& rows = P.colRows[k];
     const int64_t nr = (int64_t)rows.size();
@@ -805,35 +828,36 @@ bool beFactor(const Problem& P, std::vector<double>& S) {
   return true;
 }
 // L L^T x = r in place (r padded to nb * kB)
-void beSolve(const Problem& P, const std::vector<double>& L, std::vector<double>& r) {
+template <typename T>
+void beSolve(const Problem& P, const std::vector<T>& L, std::vector<T>& r) {
   for (int64_t ib = 0; ib < P.nb; ib++) {
-    double* ri = &r[ib * kB];
+    T* ri = &r[ib * kB];
     for (int64_t jb = P.bFirst[ib]; jb < ib; jb++) {
-      const double* B = blkPtr(P, L, ib, jb);
-      const double* xj = &r[jb * kB];
+      const T* B = blkPtr(P, L, ib, jb);
+      const T* xj = &r[jb * kB];
       for (int i = 0; i < kB; i++) {
-        double s = 0.0;
+        T s = 0.0;
         for (int c = 0; c < kB; c++) s += B[i * kB + c] * xj[c];
         ri[i] -= s;
       }
     }
-    const double* D = blkPtr(P, L, ib, ib);
+    const T* D = blkPtr(P, L, ib, ib);
     for (int i = 0; i < kB; i++) {
-      double s = ri[i];
+      T s = ri[i];
       for (int c = 0; c < i; c++) s -= D[i * kB + c] * ri[c];
       ri[i] = s / D[i * kB + i];
     }
   }
   for (int64_t ib = P.nb - 1; ib >= 0; ib--) {
-    double* xi = &r[ib * kB];
-    const double* D = blkPtr(P, L, ib, ib);
+    T* xi = &r[ib * kB];
+    const T* D = blkPtr(P, L, ib, ib);
     for (int i = kB - 1; i >= 0; i--) {
       xi[i] /= D[i * kB + i];
       for (int c = 0; c < i; c++) xi[c] -= D[i * kB + c] * xi[i];
     }
     for (int64_t jb = P.bFirst[ib]; jb < ib; jb++) {
-      const double* B = blkPtr(P, L, ib, jb);
-      double* yj = &r[jb * kB];
+      const T* B = blkPtr(P, L, ib, jb);
+      T* yj = &r[jb * kB];
       for (int i = 0; i < kB; i++)
         for (int c = 0; c < kB; c++) yj[c] -= B[i * kB + c] * xi[i];
     }
@@ -865,7 +889,11 @@ void skylineSymv(const Problem& P, const std::vector<double>& x, std::vector<dou
 
 // Preconditioner::operator(): IdentityPrecond (Preconditioner.h:27-48) or BlockJacobiPrecond
 // (:50-112, per parameter block: L y = r, L^T z = y)
+void gsApply(const Problem& P, const std::vector<double>& r, std::vector<double>& z);
+void lpApply(const Problem& P, const std::vector<double>& r, std::vector<double>& z);
 void precond(const Problem& P, const std::vector<double>& r, std::vector<double>& z) {
+  if (P.solverType == 3) return gsApply(P, r, z);
+  if (P.solverType == 4) return lpApply(P, r, z);
   z = r;
   if (P.solverType != 2) return;
   const int64_t nRP = (int64_t)P.redStart.size() - 1;
@@ -885,6 +913,136 @@ void precond(const Problem& P, const std::vector<double>& r, std::vector<double>
       t[i] = v / L[i * n + i];
     }
   }
+}
+
+// ---- BlockGaussSeidelPrecond: pseudoFactorFrom (every diagonal block factored, every off-diagonal block
+// times L_JJ^-T, no Schur updates) of S in the block order, then z = (L L^T)^-1 r with that L
+bool gsInit(Problem& P) {
+  if (P.gsPos.empty()) {  // default block order: this oracle's reduced order
+    P.gsPos.resize(P.nRed);
+    std::iota(P.gsPos.begin(), P.gsPos.end(), (int64_t)0);
+    P.gsN = P.nb * kB;
+  }
+  const int64_t nT = (P.gsN + kB - 1) / kB;
+  std::map<std::pair<int64_t, int64_t>, std::vector<double>> tiles;
+  auto tile = [&](int64_t I, int64_t J) -> std::vector<double>& {
+    auto& t = tiles[{I, J}];
+    if (t.empty()) t.assign(kB * kB, 0.0);
+    return t;
+  };
+  for (int64_t ib = 0; ib < P.nb; ib++)
+    for (int64_t jb = P.bFirst[ib]; jb <= ib; jb++) {
+      const double* B = blkPtr(P, P.L, ib, jb);
+      for (int i = 0; i < kB; i++) {
+        const int64_t r = ib * kB + i;
+        if (r >= P.nRed) break;
+        for (int c = 0; c < kB; c++) {
+          const int64_t col = jb * kB + c;
+          if (col > r) break;
+          const double v = B[i * kB + c];
+          if (v == 0.0) continue;
+          int64_t R = P.gsPos[r], C = P.gsPos[col];
+          if (R < C) std::swap(R, C);
+          tile(R / kB, C / kB)[(R % kB) * kB + C % kB] += v;
+        }
+      }
+    }
+  std::vector<uint8_t> hit(nT * kB, 0);
+  for (int64_t r = 0; r < P.nRed; r++) hit[P.gsPos[r]] = 1;
+  for (int64_t I = 0; I < nT; I++) {
+    auto& D = tile(I, I);
+    for (int i = 0; i < kB; i++)
+      if (!hit[I * kB + i]) D[i * kB + i] = 1.0;  // identity padding rows
+  }
+  P.gsRow.assign(nT, {});
+  P.gsTiles.clear();
+  for (auto& [ij, t] : tiles) {
+    P.gsRow[ij.first].push_back({ij.second, P.gsTiles.size()});
+    P.gsTiles.insert(P.gsTiles.end(), t.begin(), t.end());
+  }
+  for (int64_t I = 0; I < nT; I++)  // diagonal tiles (the last entry of each row)
+    if (!potrfBlk(&P.gsTiles[P.gsRow[I].back().second])) return false;
+  for (int64_t I = 0; I < nT; I++)
+    for (size_t q = 0; q + 1 < P.gsRow[I].size(); q++) {
+      const auto [J, off] = P.gsRow[I][q];
+      trsmBlk(&P.gsTiles[off], &P.gsTiles[P.gsRow[J].back().second]);
+    }
+  return true;
+}
+void gsApply(const Problem& P, const std::vector<double>& r, std::vector<double>& z) {
+  const int64_t nT = (int64_t)P.gsRow.size();
+  std::vector<double> v(nT * kB, 0.0);
+  for (int64_t i = 0; i < P.nRed; i++) v[P.gsPos[i]] = r[i];
+  for (int64_t I = 0; I < nT; I++) {  // forward: L y = r
+    double* vi = &v[I * kB];
+    const auto& row = P.gsRow[I];
+    for (size_t q = 0; q + 1 < row.size(); q++) {
+      const double* B = &P.gsTiles[row[q].second];
+      const double* vj = &v[row[q].first * kB];
+      for (int i = 0; i < kB; i++) {
+        double s = 0.0;
+        for (int c = 0; c < kB; c++) s += B[i * kB + c] * vj[c];
+        vi[i] -= s;
+      }
+    }
+    const double* D = &P.gsTiles[row.back().second];
+    for (int i = 0; i < kB; i++) {
+      double s = vi[i];
+      for (int c = 0; c < i; c++) s -= D[i * kB + c] * vi[c];
+      vi[i] = s / D[i * kB + i];
+    }
+  }
+  for (int64_t I = nT - 1; I >= 0; I--) {  // backward: L^T z = y
+    double* vi = &v[I * kB];
+    const auto& row = P.gsRow[I];
+    const double* D = &P.gsTiles[row.back().second];
+    for (int i = kB - 1; i >= 0; i--) {
+      vi[i] /= D[i * kB + i];
+      for (int c = 0; c < i; c++) vi[c] -= D[i * kB + c] * vi[i];
+    }
+    for (size_t q = 0; q + 1 < row.size(); q++) {
+      const double* B = &P.gsTiles[row[q].second];
+      double* vj = &v[row[q].first * kB];
+      for (int i = 0; i < kB; i++)
+        for (int c = 0; c < kB; c++) vj[c] -= B[i * kB + c] * vi[i];
+    }
+  }
+  z.resize(P.nRed);
+  for (int64_t i = 0; i < P.nRed; i++) z[i] = v[P.gsPos[i]];
+}
+
+// ---- LowerPrecSolvePrecond::init: S cast to fp32 and factored (the full Cholesky of this oracle's block
+// envelope); on breakdown the diagonal is raised and the factorization retried, epsilon = 1e-8, then x3.
+// Restated as written (Preconditioner.h:201-209): `diagBlock` is already the diagonal vector, so
+// `diagBlock.diagonal() *= 1 + epsilon` scales only its first entry, and every entry gets + epsilon.
+bool lpInit(Problem& P) {
+  float eps = 0.0f;
+  for (int attempt = 0; attempt < 200; attempt++) {
+    P.lpL.assign(P.L.begin(), P.L.end());
+    if (eps > 0) {
+      for (int64_t rp = 0; rp + 1 < (int64_t)P.redStart.size(); rp++) {
+        const int64_t o = P.redStart[rp];
+        P.lpL[redElem(P, o, o)] *= 1.0f + eps;
+        for (int64_t r = o; r < P.redStart[rp + 1]; r++) P.lpL[redElem(P, r, r)] += eps;
+      }
+      eps *= 3.0f;
+    } else {
+      eps = 1e-8f;
+    }
+    if (beFactor(P, P.lpL)) {
+      double sum = 0.0;
+      for (float v : P.lpL) sum += v;
+      if (std::isfinite(sum)) return true;
+    }
+  }
+  return false;
+}
+void lpApply(const Problem& P, const std::vector<double>& r, std::vector<double>& z) {
+  std::vector<float> t(P.nb * kB, 0.0f);
+  for (int64_t i = 0; i < P.nRed; i++) t[i] = (float)r[i];
+  beSolve(P, P.lpL, t);
+  z.resize(P.nRed);
+  for (int64_t i = 0; i < P.nRed; i++) z[i] = (double)t[i];
 }
 
 double vdot(const std::vector<double>& a, const std::vector<double>& b) {
@@ -1008,6 +1166,8 @@ bool factorAndSolve(Problem& P, double lambda, bool doFactor, const std::vector<
         for (int i = 0; i < n * n; i++) P.jacL.push_back(B.a[i]);
         P.jacOff.push_back((int64_t)P.jacL.size());
       }
+      if (P.solverType == 3 && !gsInit(P)) return false;
+      if (P.solverType == 4 && !lpInit(P)) return false;
       P.phaseMs[2] = std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
       return solveOnly(P, rhs, x);
     }
@@ -1352,15 +1512,33 @@ int ref_set_solver(void* h, int type, int maxIt, double tol) {
     g_err = "unknown solver type";
     return -1;
   }
-  if (type == 3 || type == 4) {  // the tile Gauss-Seidel pseudo-factor / fp32 factor: GPU-side only
-    g_err = "oracle: PCG with the Gauss-Seidel or lower-precision preconditioner is not restated";
-    return -6;
-  }
   if (maxIt < 1) {
     g_err = "pcg_max_iterations must be >= 1";
     return -1;
   }
   P.solverType = type, P.pcgMaxIt = maxIt, P.pcgTol = tol;
+  return 0;
+}
+// the block order of the Gauss-Seidel preconditioner: variable (kinds[i], handles[i]) starts at row
+// offsets[i] of an order of n_pad rows cut into 64-row blocks (vb_reduced_layout of the HIP engine);
+// rows no variable occupies are identity padding.  After ref_finalize.
+int ref_set_block_layout(void* h, int64_t n, const int32_t* kinds, const int32_t* handles, const int64_t* offsets,
+                         int64_t nPad) {
+  Problem& P = *(Problem*)h;
+  if (!P.finalized) return (g_err = "ref_set_block_layout before ref_finalize", -2);
+  std::vector<int64_t> pos(P.nRed, -1);
+  for (int64_t i = 0; i < n; i++) {
+    if (kinds[i] < 0 || kinds[i] >= 9 || handles[i] < 0 || handles[i] >= (int64_t)P.pidx[kinds[i]].size())
+      return (g_err = "bad variable in the block layout", -1);
+    const int64_t p = P.pidx[kinds[i]][handles[i]];
+    if (p < P.nPts) return (g_err = "block layout names a point or an unregistered variable", -1);
+    const int64_t o = P.redStart[P.redPos[p]];
+    for (int j = 0; j < P.pdim[p]; j++) pos[o + j] = offsets[i] + j;
+  }
+  for (int64_t r = 0; r < P.nRed; r++)
+    if (pos[r] < 0 || pos[r] >= nPad) return (g_err = "block layout does not cover the reduced system", -1);
+  P.gsPos = std::move(pos);
+  P.gsN = nPad;
   return 0;
 }
 int ref_debug_negate_model_reduction(void* h, int iteration) {
@@ -2049,3 +2227,171 @@ extern "C" {
 // parameter index of a variable (-1: constant / unregistered); points occupy [0, nPts)
 int64_t ref_var_param(void* h, int kind, int64_t handle) { return ((Problem*)h)->pidx[kind][handle]; }
 }  // extern "C"
+
+// ---------------------------------------------------------------- TestPCG restated
+// lib/small_thing/tests/TestPCG.cpp:28-129 (runPreconditionerTest), on this oracle's own PCG and
+// preconditioners (pcgSolve / precond / gsInit / lpInit on the block-envelope storage): a random
+// block-sparse SPD matrix of 215 parameters of size 2..3, the first 100 an independent set (no couplings
+// among them) that is eliminated exactly, randomized damping U(0.1, 0.5) * order on every diagonal
+// block, PCG on the reduced system (desired residual 3e-10, <= 40 iterations), back-substitution, and
+// the relative residual of the full system.  BaSpaCho's testing_utils (randomCols, makeIndependentElimSet,
+// randomData) are absent: the structure comes from this function's own seeded generator with the
+// reference's sizes and densities.  out = {PCG iterations, PCG relative residual, full-system relative
+// residual, reduced order}.
+namespace {
+void initDenseReduced(Problem& Q, const std::vector<int>& sizes, const std::vector<double>& S, int64_t n) {
+  Q.redStart.assign(sizes.size() + 1, 0);
+  for (size_t i = 0; i < sizes.size(); i++) Q.redStart[i + 1] = Q.redStart[i] + sizes[i];
+  Q.nRed = n;
+  Q.rowFirst.assign(n, 0);
+  for (size_t p = 0; p < sizes.size(); p++) {  // envelope per parameter block (its rows share it)
+    int64_t f = Q.redStart[p];
+    for (int64_t r = Q.redStart[p]; r < Q.redStart[p + 1]; r++)
+      for (int64_t c = 0; c < f; c++)
+        if (S[r * n + c] != 0.0) {
+          f = c;
+          break;
+        }
+    for (int64_t r = Q.redStart[p]; r < Q.redStart[p + 1]; r++) Q.rowFirst[r] = f;
+  }
+  Q.nb = (n + kB - 1) / kB;
+  Q.bFirst.assign(Q.nb, 0);
+  Q.bOff.assign(Q.nb + 1, 0);
+  for (int64_t ib = 0; ib < Q.nb; ib++) {
+    int64_t f = ib;
+    for (int64_t r = ib * kB; r < std::min(n, (ib + 1) * kB); r++) f = std::min(f, Q.rowFirst[r] / kB);
+    Q.bFirst[ib] = f;
+    Q.bOff[ib + 1] = Q.bOff[ib] + (ib - f + 1);
+  }
+  Q.colRows.assign(Q.nb, {});
+  for (int64_t ib = 0; ib < Q.nb; ib++)
+    for (int64_t k = Q.bFirst[ib]; k < ib; k++) Q.colRows[k].push_back(ib);
+  Q.L.assign((size_t)Q.bOff[Q.nb] * kB * kB, 0.0);
+  for (int64_t r = 0; r < n; r++)
+    for (int64_t c = Q.rowFirst[r]; c <= r; c++) Q.L[redElem(Q, r, c)] = S[r * n + c];
+  padIdentity(Q, Q.L);
+}
+}  // namespace
+
+extern "C" int ref_pcg_kat(int precondType, int seed, double tol, int maxIt, double* out) {
+  if (precondType < 1 || precondType > 4) return (g_err = "precondType: 1 identity, 2 jacobi, 3 gauss-seidel, 4 lower-prec", -1);
+  const int nParams = 215, nElim = 100;
+  std::mt19937 gen(57 + seed);
+  std::uniform_int_distribution<int> szd(2, 3);
+  std::uniform_real_distribution<double> val(-1.0, 1.0);
+  std::bernoulli_distribution take(0.03);
+  std::vector<int> sz(nParams);
+  std::vector<int64_t> off(nParams + 1, 0);
+  for (int i = 0; i < nParams; i++) sz[i] = szd(gen), off[i + 1] = off[i] + sz[i];
+  const int64_t n = off[nParams];
+  std::vector<double> A(n * n, 0.0);
+  auto fill = [&](int pi, int pj) {  // block (pi, pj), pi >= pj, mirrored
+    for (int a = 0; a < sz[pi]; a++)
+      for (int b = 0; b < sz[pj]; b++) {
+        if (pi == pj && b > a) continue;
+        const double v = val(gen);
+        A[(off[pi] + a) * n + off[pj] + b] = v;
+        A[(off[pj] + b) * n + off[pi] + a] = v;
+      }
+  };
+  for (int i = 0; i < nParams; i++) {
+    for (int j = 0; j < i; j++)
+      if (!(i < nElim && j < nElim) && take(gen)) fill(i, j);  // the elimination set is independent
+    fill(i, i);
+  }
+  std::uniform_real_distribution<double> damp(n * 0.1, n * 0.5);
+  for (int i = 0; i < nParams; i++) {
+    const double d = damp(gen);
+    for (int a = 0; a < sz[i]; a++) A[(off[i] + a) * n + off[i] + a] += d;
+  }
+  std::vector<double> b(n);
+  for (auto& v : b) v = val(gen);
+  // exact elimination of the independent set: per block Cholesky, S = A22 - A21 A11^-1 A12
+  const int64_t n1 = off[nElim], n2 = n - n1;
+  std::vector<Mat> L11(nElim);
+  for (int i = 0; i < nElim; i++) {
+    Mat B(sz[i], sz[i]);
+    for (int a = 0; a < sz[i]; a++)
+      for (int c = 0; c < sz[i]; c++) B(a, c) = A[(off[i] + a) * n + off[i] + c];
+    if (!cholesky(B)) return (g_err = "KAT matrix not SPD", -4);
+    L11[i] = B;
+  }
+  auto solve11 = [&](int i, double* x) {  // x <- A_ii^-1 x
+    const Mat& Lm = L11[i];
+    const int m = sz[i];
+    for (int a = 0; a < m; a++) {
+      for (int c = 0; c < a; c++) x[a] -= Lm(a, c) * x[c];
+      x[a] /= Lm(a, a);
+    }
+    for (int a = m - 1; a >= 0; a--) {
+      for (int c = a + 1; c < m; c++) x[a] -= Lm(c, a) * x[c];
+      x[a] /= Lm(a, a);
+    }
+  };
+  std::vector<double> S(n2 * n2), rhs(n2);
+  for (int64_t r = 0; r < n2; r++) {
+    for (int64_t c = 0; c < n2; c++) S[r * n2 + c] = A[(n1 + r) * n + n1 + c];
+    rhs[r] = b[n1 + r];
+  }
+  std::vector<double> t(3);
+  for (int i = 0; i < nElim; i++) {  // S -= A2i A_ii^-1 Ai2 column by column of Ai2
+    const int m = sz[i];
+    std::vector<double> Z(m * n2, 0.0);  // A_ii^-1 A_i2
+    for (int64_t c = 0; c < n2; c++) {
+      bool nz = false;
+      for (int a = 0; a < m; a++) t[a] = A[(off[i] + a) * n + n1 + c], nz |= t[a] != 0.0;
+      if (!nz) continue;
+      solve11(i, t.data());
+      for (int a = 0; a < m; a++) Z[a * n2 + c] = t[a];
+    }
+    for (int a = 0; a < m; a++) t[a] = b[off[i] + a];
+    solve11(i, t.data());
+    for (int64_t r = 0; r < n2; r++)
+      for (int a = 0; a < m; a++) {
+        const double arow = A[(n1 + r) * n + off[i] + a];
+        if (arow == 0.0) continue;
+        for (int64_t c = 0; c < n2; c++) S[r * n2 + c] -= arow * Z[a * n2 + c];
+        rhs[r] -= arow * t[a];
+      }
+  }
+  Problem Q;
+  initDenseReduced(Q, std::vector<int>(sz.begin() + nElim, sz.end()), S, n2);
+  Q.solverType = precondType, Q.pcgTol = tol, Q.pcgMaxIt = maxIt;
+  if (precondType == 2) {  // BlockJacobiPrecond::init
+    Q.jacOff.assign(1, 0);
+    for (int64_t rp = 0; rp + 1 < (int64_t)Q.redStart.size(); rp++) {
+      const int64_t o = Q.redStart[rp];
+      const int m = (int)(Q.redStart[rp + 1] - o);
+      Mat B(m, m);
+      for (int a = 0; a < m; a++)
+        for (int c = 0; c <= a; c++) B(a, c) = S[(o + a) * n2 + o + c];
+      llt(B);
+      for (int k = 0; k < m * m; k++) Q.jacL.push_back(B.a[k]);
+      Q.jacOff.push_back((int64_t)Q.jacL.size());
+    }
+  }
+  if (precondType == 3 && !gsInit(Q)) return (g_err = "gauss-seidel init breakdown", -4);
+  if (precondType == 4 && !lpInit(Q)) return (g_err = "lower-precision init breakdown", -4);
+  std::vector<double> x2 = rhs;
+  pcgSolve(Q, x2);
+  // back-substitution x1 = A11^-1 (b1 - A12 x2), then the full-system residual
+  std::vector<double> x(n, 0.0);
+  for (int64_t r = 0; r < n2; r++) x[n1 + r] = x2[r];
+  for (int i = 0; i < nElim; i++) {
+    for (int a = 0; a < sz[i]; a++) {
+      double v = b[off[i] + a];
+      for (int64_t c = 0; c < n2; c++) v -= A[(off[i] + a) * n + n1 + c] * x2[c];
+      t[a] = v;
+    }
+    solve11(i, t.data());
+    for (int a = 0; a < sz[i]; a++) x[off[i] + a] = t[a];
+  }
+  double rr = 0.0, bb = 0.0;
+  for (int64_t r = 0; r < n; r++) {
+    double v = b[r];
+    for (int64_t c = 0; c < n; c++) v -= A[r * n + c] * x[c];
+    rr += v * v, bb += b[r] * b[r];
+  }
+  out[0] = Q.pcgIters, out[1] = Q.pcgRel, out[2] = std::sqrt(rr / bb), out[3] = (double)n2;
+  return 0;
+}

@@ -72,6 +72,14 @@ class RefEngine(CEngineBase):
                                                                     C.byref(c), st))
         return c.value, tuple(st)
 
+    def set_block_layout(self, kinds, handles, offsets, padded_order: int):
+        """Block order of the Gauss-Seidel preconditioner (ref_set_block_layout): e.g. the HIP engine's
+        reduced_layout(), so both pseudo-factor the same 64 x 64 blocks."""
+        k, hh = np.ascontiguousarray(kinds, np.int32), np.ascontiguousarray(handles, np.int32)
+        o = np.ascontiguousarray(offsets, np.int64)
+        f = self._fn("set_block_layout", [C.c_int64, P, P, P, C.c_int64])
+        self._check(f(self.h, len(k), k.ctypes.data, hh.ctypes.data, o.ctypes.data, int(padded_order)))
+
     def set_threads(self, n: int):
         """OpenMP threads of the factor loops, point elimination and block Cholesky (1 = the
         deterministic single-thread restatement)."""
@@ -120,3 +128,17 @@ class RefEngine(CEngineBase):
 
     def var_tdim(self, kind, handle):
         return self._fn("var_tdim", [C.c_int, C.c_int64])(self.h, kind, handle)
+
+
+def pcg_kat(precond: int, seed: int = 37, tol: float = 3e-10, max_it: int = 40):
+    """TestPCG.cpp:28-129 restated (oracle/refcpu.cpp ref_pcg_kat): (PCG iterations, PCG relative
+    residual, full-system relative residual, reduced order)."""
+    lib = load()
+    f = lib.ref_pcg_kat
+    f.argtypes = [C.c_int, C.c_int, C.c_double, C.c_int, C.POINTER(C.c_double)]
+    out = (C.c_double * 4)()
+    rc = f(precond, seed, tol, max_it, out)
+    if rc:
+        lib.ref_last_error.restype = C.c_char_p
+        raise RuntimeError(lib.ref_last_error().decode())
+    return int(out[0]), out[1], out[2], int(out[3])

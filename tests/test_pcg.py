@@ -1,16 +1,18 @@
 """Iterative reduced solve (Optimizer.cpp:232-331 "semi-precond": point elimination, then PCG.cpp on
 the Schur-reduced system, with the preconditioners of Preconditioner.h).
 
-CPU (oracle): PCG converged to a tight residual reproduces the direct solve's step, for the identity
-and block-Jacobi preconditioners; an iteration cap stops it with the reference's Result semantics.
+CPU (oracle): TestPCG.cpp restated (iteration caps and full-system residual for all four
+preconditioners); PCG converged to a tight residual reproduces the direct solve's step for every
+preconditioner; an iteration cap stops it with the reference's Result semantics.
 GPU (through the C-ABI, -m gpu):
   - identity and block Jacobi against the oracle running the same PCG: iteration count equal, steps
     within 1e-9 (Jacobi, 40 iterations) / 1e-6 (identity, 10 iterations) relative (max-abs / max|ref|;
     the tile S x and the dot products sum in another order, and identity-preconditioned CG amplifies
     that round-off exponentially: see the test);
-  - block Gauss-Seidel (tile pseudo-factor; not restated in the oracle, BaSpaCho's supernode blocks
-    being unknowable here) through its size-independent property: converged, it reproduces the direct
-    step, in fewer iterations than block Jacobi;
+  - block Gauss-Seidel (the tile pseudo-factor) against the oracle's restatement over the GPU's own
+    64 x 64 tiles (BaSpaCho's supernode blocks are unknowable here, so the oracle adopts the GPU's
+    block order), capped at 40 iterations; and converged, it reproduces the direct step in fewer
+    iterations than block Jacobi;
   - a full optimize with PCG Jacobi (40 iterations, as the reference's default) takes the oracle's
     LM trajectory: same iteration count, final cost within 1e-7 relative;
   - the device stop test (iterations queued 8 at a time) stops at the oracle's iteration count.
@@ -40,7 +42,7 @@ LAM = 1e-2
 
 
 @pytest.mark.parametrize("solver", [SOLVER_PCG_TRIVIAL, SOLVER_PCG_JACOBI])
-def test_oracle_pcg_converges_to_direct_step(solver):
+def test_oracle_pcg_converges_to_direct_step(solver):  # (Gauss-Seidel / lower precision: below)
     d, _ = make(RefEngine, "A")
     md, sd = steps(d, LAM)
     e, _ = make(RefEngine, "A")
@@ -69,13 +71,33 @@ def test_oracle_pcg_jacobi_beats_identity_and_caps_iterations():
     assert it == 3 and res > 1e-30
 
 
-def test_oracle_rejects_unrestated_preconditioners():
+@pytest.mark.parametrize("seed", [37, 1, 2])
+@pytest.mark.parametrize("precond,cap", [(SOLVER_PCG_TRIVIAL, 30), (SOLVER_PCG_JACOBI, 12),
+                                          (SOLVER_PCG_GAUSS_SEIDEL, 6), (SOLVER_PCG_LOWER_PREC, 5)])
+def test_pcg_kat_restated(precond, cap, seed):
+    """TestPCG.cpp:28-145 restated on the oracle's PCG and preconditioners (ref_pcg_kat): random
+    block-sparse SPD system of 215 parameters (sizes 2..3, the first 100 an independent set eliminated
+    exactly, damping U(0.1, 0.5) x order), PCG at residual 3e-10 / 40 iterations, back-substitution:
+    fewer iterations than the reference's caps (30 / 12 / 6 / 5 for identity / Jacobi / Gauss-Seidel /
+    lower precision) and relative residual of the full system below 1e-9 (TestPCG.cpp:115-128)."""
+    from oracle.refcpu import pcg_kat
+    its, pcg_res, full_res, order = pcg_kat(precond, seed)
+    assert its < cap and pcg_res < 3e-10 and full_res < 1e-9 and order > 250
+
+
+@pytest.mark.parametrize("solver", [SOLVER_PCG_GAUSS_SEIDEL, SOLVER_PCG_LOWER_PREC])
+def test_oracle_gs_and_lower_prec_converge_to_direct_step(solver):
+    d, _ = make(RefEngine, "A")
+    md, sd = steps(d, LAM)
     e, _ = make(RefEngine, "A")
-    for s in (SOLVER_PCG_GAUSS_SEIDEL, SOLVER_PCG_LOWER_PREC):
-        with pytest.raises(Exception):
-            e.set_solver(s)
-    with pytest.raises(Exception):
-        e.set_solver(SOLVER_PCG_JACOBI, 0)
+    e.set_solver(solver, 2000, 1e-13)
+    me, se = steps(e, LAM)
+    it, res = e.pcg_stats()
+    assert res < 1e-13 and it < 2000
+    assert abs(me - md) <= 1e-8 * abs(md)
+    for k in range(NUM_VAR_KINDS - 1):
+        if sd[k].size:
+            assert rel(se[k], sd[k]) < 1e-7, VAR_NAMES[k]
 
 
 # ------------------------------------------------------------------ GPU
@@ -106,6 +128,30 @@ def test_gpu_pcg_matches_oracle(which, solver):
             continue
         assert rel(og["step"][k], orf["step"][k]) < tol, VAR_NAMES[k]
         assert rel(og["substep"][k], orf["substep"][k]) < 10 * tol, VAR_NAMES[k]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["A", "miniB"])
+def test_gpu_pcg_gauss_seidel_matches_oracle(which):
+    """Block Gauss-Seidel (Preconditioner.h:117-160) capped at the reference's 40 iterations, against the
+    oracle's restatement over the same blocks: the oracle takes the GPU's reduced ordering and its 64 x 64
+    tiles (vb_reduced_layout -> ref_set_block_layout), pseudo-factors them and applies (L L^T)^-1.  Same
+    iteration count, steps within 1e-9 relative (summation order of S, the tile potrf / trsm)."""
+    g, _ = make(hip(), which)
+    r, _ = make(RefEngine, which)
+    r.set_block_layout(*g.reduced_layout())
+    for e in (g, r):
+        e.set_solver(SOLVER_PCG_GAUSS_SEIDEL, 40, 1e-10)
+    og, orf = one_step(g), one_step(r)
+    assert g.pcg_stats()[0] == r.pcg_stats()[0]
+    print(f"GS {which}: {r.pcg_stats()} vs GPU {g.pcg_stats()}")
+    assert abs(og["model_red"] - orf["model_red"]) <= 1e-9 * abs(orf["model_red"])
+    assert abs(og["cost1"] - orf["cost1"]) <= 1e-9 * abs(orf["cost1"])
+    for k in range(NUM_VAR_KINDS - 1):
+        if orf["step"][k].size == 0:
+            continue
+        assert rel(og["step"][k], orf["step"][k]) < 1e-9, VAR_NAMES[k]
+        assert rel(og["substep"][k], orf["substep"][k]) < 1e-8, VAR_NAMES[k]
 
 
 @pytest.mark.gpu

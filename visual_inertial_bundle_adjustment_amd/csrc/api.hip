@@ -2007,6 +2007,18 @@ int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double p
   h->solverType = solver_type, h->pcgMaxIt = pcg_max_iterations, h->pcgTol = pcg_desired_residual;
   return 0;
 }
+int vb_reduced_layout(vb_handle h, int32_t* kinds, int32_t* handles, int64_t* offsets, int64_t* n, int64_t* padded_order) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_reduced_layout before vb_finalize");
+  const int64_t nRV = (int64_t)h->rvKind.size();
+  if (n) *n = nRV;
+  if (padded_order) *padded_order = (int64_t)h->d.nT * TS;
+  for (int64_t i = 0; i < nRV; i++) {
+    if (kinds) kinds[i] = h->rvKind[i];
+    if (handles) handles[i] = h->rvHandle[i];
+    if (offsets) offsets[i] = h->rvOff[i];
+  }
+  return 0;
+}
 int vb_debug_negate_model_reduction(vb_handle h, int iteration) {
   if (!h) return fail(VB_E_ARG, "null handle");
   h->faultNegModelRedIt = iteration;

@@ -206,6 +206,18 @@ class CEngineBase:
         self._check(self._fn("set_solver", [C.c_int, C.c_int, C.c_double])(
             self.h, int(solver_type), int(pcg_max_iterations), float(pcg_desired_residual)))
 
+    def reduced_layout(self):
+        """(kinds, handles, offsets, padded order) of the reduced variables in this handle's ordering
+        (vb_reduced_layout)."""
+        n, npad = C.c_int64(), C.c_int64()
+        f = self._fn("reduced_layout", [P, P, P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)])
+        self._check(f(self.h, None, None, None, C.byref(n), C.byref(npad)))
+        k = np.zeros(n.value, np.int32)
+        hh = np.zeros(n.value, np.int32)
+        o = np.zeros(n.value, np.int64)
+        self._check(f(self.h, k.ctypes.data, hh.ctypes.data, o.ctypes.data, C.byref(n), C.byref(npad)))
+        return k, hh, o, npad.value
+
     def debug_negate_model_reduction(self, iteration: int):
         """Test fault injection: negate the model cost reduction in LM iteration `iteration` of the next
         optimize (Optimizer.cpp:835-854 branch); -1 disables."""
