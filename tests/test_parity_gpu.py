@@ -55,6 +55,23 @@ def test_one_lm_step_matches_oracle(which):
     assert_step_parity(one_step(g), one_step(r))
 
 
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_fused_factor_levels_match_oracle(mode, monkeypatch):
+    """The alternative level forms of the tile Cholesky (VIBA_FUSED_FACTOR, api.hip factorSeq): 1 = one
+    factor_level_kernel launch per level (fan-in, potrf and trsm with in-kernel hand-offs), 2 = fan-in
+    launch + one potrf/trsm launch.  One LM step and a 6-iteration optimize on miniB (the second
+    exercises graph replays: the hand-off flags carry a per-factorization epoch) against the oracle."""
+    monkeypatch.setenv("VIBA_FUSED_FACTOR", mode)
+    g, _ = make(hip(), "miniB")
+    r, _ = make(RefEngine, "miniB")
+    assert_step_parity(one_step(g), one_step(r))
+    from visual_inertial_bundle_adjustment_amd.engine import Settings
+    s = Settings.default(max_num_iterations=6)
+    sg, sr = g.optimize(s), r.optimize(s)
+    assert sg.num_iterations == sr.num_iterations
+    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
+
+
 @pytest.mark.parametrize("which", ["A", "miniB"])
 def test_optimize_trajectory_matches_oracle(which):
     g, _ = make(hip(), which)

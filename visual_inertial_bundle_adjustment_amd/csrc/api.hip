@@ -33,6 +33,9 @@ void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
                  hipStream_t st);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
+void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
+                         unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st);
+void launch_bump_epoch(unsigned* epoch, hipStream_t st);
 void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
                       double* y, const double* stop, hipStream_t st);
 void launch_jacobi_init(const Dev& d, double* jac, hipStream_t st);
@@ -211,6 +214,9 @@ int alloc0(T** dptr, size_t n) {
 // task lists over the same columns (solver.hip fwd/bwd_fanout_kernel).
 struct Sched {
   std::vector<int64_t> lvP, lvT, lvU;
+  std::vector<int64_t> lvF, lvFd;   // factor_level_kernel items per level / diagonal items (padded) per level
+  std::vector<int64_t> lvPT, lvPd;  // the same for the potrf + trsm-only items (fusedFactor 2)
+  FacItem *facD = nullptr, *ptD = nullptr;
   int32_t nLevels = 0;
   int64_t nPairs = 0;
   int32_t *potrfTileD = nullptr, *potrfColD = nullptr, *trsmDiagD = nullptr, *trsmTargetD = nullptr,
@@ -274,6 +280,10 @@ struct vb_handle_s {
   int numCUs = 256;
   bool legacySolve = false;  // VIBA_SOLVE_LEGACY=1: one launch pair per tile column
   double *dinv = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
+  unsigned* facSync = nullptr;  // factor_level_kernel: per-tile arrival tickets, per-column flags, epoch
+  // VIBA_FUSED_FACTOR: 0 (default) fanin / potrf / trsm launches per level; 1 one factor_level_kernel
+  // launch per level; 2 fanin + one potrf/trsm launch.  Measured on config C (r02): 14.5 / 20.1 / 15.2 ms
+  int fusedFactor = 0;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool sharded = false;  // vb_set_landmark_shard called
@@ -1129,6 +1139,8 @@ int doFinalize(vb_handle h) {
       // level so the launch has ~fanWgs workgroups (>= 4 contributions per chunk: one per wave)
       std::vector<int32_t> pT, pC, tD, tT, tC, fan;
       S.lvP.assign(nLev + 1, 0), S.lvT.assign(nLev + 1, 0), S.lvU.assign(nLev + 1, 0);
+      S.lvF.assign(nLev + 1, 0), S.lvFd.assign(nLev, 0), S.lvPT.assign(nLev + 1, 0), S.lvPd.assign(nLev, 0);
+      std::vector<FacItem> facItems, ptItems;
       for (int32_t L = 0; L < nLev; L++) {
         int64_t total = 0;
         for (int32_t J : cols[L])
@@ -1169,6 +1181,45 @@ int doFinalize(vb_handle h) {
             for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
         }
         S.lvP[L + 1] = (int64_t)pT.size(), S.lvT[L + 1] = (int64_t)tT.size(), S.lvU[L + 1] = (int64_t)fan.size() / 4;
+        // the same level as factor_level_kernel items: every diagonal tile of a factored column first
+        // (padded to a multiple of 8), then the off-diagonal tiles and the fan-in-only targets; a
+        // factored tile without contributions still gets one item (its potrf / trsm)
+        std::vector<FacItem> dg, od;
+        for (int32_t J : cols[L]) {
+          const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+          const bool fac = colSel(J), tgt = tgtSel(J);
+          if (!fac && !tgt) continue;
+          for (int64_t q = 0; q < n; q++) {
+            const int32_t t = h->colTilesH[c0 + q];
+            const int64_t b = ccnt[t], m = tgt ? ccnt[t + 1] - b : 0;
+            if (m == 0 && !fac) continue;
+            const int64_t nch = std::max<int64_t>(1, (m + cs - 1) / cs);
+            const int32_t kind = fac ? (q == 0 ? 1 : 2) : 0;
+            for (int64_t k = 0; k < nch; k++) {
+              const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
+              const FacItem it{t, (int32_t)s0, (int32_t)(s1 - s0), (int32_t)nch, kind, J, h->colTilesH[c0], 0};
+              (kind == 1 ? dg : od).push_back(it);
+            }
+          }
+        }
+        while (dg.size() % 8) dg.push_back(FacItem{0, 0, -1, 1, 0, 0, 0, 0});
+        S.lvFd[L] = (int64_t)dg.size();
+        facItems.insert(facItems.end(), dg.begin(), dg.end());
+        facItems.insert(facItems.end(), od.begin(), od.end());
+        S.lvF[L + 1] = (int64_t)facItems.size();
+        // the potrf + trsm-only form (after a fanin_kernel launch): one item per factored tile, no fan-in
+        std::vector<FacItem> dg2, od2;
+        for (int32_t J : cols[L]) {
+          if (!colSel(J)) continue;
+          const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+          for (int64_t q = 0; q < n; q++)
+            (q == 0 ? dg2 : od2).push_back(FacItem{h->colTilesH[c0 + q], 0, 0, 1, q == 0 ? 1 : 2, J, h->colTilesH[c0], 0});
+        }
+        while (dg2.size() % 8) dg2.push_back(FacItem{0, 0, -1, 1, 0, 0, 0, 0});
+        S.lvPd[L] = (int64_t)dg2.size();
+        ptItems.insert(ptItems.end(), dg2.begin(), dg2.end());
+        ptItems.insert(ptItems.end(), od2.begin(), od2.end());
+        S.lvPT[L + 1] = (int64_t)ptItems.size();
       }
       S.nLevels = nLev, S.nPairs = ccnt[nTiles];
       // fan-out solve task lists, by elimination level: every task of a level only waits on tasks of
@@ -1196,7 +1247,7 @@ int doFinalize(vb_handle h) {
       if (upload(&S.potrfTileD, pT) || upload(&S.potrfColD, pC) || upload(&S.trsmDiagD, tD) ||
           upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.updD, fan) ||
           upload(&S.fanPairsD, pairs) || upload(&S.tasksFD, tf) || upload(&S.tasksBD, tb) ||
-          upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre))
+          upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.facD, facItems) || upload(&S.ptD, ptItems))
         return VB_E_HIP;
       S.built = true;
       return 0;
@@ -1320,7 +1371,9 @@ int doFinalize(vb_handle h) {
   if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) ||
       upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
     return VB_E_HIP;
-  if (alloc0(&h->dinv, (size_t)(nT + 1) * 1024) || alloc0(&h->linv, (size_t)nT * TS * TS)) return VB_E_HIP;
+  if (alloc0(&h->dinv, (size_t)(nT + 1) * 1024) || alloc0(&h->linv, (size_t)nT * TS * TS) ||
+      alloc0(&h->facSync, (size_t)nTiles + nT + 1))
+    return VB_E_HIP;
   d.nRS = h->nRS;
   if (h->rsDevice) {
     // table capacity: the IMU samples of [mid - half, mid + half] widened by 20 ms on both sides (the
@@ -1387,6 +1440,35 @@ void visualCostShard(vb_handle h, int comparable) {
 
 void factorSeq(vb_handle h, const Sched& S) {
   Dev& d = h->d;
+  if (h->fusedFactor == 2) {  // per level: fanin_kernel, then one potrf + trsm launch (no fan-in items)
+    unsigned* epoch = h->facSync + d.nTiles + d.nT;
+    launch_bump_epoch(epoch, h->st);
+    for (int32_t L = 0; L < S.nLevels; L++) {
+      const int64_t u0 = S.lvU[L], f0 = S.lvPT[L];
+      profBegin(h, KF_GEMM);
+      launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
+      profEnd(h, KF_GEMM);
+      profBegin(h, KF_POTRF);
+      launch_factor_level(d, S.ptD + f0, (int)(S.lvPT[L + 1] - f0), (int)S.lvPd[L], S.fanPairsD, h->facSync,
+                          h->facSync + d.nTiles, epoch, h->dinv, h->st);
+      profEnd(h, KF_POTRF);
+    }
+    launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
+    return;
+  }
+  if (h->fusedFactor) {  // one factor_level_kernel launch per level (fan-in + potrf + trsm)
+    unsigned* epoch = h->facSync + d.nTiles + d.nT;
+    launch_bump_epoch(epoch, h->st);
+    for (int32_t L = 0; L < S.nLevels; L++) {
+      const int64_t f0 = S.lvF[L];
+      profBegin(h, KF_GEMM);
+      launch_factor_level(d, S.facD + f0, (int)(S.lvF[L + 1] - f0), (int)S.lvFd[L], S.fanPairsD, h->facSync,
+                          h->facSync + d.nTiles, epoch, h->dinv, h->st);
+      profEnd(h, KF_GEMM);
+    }
+    launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
+    return;
+  }
   for (int32_t L = 0; L < S.nLevels; L++) {
     const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
     profBegin(h, KF_GEMM);
@@ -1658,6 +1740,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   vb_handle h = new vb_handle_s();
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
+  if (const char* e = getenv("VIBA_FUSED_FACTOR")) h->fusedFactor = atoi(e);
   if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
   {
     hipDeviceProp_t prop;
@@ -1686,7 +1769,7 @@ int vb_destroy(vb_handle h) {
                   d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
-                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS};
+                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->facSync};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int k = 0; k < 9; k++) {
@@ -1710,7 +1793,7 @@ int vb_destroy(vb_handle h) {
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
     void* sp[] = {S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.updD, S.fanPairsD,
-                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD};
+                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD};
     for (void* p : sp)
       if (p) hipFree(p);
     if (S.graph) hipGraphExecDestroy(S.graph);

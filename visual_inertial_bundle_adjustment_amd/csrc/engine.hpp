@@ -94,6 +94,12 @@ struct TileEnt {
   uint64_t maskI, maskJ;  // tile rows (r % 64) of those columns; ascending, so row r is column
                           // popcount(mask & ((1 << r) - 1)) of the run
 };
+// one work item of factor_level_kernel (solver.hip): fan-in of contributions [first, first + count) into
+// tile `target` (its list split over nch items), then kind 1 potrf (diagonal of column J) / 2 trsm with
+// the diagonal tile diagTile of column J / 0 nothing; count < 0: padding no-op
+struct FacItem {
+  int32_t target, first, count, nch, kind, J, diagTile, pad;
+};
 struct TileWork {
   int32_t tile, I, J, count;  // count <= 256 landmark entries
   int64_t start;              // into tileEnts

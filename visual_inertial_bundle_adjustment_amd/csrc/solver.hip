@@ -750,27 +750,29 @@ __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS
   for (int c = 0; c < 16; c++) s[c] = scratch[lr * 16 + c];
   Chol16<0>::run(s, invd, lane, bad);
   __builtin_amdgcn_wave_barrier();  // every lane has read S
-  if (lane < 16) {
+  if (lane < 16) {  // L_ii into the scratch (for X below) and into T; s dies here
 #pragma unroll
-    for (int c = 0; c < 16; c++) scratch[lane * 16 + c] = (c <= lane) ? s[c] : 0.0;
+    for (int c = 0; c < 16; c++) {
+      const double v = (c <= lane) ? s[c] : 0.0;
+      scratch[lane * 16 + c] = v;
+      T[(16 * i + c) * TS + 16 * i + lane] = v;
+    }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double acc[16], x[16];
+  double acc[16];  // becomes column lr of X = L_ii^-1 in place (x_k = acc_k / L_kk)
 #pragma unroll
   for (int r = 0; r < 16; r++) acc[r] = (r == lr) ? 1.0 : 0.0;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    x[k] = acc[k] * invd[k];
+    acc[k] *= invd[k];
 #pragma unroll
-    for (int r = k + 1; r < 16; r++) acc[r] -= scratch[r * 16 + k] * x[k];
+    for (int r = k + 1; r < 16; r++) acc[r] -= scratch[r * 16 + k] * acc[k];
   }
   if (lane < 16) {
 #pragma unroll
-    for (int c = 0; c < 16; c++) T[(16 * i + c) * TS + 16 * i + lane] = (c <= lane) ? s[c] : 0.0;
-#pragma unroll
-    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = (r >= lane) ? x[r] : 0.0;
+    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = (r >= lane) ? acc[r] : 0.0;
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -915,17 +917,17 @@ __device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, 
   }
 }
 
-__global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
-  __shared__ double stg[kFanRing * kStage];
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) unsigned int guint;
+
+// Fan-in accumulation of contributions [start, start + count) of one target: acc = sum L_IK L_JK^T over
+// the wave's 32 x 32 quadrant (ring in `stg`; every wave passes a barrier per stage, so all waves call it)
+__device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, int32_t start, int32_t count,
+                                            double* stg, int wave, int lane, double4_t (&acc)[2][2]) {
   static_assert(kGlds * (kFanRing - 1) <= 63 && kFanRing <= 8 && kFanRing >= 3, "vmcnt range");
-  const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  double* C = d.tiles + (int64_t)wk[0] * TS * TS;
-  const int32_t start = wk[1], nst = (TS / kFanK) * wk[2];
-  const bool atomic = wk[3] != 0;
-  double4_t acc[2][2];
+  const int32_t nst = (TS / kFanK) * count;
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
@@ -975,6 +977,13 @@ __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, 
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+// C -= acc (the wave's quadrant): agent-scope fp64 atomics when the target's list is split over
+// several workgroups, else a read-modify-write with all 16 loads in flight before the stores
+__device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const double4_t (&acc)[2][2]) {
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
   double* Cw = C + (pb + l4) * TS + qb + l15;
   if (atomic) {
 #pragma unroll
@@ -983,7 +992,7 @@ __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, 
       for (int b = 0; b < 2; b++)
 #pragma unroll
         for (int r = 0; r < 4; r++) atomicAdd(Cw + (a * 16 + 4 * r) * TS + b * 16, -acc[a][b][r]);
-  } else {  // all 16 loads in flight, then the stores
+  } else {
     double v[2][2][4];
 #pragma unroll
     for (int a = 0; a < 2; a++)
@@ -998,6 +1007,117 @@ __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, 
 #pragma unroll
         for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + b * 16] = v[a][b][r] - acc[a][b][r];
   }
+}
+
+__global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
+  __shared__ double stg[kFanRing * kStage];
+  const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double4_t acc[2][2];
+  fanin_accum(d, pairs, wk[1], wk[2], stg, wave, lane, acc);
+  fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
+}
+
+// One elimination level of the tile Cholesky in ONE launch (fan-in + potrf + trsm; the 3-launch form is
+// fanin_kernel / potrf_kernel / trsm_kernel).  Item b (FacItem, 8 int32): fan-in of `count`
+// contributions into `target` -- its list may be split over `nch` items (atomics + an arrival ticket
+// cnt[target]: the last arriver finishes the tile) -- then by kind:
+//   1  diagonal tile of column J: wave 0 factors it (potrf_blocked in LDS, reusing the ring), writes L_JJ
+//      and the 16 x 16 block inverses dinv[J], and publishes colFlag[J];
+//   2  off-diagonal tile (I, J): waits for colFlag[J], then X = A L_JJ^-T on all four waves;
+//   0  fan-in only (a partial ROOT tile of a partitioned factorization).
+// Items [0, nDiag) are the diagonal ones (padded to a multiple of 8 with count < 0 no-ops); block b
+// < nDiag runs item b, the rest run the off-diagonal items in XCD-contiguous ranges (xcd_block), so on
+// every XCD all diagonal items are dispatched before any item that waits: no deadlock whatever the
+// occupancy, and the potrf latency overlaps the off-diagonal fan-in.  Hand-offs per the guide's G16
+// recipe (every wave s_waitcnt vmcnt(0) -> barrier -> lane 0 agent release -> s_waitcnt -> relaxed
+// agent ticket / flag; consumer: poll relaxed, agent acquire, s_waitcnt, barrier, plain loads).
+// No per-factorization reset: tickets are cumulative (every factorization adds exactly nch per split
+// target, so the last arriver is the one whose add makes the count a multiple of nch), and a column's
+// flag holds the epoch of the factorization that published it (epoch = *epochPtr, bumped by a one-thread
+// kernel ahead of every factorization).  (A memset node ahead of the launches in the captured graph
+// left stale flags visible on replays.)  Spins are bounded (error flag 16).
+__device__ __forceinline__ void release_agent() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void acquire_agent() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ void bump_epoch_kernel(unsigned* epoch) { __hip_atomic_fetch_add((guint*)epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__global__ void __launch_bounds__(256, 3) factor_level_kernel(Dev d, const FacItem* items, int nDiag, const int32_t* pairs,
+                                                           unsigned* cnt, unsigned* colFlag, const unsigned* epochPtr,
+                                                           double* dinvAll) {
+  __shared__ double stg[kFanRing * kStage];
+  __shared__ int sLast;
+  const int b = (int)blockIdx.x;
+  const FacItem it = items[b < nDiag ? b : nDiag + (int)xcd_block(b - nDiag, (int64_t)gridDim.x - nDiag)];
+  if (it.count < 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double* C = d.tiles + (int64_t)it.target * TS * TS;
+  if (it.count > 0) {
+    double4_t acc[2][2];
+    fanin_accum(d, pairs, it.first, it.count, stg, wave, lane, acc);
+    fanin_store(C, it.nch > 1, wave, lane, acc);
+  }
+  if (it.kind == 0) return;
+  // this workgroup's part of the target is out; is the tile complete?
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    if (it.nch > 1) {
+      release_agent();
+      sLast = (__hip_atomic_fetch_add((guint*)&cnt[it.target], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) %
+                  (unsigned)it.nch == 0u;
+    } else {
+      sLast = 1;
+    }
+    if (sLast) acquire_agent();
+  }
+  __syncthreads();
+  if (!sLast) return;
+  if (it.kind == 1) {
+    if (wave != 0) return;
+    double* T = stg;                     // 64 x 64 tile (32 KB)
+    double* scratch = stg + TS * TS;     // 256 doubles
+    double* dinvS = scratch + 256;       // 4 x 16 x 16 block inverses
+#pragma unroll 16
+    for (int c = 0; c < TS; c++) T[c * TS + lane] = C[c * TS + lane];
+    __builtin_amdgcn_wave_barrier();
+    potrf_blocked(T, scratch, dinvS, lane, d.err);
+    lds_to_global(C, T, TS * TS, lane, 64);
+    lds_to_global(dinvAll + (int64_t)it.J * 1024, dinvS, 1024, lane, 64);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      release_agent();
+      __hip_atomic_store((guint*)&colFlag[it.J], __hip_atomic_load((guint*)epochPtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  // kind 2: wait for L_JJ
+  if (tid == 0) {
+    const unsigned ep = __hip_atomic_load((guint*)epochPtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned v = 0;
+    for (unsigned spins = 0;; spins++) {
+      v = __hip_atomic_load((guint*)&colFlag[it.J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == ep || spins > (1u << 24)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (v != ep) atomicOr(d.err, 16);
+    acquire_agent();
+  }
+  __syncthreads();
+  double4_t Xt[4];
+  trsm_rowblock<4>(C, d.tiles + (int64_t)it.diagTile * TS * TS, dinvAll + (int64_t)it.J * 1024, wave, lane, Xt);
+  const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) C[(16 * k + lq + 4 * r) * TS + 16 * wave + lr] = Xt[k][r];
 }
 
 // Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
@@ -1097,8 +1217,6 @@ __global__ void __launch_bounds__(64) bwd_kernel(Dev d, int J, const int32_t* ro
 // vmcnt(0)), then one lane sets the flag (agent-scope atomic store); consumers poll the flag relaxed
 // with s_sleep and read the payload with sc1 loads only (never plain / flat loads of it).  Flags are
 // zeroed by a memset before every launch; spins are bounded (error flag 16 on timeout).
-typedef __attribute__((address_space(1))) double gdouble;
-typedef __attribute__((address_space(1))) unsigned int guint;
 
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __hip_atomic_load((gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1478,6 +1596,11 @@ void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, cons
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
   if (n > 0) launchK(fanin_kernel, dim3(n), dim3(256), 0, st, d, work, pairs);
 }
+void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
+                         unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st) {
+  if (n > 0) launchK(factor_level_kernel, dim3(n), dim3(256), 0, st, d, items, nDiag, pairs, cnt, colFlag, epoch, dinv);
+}
+void launch_bump_epoch(unsigned* epoch, hipStream_t st) { hipLaunchKernelGGL(bump_epoch_kernel, dim3(1), dim3(1), 0, st, epoch); }
 // inverses of the diagonal factor tiles of the listed columns (all columns if cols == nullptr)
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(diag_inverse_kernel, dim3((unsigned)n), dim3(64), 0, st, d, cols, linv);
