@@ -34,6 +34,7 @@
 #include <string>
 #include <unordered_map>
 #include "ref_factors.hpp"
+#include "ref_preint.hpp"
 
 using namespace refcpu;
 
@@ -91,6 +92,13 @@ struct Problem {
   std::vector<int64_t> rsMid, rsHalf;
   std::vector<int32_t> rsCalib;
   int32_t rsGravity = -1;
+  // --recompute-preint (InertialFactors.cpp:19-70): IMU streams by IMU index (imuStreams[0] aliases
+  // `imu`), per-IMU noise model, and per inertial factor row (kinds 1..3) its IMU and interval [us]
+  std::vector<std::vector<ImuMeas>> imuStreams;
+  std::vector<ImuNoise> imuNoise;
+  std::vector<int32_t> preImu[4];
+  std::vector<int64_t> preT0[4], preT1[4];
+  bool recomputePreint = false;
   bool finalized = false;
 
   // registration
@@ -1306,6 +1314,7 @@ void applyStepRaw(Problem& P, const std::vector<double>& st, double raw[3]) {
 }  // namespace
 
 // ====================================================================== C ABI (oracle)
+extern "C" int ref_update_preintegrations(void* h);
 extern "C" {
 
 typedef void (*ref_log_cb)(const char*, void*);
@@ -1652,6 +1661,7 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
   while (true) {
     const auto tIt = std::chrono::steady_clock::now();
     if (!P.rsMid.empty() && (rc = ref_update_rs_tables(h))) return rc;  // ark_vi_ba's preStepCallback
+    if (P.recomputePreint && (rc = ref_update_preintegrations(h))) return rc;  // --recompute-preint
     P.phaseMs[7] = msSince(tIt);
     if (pre) pre(it, user);
     double prevCost;
@@ -2395,3 +2405,313 @@ extern "C" int ref_pcg_kat(int precondType, int seed, double tol, int maxIt, dou
   out[0] = Q.pcgIters, out[1] = Q.pcgRel, out[2] = std::sqrt(rr / bb), out[3] = (double)n2;
   return 0;
 }
+
+// ---------------------------------------------------------------- IMU preintegration (ref_preint.hpp)
+// computePreIntegration (PreIntegration.cpp:136-275) on explicit inputs, the Problem-level
+// --recompute-preint (SingleSessionAdapter::regenerateAllPreintegrationsFromImuMeasurements,
+// InertialFactors.cpp:19-70), and the restated TestPreIntegration.cpp:104-203 known-answer checks.
+namespace {
+std::vector<ImuMeas> toMeas(int64_t n, const int64_t* tNs, const double* gyro, const double* accel) {
+  std::vector<ImuMeas> m(n);
+  for (int64_t i = 0; i < n; i++)
+    m[i] = ImuMeas{tNs[i], v3(gyro[3 * i], gyro[3 * i + 1], gyro[3 * i + 2]),
+                   v3(accel[3 * i], accel[3 * i + 1], accel[3 * i + 2])};
+  return m;
+}
+// the VB_PREINT_CONSTS row: [R q, dV, dP, dtSec, J 9 x 23 col-major, rvpCov 9 x 9 col-major, calibEvalPoint 32]
+void packPreint(const PreIntResult& r, const ImuModel& m, double* o) {
+  std::fill(o, o + 331, 0.0);
+  for (int i = 0; i < 4; i++) o[i] = r.rvp.R.q[i];
+  for (int i = 0; i < 3; i++) o[4 + i] = r.rvp.dV[i], o[7 + i] = r.rvp.dP[i];
+  o[10] = r.rvp.dt;
+  for (int j = 0; j < r.J.c; j++)
+    for (int i = 0; i < 9; i++) o[11 + j * 9 + i] = r.J(i, j);
+  for (int i = 0; i < 81; i++) o[11 + 207 + i] = r.cov.a[i];
+  for (int i = 0; i < 32; i++) o[11 + 207 + 81 + i] = m.d[i];
+}
+ImuModel modelOf(const double* c32) {
+  ImuModel m;
+  std::copy(c32, c32 + 32, m.d);
+  return m;
+}
+// factoryImuParams + normalizeImuParams (ImuUtils.cpp:14-51), in this oracle's 32-double layout
+ImuModel factoryImuParams() {
+  ImuModel p;
+  const double gs[3] = {0.9975922107696533, 0.9992708563804626, 1.002429008483887};
+  const double as[3] = {1.00313138961792, 0.9989509582519531, 1.00210428237915};
+  const double ab[3] = {-0.03137952834367752, -0.1199406236410141, 0.04399538785219193};
+  const double gb[3] = {0.001339819049462676, 0.0001755904668243602, -0.001454736455343664};
+  const double aN[3][3] = {{1, 1.941762820933945e-05, -0.000217802997212857}, {0, 0.9999973177909851, -0.002304504392668605}, {0, 0, 1}};
+  const double gN[3][3] = {{0.9999923706054688, -0.003904011566191912, 4.595328937284648e-05},
+                           {0.003785371780395508, 0.999991774559021, -0.001455615041777492},
+                           {0.0010240338742733, 0.003811037633568048, 0.9999921917915344}};
+  for (int i = 0; i < 3; i++) p.d[i] = gs[i], p.d[3 + i] = as[i], p.d[6 + i] = gb[i], p.d[9 + i] = ab[i];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) p.gN(i, j) = gN[i][j], p.aN(i, j) = aN[i][j];
+  p.dtAccel() = 0.002755688270553946;
+  p.dtGyro() = 0.004112016409635544;
+  p.gN(0, 0) = std::sqrt(1.0 - (p.gN(0, 1) * p.gN(0, 1) + p.gN(0, 2) * p.gN(0, 2)));
+  p.gN(1, 1) = std::sqrt(1.0 - p.gN(1, 0) * p.gN(1, 0) - p.gN(1, 2) * p.gN(1, 2));
+  p.gN(2, 2) = std::sqrt(1.0 - (p.gN(2, 0) * p.gN(2, 0) + p.gN(2, 1) * p.gN(2, 1)));
+  p.aN(0, 0) = std::sqrt(1.0 - (p.aN(0, 1) * p.aN(0, 1) + p.aN(0, 2) * p.aN(0, 2)));
+  p.aN(1, 1) = std::sqrt(1.0 - p.aN(1, 2) * p.aN(1, 2));
+  p.aN(2, 2) = 1.0;
+  p.aN(1, 0) = p.aN(2, 0) = p.aN(2, 1) = 0.0;
+  return p;
+}
+// cyclic Jacobi eigenvalues of a symmetric n x n matrix (col-major), ascending
+std::vector<double> symEigenvalues(Mat A) {
+  const int n = A.r;
+  for (int sweep = 0; sweep < 100; sweep++) {
+    double off = 0;
+    for (int p = 0; p < n; p++)
+      for (int q = p + 1; q < n; q++) off += A(p, q) * A(p, q);
+    if (off < 1e-30) break;
+    for (int p = 0; p < n; p++)
+      for (int q = p + 1; q < n; q++) {
+        if (A(p, q) == 0.0) continue;
+        const double th = 0.5 * (A(q, q) - A(p, p)) / A(p, q);
+        const double t = (th >= 0 ? 1.0 : -1.0) / (std::abs(th) + std::sqrt(th * th + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), sn = t * c;
+        for (int k = 0; k < n; k++) {
+          const double akp = A(k, p), akq = A(k, q);
+          A(k, p) = c * akp - sn * akq, A(k, q) = sn * akp + c * akq;
+        }
+        for (int k = 0; k < n; k++) {
+          const double apk = A(p, k), aqk = A(q, k);
+          A(p, k) = c * apk - sn * aqk, A(q, k) = sn * apk + c * aqk;
+        }
+      }
+  }
+  std::vector<double> ev(n);
+  for (int i = 0; i < n; i++) ev[i] = A(i, i);
+  std::sort(ev.begin(), ev.end());
+  return ev;
+}
+}  // namespace
+
+extern "C" {
+int ref_preintegrate(int64_t n, const int64_t* tNs, const double* gyro, const double* accel, const double* calib32,
+                     int mask, const double* noise6, int64_t t0Us, int64_t t1Us, double* out331) {
+  try {
+    ImuNoise nz;
+    if (noise6) nz.accelVar = v3(noise6[0], noise6[1], noise6[2]), nz.gyroVar = v3(noise6[3], noise6[4], noise6[5]);
+    const ImuModel m = modelOf(calib32);
+    const PreIntResult r = computePreIntegration(ImuJacInd(mask), toMeas(n, tNs, gyro, accel), m, nz, t0Us, t1Us);
+    packPreint(r, m, out331);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+int ref_integrate_measurements(int64_t n, const int64_t* tNs, const double* gyro, const double* accel,
+                               const double* calib32, int64_t t0Us, int64_t t1Us, double* out11) {
+  try {
+    packRvp(integrateMeasurements(toMeas(n, tNs, gyro, accel), modelOf(calib32), t0Us, t1Us), out11);
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+void ref_imu_calib_boxplus(const double* calib32, int mask, const double* delta, double* out32) {
+  ImuModel m = modelOf(calib32);
+  imu_boxPlus(m, ImuJacInd(mask), delta);
+  std::copy(m.d, m.d + 32, out32);
+}
+void ref_factory_imu_params(double* out32) {
+  const ImuModel m = factoryImuParams();
+  std::copy(m.d, m.d + 32, out32);
+}
+
+int ref_set_imu_stream(void* h, int imu, int64_t n, const int64_t* tNs, const double* gyro, const double* accel) {
+  Problem& P = *(Problem*)h;
+  if (imu < 0) return (g_err = "bad IMU index", -1);
+  if (imu == 0) return ref_set_imu_measurements(h, n, tNs, gyro, accel);
+  if ((int)P.imuStreams.size() <= imu) P.imuStreams.resize(imu + 1);
+  P.imuStreams[imu] = toMeas(n, tNs, gyro, accel);
+  for (int64_t i = 1; i < n; i++)
+    if (tNs[i] <= tNs[i - 1]) return (g_err = "IMU timestamps must increase", -1);
+  return 0;
+}
+int ref_set_imu_noise(void* h, int imu, const double* accelVar3, const double* gyroVar3) {
+  Problem& P = *(Problem*)h;
+  if (imu < 0) return (g_err = "bad IMU index", -1);
+  if ((int)P.imuNoise.size() <= imu) P.imuNoise.resize(imu + 1);
+  P.imuNoise[imu].accelVar = v3(accelVar3[0], accelVar3[1], accelVar3[2]);
+  P.imuNoise[imu].gyroVar = v3(gyroVar3[0], gyroVar3[1], gyroVar3[2]);
+  return 0;
+}
+int ref_set_preint_sources(void* h, int kind, int64_t n, const int32_t* imu, const int64_t* t0Us, const int64_t* t1Us) {
+  Problem& P = *(Problem*)h;
+  if (kind < 1 || kind > 3) return (g_err = "preintegration sources: inertial kinds 1..3 only", -1);
+  if (n != (int64_t)P.fint[kind].size()) return (g_err = "preintegration sources: one per factor row", -1);
+  P.preImu[kind].assign(imu, imu + n);
+  P.preT0[kind].assign(t0Us, t0Us + n);
+  P.preT1[kind].assign(t1Us, t1Us + n);
+  return 0;
+}
+int ref_set_recompute_preint(void* h, int on) {
+  ((Problem*)h)->recomputePreint = on != 0;
+  return 0;
+}
+// every registered inertial row: computePreIntegration from its IMU's stream over its interval, with
+// the factor's own IMU-calibration variable as the evaluation point (generatePreintegration, :19-41)
+int ref_update_preintegrations(void* h) {
+  Problem& P = *(Problem*)h;
+  try {
+    for (int fk = 1; fk <= 3; fk++) {
+      const int nv = kNumVars[fk];
+      for (size_t r = 0; r < P.preImu[fk].size(); r++) {
+        const int imu = P.preImu[fk][r];
+        const std::vector<ImuMeas>& meas = imu == 0 ? P.imu : P.imuStreams.at(imu);
+        const ImuNoise nz = imu < (int)P.imuNoise.size() ? P.imuNoise[imu] : ImuNoise();
+        const ImuModel m = modelOf(&P.data[6][(size_t)P.fvars[fk][r * nv] * 32]);
+        const PreIntResult res = computePreIntegration(P.jac, meas, m, nz, P.preT0[fk][r], P.preT1[fk][r]);
+        packPreint(res, m, &P.fconst[fk][r * 331]);
+      }
+    }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+int ref_get_factor_consts(void* h, int kind, int64_t row, double* out) {
+  Problem& P = *(Problem*)h;
+  if (kind < 0 || kind >= 14 || row < 0 || row >= (int64_t)P.fint[kind].size()) return (g_err = "bad factor row", -1);
+  std::copy(&P.fconst[kind][row * kNumConsts[kind]], &P.fconst[kind][(row + 1) * kNumConsts[kind]], out);
+  return 0;
+}
+
+// TestPreIntegration.PreInt (TestPreIntegration.cpp:104-148) restated: analytic calibration Jacobian
+// of computePreIntegration against central differences of integrateMeasurements (boxPlus +-EPS,
+// EPS 1e-7 reference time offset / 3e-9 gyro-accel offset / 1e-6 else), relative to max(|J_num|, 1),
+// over nOuter calibrations (factory, then randomly perturbed by 0.05 from q > 2; every even q with
+// dtReferenceAccel = dtReferenceGyro) x nInner random 2 s measurement streams, interval [0.85, 1.15] s.
+// out3 = max delta over {the other columns, the reference time offset column, the gyro-accel column}.
+int ref_preint_kat(int seed, int nOuter, int nInner, double* out3) {
+  try {
+    std::mt19937 g(seed);
+    std::normal_distribution<> N(0, 1);
+    const ImuJacInd ji(0xff);
+    const ImuNoise nz;
+    out3[0] = out3[1] = out3[2] = 0.0;
+    for (int q = 0; q < nOuter; q++) {
+      ImuModel p = factoryImuParams();
+      if (q > 2) {
+        std::vector<double> d(ji.size);
+        for (auto& x : d) x = N(g) * 0.05;
+        imu_boxPlus(p, ji, d.data());
+      }
+      if (q % 2 == 0) p.dtAccel() = p.dtGyro();
+      const int64_t t0 = 850000, t1 = 1150000;
+      for (int w = 0; w < nInner; w++) {
+        std::vector<ImuMeas> meas;
+        for (int64_t t = 0; t < 2000000; t += 1000) {
+          V3 a, gy;
+          for (int i = 0; i < 3; i++) a[i] = N(g) / std::sqrt(3.0) * 9.81 * 2;
+          for (int i = 0; i < 3; i++) gy[i] = N(g) / std::sqrt(3.0) * M_PI;
+          meas.push_back(ImuMeas{t * 1000, gy, a});
+        }
+        const PreIntResult an = computePreIntegration(ji, meas, p, nz, t0, t1);
+        const RVP r0 = integrateMeasurements(meas, p, t0, t1);
+        for (int i = 0; i < ji.size; i++) {
+          const double eps = i == ji.rT ? 1e-7 : i == ji.gaT ? 3e-9 : 1e-6;
+          std::vector<double> d(ji.size, 0.0);
+          ImuModel pp = p, pm = p;
+          d[i] = eps;
+          imu_boxPlus(pp, ji, d.data());
+          d[i] = -eps;
+          imu_boxPlus(pm, ji, d.data());
+          double bp[9], bm[9];
+          rvp_boxMinus(integrateMeasurements(meas, pp, t0, t1), r0, bp);
+          rvp_boxMinus(integrateMeasurements(meas, pm, t0, t1), r0, bm);
+          for (int k = 0; k < 9; k++) {
+            const double num = (bp[k] - bm[k]) / (2.0 * eps);
+            const double rel = std::abs(an.J(k, i) - num) / std::max(std::abs(num), 1.0);
+            double& slot = out3[i == ji.rT ? 1 : i == ji.gaT ? 2 : 0];
+            slot = std::max(slot, rel);
+          }
+        }
+      }
+    }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+
+// TestPreIntegration.Covariance (TestPreIntegration.cpp:150-203) restated for one seed: the
+// preintegration covariance whitens the spread of integrateMeasurements over randomized measurement
+// noise (samples beyond the approximate 4-sigma chi2 bound dropped); out9 = eigenvalues of the
+// whitened sample covariance, ascending (the reference expects the extremes within 0.04 of 1).
+int ref_preint_cov_kat(int q, int nSamples, double* out9, int64_t* added) {
+  try {
+    const int seed = 39 + q;
+    std::mt19937 g(seed);
+    std::normal_distribution<> N(0, 1);
+    const ImuJacInd ji(0xff);
+    const ImuNoise nz;
+    ImuModel p = factoryImuParams();
+    if (q > 1) {
+      std::vector<double> d(ji.size);
+      for (auto& x : d) x = N(g) * 0.005;
+      imu_boxPlus(p, ji, d.data());
+    }
+    const int64_t t0 = 50000, t1 = 150000;
+    std::vector<ImuMeas> meas;
+    for (int64_t t = 0; t < 200000; t += 1000) {
+      V3 a, gy;
+      for (int i = 0; i < 3; i++) a[i] = N(g) / std::sqrt(3.0) * 9.81 * 2;
+      for (int i = 0; i < 3; i++) gy[i] = N(g) / std::sqrt(3.0) * M_PI;
+      meas.push_back(ImuMeas{t * 1000, gy, a});
+    }
+    const PreIntResult pr = computePreIntegration(ji, meas, p, nz, t0, t1);
+    Mat L = pr.cov;
+    if (!cholesky(L)) return (g_err = "covariance not SPD", -4);
+    // whiteNoise = L^-1 (lower triangular solve of the identity)
+    Mat W(9, 9);
+    for (int c = 0; c < 9; c++)
+      for (int i = 0; i < 9; i++) {
+        double s = (i == c) ? 1.0 : 0.0;
+        for (int k = 0; k < i; k++) s -= L(i, k) * W(k, c);
+        W(i, c) = s / L(i, i);
+      }
+    Mat S(9, 9);
+    int64_t n = 0;
+    std::vector<ImuMeas> rm(meas.size());
+    V3 sa, sg;
+    for (int i = 0; i < 3; i++) sa[i] = std::sqrt(nz.accelVar[i]), sg[i] = std::sqrt(nz.gyroVar[i]);
+    for (int s = 0; s < nSamples; s++) {
+      for (size_t i = 0; i < meas.size(); i++) {
+        rm[i] = meas[i];
+        for (int k = 0; k < 3; k++) rm[i].accel[k] += sa[k] * N(g);
+        for (int k = 0; k < 3; k++) rm[i].gyro[k] += sg[k] * N(g);
+      }
+      double bm[9], wn[9];
+      rvp_boxMinus(integrateMeasurements(rm, p, t0, t1), pr.rvp, bm);
+      double sq = 0;
+      for (int i = 0; i < 9; i++) {
+        double x = 0;
+        for (int k = 0; k < 9; k++) x += W(i, k) * bm[k];
+        wn[i] = x, sq += x * x;
+      }
+      if (sq > 9 + 4 * std::sqrt(2.0 * 9)) continue;
+      for (int j = 0; j < 9; j++)
+        for (int i = 0; i < 9; i++) S(i, j) += wn[i] * wn[j];
+      n++;
+    }
+    for (auto& v : S.a) v /= (double)n;
+    const std::vector<double> ev = symEigenvalues(S);
+    for (int i = 0; i < 9; i++) out9[i] = ev[i];
+    *added = n;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+}  // extern "C"

@@ -23,7 +23,7 @@ P = C.c_void_p
 
 def build_oracle(force: bool = False) -> str:
     """Compile the oracle (g++, no external deps) into oracle/_ref/."""
-    src = [os.path.join(HERE, f) for f in ("refcpu.cpp", "ref_factors.hpp", "ref_math.hpp")]
+    src = [os.path.join(HERE, f) for f in ("refcpu.cpp", "ref_factors.hpp", "ref_math.hpp", "ref_preint.hpp")]
     if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s)
                                                    for s in src):
         return LIB
@@ -142,3 +142,72 @@ def pcg_kat(precond: int, seed: int = 37, tol: float = 3e-10, max_it: int = 40):
         lib.ref_last_error.restype = C.c_char_p
         raise RuntimeError(lib.ref_last_error().decode())
     return int(out[0]), out[1], out[2], int(out[3])
+
+
+def _err(lib):
+    lib.ref_last_error.restype = C.c_char_p
+    return RuntimeError(lib.ref_last_error().decode())
+
+
+def preintegrate(t_ns, gyro, accel, calib32, t0_us: int, t1_us: int, mask: int = 0xFF, noise6=None):
+    """computePreIntegration (PreIntegration.cpp:136-275) on the oracle: the VB_PREINT_CONSTS row
+    [R q, dV, dP, dtSec, J 9x23 col-major, rvpCov 9x9 col-major, calibEvalPoint 32]."""
+    lib = load()
+    t = np.ascontiguousarray(t_ns, np.int64)
+    g, a = np.ascontiguousarray(gyro, np.float64), np.ascontiguousarray(accel, np.float64)
+    c = np.ascontiguousarray(calib32, np.float64)
+    nz = None if noise6 is None else np.ascontiguousarray(noise6, np.float64)
+    out = np.zeros(331)
+    f = lib.ref_preintegrate
+    f.argtypes = [C.c_int64, P, P, P, P, C.c_int, P, C.c_int64, C.c_int64, P]
+    if f(len(t), t.ctypes.data, g.ctypes.data, a.ctypes.data, c.ctypes.data, mask,
+         None if nz is None else nz.ctypes.data, t0_us, t1_us, out.ctypes.data):
+        raise _err(lib)
+    return out
+
+
+def integrate_measurements(t_ns, gyro, accel, calib32, t0_us: int, t1_us: int):
+    """integrateMeasurements (PreIntegration.cpp:277-307): RVP [q 4, dV, dP, dtSec]."""
+    lib = load()
+    t = np.ascontiguousarray(t_ns, np.int64)
+    g, a = np.ascontiguousarray(gyro, np.float64), np.ascontiguousarray(accel, np.float64)
+    c = np.ascontiguousarray(calib32, np.float64)
+    out = np.zeros(11)
+    f = lib.ref_integrate_measurements
+    f.argtypes = [C.c_int64, P, P, P, P, C.c_int64, C.c_int64, P]
+    if f(len(t), t.ctypes.data, g.ctypes.data, a.ctypes.data, c.ctypes.data, t0_us, t1_us, out.ctypes.data):
+        raise _err(lib)
+    return out
+
+
+def factory_imu_params() -> np.ndarray:
+    """factoryImuParams (ImuUtils.cpp:33-51) in the 32-double ImuCalibParam layout."""
+    lib = load()
+    out = np.zeros(32)
+    lib.ref_factory_imu_params.argtypes = [P]
+    lib.ref_factory_imu_params(out.ctypes.data)
+    return out
+
+
+def preint_kat(seed: int = 43, n_outer: int = 250, n_inner: int = 5):
+    """TestPreIntegration.PreInt (TestPreIntegration.cpp:104-148) restated: max relative delta of the
+    analytic vs numeric calibration Jacobian over (other columns, reference time offset, gyro-accel
+    time offset)."""
+    lib = load()
+    out = (C.c_double * 3)()
+    lib.ref_preint_kat.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    if lib.ref_preint_kat(seed, n_outer, n_inner, out):
+        raise _err(lib)
+    return tuple(out)
+
+
+def preint_cov_kat(q: int, n_samples: int = 250_000):
+    """TestPreIntegration.Covariance (TestPreIntegration.cpp:150-203) restated for case q (seed 39 + q):
+    (eigenvalues of the whitened sample covariance, ascending; samples kept)."""
+    lib = load()
+    out = (C.c_double * 9)()
+    n = C.c_int64()
+    lib.ref_preint_cov_kat.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)]
+    if lib.ref_preint_cov_kat(q, n_samples, out, C.byref(n)):
+        raise _err(lib)
+    return np.array(out[:]), n.value

@@ -7,6 +7,11 @@ finite differences.  ORACLE / TEST INFRASTRUCTURE: checks oracle/refcpu, never t
   * TestOptimizer.cpp:22-50 (Simple): spring chain converges to unit spacing within 1e-8.
   * Factor.h:256-387 (verifyJacobians): every factor kind's analytic Jacobian vs central
     differences through the variables' own box-plus.
+  * TestPreIntegration.cpp:104-203 (PreInt, Covariance): computePreIntegration's calibration Jacobian
+    against central differences of integrateMeasurements (1e-6; gyro-accel time offset 1e-4), and its
+    covariance whitening the spread of noisy re-integrations (extreme eigenvalues within 0.04 of 1).
+    Fewer cases than the reference (CPU suite time): 60 x 2 calibrations x streams instead of 250 x 5,
+    60k noise samples for two of its 20 seeds instead of 250k.
 """
 from __future__ import annotations
 
@@ -205,3 +210,35 @@ def test_factor_jacobians_fd(which):
             assert w < tol, f"{FACTOR_NAMES[kind]}[{k}] Jacobian mismatch {w:.3e}"
             checked += 1
     assert checked > 0
+
+
+def test_preintegration_jacobian_kat():  # TestPreIntegration.PreInt (TestPreIntegration.cpp:104-148)
+    from oracle.refcpu import preint_kat
+    other, ref_offset, gyro_accel_offset = preint_kat(43, 60, 2)
+    assert other < 1e-6 and ref_offset < 1e-6 and gyro_accel_offset < 1e-4, (other, ref_offset, gyro_accel_offset)
+
+
+@pytest.mark.parametrize("q", [0, 3])
+def test_preintegration_covariance_kat(q):  # TestPreIntegration.Covariance (:150-203)
+    from oracle.refcpu import preint_cov_kat
+    ev, kept = preint_cov_kat(q, 60_000)
+    assert kept > 0.99 * 60_000
+    assert abs(ev[0] - 1) < 0.04 and abs(ev[-1] - 1) < 0.04, ev
+
+
+def test_preintegration_matches_integrate_measurements():
+    """computePreIntegration's RVP is integrateMeasurements' (same steps; the two compensation forms of
+    CompensateJac.cpp and ImuMeasurementModelParameters.h differ by round-off only), and the ref
+    time-offset column is the derivative of the RVP wrt a shift of the whole interval."""
+    from oracle.refcpu import factory_imu_params, integrate_measurements, preintegrate
+    rng = np.random.default_rng(5)
+    t = np.arange(0, 400_000, 1000) * 1000
+    g, a = rng.normal(size=(len(t), 3)) * 0.5, rng.normal(size=(len(t), 3)) * 3 + [0, 0, 9.81]
+    c = factory_imu_params()
+    pre = preintegrate(t, g, a, c, 100_000, 250_000)
+    rvp = integrate_measurements(t, g, a, c, 100_000, 250_000)
+    assert np.allclose(pre[:11], rvp, rtol=0, atol=1e-12)
+    assert pre[10] == pytest.approx(0.15)
+    cov = pre[218:299].reshape(9, 9)
+    assert np.allclose(cov, cov.T, atol=1e-18) and np.linalg.eigvalsh(cov).min() > 0
+    assert np.array_equal(pre[299:331], c)

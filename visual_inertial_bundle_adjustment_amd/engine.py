@@ -136,6 +136,44 @@ class CEngineBase:
         self._check(f(self.h, len(t), t.ctypes.data_as(C.POINTER(C.c_int64)), g.ctypes.data_as(_dp),
                       a.ctypes.data_as(_dp)))
 
+    def set_imu_stream(self, imu: int, timestamp_ns, gyro, accel):
+        """Measurement stream of IMU `imu` (vb_set_imu_stream; imu 0 = the IMU-0 stream above)."""
+        t = _arr(timestamp_ns, np.int64)
+        g, a = _arr(gyro, np.float64).reshape(-1, 3), _arr(accel, np.float64).reshape(-1, 3)
+        f = self._fn("set_imu_stream", [C.c_int, C.c_int64, C.POINTER(C.c_int64), _dp, _dp])
+        self._check(f(self.h, int(imu), len(t), t.ctypes.data_as(C.POINTER(C.c_int64)), g.ctypes.data_as(_dp),
+                      a.ctypes.data_as(_dp)))
+
+    def set_imu_noise(self, imu: int, accel_var, gyro_var):
+        """Sample variances of IMU `imu` (ImuNoiseModelParameters accel/gyroSampleVariance)."""
+        a, g = _arr(accel_var, np.float64), _arr(gyro_var, np.float64)
+        self._check(self._fn("set_imu_noise", [C.c_int, _dp, _dp])(self.h, int(imu), a.ctypes.data_as(_dp),
+                                                                     g.ctypes.data_as(_dp)))
+
+    def set_preint_sources(self, kind: int, imu, t0_us, t1_us):
+        """--recompute-preint inputs of the inertial factor rows of `kind` (1..3, vb_add_factors order):
+        the IMU and the interval [us] each preintegration integrates (InertialFactors.cpp:19-70)."""
+        i, a, b = _arr(imu, np.int32), _arr(t0_us, np.int64), _arr(t1_us, np.int64)
+        f = self._fn("set_preint_sources", [C.c_int, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                                            C.POINTER(C.c_int64)])
+        self._check(f(self.h, int(kind), len(i), i.ctypes.data_as(C.POINTER(C.c_int32)),
+                      a.ctypes.data_as(C.POINTER(C.c_int64)), b.ctypes.data_as(C.POINTER(C.c_int64))))
+
+    def update_preintegrations(self):
+        """computePreIntegration of every registered inertial row at the current calibration."""
+        self._check(self._fn("update_preintegrations", [])(self.h))
+
+    def set_recompute_preint(self, on: bool = True):
+        """optimize() recomputes the preintegrations at the start of every iteration (--recompute-preint)."""
+        self._check(self._fn("set_recompute_preint", [C.c_int])(self.h, int(bool(on))))
+
+    def get_factor_consts(self, kind: int, row: int) -> np.ndarray:
+        from .kinds import factor_num_consts
+        out = np.zeros(factor_num_consts(kind))
+        self._check(self._fn("get_factor_consts", [C.c_int, C.c_int64, _dp])(self.h, int(kind), int(row),
+                                                                             out.ctypes.data_as(_dp)))
+        return out
+
     def set_rs_rigs(self, midpoint_us, half_length_us, imu_calib, gravity_var=0):
         """Per-table rebuild inputs (vb_set_rs_rigs): RollingShutterData's midpoint / half length and
         the IMU calibration variable of updateRollingShutterData (InitCalibration.cpp:316-325)."""
