@@ -66,7 +66,7 @@ def host_threads() -> tuple[int, int]:
     return max(1, min(nproc, share)), nproc
 
 
-def cpu_baseline(p, name: str = "C", steps: int = 1):
+def cpu_baseline(p, name: str = "C", steps: int = 1, recompute_preint: bool = False):
     """The CPU baseline of BASELINE.md, measured on the FULL workload (no slice, no extrapolation):
     oracle/refcpu (this repository's restatement of the reference path: factor functors, the LM loop,
     point elimination + blocked Cholesky) runs `steps` iterations of Optimizer::optimize on the same
@@ -78,7 +78,7 @@ def cpu_baseline(p, name: str = "C", steps: int = 1):
     from visual_inertial_bundle_adjustment_amd.engine import Settings
     t = time.perf_counter()
     e = RefEngine(imu_calib_options=p.imu_calib_options)
-    synth.load_into(e, p, rs_device=True)
+    synth.load_into(e, p, rs_device=True, recompute_preint=recompute_preint)
     log(f"[bench] cpu baseline: oracle loaded in {time.perf_counter() - t:.1f}s")
     nthr, nproc = host_threads()
     runs = {}
@@ -151,6 +151,9 @@ def main():
                          "the identity / block-Jacobi / block-Gauss-Seidel preconditioner")
     ap.add_argument("--pcg-iterations", type=int, default=40, help="pcgMaxIterations (Optimizer.h:44)")
     ap.add_argument("--pcg-residual", type=float, default=1e-10, help="pcgDesiredResidual (Optimizer.h:45)")
+    ap.add_argument("--recompute-preint", action="store_true",
+                    help="ark_vi_ba --recompute-preint: every iteration re-preintegrates every inertial factor "
+                         "from the IMU stream on the device (preint.hip)")
     args = ap.parse_args()
     if args.solver != "direct" and args.profile_family == KF_GEMM:
         args.profile_family = KF_SYMV  # no fan-in without the factorization: the PCG product instead
@@ -174,7 +177,7 @@ def main():
         tolerance = mixed_vs_fp64(p, local, args.rs_tables == "device")
         log(f"[bench] mixed vs fp64, first LM step: {tolerance}")
     e = HipEngine(imu_calib_options=p.imu_calib_options, device=local, precision=args.precision)
-    synth.load_into(e, p, rs_device=args.rs_tables == "device")
+    synth.load_into(e, p, rs_device=args.rs_tables == "device", recompute_preint=args.recompute_preint)
     e.set_solver(SOLVERS[args.solver], args.pcg_iterations, args.pcg_residual)
     st = e.problem_stats()
     log(f"[bench] finalize {time.perf_counter() - t:.1f}s; reduced order {st[3]}, tiles {st[5]} "
@@ -256,7 +259,7 @@ def main():
     if not args.no_cpu_baseline:
         e.close()  # free the device before the host run
         try:
-            cpu = cpu_baseline(p, args.config)
+            cpu = cpu_baseline(p, args.config, recompute_preint=args.recompute_preint)
         except Exception as ex:  # the baseline must never hide the GPU number
             log(f"[bench] cpu baseline failed: {ex}")
     out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,

@@ -1,0 +1,161 @@
+"""--recompute-preint: computePreIntegration (PreIntegration.cpp:136-275) of every inertial
+factor row from raw IMU streams, as SingleSessionAdapter::regenerateAllPreintegrationsFromImuMeasurements
+(InertialFactors.cpp:19-70) does, on the device (preint.hip) against the oracle's restatement
+(oracle/ref_preint.hpp, itself pinned by the TestPreIntegration.cpp KATs in test_oracle_kat.py).
+
+Inputs: miniB, whose generator emits a 1 kHz IMU-0 stream (csrc/synth.cpp).  Kind-1 rows integrate IMU 0
+over [t_prev, t_next] of their rigs; the secondary-IMU rows (kinds 2, 3) integrate an IMU-1 stream made
+from IMU 0's samples shifted by 0.3 ms with a gyro offset, under non-default sample variances, so both
+streams and both noise models are exercised.
+
+Tolerances (fp64; only FMA contraction and transcendental ulps differ, compounded over ~100 steps):
+  RVP and calibration Jacobian  1e-11 relative to the largest entry of the row block
+  covariance                    1e-10 relative;  whitening square root 1e-9 relative
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from oracle.refcpu import RefEngine
+from parity_util import one_step, rel
+from visual_inertial_bundle_adjustment_amd import synth
+from visual_inertial_bundle_adjustment_amd.kinds import NUM_VAR_KINDS, VAR_NAMES
+
+PREINT_KINDS = (1, 2, 3)
+NEXT_RIG_COL = {1: 3, 2: 4, 3: 5}  # var column of the next rig in vb_add_factors order (vb_factor_kind)
+
+
+def _imu1_stream(p):
+    t = p.imu_t + 300_000
+    g = p.imu_gyro + np.array([2e-3, -1e-3, 5e-4])
+    a = p.imu_accel * 1.001
+    return t, g, a
+
+
+def _sources(p, kind):
+    fv = p.fvars[kind]
+    t0 = p.rs_mid[fv[:, 1]]
+    t1 = p.rs_mid[fv[:, NEXT_RIG_COL[kind]]]
+    imu = np.zeros(len(fv), np.int32) if kind == 1 else np.ones(len(fv), np.int32)
+    return imu, t0, t1
+
+
+def build(cls, p, recompute=False, update=True):
+    e = cls(imu_calib_options=p.imu_calib_options)
+    synth.load_into(e, p, finalize=False, rs_device=True)
+    e.set_imu_stream(1, *_imu1_stream(p))
+    e.set_imu_noise(1, [4e-3, 5e-3, 6e-3], [2e-5, 3e-5, 4e-5])
+    for k in PREINT_KINDS:
+        if len(p.fvars[k]):
+            e.set_preint_sources(k, *_sources(p, k))
+    e.finalize()
+    e.update_rs_tables()
+    if update:
+        e.update_preintegrations()
+    if recompute:
+        e.set_recompute_preint(True)
+    return e
+
+
+def rows(e, p):
+    return {k: np.array([e.get_factor_consts(k, r) for r in range(len(p.fvars[k]))]) for k in PREINT_KINDS}
+
+
+def assert_rows_match(a, b, tol_rvp=1e-11, tol_cov=1e-10, tol_calib=0.0):
+    for k in PREINT_KINDS:
+        if not len(b[k]):
+            continue
+        x, y = a[k], b[k]
+        assert rel(x[:, :4], y[:, :4]) < tol_rvp, (k, "R")
+        assert rel(x[:, 4:7], y[:, 4:7]) < tol_rvp, (k, "dV")
+        assert rel(x[:, 7:10], y[:, 7:10]) < tol_rvp, (k, "dP")
+        assert np.array_equal(x[:, 10], y[:, 10]), (k, "dt")
+        for r in range(len(y)):  # per row: columns of the Jacobian span many orders of magnitude
+            assert rel(x[r, 11:218], y[r, 11:218]) < tol_rvp, (k, r, "J")
+            assert rel(x[r, 218:299], y[r, 218:299]) < tol_cov, (k, r, "cov")
+        assert rel(x[:, 299:331], y[:, 299:331]) <= tol_calib, (k, "calibration evaluation point")
+
+
+# ------------------------------------------------------------------ CPU: the oracle's Problem-level form
+def test_oracle_problem_preintegration_matches_direct_call():
+    """ref_update_preintegrations packs exactly what ref_preintegrate returns for the row's inputs (the
+    factor's IMU-calibration variable as the evaluation point), for both streams and noise models."""
+    from oracle.refcpu import preintegrate
+    p = synth.generate(synth.config("miniB"))
+    r = build(RefEngine, p)
+    got = rows(r, p)
+    calib = p.vars[6]
+    for k in PREINT_KINDS:
+        imu, t0, t1 = _sources(p, k)
+        for i in range(0, len(p.fvars[k]), 17):
+            t, g, a = (p.imu_t, p.imu_gyro, p.imu_accel) if imu[i] == 0 else _imu1_stream(p)
+            noise = None if imu[i] == 0 else [4e-3, 5e-3, 6e-3, 2e-5, 3e-5, 4e-5]
+            ref = preintegrate(t, g, a, calib[p.fvars[k][i, 0]], int(t0[i]), int(t1[i]), p.imu_calib_options, noise)
+            assert np.array_equal(got[k][i], ref), (k, i)
+
+
+def test_oracle_preintegration_uncovered_interval_is_an_error():
+    from visual_inertial_bundle_adjustment_amd.engine import VbError
+    p = synth.generate(synth.config("miniB"))
+    r = build(RefEngine, p, update=False)
+    r.set_preint_sources(1, np.zeros(len(p.fvars[1]), np.int32), p.rs_mid[p.fvars[1][:, 1]],
+                         p.rs_mid[p.fvars[1][:, 3]] + 10**9)
+    with pytest.raises(VbError):
+        r.update_preintegrations()
+
+
+# ------------------------------------------------------------------ GPU against the oracle
+@pytest.mark.gpu
+def test_device_preintegration_matches_oracle():
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    p = synth.generate(synth.config("miniB"))
+    g, r = build(HipEngine, p), build(RefEngine, p)
+    assert_rows_match(rows(g, p), rows(r, p))
+
+
+@pytest.mark.gpu
+def test_step_on_recomputed_preintegrations_matches_oracle():
+    """one LM step on the recomputed preintegrations (the whitening square root refreshed on the device),
+    then the preintegrations again at the stepped calibration"""
+    from test_parity_gpu import assert_step_parity
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    p = synth.generate(synth.config("miniB"))
+    g, r = build(HipEngine, p), build(RefEngine, p)
+    assert_step_parity(one_step(g), one_step(r))
+    for e in (g, r):
+        e.apply_step(0)
+        e.update_preintegrations()
+    assert_rows_match(rows(g, p), rows(r, p), 1e-9, 1e-8, 1e-10)  # the stepped calibrations differ by the step tolerance
+
+
+@pytest.mark.gpu
+def test_optimize_with_recompute_preint_matches_oracle():
+    """vb_optimize with --recompute-preint: the preintegrations are recomputed at the start of every
+    iteration (after the rolling-shutter rebuild, as the oracle); same LM trajectory."""
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
+    p = synth.generate(synth.config("miniB"))
+    g, r = build(HipEngine, p, recompute=True), build(RefEngine, p, recompute=True)
+    s = Settings.default(max_num_iterations=6)
+    sg, sr = g.optimize(s), r.optimize(s)
+    assert sg.num_iterations == sr.num_iterations
+    assert abs(sg.initial_cost - sr.initial_cost) <= 1e-10 * sr.initial_cost
+    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
+    for k in range(1, NUM_VAR_KINDS - 1):
+        if len(g.get_vars(k)):
+            assert rel(g.get_vars(k), r.get_vars(k)) < 1e-7, VAR_NAMES[k]
+
+
+@pytest.mark.gpu
+def test_device_preintegration_uncovered_interval_is_an_error():
+    """an interval past the end of the stream: VB_E_RANGE (enumIntegrationSteps throws in the reference)"""
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine, VbError
+    p = synth.generate(synth.config("miniB"))
+    g = HipEngine(imu_calib_options=p.imu_calib_options)
+    synth.load_into(g, p, finalize=False, rs_device=True)
+    g.set_preint_sources(1, np.zeros(len(p.fvars[1]), np.int32), p.rs_mid[p.fvars[1][:, 1]],
+                         p.rs_mid[p.fvars[1][:, 3]] + 10**9)
+    g.finalize()
+    with pytest.raises(VbError) as ex:
+        g.update_preintegrations()
+    assert ex.value.code == -5

@@ -24,6 +24,7 @@ void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo,
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_rs_build(const Dev& d, hipStream_t st);
+void launch_preint(const Dev& d, const PreintArgs& pa, hipStream_t st);
 void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gObs, const int32_t* gPt, int64_t nG,
                           double* backups, double* acc, hipStream_t st);
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
@@ -78,6 +79,8 @@ constexpr int kVarData[9] = {3, 7, 3, 3, 24, 7, 32, 7, 4};
 constexpr int kMaxTan[9] = {3, 6, 3, 3, 17, 6, 23, 6, 2};
 constexpr int kNumVars[14] = {5, 6, 9, 10, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1};
 constexpr int kNumConsts[14] = {6, 331, 331, 331, 4, 23, 17, 6, 6, 43, 55, 41, 13, 13};
+// ImuNoiseModelParameters::reset sample variances (imu_types/ImuNoiseModelParameters.h:78-80): accel 3, gyro 3
+constexpr double kDefaultImuNoise[6] = {6.6297049e-3, 6.6297049e-3, 6.6297049e-3, 2.7415568e-05, 2.7415568e-05, 2.7415568e-05};
 const int kFK[14][10] = {{0, 1, 5, 4, 2}, {6, 1, 2, 1, 2, 8}, {6, 1, 2, 3, 1, 2, 3, 7, 8},
                          {6, 1, 2, 3, 7, 1, 2, 3, 7, 8}, {3, 7}, {6, 6}, {4, 4}, {7, 7}, {5, 5}, {1}, {6}, {4},
                          {5}, {7}};
@@ -198,12 +201,18 @@ int upload(T** dptr, const std::vector<T>& v) {
   const size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
   HIPCHK(hipMalloc((void**)dptr, bytes));
   if (!v.empty()) HIPCHK(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  // the engine's streams are non-blocking: they do not order behind the null stream the copy runs on
+  HIPCHK(hipStreamSynchronize(nullptr));
   return 0;
 }
 template <typename T>
 int alloc0(T** dptr, size_t n) {
   HIPCHK(hipMalloc((void**)dptr, std::max<size_t>(1, n) * sizeof(T)));
   HIPCHK(hipMemset(*dptr, 0, std::max<size_t>(1, n) * sizeof(T)));
+  // hipMemset may return before the clear lands, and the engine's non-blocking streams do not order
+  // behind it: a buffer allocated mid-run (the Gauss-Seidel pseudo-factor store) was once copied into
+  // before its clear ran, leaving zero diagonal tiles (a "Cholesky breakdown" only in long test runs)
+  HIPCHK(hipStreamSynchronize(nullptr));
   return 0;
 }
 
@@ -243,6 +252,14 @@ struct vb_handle_s {
   std::vector<int32_t> rsCalib;
   int32_t rsGravVar = -1;
   bool rsDevice = false, rsTimed = false;
+  // --recompute-preint (vb_set_imu_stream / vb_set_imu_noise / vb_set_preint_sources): IMU streams
+  // 1.. (stream 0 is imuT / imuV), per IMU sample variances, per inertial row its IMU and interval
+  std::vector<std::vector<int64_t>> piT;
+  std::vector<std::vector<double>> piV;
+  std::vector<double> piNoise;  // 6 per IMU: accel var 3, gyro var 3
+  std::vector<PreintSrc> piSrc;
+  PreintArgs pi;
+  bool recomputePreint = false;
   // point refinement groups (built at the first vb_refine_points): observations by point
   int64_t nRefG = 0;
   int64_t* refStartD = nullptr;
@@ -379,6 +396,8 @@ int checkRsErr(vb_handle h, int32_t e) {
   if (e & 1) return fail(VB_E_RANGE, "enumIntegrationSteps: IMU measurements do not cover the rolling-shutter interval");
   if (e & 2) return fail(VB_E_NUMERIC, "RollingShutterData::compute: non-increasing sample times");
   if (e & 4) return fail(VB_E_STATE, "internal: rolling-shutter table capacity exceeded");
+  if (e & 8) return fail(VB_E_RANGE, "enumIntegrationSteps: IMU measurements do not cover a preintegration interval");
+  if (e & 16) return fail(VB_E_NUMERIC, "computePreIntegration: covariance not positive definite");
   return 0;
 }
 
@@ -1315,6 +1334,34 @@ int doFinalize(vb_handle h) {
       (alloc0(&d.sJ, (size_t)d.nSmallStage * kSmallJ) || alloc0(&d.sE, (size_t)d.nSmallStage * kSmallE) ||
        alloc0(&d.sMeta, (size_t)d.nSmallStage * kSmallMeta)))
     return VB_E_HIP;
+  // ---------------- --recompute-preint inputs (preint.hip)
+  if (!h->piSrc.empty()) {
+    const int nStreams = (int)std::max<size_t>(1, h->piT.size());
+    std::vector<int64_t> off(nStreams + 1, 0), tAll;
+    std::vector<double> vAll;
+    for (int s = 0; s < nStreams; s++) {
+      const std::vector<int64_t>& t = s == 0 ? h->imuT : h->piT[s];
+      const std::vector<double>& v = s == 0 ? h->imuV : h->piV[s];
+      tAll.insert(tAll.end(), t.begin(), t.end());
+      vAll.insert(vAll.end(), v.begin(), v.end());
+      off[s + 1] = (int64_t)tAll.size();
+    }
+    for (const PreintSrc& p : h->piSrc)
+      if (p.imu < 0 || p.imu >= nStreams || off[p.imu + 1] == off[p.imu])
+        return fail(VB_E_ARG, "preintegration source names an IMU without a measurement stream");
+    std::vector<double> noise((size_t)nStreams * 6);
+    for (int s = 0; s < nStreams; s++)
+      for (int k = 0; k < 6; k++)
+        noise[s * 6 + k] = 6 * s + k < (int)h->piNoise.size() ? h->piNoise[6 * s + k] : kDefaultImuNoise[k];
+    h->piNoise = noise;
+    PreintSrc* srcD = nullptr;
+    int64_t *tD = nullptr, *offD = nullptr;
+    double *vD = nullptr, *nD = nullptr;
+    if (upload(&srcD, h->piSrc) || upload(&tD, tAll) || upload(&vD, vAll) || upload(&offD, off) || upload(&nD, noise))
+      return VB_E_HIP;
+    h->pi.src = srcD, h->pi.t = tD, h->pi.v = vD, h->pi.off = offD, h->pi.noise = nD;
+    h->pi.n = (int64_t)h->piSrc.size();
+  }
   // ---------------- uploads
   for (int k = 0; k < 9; k++) {
     if (upload(&d.var[k], h->data[k])) return VB_E_HIP;
@@ -1769,7 +1816,8 @@ int vb_destroy(vb_handle h) {
                   d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
-                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->facSync};
+                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->facSync,
+                  (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int k = 0; k < 9; k++) {
@@ -1875,10 +1923,11 @@ int vb_set_rs_rigs(vb_handle h, int32_t nt, const int64_t* mid_us, const int64_t
 }
 
 // enqueue the rebuild; its errors surface at the next synchronising check (checkErr reads err[1])
-int rsUpdateAsync(vb_handle h) {
+int rsUpdateAsync(vb_handle h, bool tables = true, bool preint = false) {
   HIPCHK(hipMemsetAsync(h->d.err + 1, 0, sizeof(int32_t), h->st));
   HIPCHK(hipEventRecord(h->ev[8], h->st));
-  launch_rs_build(h->d, h->st);
+  if (tables) launch_rs_build(h->d, h->st);
+  if (preint) launch_preint(h->d, h->pi, h->st);
   HIPCHK(hipEventRecord(h->ev[9], h->st));
   h->rsTimed = true;
   return 0;
@@ -1892,6 +1941,88 @@ int vb_update_rs_tables(vb_handle h) {
   HIPCHK(hipMemcpyAsync(&e, h->d.err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
   return checkRsErr(h, e);
+}
+
+int vb_set_imu_stream(vb_handle h, int imu, int64_t n, const int64_t* timestamp_ns, const double* gyro,
+                      const double* accel) {
+  if (!h || imu < 0 || n < 0 || (n && (!timestamp_ns || !gyro || !accel))) return fail(VB_E_ARG, "bad vb_set_imu_stream arguments");
+  if (imu == 0) return vb_set_imu_measurements(h, n, timestamp_ns, gyro, accel);
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_imu_stream after vb_finalize");
+  if ((int)h->piT.size() <= imu) h->piT.resize(imu + 1), h->piV.resize(imu + 1);
+  std::vector<int64_t>& t = h->piT[imu];
+  std::vector<double>& v = h->piV[imu];
+  t.assign(timestamp_ns, timestamp_ns + n);
+  v.resize((size_t)n * 6);
+  for (int64_t i = 0; i < n; i++) {
+    if (i && timestamp_ns[i] <= timestamp_ns[i - 1]) return fail(VB_E_ARG, "IMU timestamps must increase");
+    for (int k = 0; k < 3; k++) v[6 * i + k] = gyro[3 * i + k], v[6 * i + 3 + k] = accel[3 * i + k];
+  }
+  return 0;
+}
+
+int vb_set_imu_noise(vb_handle h, int imu, const double* accel_var, const double* gyro_var) {
+  if (!h || imu < 0 || !accel_var || !gyro_var) return fail(VB_E_ARG, "bad vb_set_imu_noise arguments");
+  if (h->finalized && (h->pi.n == 0 || 6 * imu + 6 > (int)h->piNoise.size()))
+    return fail(VB_E_STATE, "vb_set_imu_noise after vb_finalize for an IMU without preintegration sources");
+  if ((int)h->piNoise.size() < 6 * imu + 6) {
+    const size_t was = h->piNoise.size();
+    h->piNoise.resize(6 * imu + 6);
+    for (size_t k = was; k < h->piNoise.size(); k++) h->piNoise[k] = kDefaultImuNoise[k % 6];
+  }
+  for (int k = 0; k < 3; k++) h->piNoise[6 * imu + k] = accel_var[k], h->piNoise[6 * imu + 3 + k] = gyro_var[k];
+  if (h->finalized) {
+    HIPCHK(hipMemcpyAsync(const_cast<double*>(h->pi.noise) + 6 * imu, &h->piNoise[6 * imu], 6 * sizeof(double),
+                          hipMemcpyHostToDevice, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+  }
+  return 0;
+}
+
+int vb_set_preint_sources(vb_handle h, int kind, int64_t n, const int32_t* imu, const int64_t* t0_us,
+                          const int64_t* t1_us) {
+  if (!h || kind < VB_F_IMU || kind > VB_F_IMU_SEC_SPLIT || n < 0 || (n && (!imu || !t0_us || !t1_us)))
+    return fail(VB_E_ARG, "bad vb_set_preint_sources arguments (inertial kinds only)");
+  if (h->finalized) return fail(VB_E_STATE, "vb_set_preint_sources after vb_finalize");
+  if (n != (int64_t)h->fint[kind].size()) return fail(VB_E_ARG, "vb_set_preint_sources: one source per factor row of the kind");
+  std::vector<PreintSrc> keep;
+  for (const PreintSrc& p : h->piSrc)
+    if (p.kind != kind) keep.push_back(p);
+  for (int64_t r = 0; r < n; r++) {
+    if (imu[r] < 0) return fail(VB_E_ARG, "vb_set_preint_sources: bad IMU index");
+    if (t1_us[r] <= t0_us[r]) return fail(VB_E_ARG, "vb_set_preint_sources: empty interval");
+    keep.push_back(PreintSrc{kind, imu[r], r, t0_us[r], t1_us[r]});
+  }
+  h->piSrc.swap(keep);
+  return 0;
+}
+
+int vb_set_recompute_preint(vb_handle h, int on) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  h->recomputePreint = on != 0;
+  return 0;
+}
+
+int vb_update_preintegrations(vb_handle h) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_update_preintegrations before vb_finalize");
+  if (h->pi.n == 0) return 0;
+  if (int rc = rsUpdateAsync(h, false, true)) return rc;
+  int32_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, h->d.err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkRsErr(h, e);
+}
+
+int vb_get_factor_consts(vb_handle h, int kind, int64_t row, double* out) {
+  if (!h || kind < 0 || kind >= 14 || !out || row < 0 || row >= (int64_t)h->fint[kind].size())
+    return fail(VB_E_ARG, "bad vb_get_factor_consts arguments");
+  if (!h->finalized || kind == VB_F_VISUAL) {
+    std::copy(&h->fconst[kind][row * kNumConsts[kind]], &h->fconst[kind][(row + 1) * kNumConsts[kind]], out);
+    return 0;
+  }
+  const SmallFactors& sf = h->d.sf[kind];
+  HIPCHK(hipMemcpyAsync(out, sf.consts + row * sf.nc, kNumConsts[kind] * sizeof(double), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  return 0;
 }
 
 int vb_refine_points(vb_handle h, double* costs, int64_t* stats) {
@@ -2107,6 +2238,15 @@ int vb_debug_negate_model_reduction(vb_handle h, int iteration) {
   h->faultNegModelRedIt = iteration;
   return 0;
 }
+// slot of tile (I, J) of the reduced tile store (vb_reduced_buffers), -1 when it is not stored
+int vb_debug_tile_slot(vb_handle h, int32_t I, int32_t J, int64_t* slot) {
+  if (!h || !h->finalized || !slot) return fail(VB_E_STATE, "vb_debug_tile_slot before vb_finalize");
+  *slot = -1;
+  if (I < J || J < 0 || I >= h->d.nT) return 0;
+  for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++)
+    if (h->colRowsH[c] == I) *slot = h->colTilesH[c];
+  return 0;
+}
 int vb_pcg_stats(vb_handle h, int32_t* iterations, double* relative_residual) {
   if (!h) return fail(VB_E_ARG, "null handle");
   if (iterations) *iterations = h->pcgIters;
@@ -2304,7 +2444,9 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
   while (true) {
     auto t0 = std::chrono::steady_clock::now();
     // ark_vi_ba's preStepCallback (main_AriaKit_ViBa.cpp:95-101): updateRollingShutterData
-    if (h->rsDevice && (rc = rsUpdateAsync(h))) return rc;
+    // and, under --recompute-preint, the preintegrations from the IMU streams (InertialFactors.cpp:19-70)
+    const bool preint = h->recomputePreint && h->pi.n > 0;
+    if ((h->rsDevice || preint) && (rc = rsUpdateAsync(h, h->rsDevice, preint))) return rc;
     if (pre) pre(it, user);
     double prevCost;
     if ((rc = vb_linearize(h, 1, dontRetry, &prevCost))) return rc;

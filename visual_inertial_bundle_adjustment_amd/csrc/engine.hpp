@@ -61,6 +61,22 @@ struct ImuIdx {
   int gB, aB, gS, aS, gN, aN, rT, gaT, size;
 };
 
+// --recompute-preint (preint.hip): one inertial factor row to re-preintegrate -- its kind (1..3), row,
+// IMU and interval [us]; the IMU streams concatenated (stream s = samples off[s] .. off[s + 1]: stamps
+// [ns], [gyro 3, accel 3]), per IMU the sample variances [accel 3, gyro 3]
+struct PreintSrc {
+  int32_t kind, imu;
+  int64_t row, t0Us, t1Us;
+};
+struct PreintArgs {
+  const PreintSrc* src = nullptr;
+  int64_t n = 0;
+  const int64_t* t = nullptr;
+  const double* v = nullptr;
+  const int64_t* off = nullptr;
+  const double* noise = nullptr;
+};
+
 struct LossParams {
   double a, b, k2, h;
 };
