@@ -157,6 +157,7 @@ struct Problem {
   // landmark shard (multi-device controller test): points [lmB, lmE) of the elimination range;
   // the root also owns the constant-point observations and every non-visual factor
   int64_t lmB = 0, lmE = -1;
+  int partRank = 0, partWorld = 1;  // ref_set_partition: contiguous landmark cut, rank 0 the root
   bool root = true;
   std::vector<double> rRed, zS, zNewS;  // partial reduced RHS / per-point z of the shard
   std::vector<double> backup[9];
@@ -620,13 +621,16 @@ double singleGradHess(Problem& P, int fk, int64_t k, double* g, bool hess, bool 
   return ret;
 }
 
+void shardRange(const Problem& P, int64_t& b, int64_t& e);
 // does this handle own factor (fk, k)?  (visual: by its point; others: the root)
 bool inShard(const Problem& P, int fk, int64_t k) {
   if (fk != 0) return P.root;
   const int32_t pt = P.fvars[0][(size_t)k * 5];
   const int64_t pi = P.pidx[0][pt];
   if (pi < 0) return P.root;
-  return pi >= P.lmB && pi < (P.lmE < 0 ? P.nPts : P.lmE);
+  int64_t b, e;
+  shardRange(P, b, e);
+  return pi >= b && pi < e;
 }
 
 // the factor loop of FactorStore::computeGradHess / computeCost (Factor.h:704-734, 664-701): serial, or
@@ -1263,9 +1267,10 @@ void applyStep(Problem& P, const std::vector<double>& st, double ratios[3]) {
 void applyStepRaw(Problem& P, const std::vector<double>& st, double raw[3]) {
   double maxR = 0, sq = 0, sum = 0;
   const int64_t nParams = (int64_t)P.params.size();
-  const int64_t lmE = P.lmE < 0 ? P.nPts : P.lmE;
+  int64_t lmB, lmE;
+  shardRange(P, lmB, lmE);
   for (int64_t p = 0; p < nParams; p++) {
-    if (p < P.nPts && (p < P.lmB || p >= lmE)) continue;
+    if (p < P.nPts && (p < lmB || p >= lmE)) continue;
     const bool counted = p < P.nPts || P.root;
     const int kind = P.params[p].kind, h = P.params[p].handle;
     const double* s = &st[P.pstart[p]];
@@ -2073,7 +2078,13 @@ void shardPointY(const Problem& P, int64_t pt, const double* V, std::vector<Mat>
     Y.push_back(Wb);
   }
 }
-void shardRange(const Problem& P, int64_t& b, int64_t& e) { b = P.lmB, e = P.lmE < 0 ? P.nPts : P.lmE; }
+void shardRange(const Problem& P, int64_t& b, int64_t& e) {
+  if (P.partWorld > 1) {
+    b = P.nPts * P.partRank / P.partWorld, e = P.nPts * (P.partRank + 1) / P.partWorld;
+    return;
+  }
+  b = P.lmB, e = P.lmE < 0 ? P.nPts : P.lmE;
+}
 // r = g_red - sum_{shard points} Y^T z, z = L^-1 g_p (stored in zOut)
 void shardRhs(Problem& P, const std::vector<double>& g, std::vector<double>& zOut) {
   P.rRed.assign(P.nRed, 0.0);
@@ -2230,6 +2241,50 @@ int ref_back_substitute(void* h, double* mcr) { return ref_back_substitute_which
 int ref_assemble_new_rhs(void* h) {
   Problem& P = *(Problem*)h;
   shardRhs(P, P.gradNew, P.zNewS);
+  return 0;
+}
+
+// The partitioned-factorization protocol of the HIP engine (vb_set_partition, vb_factor_part,
+// vb_solve_part, vb_part_exchange, vb_share_x; include/viba_hip.h, distributed.PartitionedOptimizer)
+// restated on this oracle's whole-system storage, so the controller's exchange sequence runs on CPU
+// ranks (gloo): rank r owns the r-th contiguous cut of the landmarks, rank 0 the small factors and the
+// identity damping (the shard semantics above); the "ROOT" exchange is the whole partial system and
+// RHS, rank 0 factors and solves it, and the subtree phases have no work.  The nested-dissection
+// subtrees themselves are the HIP engine's; their arithmetic is checked against this oracle by
+// tests/test_distributed_gpu.py.
+int ref_set_partition(void* h, int rank, int world) {
+  Problem& P = *(Problem*)h;
+  if (world < 1 || (world & (world - 1)) || rank < 0 || rank >= world) return (g_err = "bad partition", -1);
+  P.partRank = rank, P.partWorld = world, P.root = rank == 0;
+  return 0;
+}
+int ref_factor_part(void* h, int which) {
+  Problem& P = *(Problem*)h;
+  if (which == 1 && P.partRank == 0 && !beFactor(P, P.L)) return (g_err = "cholesky breakdown", -4);
+  return 0;
+}
+int ref_solve_part(void* h, int phase) {
+  Problem& P = *(Problem*)h;
+  if (phase == 1 && P.partRank == 0) shardSolve(P, P.rRed);
+  return 0;
+}
+int ref_part_exchange(void* h, int what, int /*dir: in place*/, double** buf, int64_t* len) {
+  Problem& P = *(Problem*)h;
+  std::vector<double>& v = what == 0 ? P.L : P.rRed;
+  if (buf) *buf = v.data();
+  if (len) *len = (int64_t)v.size();
+  return 0;
+}
+int ref_share_x(void* h, double** buf, int64_t* len) {
+  Problem& P = *(Problem*)h;
+  if (P.partRank != 0) std::fill(P.rRed.begin(), P.rRed.end(), 0.0);
+  if (buf) *buf = P.rRed.data();
+  if (len) *len = (int64_t)P.rRed.size();
+  return 0;
+}
+int ref_part_info(void* h, int64_t* out5) {
+  Problem& P = *(Problem*)h;
+  out5[0] = 0, out5[1] = P.nRed, out5[2] = 0, out5[3] = 0, out5[4] = (int64_t)P.L.size();
   return 0;
 }
 }  // extern "C"

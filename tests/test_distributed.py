@@ -77,3 +77,50 @@ def test_two_shards_match_single_process(which, its, tmp_path):
     pts = np.where(r[0]["own"][:, None], r[0]["pts"], r[1]["pts"])
     assert np.all(r[0]["own"] ^ r[1]["own"] | ~(r[0]["own"] | r[1]["own"]))
     assert rel(pts, e.get_vars(0)) < tol
+
+
+def _part_worker(rank, world, port, which, its, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "tests")]
+    import torch.distributed as dist
+    from oracle.refcpu import RefEngine
+    from visual_inertial_bundle_adjustment_amd import synth
+    from visual_inertial_bundle_adjustment_amd.distributed import PartitionedOptimizer, ShardComm
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = synth.generate(synth.config(which))
+    e = RefEngine(imu_calib_options=p.imu_calib_options)
+    e.set_partition(rank, world)
+    synth.load_into(e, p)
+    s = PartitionedOptimizer(e, ShardComm(rank, world, None)).optimize(_settings(its))
+    res = {"iters": s.num_iterations, "initial": s.initial_cost, "final": s.final_cost}
+    for k in range(1, 8):
+        res[f"v{k}"] = e.get_vars(k)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_partitioned_controller_matches_single_process(world, tmp_path):
+    """distributed.PartitionedOptimizer (the default multi-GPU mode) on gloo CPU ranks over the oracle's
+    restatement of the partition protocol (refcpu.cpp ref_set_partition & co.: every exchange the HIP
+    engine makes -- ROOT tiles and forward rows reduced to rank 0, ROOT factor + solve there, x rows
+    broadcast, x shared by all-reduce, per-rank back-substitution of its landmarks -- carries the whole
+    partial system here): same LM trajectory as the single-process oracle."""
+    from oracle.refcpu import RefEngine
+    from parity_util import make, rel
+    which, its = "miniB", 6
+    mp.spawn(_part_worker, args=(world, _free_port(), which, its, str(tmp_path)), nprocs=world, join=True)
+    r = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
+    e, _ = make(RefEngine, which)
+    s = e.optimize(_settings(its))
+    for k in range(world):
+        assert int(r[k]["iters"]) == s.num_iterations
+        assert abs(float(r[k]["initial"]) - s.initial_cost) <= 1e-11 * s.initial_cost
+        assert abs(float(r[k]["final"]) - s.final_cost) <= 1e-9 * s.final_cost
+        for kind in range(1, 8):
+            ref = e.get_vars(kind)
+            if len(ref):
+                assert rel(r[k][f"v{kind}"], ref) < 1e-7, kind

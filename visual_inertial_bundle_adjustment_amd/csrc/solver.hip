@@ -99,7 +99,8 @@ __device__ __forceinline__ void landmark_eliminate(const Dev& d, double lambda, 
     d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
   }
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  rec_t* Y = d.Y + d.lmY[l];
+  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
+  const int64_t yq = d.nYcol;
   for (int64_t c = lane; c < ncol; c += 64) {
     const int32_t b = d.pcBlk[cb + c];
     const int j = (int)(c - d.blkCol[b]);
@@ -118,7 +119,7 @@ __device__ __forceinline__ void landmark_eliminate(const Dev& d, double lambda, 
     const double y0 = w0 / l00;
     const double y1 = (w1 - l10 * y0) / l11;
     const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
-    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
+    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
   }
 }
 __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int mode, int64_t lo, int64_t hi) {
@@ -204,12 +205,13 @@ __global__ void __launch_bounds__(256) landmark_obs_kernel(Dev d, double lambda,
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  rec_t* Y = d.Y + d.lmY[l];
+  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
+  const int64_t yq = d.nYcol;
   for (int64_t c = lane; c < ncol; c += 64) {
     const double y0 = W[3 * c] / l00;
     const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
     const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
-    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
+    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
   }
 }
 
@@ -279,12 +281,13 @@ __global__ void __launch_bounds__(256) landmark_obs_wg_kernel(Dev d, double lamb
   }
   __syncthreads();
   const double l00 = Ls[0], l10 = Ls[1], l20 = Ls[2], l11 = Ls[3], l21 = Ls[4], l22 = Ls[5];
-  rec_t* Y = d.Y + d.lmY[l];
+  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
+  const int64_t yq = d.nYcol;
   for (int64_t c = tid; c < ncol; c += 256) {
     const double y0 = W[3 * c] / l00;
     const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
     const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
-    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
+    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
   }
 }
 
@@ -350,6 +353,10 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 #endif
 constexpr int kCh = VIBA_SCHUR_CH;  // landmarks per task
 constexpr int kTR = VIBA_SCHUR_TR;  // compact block rows per task (1 or 2)
+#ifndef VIBA_SCHUR_PF
+#define VIBA_SCHUR_PF 1
+#endif
+constexpr int kPF = VIBA_SCHUR_PF;  // k-steps of operand gathers in flight
 
 __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
   __shared__ double C[TS * TS];
@@ -418,27 +425,33 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
 #pragma unroll
         for (int i = 0; i < kTR; i++) {
           const int m = 16 * (a0 + i) + l15;
-          av[i] = (kv && m < nJ) ? d.Y[3 * (cJ + m) + q] : (rec_t)0;
+          av[i] = (kv && m < nJ) ? d.Y[q * d.nYcol + cJ + m] : (rec_t)0;
         }
 #pragma unroll
         for (int b = 0; b < 4; b++) {
           const int n = 16 * b + l15;
-          bv[b] = (kv && b < nbI && n < nI) ? d.Y[3 * (cI + n) + q] : (rec_t)0;
+          bv[b] = (kv && b < nbI && n < nI) ? d.Y[q * d.nYcol + cI + n] : (rec_t)0;
         }
       };
-      rec_t av[kTR], bv[4], av2[kTR], bv2[4];
-      ld(0, av, bv);
-      for (int ks = 0; ks < nks; ks++) {
-        if (ks + 1 < nks) ld(ks + 1, av2, bv2);
+      // kPF k-steps of operand gathers in flight: a ring of register sets, refilled right after its
+      // MFMAs issue (the gathers are scattered 8 B loads, mostly L2 hits; one step ahead left the
+      // waves waiting on them)
+      rec_t av[kPF][kTR], bv[kPF][4];
 #pragma unroll
-        for (int i = 0; i < kTR; i++)
+      for (int p = 0; p < kPF; p++)
+        if (p < nks) ld(p, av[p], bv[p]);
+      for (int ks0 = 0; ks0 < nks; ks0 += kPF) {
 #pragma unroll
-          for (int b = 0; b < 4; b++)
-            if (a0 + i < nbJ && b < nbI && !(diag && a0 + i > b)) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
+        for (int p = 0; p < kPF; p++) {
+          if (ks0 + p < nks) {
 #pragma unroll
-        for (int i = 0; i < kTR; i++) av[i] = av2[i];
+            for (int i = 0; i < kTR; i++)
 #pragma unroll
-        for (int b = 0; b < 4; b++) bv[b] = bv2[b];
+              for (int b = 0; b < 4; b++)
+                if (a0 + i < nbJ && b < nbI && !(diag && a0 + i > b)) acc[i][b] = mfma_h(av[p][i], bv[p][b], acc[i][b]);
+            if (ks0 + p + kPF < nks) ld(ks0 + p + kPF, av[p], bv[p]);
+          }
+        }
       }
 #pragma unroll
       for (int i = 0; i < kTR; i++)
@@ -454,9 +467,9 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
       if (diag && a0 == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
         double racc = 0.0;
         for (int e = c0; e < c0 + nl; e++) {
-          const rec_t* y = d.Y + 3 * ((int64_t)ecol[e][0] + lane);
+          const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
           const double* zz = d.z + 3 * (int64_t)ents[e].lm;
-          racc += (double)y[0] * zz[0] + (double)y[1] * zz[1] + (double)y[2] * zz[2];
+          racc += (double)y[0] * zz[0] + (double)y[d.nYcol] * zz[1] + (double)y[2 * d.nYcol] * zz[2];
         }
         atomicAdd(&rq[posI[lane]], -racc);
       }
@@ -621,10 +634,11 @@ __global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
     for (int64_t idx = d.lxStart[X1] + tid; idx < d.lxStart[X1 + 1]; idx += blockDim.x) {
       const int64_t l = d.lxLm[idx];
       if (l < d.lmB || l >= d.lmE) continue;
-      const rec_t* y1 = d.Y + d.lmY[l] + 3 * d.lxCol[idx];
+      const rec_t* y1 = d.Y + d.lmY[l] / 3 + d.lxCol[idx];
+      const int64_t yq = d.nYcol;
       const double z0 = d.zNew[l * 3], z1 = d.zNew[l * 3 + 1], z2 = d.zNew[l * 3 + 2];
       for (int j = 0; j < d1; j++)
-        atomicAdd(&g[j], (double)y1[3 * j] * z0 + (double)y1[3 * j + 1] * z1 + (double)y1[3 * j + 2] * z2);
+        atomicAdd(&g[j], (double)y1[j] * z0 + (double)y1[yq + j] * z1 + (double)y1[2 * yq + j] * z2);
     }
   }
   __syncthreads();
@@ -1392,11 +1406,12 @@ __global__ void __launch_bounds__(256) backsub_kernel(Dev d, int mode, int64_t l
   const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= hi) return;
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  const rec_t* Y = d.Y + d.lmY[l];
+  const rec_t* Y = d.Y + cb;
+  const int64_t yq = d.nYcol;
   double t0 = 0, t1 = 0, t2 = 0;
   for (int64_t c = lane; c < ncol; c += 64) {
     const double v = xr[d.pcRow[cb + c]];
-    t0 += Y[3 * c] * v, t1 += Y[3 * c + 1] * v, t2 += Y[3 * c + 2] * v;
+    t0 += Y[c] * v, t1 += Y[yq + c] * v, t2 += Y[2 * yq + c] * v;
   }
   t0 = wave_sum(t0), t1 = wave_sum(t1), t2 = wave_sum(t2);
   if (lane != 0) return;

@@ -344,6 +344,34 @@ class CEngineBase:
                                                               out.ctypes.data_as(_dp)))
         return out
 
+    # partitioned factorization (vb_set_partition & co.; the oracle restates the protocol)
+    def set_partition(self, rank: int, world: int):
+        self._check(self._fn("set_partition", [C.c_int, C.c_int])(self.h, rank, world))
+
+    def factor_part(self, which: int):
+        self._check(self._fn("factor_part", [C.c_int])(self.h, which))
+
+    def solve_part(self, phase: int):
+        self._check(self._fn("solve_part", [C.c_int])(self.h, phase))
+
+    def part_exchange(self, what: int, direction: int):
+        """(device pointer, length in doubles) of the engine-owned exchange buffer of `what`
+        (0 ROOT tiles, 1 ROOT rows of the forward work vector, 2 ROOT rows of x)."""
+        b, n = P(), C.c_int64()
+        self._check(self._fn("part_exchange", [C.c_int, C.c_int, C.POINTER(P), C.POINTER(C.c_int64)])(
+            self.h, what, direction, C.byref(b), C.byref(n)))
+        return b.value, n.value
+
+    def part_info(self):
+        out = (C.c_int64 * 5)()
+        self._check(self._fn("part_info", [C.c_int64 * 5])(self.h, out))
+        return list(out)
+
+    def share_x(self):
+        b, n = P(), C.c_int64()
+        self._check(self._fn("share_x", [C.POINTER(P), C.POINTER(C.c_int64)])(self.h, C.byref(b), C.byref(n)))
+        return b.value, n.value
+
 
 class HipEngine(CEngineBase):
     """The MI355X LM engine. One instance = one vb_handle = one HIP stream on `device`."""
@@ -443,33 +471,6 @@ class HipEngine(CEngineBase):
         self._check(self._fn("add_tiles", [C.c_void_p, C.c_int64, C.c_void_p])(self.h, tiles_dev, n, buf_dev))
 
     # partitioned factorization (HIP engine only; include/viba_hip.h vb_set_partition)
-    def set_partition(self, rank: int, world: int):
-        self._check(self._fn("set_partition", [C.c_int, C.c_int])(self.h, rank, world))
-
-    def factor_part(self, which: int):
-        self._check(self._fn("factor_part", [C.c_int])(self.h, which))
-
-    def solve_part(self, phase: int):
-        self._check(self._fn("solve_part", [C.c_int])(self.h, phase))
-
-    def part_exchange(self, what: int, direction: int):
-        """(device pointer, length in doubles) of the engine-owned exchange buffer of `what`
-        (0 ROOT tiles, 1 ROOT rows of the forward work vector, 2 ROOT rows of x)."""
-        b, n = P(), C.c_int64()
-        self._check(self._fn("part_exchange", [C.c_int, C.c_int, C.POINTER(P), C.POINTER(C.c_int64)])(
-            self.h, what, direction, C.byref(b), C.byref(n)))
-        return b.value, n.value
-
-    def part_info(self):
-        out = (C.c_int64 * 5)()
-        self._check(self._fn("part_info", [C.c_int64 * 5])(self.h, out))
-        return list(out)
-
-    def share_x(self):
-        b, n = P(), C.c_int64()
-        self._check(self._fn("share_x", [C.POINTER(P), C.POINTER(C.c_int64)])(self.h, C.byref(b), C.byref(n)))
-        return b.value, n.value
-
     def bench_kernel(self, which: int, iters: int = 200) -> float:
         us = C.c_double()
         self._check(self._fn("bench_kernel", [C.c_int, C.c_int, _dp])(self.h, which, iters, C.byref(us)))
