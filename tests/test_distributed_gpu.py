@@ -1,6 +1,6 @@
 """Landmark-sharded LM on the HIP engine: two processes (each a shard, both on cuda:0, gloo with
-host staging instead of RCCL on this one-GPU test box) reproduce the single-GPU vb_optimize run:
-same iterations, costs to 1e-9, variables to 1e-7 (summation order across shards differs)."""
+host staging instead of RCCL on this one-GPU test box) reproduce the single-GPU vb_optimize run and the
+CPU oracle's: same iterations, costs to 1e-9, variables to 1e-7 (summation order across shards differs)."""
 from __future__ import annotations
 
 import os
@@ -55,19 +55,22 @@ def _worker(rank, world, port, which, its, out_dir, mode="shard"):
 
 
 def _check_against_single(tmp_path, world, which, its):
+    """every rank against the single-GPU engine AND the CPU oracle (oracle/refcpu) on the same inputs"""
+    from oracle.refcpu import RefEngine
     from parity_util import make, rel
     from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
     r = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
-    e, _ = make(HipEngine, which)
-    s = e.optimize(Settings.default(max_num_iterations=its))
-    for k in range(world):
-        assert int(r[k]["iters"]) == s.num_iterations
-        assert abs(float(r[k]["initial"]) - s.initial_cost) <= 1e-11 * s.initial_cost
-        assert abs(float(r[k]["final"]) - s.final_cost) <= 1e-9 * s.final_cost
-        for kind in range(1, 8):
-            ref = e.get_vars(kind)
-            if len(ref):
-                assert rel(r[k][f"v{kind}"], ref) < 1e-7, kind
+    for cls in (HipEngine, RefEngine):
+        e, _ = make(cls, which)
+        s = e.optimize(Settings.default(max_num_iterations=its))
+        for k in range(world):
+            assert int(r[k]["iters"]) == s.num_iterations, cls
+            assert abs(float(r[k]["initial"]) - s.initial_cost) <= 1e-11 * s.initial_cost, cls
+            assert abs(float(r[k]["final"]) - s.final_cost) <= 1e-9 * s.final_cost, cls
+            for kind in range(1, 8):
+                ref = e.get_vars(kind)
+                if len(ref):
+                    assert rel(r[k][f"v{kind}"], ref) < 1e-7, (cls, kind)
 
 
 @pytest.mark.parametrize("which,its", [("miniB", 8)])

@@ -1396,7 +1396,8 @@ int doFinalize(vb_handle h) {
       upload(&d.bxStart, bxStart) || upload(&d.bxEnt, bxEnt))
     return VB_E_HIP;
   if (alloc0(&d.Vchol, nPts * 6) || alloc0(&d.gp, nPts * 3) || alloc0(&d.z, nPts * 3) || alloc0(&d.xp, nPts * 3) ||
-      alloc0(&d.Y, lmY[nPts]) || alloc0(&d.gpNew, nPts * 3) || alloc0(&d.zNew, nPts * 3))
+      alloc0(&d.Y, lmY[nPts] + 128) || alloc0(&d.yZero, 128) ||  // + the over-read of the Schur gathers
+      alloc0(&d.gpNew, nPts * 3) || alloc0(&d.zNew, nPts * 3))
     return VB_E_HIP;
   if (upload(&d.oxStart, oxStart) || upload(&d.oxObs, oxObs) || upload(&d.oxSlot, oxSlot) ||
       upload(&d.lxStart, lxStart) || upload(&d.lxLm, lxLm) || upload(&d.lxCol, lxCol))
@@ -1810,7 +1811,7 @@ int vb_destroy(vb_handle h) {
   Dev& d = h->d;
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
-                  d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
+                  d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.yZero, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.err, h->colTilesD,

@@ -358,7 +358,75 @@ constexpr int kTR = VIBA_SCHUR_TR;  // compact block rows per task (1 or 2)
 #endif
 constexpr int kPF = VIBA_SCHUR_PF;  // k-steps of operand gathers in flight
 
-__global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
+// One task's K loop: acc[i][b] += A_i^T B_b over the dense K rows (3 per landmark) of landmarks
+// c0 .. c0 + rows / 3, A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block
+// b < NBI.  Lane (l4, l15) at k-step ks takes K row kr = 4 ks + l4, i.e. plane q = kr % 3 of landmark
+// c0 + kr / 3 (advanced incrementally), and gathers its NR + NBI operands at fixed offsets 16 i / 16 b
+// from the landmark's first panel column in tile J / I.  Columns past nJ / nI load neighbouring
+// panel data into accumulator rows / columns that are never stored; K rows past `rows` read the zero
+// pad.  The next step's gathers are issued before the current step's MFMAs.
+template <int NBI, int NR, bool DIAG>
+__device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0, int rows, int a0, int l4, int l15,
+                                           const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
+  hacc4_t acc[NR][NBI];
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int b = 0; b < NBI; b++) acc[i][b] = hacc4_t{0, 0, 0, 0};
+  const int nks = (rows + 3) >> 2;
+  const int64_t pq = d.nYcol;
+  const rec_t* Y = d.Y;
+  const rec_t* zp = d.yZero + l15;
+  int kr = l4, e = c0 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
+  auto ld = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
+    const bool kv = kr < rows;
+    const uint2 c = ec[kv ? e : c0];
+    const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
+    const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
+    const rec_t* pI = kv ? base + c.x : zp;
+#pragma unroll
+    for (int i = 0; i < NR; i++) av[i] = pJ[16 * i];
+#pragma unroll
+    for (int b = 0; b < NBI; b++) bv[b] = pI[16 * b];
+    kr += 4, e += 1, q += 1;
+    if (q == 3) q = 0, e += 1;
+  };
+  auto mm = [&](const rec_t (&av)[NR], const rec_t (&bv)[NBI]) {
+#pragma unroll
+    for (int i = 0; i < NR; i++)
+#pragma unroll
+      for (int b = 0; b < NBI; b++)
+        if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
+  };
+  rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
+  ld(a0v, b0v);
+  for (int ks = 0; ks < nks; ks += 2) {
+    if (ks + 1 < nks) ld(a1v, b1v);
+    mm(a0v, b0v);
+    if (ks + 2 < nks) ld(a0v, b0v);
+    if (ks + 1 < nks) mm(a1v, b1v);
+  }
+  // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
+  int colT[NBI];
+#pragma unroll
+  for (int b = 0; b < NBI; b++) {
+    const int n = 16 * b + l15;
+    colT[b] = n < nI ? posI[n] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q;
+      if (m >= nJ) continue;
+      double* Cr = C + posJ[m] * TS;
+#pragma unroll
+      for (int b = 0; b < NBI; b++)
+        if ((!DIAG || a0 + i <= b) && colT[b] >= 0) atomicAdd(Cr + colT[b], -(double)acc[i][b][q]);
+    }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run2_kernel(Dev d, double lambda) {
   __shared__ double C[TS * TS];
   __shared__ uint32_t ecol[256][2];  // the entries' first panel columns (colI, colJ); the rest from global
   __shared__ int16_t runStart[258];
@@ -391,6 +459,7 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
   const int nRuns = nRunsS;
   uint8_t* posI = posW[wave][0];
   uint8_t* posJ = posW[wave][1];
+  const uint2* ec2 = reinterpret_cast<const uint2*>(&ecol[0][0]);
   int task = 0;
   for (int r = 0; r < nRuns; r++) {
     const int e0 = runStart[r], e1 = runStart[r + 1];
@@ -411,59 +480,24 @@ __global__ void __launch_bounds__(256) schur_run2_kernel(Dev d, double lambda) {
         mapped = true;
       }
       const int ch = t / nbR, a0 = kTR * (t - ch * nbR);
-      const int c0 = e0 + ch * kCh, nl = min(kCh, e1 - c0), rows = 3 * nl, nks = (rows + 3) >> 2;
-      hacc4_t acc[kTR][4];
-#pragma unroll
-      for (int i = 0; i < kTR; i++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) acc[i][b] = hacc4_t{0, 0, 0, 0};
-      auto ld = [&](int ks, rec_t (&av)[kTR], rec_t (&bv)[4]) {
-        const int kr = 4 * ks + l4;
-        const bool kv = kr < rows;
-        const int e = c0 + (kv ? kr / 3 : 0), q = kv ? kr - 3 * (kr / 3) : 0;
-        const int64_t cI = ecol[e][0], cJ = ecol[e][diag ? 0 : 1];
-#pragma unroll
-        for (int i = 0; i < kTR; i++) {
-          const int m = 16 * (a0 + i) + l15;
-          av[i] = (kv && m < nJ) ? d.Y[q * d.nYcol + cJ + m] : (rec_t)0;
-        }
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const int n = 16 * b + l15;
-          bv[b] = (kv && b < nbI && n < nI) ? d.Y[q * d.nYcol + cI + n] : (rec_t)0;
-        }
-      };
-      // kPF k-steps of operand gathers in flight: a ring of register sets, refilled right after its
-      // MFMAs issue (the gathers are scattered 8 B loads, mostly L2 hits; one step ahead left the
-      // waves waiting on them)
-      rec_t av[kPF][kTR], bv[kPF][4];
-#pragma unroll
-      for (int p = 0; p < kPF; p++)
-        if (p < nks) ld(p, av[p], bv[p]);
-      for (int ks0 = 0; ks0 < nks; ks0 += kPF) {
-#pragma unroll
-        for (int p = 0; p < kPF; p++) {
-          if (ks0 + p < nks) {
-#pragma unroll
-            for (int i = 0; i < kTR; i++)
-#pragma unroll
-              for (int b = 0; b < 4; b++)
-                if (a0 + i < nbJ && b < nbI && !(diag && a0 + i > b)) acc[i][b] = mfma_h(av[p][i], bv[p][b], acc[i][b]);
-            if (ks0 + p + kPF < nks) ld(ks0 + p + kPF, av[p], bv[p]);
-          }
-        }
+      const int c0 = e0 + ch * kCh, nl = min(kCh, e1 - c0), rows = 3 * nl;
+      // one specialised task (k-loop + epilogue) per (I-side blocks, J-side rows of this task, diagonal
+      // tile): no per-MFMA predicates, gathers at immediate offsets from per-step base pointers
+      const int nr = min(kTR, nbJ - a0);
+      const int sel = ((nbI - 1) * 2 + (nr - 1)) * 2 + (diag ? 1 : 0);
+      switch (sel) {
+#define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
+  case ((NBI - 1) * 2 + (NR - 1)) * 2:                                                                \
+    schur_task<NBI, NR, false>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                 \
+    break;                                                                                            \
+  case ((NBI - 1) * 2 + (NR - 1)) * 2 + 1:                                                            \
+    schur_task<NBI, NR, true>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                  \
+    break;
+        VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(2, 2)
+        VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 1) VIBA_SCHUR_CASE(4, 2)
+#undef VIBA_SCHUR_CASE
+        default: break;
       }
-#pragma unroll
-      for (int i = 0; i < kTR; i++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          if (a0 + i >= nbJ || b >= nbI || (diag && a0 + i > b)) continue;
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q, n = 16 * b + l15;
-            if (m < nJ && n < nI) atomicAdd(&C[posJ[m] * TS + posI[n]], -(double)acc[i][b][q]);
-          }
-        }
       if (diag && a0 == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
         double racc = 0.0;
         for (int e = c0; e < c0 + nl; e++) {
