@@ -22,9 +22,17 @@ root vb_solve_reduced -> broadcast -> vb_back_substitute_which(1)).
 
 The controller is engine-agnostic: the HIP engine (device buffers, RCCL) in production, the CPU
 oracle (host buffers, gloo) in the CPU tests.
+
+Stream ordering, not host round trips: with the HIP engine, the loop runs with torch's current stream
+set to the engine's own HIP stream (torch.cuda.ExternalStream over vb_stream).  RCCL then queues
+each collective behind the engine kernels that produced its input, and the engine kernels that
+consume its output queue behind the collective, so no exchange needs a stream or device
+synchronisation; the host waits only where the LM logic reads a scalar (cost, model reduction,
+step ratios), as Optimizer::optimize does.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 import os
@@ -117,8 +125,7 @@ class ShardComm:
                 for w in dist.batch_isend_irecv(ops):
                     w.wait()
             for r, n, b in bufs:
-                b = b.to(self.device)
-                torch.cuda.synchronize(self.device)
+                b = b.to(self.device)  # gloo: host -> device copy on the engine stream; nccl: no-op
                 engine.add_tiles(tile_lists[r].data_ptr(), n, b.data_ptr())
         else:
             ptr, n = engine.pack_shard_tiles()
@@ -161,6 +168,8 @@ class ShardedOptimizer:
     def __init__(self, engine, comm: ShardComm):
         self.e, self.c = engine, comm
         self.n_params = engine.num_params()
+        self.ext = self._engine_stream(engine, comm)
+        self.n_factor = 0  # reduced factorizations run (the bench's roofline)
         first, cnt = engine.shard_tile_range()
         self.bands = comm.all_gather_obj((first, cnt))
         # HIP engine: exact tile sets (the nested-dissection order spreads a shard's contributions
@@ -170,6 +179,19 @@ class ShardedOptimizer:
             lists = comm.all_gather_obj(engine.shard_tiles().tolist())
             self.tile_lists = [comm.torch.tensor(t, dtype=comm.torch.int32, device=comm.device) for t in lists]
         self.sync = getattr(engine, "synchronize", lambda: None)
+
+    @staticmethod
+    def _engine_stream(engine, comm):
+        """torch.cuda.ExternalStream over the engine's HIP stream (None for host engines)."""
+        if comm.device is None or comm.device.type == "cpu" or not hasattr(engine, "stream_ptr"):
+            return None
+        return comm.torch.cuda.ExternalStream(engine.stream_ptr(), device=comm.device)
+
+    def on_engine_stream(self):
+        """Context in which torch (and so RCCL) issues on the engine's stream."""
+        if self.ext is None:
+            return contextlib.nullcontext()
+        return self.c.torch.cuda.stream(self.ext)
 
     def _buffers(self):
         m, nm, r, nr = self.e.reduced_buffers()
@@ -182,6 +204,7 @@ class ShardedOptimizer:
 
     def damp_factor_solve(self, lam):
         e, c = self.e, self.c
+        self.n_factor += 1
         e.assemble_reduced(lam)
         S, b = self._buffers()
         if self.tile_lists is not None:
@@ -227,11 +250,16 @@ class ShardedOptimizer:
         return out[0], tuple(int(round(x)) for x in out[1:])
 
     def sync_torch(self):
-        if self.c.device is not None and self.c.device.type != "cpu":
+        """Order torch's work before the engine's: a no-op on the engine's own stream."""
+        if self.ext is None and self.c.device is not None and self.c.device.type != "cpu":
             self.c.torch.cuda.synchronize(self.c.device)
 
     # the loop ---------------------------------------------------------------------------
     def optimize(self, s: Settings | None = None) -> Summary:
+        with self.on_engine_stream():
+            return self._optimize(s)
+
+    def _optimize(self, s: Settings | None = None) -> Summary:
         s = s or Settings.default()
         e = self.e
         damping = s.damping
@@ -336,6 +364,8 @@ class PartitionedOptimizer(ShardedOptimizer):
     def __init__(self, engine, comm: ShardComm):
         self.e, self.c = engine, comm
         self.n_params = engine.num_params()
+        self.ext = self._engine_stream(engine, comm)
+        self.n_factor = 0
         self.tile_lists = None
 
     def _exchange(self, what, reduce):
@@ -372,6 +402,7 @@ class PartitionedOptimizer(ShardedOptimizer):
 
     def damp_factor_solve(self, lam):
         e, c = self.e, self.c
+        self.n_factor += 1
         e.assemble_reduced(lam)
         e.factor_part(0)
         self._exchange(0, True)
@@ -466,6 +497,9 @@ def run_sharded(args, rank: int, world: int, local: int):
                                 distance_from_troubled_iteration=0)
     if args.warmup:
         opt.optimize(settings(args.warmup))
+    # roofline: every fan-in launch of this rank timed with HIP events on the engine stream (family 4)
+    e.profile_kernel(4)
+    opt.n_factor = 0
     e.synchronize()
     dist.barrier()
     torch.cuda.synchronize(dev)
@@ -479,16 +513,46 @@ def run_sharded(args, rank: int, world: int, local: int):
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = t.item()
     iters = s.num_iterations
-    if rank == 0:
-        out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
-               "unit": "LM iterations/s", "n_gpus": world, "steps": iters, "warmup": args.warmup,
-               "ms_per_step": elapsed * 1e3 / max(1, iters), "higher_is_better": True, "scaling": "strong",
-               "vs_baseline": None, "dtype": "f64" if getattr(args, "precision", "fp64") == "fp64" else "f32/f64",
-               "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
-               "config": {"workload": f"config {args.config}: {st[0]} obs, {p.num_points} landmarks, "
-                                      f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",
-                          "parallelism": parallelism},
-               "roofline": None, "cpu_baseline": None,
-               "cost": [s.initial_cost, s.final_cost]}
-        print(json.dumps(out), flush=True)
+    launches, kms = e.kernel_time()
+    e.profile_kernel(-1)
+    if mode == "partition":
+        pi = e.part_info()
+        contrib = pi[2] + pi[3]  # this rank's subtree schedule (+ the ROOT schedule on rank 0)
+    else:
+        contrib = st[6] if rank == 0 else 0
+    flops = float(opt.n_factor) * contrib * 2.0 * 64 ** 3
+    per_rank = comm.all_gather_obj((launches, kms, flops))
+    ph = e.phase_times()
     dist.destroy_process_group()
+    if rank != 0:
+        return
+    FP64_MFMA_PEAK_TF = 78.6
+    l0, k0, f0 = per_rank[0]
+    achieved = f0 / max(1e-12, k0 * 1e-3) / 1e12
+    roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+            "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
+            "kernel": "fanin_kernel on rank 0 (its subtree + the ROOT separators), HIP events on the engine stream",
+            "flops_per_launch": f0 / max(1, l0), "avg_launch_ms": k0 / max(1, l0), "launches": l0,
+            "per_rank_tflops": [f / max(1e-12, k * 1e-3) / 1e12 for _, k, f in per_rank]}
+    log(f"[bench] timed {iters} its in {elapsed:.3f}s; rank 0 last it: lin {ph.linearize_ms:.2f} schur "
+        f"{ph.schur_ms:.2f} factor {ph.factor_ms:.2f} solve {ph.solve_ms:.2f} ms; fan-in {achieved:.1f} TF/s")
+    cpu = None
+    if not args.no_cpu_baseline:
+        e.close()
+        try:
+            from bench import cpu_baseline
+            cpu = cpu_baseline(p, args.config)
+        except Exception as ex:  # the baseline must never hide the GPU number
+            log(f"[bench] cpu baseline failed: {ex}")
+    out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
+           "unit": "LM iterations/s", "n_gpus": world, "steps": iters, "warmup": args.warmup,
+           "ms_per_step": elapsed * 1e3 / max(1, iters), "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "f64" if getattr(args, "precision", "fp64") == "fp64" else "f32/f64",
+           "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
+           "config": {"workload": f"config {args.config}: {st[0]} obs, {p.num_points} landmarks, "
+                                  f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",
+                      "parallelism": parallelism},
+           "roofline": roof, "cpu_baseline": cpu,
+           "phases_ms_rank0": {k: round(getattr(ph, k), 3) for k, _ in ph._fields_},
+           "cost": [s.initial_cost, s.final_cost]}
+    print(json.dumps(out), flush=True)

@@ -476,11 +476,15 @@ class HipEngine(CEngineBase):
         self._check(self._fn("bench_kernel", [C.c_int, C.c_int, _dp])(self.h, which, iters, C.byref(us)))
         return us.value
 
-    def synchronize(self):
+    def stream_ptr(self) -> int:
+        """The handle's hipStream_t (vb_stream), for torch.cuda.ExternalStream / RCCL interop."""
         self.lib.vb_stream.restype = P
         self.lib.vb_stream.argtypes = [P]
+        return self.lib.vb_stream(self.h)
+
+    def synchronize(self):
         from ._lib import hip_stream_sync
-        hip_stream_sync(self.lib.vb_stream(self.h))
+        hip_stream_sync(self.stream_ptr())
 
     def phase_times(self) -> PhaseTimes:
         t = PhaseTimes()
