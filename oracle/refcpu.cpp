@@ -2560,6 +2560,20 @@ int ref_preintegrate(int64_t n, const int64_t* tNs, const double* gyro, const do
   }
   return 0;
 }
+// PreIntegration::omegaAtEnd of computePreIntegration (PreIntegration.cpp:272), the omega prior input of
+// addOmegaPriors (viba/single_session/OmegaPriors.cpp:19-31)
+int ref_preint_omega_at_end(int64_t n, const int64_t* tNs, const double* gyro, const double* accel,
+                            const double* calib32, int64_t t0Us, int64_t t1Us, double* out3) {
+  try {
+    const ImuModel m = modelOf(calib32);
+    const PreIntResult r = computePreIntegration(ImuJacInd(0xFF), toMeas(n, tNs, gyro, accel), m, ImuNoise(), t0Us, t1Us);
+    for (int i = 0; i < 3; i++) out3[i] = r.omegaAtEnd[i];
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
 int ref_integrate_measurements(int64_t n, const int64_t* tNs, const double* gyro, const double* accel,
                                const double* calib32, int64_t t0Us, int64_t t1Us, double* out11) {
   try {

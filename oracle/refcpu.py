@@ -166,6 +166,20 @@ def preintegrate(t_ns, gyro, accel, calib32, t0_us: int, t1_us: int, mask: int =
     return out
 
 
+def preint_omega_at_end(t_ns, gyro, accel, calib32, t0_us: int, t1_us: int) -> np.ndarray:
+    """PreIntegration::omegaAtEnd of computePreIntegration (PreIntegration.cpp:272) on the oracle."""
+    lib = load()
+    t = np.ascontiguousarray(t_ns, np.int64)
+    g, a = np.ascontiguousarray(gyro, np.float64), np.ascontiguousarray(accel, np.float64)
+    c = np.ascontiguousarray(calib32, np.float64)
+    out = np.zeros(3)
+    f = lib.ref_preint_omega_at_end
+    f.argtypes = [C.c_int64, P, P, P, P, C.c_int64, C.c_int64, P]
+    if f(len(t), t.ctypes.data, g.ctypes.data, a.ctypes.data, c.ctypes.data, t0_us, t1_us, out.ctypes.data):
+        raise _err(lib)
+    return out
+
+
 def integrate_measurements(t_ns, gyro, accel, calib32, t0_us: int, t1_us: int):
     """integrateMeasurements (PreIntegration.cpp:277-307): RVP [q 4, dV, dP, dtSec]."""
     lib = load()

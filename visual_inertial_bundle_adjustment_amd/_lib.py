@@ -8,6 +8,7 @@ LIB_DIR = os.environ.get("VIBA_LIB_DIR", os.path.join(os.path.dirname(os.path.ab
 HIP_LIB = os.path.join(LIB_DIR, "libviba_hip.so")
 HIP_LIB_MIXED = os.path.join(LIB_DIR, "libviba_hip_mixed.so")  # config E build (VIBA_MIXED=1)
 SYNTH_LIB = os.path.join(LIB_DIR, "libviba_synth.so")
+HOST_LIB = os.path.join(LIB_DIR, "libviba_host.so")  # session adapter host code (csrc/session.cpp)
 
 _synth = None
 _hip = None
@@ -55,6 +56,22 @@ def load_synth_lib() -> C.CDLL:
             f.argtypes = [P]
         _synth = lib
     return _synth
+
+
+_host = None
+
+
+def load_host_lib() -> C.CDLL:
+    global _host
+    if _host is None:
+        lib = _load(HOST_LIB)
+        P = C.c_void_p
+        lib.vbh_triangulate.argtypes = [C.c_int64] + [P] * 10
+        lib.vbh_triangulate.restype = C.c_int
+        lib.vbh_project.argtypes = [P, P, P]
+        lib.vbh_unproject.argtypes = [P, P, P]
+        _host = lib
+    return _host
 
 
 def load_hip_lib(mixed: bool = False) -> C.CDLL:

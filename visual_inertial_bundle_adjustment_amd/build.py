@@ -4,6 +4,7 @@
     lib/libviba_hip_mixed.so  the same with -DVIBA_MIXED=1 (config E: fp32 Jacobian records / Schur
                           products, fp64 Cholesky; csrc/engine.hpp)
     lib/libviba_synth.so  synthetic problem generator (g++)
+    lib/libviba_host.so   host side of the session adapter: initial point triangulation (g++)
 """
 from __future__ import annotations
 
@@ -47,6 +48,12 @@ def build(force: bool = False, verbose: bool = False) -> list[str]:
     if force or not _newer(synth, [src] + headers):
         _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", synth, src])
     out.append(synth)
+    # host side of the session adapter
+    host = os.path.join(LIB, "libviba_host.so")
+    src = os.path.join(CSRC, "session.cpp")
+    if force or not _newer(host, [src]):
+        _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", host, src])
+    out.append(host)
     # HIP libraries (fp64, mixed): compile objects in parallel, then link
     variants = [("libviba_hip.so", LIB, []), ("libviba_hip_mixed.so", os.path.join(LIB, "mixed"), ["-DVIBA_MIXED=1"])]
     objs = {name: [] for name, _, _ in variants}
