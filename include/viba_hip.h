@@ -309,6 +309,17 @@ int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double p
  * blocks are these tiles.  Any pointer may be NULL (n alone queries the count).  After vb_finalize. */
 int vb_reduced_layout(vb_handle h, int32_t* kinds, int32_t* handles, int64_t* offsets, int64_t* n,
                       int64_t* padded_order);
+/* Optimizer::computeJointCovariances (lib/small_thing/Optimizer.cpp:503-611; computeCovariances :613-697
+ * is the one-variable-per-block case): at the current variables, linearize without touching the cost
+ * cache, damp by `damping` (addDamping), factor; while the factor breaks down, raise the damping
+ * (+1e-9 below 1e-9, else x2, :530-545).  Block q lists variables [block_start[q], block_start[q + 1])
+ * of (kinds, handles); its joint covariance (the matching rows and columns of H^-1, H the damped
+ * Hessian) is written column-major, sum of tangent dims squared, after the previous block's.  Reduced
+ * variables only: landmark points are eliminated by this engine (VB_E_UNSUPPORTED), constant variables
+ * have no covariance (VB_E_ARG).  One reduced solve per column on the device.  used_damping (may be
+ * NULL) receives the damping of the factor that succeeded.  Invalidates the LM state of the handle. */
+int vb_compute_covariances(vb_handle h, double damping, int64_t n_blocks, const int64_t* block_start,
+                           const int32_t* kinds, const int32_t* handles, double* out, double* used_damping);
 /* test fault injection: in iteration `iteration` (0-based, -1 = off) of the next vb_optimize calls the
  * model cost reduction is negated, which takes the reference's "quadratic model failing numerically"
  * branch (Optimizer.cpp:835-854: damping *= dampingAdjustOnFail, the step is kept) */

@@ -2170,6 +2170,64 @@ int ref_assemble_reduced(void* h, double lambda) {
   shardRhs(P, P.grad, P.zS);
   return 0;
 }
+// Optimizer::computeJointCovariances (Optimizer.cpp:503-611) on the oracle: linearize without touching
+// the cost cache, addDamping, factor (points eliminated, then the blocked reduced Cholesky); while the
+// factor breaks down damping += 1e-9 (below 1e-9) or *= 2; then per column of each block H x = e over
+// the FULL order (points included), keeping the block's rows.  Same argument layout as
+// vb_compute_covariances; points are allowed here.
+int ref_compute_covariances(void* h, double damping, int64_t nBlocks, const int64_t* blockStart, const int32_t* kinds,
+                            const int32_t* handles, double* out, double* usedDamping) {
+  Problem& P = *(Problem*)h;
+  const int64_t nv = nBlocks ? blockStart[nBlocks] : 0;
+  std::vector<int64_t> pv(nv);
+  for (int64_t i = 0; i < nv; i++) {
+    if (kinds[i] < 0 || kinds[i] >= 8 || handles[i] < 0 || handles[i] >= (int64_t)P.pidx[kinds[i]].size()) {
+      g_err = "covariance of an unknown variable";
+      return -2;
+    }
+    pv[i] = P.pidx[kinds[i]][handles[i]];
+    if (pv[i] < 0) {
+      g_err = "covariance of a constant variable";
+      return -2;
+    }
+  }
+  std::fill(P.grad.begin(), P.grad.end(), 0.0);
+  try {
+    computeGradHess(P, P.grad.data(), true, false, false);
+  } catch (std::range_error& e) {
+    g_err = e.what();
+    return -5;
+  }
+  std::vector<double> rhs(P.order, 0.0), x;
+  double lam = damping;
+  for (int attempt = 0;; attempt++) {
+    if (factorAndSolve(P, lam, true, rhs, x)) break;
+    if (attempt > 200) {
+      g_err = "covariances: factor keeps breaking down";
+      return -4;
+    }
+    lam = lam < 1e-9 ? lam + 1e-9 : lam * 2.0;
+  }
+  if (usedDamping) *usedDamping = lam;
+  double* o = out;
+  for (int64_t q = 0; q < nBlocks; q++) {
+    const int64_t b = blockStart[q], e = blockStart[q + 1];
+    std::vector<int64_t> off(e - b + 1, 0);
+    for (int64_t i = b; i < e; i++) off[i - b + 1] = off[i - b] + P.pdim[pv[i]];
+    const int64_t n = off.back();
+    for (int64_t i = b; i < e; i++)
+      for (int c = 0; c < P.pdim[pv[i]]; c++) {
+        rhs[P.pstart[pv[i]] + c] = 1.0;
+        factorAndSolve(P, lam, false, rhs, x);
+        rhs[P.pstart[pv[i]] + c] = 0.0;
+        const int64_t col = off[i - b] + c;
+        for (int64_t j = b; j < e; j++)
+          for (int r = 0; r < P.pdim[pv[j]]; r++) o[col * n + off[j - b] + r] = x[P.pstart[pv[j]] + r];
+      }
+    o += n * n;
+  }
+  return 0;
+}
 int ref_reduced_buffers(void* h, double** L, int64_t* nL, double** r, int64_t* nr) {
   Problem& P = *(Problem*)h;
   if (L) *L = P.L.data();

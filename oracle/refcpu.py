@@ -50,6 +50,7 @@ class RefEngine(CEngineBase):
     prefix = "ref_"
 
     def __init__(self, reproj_loss=(1.0, 3.0), imu_loss=(math.inf, math.inf), imu_calib_options=0xFF):
+        self.imu_calib_options = imu_calib_options
         lib = load()
         lib.ref_create.restype = P
         lib.ref_create.argtypes = [C.c_double] * 4 + [C.c_int]

@@ -13,6 +13,7 @@
 #include <climits>
 #include <numeric>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/viba_hip.h"
@@ -2233,6 +2234,74 @@ int vb_reduced_layout(vb_handle h, int32_t* kinds, int32_t* handles, int64_t* of
     if (offsets) offsets[i] = h->rvOff[i];
   }
   return 0;
+}
+int vb_compute_covariances(vb_handle h, double damping, int64_t n_blocks, const int64_t* block_start,
+                           const int32_t* kinds, const int32_t* handles, double* out, double* used_damping) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_compute_covariances before vb_finalize");
+  if (h->partWorld > 1 || h->sharded) return fail(VB_E_UNSUPPORTED, "covariances run on a single handle");
+  if (n_blocks < 0 || (n_blocks > 0 && (!block_start || !kinds || !handles || !out)))
+    return fail(VB_E_ARG, "vb_compute_covariances: null argument");
+  if (!h->sch[0].built) return fail(VB_E_STATE, "no factorization schedule");
+  // (kind, handle) -> reduced variable
+  std::unordered_map<int64_t, int32_t> rvOf;
+  for (size_t i = 0; i < h->rvKind.size(); i++) rvOf[((int64_t)h->rvKind[i] << 32) | (uint32_t)h->rvHandle[i]] = (int32_t)i;
+  const int64_t nv = n_blocks ? block_start[n_blocks] : 0;
+  std::vector<int32_t> rv(nv);
+  for (int64_t q = 0; q < n_blocks; q++)
+    if (block_start[q + 1] < block_start[q]) return fail(VB_E_ARG, "block_start must be non-decreasing");
+  for (int64_t i = 0; i < nv; i++) {
+    if (kinds[i] == VB_VAR_POINT) return fail(VB_E_UNSUPPORTED, "covariance of a landmark point (points are eliminated)");
+    auto it = rvOf.find(((int64_t)kinds[i] << 32) | (uint32_t)handles[i]);
+    if (it == rvOf.end()) return fail(VB_E_ARG, "covariance of a constant or unknown variable");
+    rv[i] = it->second;
+  }
+  Dev& d = h->d;
+  // initDirectSolverData + factor, retried with more damping while the factor breaks down
+  double lam = damping;
+  for (int attempt = 0;; attempt++) {
+    if (int rc = vb_linearize(h, 0, 0, nullptr)) return rc;
+    HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+    launch_landmark(d, lam, 0, d.lmB, d.lmE, h->st);
+    HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
+    launch_schur(d, lam, 1, h->st);
+    if (int rc = factorReduced(h)) return rc;
+    int32_t e = 0;
+    HIPCHK(hipMemcpyAsync(&e, d.err, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    if (!(e & (2 | 8))) {
+      if (int rc = checkErr(h)) return rc;
+      break;
+    }
+    if (attempt > 200) return fail(VB_E_NUMERIC, "covariances: factor keeps breaking down");
+    lam = lam < 1e-9 ? lam + 1e-9 : lam * 2.0;
+  }
+  if (used_damping) *used_damping = lam;
+  // one reduced solve per column: S x = e
+  const int64_t nPad = (int64_t)d.nT * TS;
+  std::vector<double> rhs(nPad, 0.0), x(nPad);
+  double* o = out;
+  for (int64_t q = 0; q < n_blocks; q++) {
+    const int64_t b = block_start[q], e = block_start[q + 1];
+    std::vector<int64_t> off(e - b + 1, 0);
+    for (int64_t i = b; i < e; i++) off[i - b + 1] = off[i - b] + h->rvDim[rv[i]];
+    const int64_t n = off.back();
+    for (int64_t i = b; i < e; i++)
+      for (int c = 0; c < h->rvDim[rv[i]]; c++) {
+        const int64_t row = h->rvOff[rv[i]] + c;
+        rhs[row] = 1.0;
+        HIPCHK(hipMemcpyAsync(h->rhsWork, rhs.data(), nPad * sizeof(double), hipMemcpyHostToDevice, h->st));
+        rhs[row] = 0.0;
+        if (int rc = solveReduced(h)) return rc;
+        HIPCHK(hipMemcpyAsync(x.data(), d.xRed, nPad * sizeof(double), hipMemcpyDeviceToHost, h->st));
+        HIPCHK(hipStreamSynchronize(h->st));
+        const int64_t col = off[i - b] + c;
+        for (int64_t j = b; j < e; j++)
+          for (int r = 0; r < h->rvDim[rv[j]]; r++) o[col * n + off[j - b] + r] = x[h->rvOff[rv[j]] + r];
+      }
+    o += n * n;
+  }
+  h->linearized = false, h->factored = false;
+  return checkErr(h);
 }
 int vb_debug_negate_model_reduction(vb_handle h, int iteration) {
   if (!h) return fail(VB_E_ARG, "null handle");

@@ -256,6 +256,45 @@ class CEngineBase:
         self._check(f(self.h, k.ctypes.data, hh.ctypes.data, o.ctypes.data, C.byref(n), C.byref(npad)))
         return k, hh, o, npad.value
 
+    def compute_covariances(self, blocks, damping: float = 1e-5):
+        """Optimizer::computeJointCovariances (Optimizer.cpp:503-611): blocks = [[(kind, handle), ...], ...];
+        returns ([joint covariance matrix per block], damping used).  vb_compute_covariances /
+        ref_compute_covariances; computeCovariances is one variable per block."""
+        kinds_, handles = [], []
+        start = [0]
+        for blk in blocks:
+            for k, hh in blk:
+                kinds_.append(int(k))
+                handles.append(int(hh))
+            start.append(len(kinds_))
+        k = np.array(kinds_, np.int32)
+        hh = np.array(handles, np.int32)
+        st = np.array(start, np.int64)
+        dims = [[self.var_tangent_dim(int(a), int(b)) for a, b in blk] for blk in blocks]
+        sizes = [sum(d) for d in dims]
+        out = np.zeros(sum(s * s for s in sizes))
+        used = C.c_double()
+        f = self._fn("compute_covariances", [C.c_double, C.c_int64, P, P, P, P, C.POINTER(C.c_double)])
+        self._check(f(self.h, float(damping), len(blocks), st.ctypes.data, k.ctypes.data, hh.ctypes.data,
+                      out.ctypes.data, C.byref(used)))
+        covs, o = [], 0
+        for s in sizes:
+            covs.append(out[o:o + s * s].reshape(s, s, order="F").copy())
+            o += s * s
+        return covs, used.value
+
+    def var_tangent_dim(self, kind: int, handle: int) -> int:
+        """tangent size of one variable (the kind's box-plus dimension; camera records and the IMU
+        calibration options decide theirs)"""
+        from .kinds import VAR_MAX_TANGENT
+        if kind == 4:
+            d = self.get_vars(4)[handle]
+            return int(d[1]) + int(d[7] != 0) + int(d[8] != 0)
+        if kind == 6:
+            mask = self.imu_calib_options
+            return sum(n for bit, n in ((1, 3), (2, 3), (4, 3), (8, 3), (16, 6), (32, 3), (64, 1), (128, 1)) if mask & bit)
+        return VAR_MAX_TANGENT[kind]
+
     def debug_negate_model_reduction(self, iteration: int):
         """Test fault injection: negate the model cost reduction in LM iteration `iteration` of the next
         optimize (Optimizer.cpp:835-854 branch); -1 disables."""
@@ -392,6 +431,7 @@ class HipEngine(CEngineBase):
         if precision not in ("fp64", "mixed"):
             raise ValueError(f"precision must be 'fp64' or 'mixed', not {precision!r}")
         self.precision = precision
+        self.imu_calib_options = imu_calib_options
         lib = load_hip_lib(mixed=precision == "mixed")
         cfg = HipEngine.Config()
         lib.vb_default_config.argtypes = [P]
