@@ -981,7 +981,13 @@ __device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, 
   const int k0 = (s % (TS / kFanK)) * kFanK;
   // constant address space: scalar loads (lgkmcnt), so no vmcnt wait drains the LDS ring
   const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
+#ifdef VIBA_FAN_EXPT
+  // measurement build only (scripts/fan_expt.py): every contribution reads the same few L2-resident tiles,
+  // which separates the kernel's memory-system time from its issue / synchronisation time
+  const int64_t tk = (c & 7), ti = 8 + (c & 7);
+#else
   const int64_t tk = pc[2 * c + 1], ti = pc[2 * c];
+#endif
   const int hi = lane >> 5;
   const int row = (2 * (lane & 31) - 16 * hi) & 63;
 #pragma unroll
