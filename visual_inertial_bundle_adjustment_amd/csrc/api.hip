@@ -31,9 +31,10 @@ void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gO
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st);
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
-void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st);
+void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st,
+                  const double* fwdB = nullptr, double* fwdY = nullptr);
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
-                 hipStream_t st);
+                 hipStream_t st, const int32_t* rows = nullptr, const double* fwdY = nullptr, double* fwdB = nullptr);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
                          unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st);
@@ -230,7 +231,7 @@ struct Sched {
   int32_t nLevels = 0;
   int64_t nPairs = 0;
   int32_t *potrfTileD = nullptr, *potrfColD = nullptr, *trsmDiagD = nullptr, *trsmTargetD = nullptr,
-          *trsmColD = nullptr, *updD = nullptr, *fanPairsD = nullptr;
+          *trsmColD = nullptr, *updD = nullptr, *fanPairsD = nullptr, *trsmRowD = nullptr;
   int32_t *tasksFD = nullptr, *tasksBD = nullptr, *expFD = nullptr, *expBD = nullptr, *preReadyD = nullptr;
   int64_t nF = 0, nB = 0, nPreReady = 0;  // preReady: rows whose x is known before the backward solve
   hipGraphExec_t graph = nullptr;
@@ -302,6 +303,9 @@ struct vb_handle_s {
   // VIBA_FUSED_FACTOR: 0 (default) fanin / potrf / trsm launches per level; 1 one factor_level_kernel
   // launch per level; 2 fanin + one potrf/trsm launch.  Measured on config C (r02): 14.5 / 20.1 / 15.2 ms
   int fusedFactor = 0;
+  // the forward solve of vb_damp_factor_solve rides the factorization's potrf / trsm launches (single
+  // handle, 3-launch levels); VIBA_FWD_IN_FACTOR=0 keeps the separate fan-out forward solve
+  bool fwdInFactor = true;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool sharded = false;  // vb_set_landmark_shard called
@@ -1157,7 +1161,7 @@ int doFinalize(vb_handle h) {
       // per level: fan-in of the level's target tiles, then potrf of its diagonals, then trsm.  A
       // target's list is cut into near-equal chunks of at most `cs` contributions, cs chosen per
       // level so the launch has ~fanWgs workgroups (>= 4 contributions per chunk: one per wave)
-      std::vector<int32_t> pT, pC, tD, tT, tC, fan;
+      std::vector<int32_t> pT, pC, tD, tT, tC, tR, fan;
       S.lvP.assign(nLev + 1, 0), S.lvT.assign(nLev + 1, 0), S.lvU.assign(nLev + 1, 0);
       S.lvF.assign(nLev + 1, 0), S.lvFd.assign(nLev, 0), S.lvPT.assign(nLev + 1, 0), S.lvPd.assign(nLev, 0);
       std::vector<FacItem> facItems, ptItems;
@@ -1171,7 +1175,8 @@ int doFinalize(vb_handle h) {
           const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
           if (colSel(J)) {
             pT.push_back(h->colTilesH[c0]), pC.push_back(J);
-            for (int64_t q = 1; q < n; q++) tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J);
+            for (int64_t q = 1; q < n; q++)
+              tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J), tR.push_back(h->colRowsH[c0 + q]);
           }
           if (!tgtSel(J)) continue;
           for (int64_t q = 0; q < n; q++) {
@@ -1265,7 +1270,7 @@ int doFinalize(vb_handle h) {
         }
       S.nF = (int64_t)tf.size() / 2, S.nB = (int64_t)tb.size() / 2, S.nPreReady = (int64_t)pre.size();
       if (upload(&S.potrfTileD, pT) || upload(&S.potrfColD, pC) || upload(&S.trsmDiagD, tD) ||
-          upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.updD, fan) ||
+          upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.trsmRowD, tR) || upload(&S.updD, fan) ||
           upload(&S.fanPairsD, pairs) || upload(&S.tasksFD, tf) || upload(&S.tasksBD, tb) ||
           upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.facD, facItems) || upload(&S.ptD, ptItems))
         return VB_E_HIP;
@@ -1487,6 +1492,11 @@ void visualCostShard(vb_handle h, int comparable) {
   profEnd(h, KF_VISUAL_COST);
 }
 
+// vb_damp_factor_solve's forward solve runs inside the factorization (potrf_forward / trsm_kernel)
+bool fwdFused(vb_handle h) {
+  return h->fwdInFactor && h->fusedFactor == 0 && h->partWorld <= 1 && !h->sharded && !h->legacySolve;
+}
+
 void factorSeq(vb_handle h, const Sched& S) {
   Dev& d = h->d;
   if (h->fusedFactor == 2) {  // per level: fanin_kernel, then one potrf + trsm launch (no fan-in items)
@@ -1518,16 +1528,21 @@ void factorSeq(vb_handle h, const Sched& S) {
     launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
     return;
   }
+  // the forward solve of rhsWork into yvec, fused (schedule 0 of a single handle only)
+  const bool fwd = fwdFused(h) && &S == &h->sch[0];
+  double* fb = fwd ? h->rhsWork : nullptr;
+  double* fy = fwd ? h->yvec : nullptr;
   for (int32_t L = 0; L < S.nLevels; L++) {
     const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
     profBegin(h, KF_GEMM);
     launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
     profEnd(h, KF_GEMM);
     profBegin(h, KF_POTRF);
-    launch_potrf(d, S.potrfTileD + p0, S.potrfColD + p0, (int)(S.lvP[L + 1] - p0), h->dinv, h->st);
+    launch_potrf(d, S.potrfTileD + p0, S.potrfColD + p0, (int)(S.lvP[L + 1] - p0), h->dinv, h->st, fb, fy);
     profEnd(h, KF_POTRF);
     profBegin(h, KF_TRSM);
-    launch_trsm(d, S.trsmDiagD + t0, S.trsmTargetD + t0, S.trsmColD + t0, (int)(S.lvT[L + 1] - t0), h->dinv, h->st);
+    launch_trsm(d, S.trsmDiagD + t0, S.trsmTargetD + t0, S.trsmColD + t0, (int)(S.lvT[L + 1] - t0), h->dinv, h->st,
+                S.trsmRowD + t0, fy, fb);
     profEnd(h, KF_TRSM);
   }
   launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
@@ -1790,6 +1805,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
   if (const char* e = getenv("VIBA_FUSED_FACTOR")) h->fusedFactor = atoi(e);
+  if (const char* e = getenv("VIBA_FWD_IN_FACTOR")) h->fwdInFactor = e[0] != '0';
   if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
   {
     hipDeviceProp_t prop;
@@ -1842,7 +1858,7 @@ int vb_destroy(vb_handle h) {
   if (h->st2) hipStreamSynchronize(h->st2), hipStreamDestroy(h->st2);
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
-    void* sp[] = {S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.updD, S.fanPairsD,
+    void* sp[] = {S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
                   S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD};
     for (void* p : sp)
       if (p) hipFree(p);
@@ -2150,16 +2166,20 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
     launch_schur(d, lambda, (h->isRoot || h->partWorld > 1) ? 1 : 0, h->st);
     profEnd(h, KF_SCHUR);
   HIPCHK(hipEventRecord(h->ev[3], h->st));
+  const bool fused = !pcgMode(h) && fwdFused(h);
+  if (fused)  // the factorization runs the forward solve of rhsWork (into yvec)
+    HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (pcgMode(h)) {
     if (int rc = precondInit(h)) return rc;
   } else if (int rc = factorReduced(h)) {
     return rc;
   }
   HIPCHK(hipEventRecord(h->ev[4], h->st));
-  HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
+  if (!fused)
+    HIPCHK(hipMemcpyAsync(h->rhsWork, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (pcgMode(h)) {
     if (int rc = pcgSolve(h)) return rc;
-  } else if (int rc = solveReduced(h)) {
+  } else if (int rc = solveReduced(h, 0, fused ? 2 : 3)) {
     return rc;
   }
   backSubstitute(h, 0);

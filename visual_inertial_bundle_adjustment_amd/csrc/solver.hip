@@ -877,7 +877,42 @@ __device__ __forceinline__ void lds_to_global(double* dst, const double* src, in
 // factor the diagonal tile of column J in place (+ its 16 x 16 block inverses); one wave
 // factor diagonal tile tiles[b] in place (+ its 16 x 16 block inverses into dinv[cols[b]]); one
 // wave per tile, all the diagonal tiles of one level per launch
-__global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileList, const int32_t* cols, double* dinvAll) {
+// forward step of the column's solve, fused into the factorization (fwdB non-null): y_J = L_JJ^-1 b_J by
+// 16-row blocks (y_i = Dinv_i (b_i - sum_{j<i} L_ij y_j)), b_J complete since every L_JK y_K update
+// landed in an earlier level's trsm launch
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void potrf_forward(const Dev& d, const double* T, const double* dinvS, double* sh, int J,
+                                              const double* b, double* y, int lane) {
+  // right-looking by 16-row blocks: lane r keeps b_r; once y_i is known every later row subtracts
+  // L(r, block i) y_i, so each block's chain is one 16-term GEMV + one 16-term update
+  double br = b[(int64_t)J * TS + lane];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    sh[64 + lane] = br;
+    wave_sync_lds();
+    if ((lane >> 4) == i) {
+      const int l = lane & 15;
+      double v = 0.0;
+#pragma unroll
+      for (int m = 0; m < 16; m++) v += dinvS[i * 256 + m * 16 + l] * sh[64 + 16 * i + m];
+      sh[16 * i + l] = v;
+    }
+    wave_sync_lds();
+    if (i < 3) {
+#pragma unroll
+      for (int m = 0; m < 16; m++) br -= T[(16 * i + m) * TS + lane] * sh[16 * i + m];
+    }
+  }
+  const int64_t row = (int64_t)J * TS + lane;
+  y[row] = row < d.nRed ? sh[lane] : 0.0;
+}
+
+__global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileList, const int32_t* cols, double* dinvAll,
+                                                   const double* fwdB, double* fwdY) {
   __shared__ double T[TS * TS];
   __shared__ double scratch[256];
   __shared__ double dinvS[1024];
@@ -896,6 +931,7 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileLis
   POTRF_T(16);
   potrf_blocked(T, scratch, dinvS, lane, d.err);
   POTRF_T(17);
+  if (fwdB) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB, fwdY, lane);
   lds_to_global(A, T, TS * TS, lane, 64);
   lds_to_global(dinvG, dinvS, 1024, lane, 64);
   POTRF_T(18);
@@ -904,7 +940,8 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileLis
 // X = A L_JJ^-T for target tile target[b] with diagonal tile diag[b] of column cols[b]; wave w =
 // 16-row block (all on MFMA); every off-diagonal tile of one level per launch
 __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagList, const int32_t* targetList,
-                                                   const int32_t* cols, const double* dinvAll) {
+                                                   const int32_t* cols, const double* dinvAll, const int32_t* rows,
+                                                   const double* fwdY, double* fwdB) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const double* L = d.tiles + (int64_t)diagList[blockIdx.x] * TS * TS;
   double* A = d.tiles + (int64_t)targetList[blockIdx.x] * TS * TS;
@@ -928,6 +965,14 @@ __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagLis
   for (int k = 0; k < 4; k++)
 #pragma unroll
     for (int s = 0; s < 4; s++) dv[k][s] = dinv[k * 256 + (4 * s + lq) * 16 + lr];
+  double yv[4][4];  // y_J entries of the fused forward solve (columns 16 k + lq + 4 r), loaded with the rest
+  if (fwdB) {
+    const double* yJ = fwdY + (int64_t)cols[blockIdx.x] * TS;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) yv[k][r] = yJ[16 * k + lq + 4 * r];
+  }
   double4_t Xt[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -945,6 +990,16 @@ __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagLis
   for (int k = 0; k < 4; k++)
 #pragma unroll
     for (int r = 0; r < 4; r++) A[(16 * k + lq + 4 * r) * TS + 16 * w + lr] = Xt[k][r];
+  if (fwdB) {  // the solve's forward update of this tile, fused: b_I -= L_IJ y_J (lane: row 16 w + lr)
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) v += Xt[k][r] * yv[k][r];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lq == 0) atomicAdd(fwdB + (int64_t)rows[blockIdx.x] * TS + 16 * w + lr, -v);
+  }
 }
 
 // Fan-in (left-looking) update of target tile (I, J): A_IJ -= sum_K L_IK L_JK^T over one chunk of the
@@ -1647,12 +1702,15 @@ void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
   }
   if (d.nRV) hipLaunchKernelGGL(reduced_grad_kernel, dim3(d.nRV), dim3(256), 0, st, d, mode);
 }
-void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st) {
-  if (n > 0) launchK(potrf_kernel, dim3(n), dim3(64), 0, st, d, tiles, cols, dinv);
+// fwdB / fwdY (may be null): the forward solve fused into the factorization (potrf: y_J from b_J;
+// trsm: b_I -= L_IJ y_J for its tile, rows[] = the tile's row I)
+void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st,
+                  const double* fwdB, double* fwdY) {
+  if (n > 0) launchK(potrf_kernel, dim3(n), dim3(64), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
 }
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
-                 hipStream_t st) {
-  if (n > 0) launchK(trsm_kernel, dim3(n), dim3(256), 0, st, d, diag, target, cols, dinv);
+                 hipStream_t st, const int32_t* rows, const double* fwdY, double* fwdB) {
+  if (n > 0) launchK(trsm_kernel, dim3(n), dim3(256), 0, st, d, diag, target, cols, dinv, rows, fwdY, fwdB);
 }
 // shard / partition exchange (vb_pack_shard_tiles, vb_add_tiles, vb_part_exchange): one block per
 // listed chunk (a 64 x 64 tile of the tile store, or a 64-row block of a reduced vector);
