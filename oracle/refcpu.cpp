@@ -2771,6 +2771,69 @@ int ref_preint_kat(int seed, int nOuter, int nInner, double* out3) {
   return 0;
 }
 
+// TestCompensateJac.CalibJac (lib/motion/preintegration/tests/TestCompensateJac.cpp:94-160) restated:
+// compensateAndJac against forward differences (EPS 1e-8) of ImuCompensation::apply over the calibration
+// box-plus and the raw measurement; factoryImuParams, perturbed by 0.1 N(0,1) from the third model on,
+// 40 random samples per model, the RNG drawn in the reference's order (the unused SignalStatistics
+// rates included).  out4 = [max |calib jac delta|, max |meas jac delta|, max |gyro value delta|,
+// max |accel value delta|].
+int ref_compensate_kat(int seed, int nModels, int nSamples, int mask, double* out4) {
+  try {
+    constexpr double EPS = 1e-8;
+    std::mt19937 g(seed);
+    auto rnd = [&g]() { return std::normal_distribution<>(0, 1)(g); };
+    const ImuJacInd ji(mask);
+    std::fill(out4, out4 + 4, 0.0);
+    for (int q = 0; q < nModels; q++) {
+      ImuModel p = factoryImuParams();
+      if (q > 1) {
+        std::vector<double> d(ji.size);
+        for (auto& x : d) x = rnd() * 0.1;
+        imu_boxPlus(p, ji, d.data());
+      }
+      const ImuCompensation comp(p);
+      for (int s = 0; s < nSamples; s++) {
+        V3 gRaw, gRate, aRaw, aRate;
+        for (int i = 0; i < 3; i++) gRaw[i] = rnd();
+        for (int i = 0; i < 3; i++) gRate[i] = rnd();
+        for (int i = 0; i < 3; i++) aRaw[i] = rnd();
+        for (int i = 0; i < 3; i++) aRate[i] = rnd();
+        V3 g0, a0, g1, a1;
+        comp.apply(gRaw, aRaw, g0, a0);
+        Mat calibJ, measJ;
+        compensateAndJac(p, ji, gRaw, aRaw, g1, a1, calibJ, measJ);
+        out4[2] = std::max(out4[2], std::sqrt(sqnorm(g0 - g1)));
+        out4[3] = std::max(out4[3], std::sqrt(sqnorm(a0 - a1)));
+        for (int i = 0; i < ji.size; i++) {
+          std::vector<double> d(ji.size, 0.0);
+          d[i] = EPS;
+          ImuModel pp = p;
+          imu_boxPlus(pp, ji, d.data());
+          V3 gp, ap;
+          ImuCompensation(pp).apply(gRaw, aRaw, gp, ap);
+          for (int k = 0; k < 3; k++) {
+            out4[0] = std::max(out4[0], std::abs((gp[k] - g0[k]) / EPS - calibJ(k, i)));
+            out4[0] = std::max(out4[0], std::abs((ap[k] - a0[k]) / EPS - calibJ(3 + k, i)));
+          }
+        }
+        for (int i = 0; i < 6; i++) {
+          V3 gP = gRaw, aP = aRaw, gp, ap;
+          (i < 3 ? gP : aP)[i % 3] += EPS;
+          comp.apply(gP, aP, gp, ap);
+          for (int k = 0; k < 3; k++) {
+            out4[1] = std::max(out4[1], std::abs((gp[k] - g0[k]) / EPS - measJ(k, i)));
+            out4[1] = std::max(out4[1], std::abs((ap[k] - a0[k]) / EPS - measJ(3 + k, i)));
+          }
+        }
+      }
+    }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+
 // TestPreIntegration.Covariance (TestPreIntegration.cpp:150-203) restated for one seed: the
 // preintegration covariance whitens the spread of integrateMeasurements over randomized measurement
 // noise (samples beyond the approximate 4-sigma chi2 bound dropped); out9 = eigenvalues of the

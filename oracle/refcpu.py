@@ -204,6 +204,18 @@ def factory_imu_params() -> np.ndarray:
     return out
 
 
+def compensate_kat(seed: int = 42, n_models: int = 10, n_samples: int = 40, mask: int = 0x3F):
+    """TestCompensateJac.CalibJac (TestCompensateJac.cpp:94-160) restated: max abs delta of the analytic
+    vs forward-difference calibration Jacobian, raw-measurement Jacobian, compensated gyro and accel
+    (mask 0x3f = ImuCalibrationOptions::allExceptTimeOffsets)."""
+    lib = load()
+    out = (C.c_double * 4)()
+    lib.ref_compensate_kat.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    if lib.ref_compensate_kat(seed, n_models, n_samples, mask, out):
+        raise _err(lib)
+    return tuple(out)
+
+
 def preint_kat(seed: int = 43, n_outer: int = 250, n_inner: int = 5):
     """TestPreIntegration.PreInt (TestPreIntegration.cpp:104-148) restated: max relative delta of the
     analytic vs numeric calibration Jacobian over (other columns, reference time offset, gyro-accel

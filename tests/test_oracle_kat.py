@@ -218,6 +218,13 @@ def test_preintegration_jacobian_kat():  # TestPreIntegration.PreInt (TestPreInt
     assert other < 1e-6 and ref_offset < 1e-6 and gyro_accel_offset < 1e-4, (other, ref_offset, gyro_accel_offset)
 
 
+def test_compensate_jacobian_kat():  # TestCompensateJac.CalibJac (TestCompensateJac.cpp:94-160)
+    from oracle.refcpu import compensate_kat
+    calib, meas, gyro, accel = compensate_kat(42, 10, 40, 0x3F)
+    assert gyro < 1e-5 and accel < 1e-5, (gyro, accel)
+    assert calib < 1.5e-6 and meas < 5e-7, (calib, meas)
+
+
 @pytest.mark.parametrize("q", [0, 3])
 def test_preintegration_covariance_kat(q):  # TestPreIntegration.Covariance (:150-203)
     from oracle.refcpu import preint_cov_kat
