@@ -221,9 +221,11 @@ def main():
     # roofline of the profiled kernel family (average launch duration from HIP events on the engine
     # stream, algorithmic work from the symbolic structure)
     avg_ms = kms / max(1, launches)
-    if args.profile_family == KF_GEMM:
-        # st[6] tile-pair contributions per factorization (2 * 64^3 flops each), st[10] levels = fan-in
-        # launches per factorization
+    if args.profile_family < 0:  # nothing profiled (the factorization runs from its HIP graph)
+        roof = None
+    elif args.profile_family == KF_GEMM:
+        # st[6] tile-pair contributions per factorization (2 * 64^3 flops each), st[10] fan-in launches
+        # per factorization
         per_launch = st[6] * 2.0 * 64 ** 3 / max(1, st[10])
         achieved = per_launch / (avg_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",

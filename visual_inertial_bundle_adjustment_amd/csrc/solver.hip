@@ -15,6 +15,7 @@
 #include "device_math.hpp"
 #include "engine.hpp"
 #include <algorithm>
+#include <string>
 
 namespace viba {
 using namespace dev;
@@ -708,13 +709,14 @@ __device__ __forceinline__ double rowbcast(double v) {
   return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xF, 0xF, true);
 }
 
-// 1 / sqrt(x): v_rsq_f64 + two Newton steps (~1 ulp; the IEEE sqrt + divide sequences are ~40
+// 1 / sqrt(x): v_rsq_f64 + one third-order refinement (the IEEE sqrt + divide sequences are ~40
 // dependent instructions on the factorization's serial chain)
 __device__ __forceinline__ double rsqrt_nr(double x) {
   double y = __builtin_amdgcn_rsq(x);
-  y = y * (1.5 - 0.5 * x * y * y);
-  y = y * (1.5 - 0.5 * x * y * y);
-  return y;
+  // one third-order step, e = 1 - x y^2: y (1 + e / 2 + 3 e^2 / 8), four dependent operations where two
+  // Newton steps take six (v_rsq_f64 is good to ~2^-23, so the result is within ~1.5 ulp either way)
+  const double e = __builtin_fma(-(x * y), y, 1.0);
+  return __builtin_fma(e * y, __builtin_fma(e, 0.375, 0.5), y);
 }
 
 // 16 x 16 Cholesky, lane r holds row r in s[0..16) (lanes >= 16 compute garbage, ignored):
@@ -776,8 +778,10 @@ __device__ __forceinline__ void trsm_rowblock(double* A, const double* L, const 
 #ifdef VIBA_POTRF_TIMING
 __device__ long long g_potrf_t[32];
 #define POTRF_T(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_potrf_t[k] = (long long)__builtin_readcyclecounter(); } while (0)
+#define POTRF_TW(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_potrf_t[k] = (long long)__builtin_readcyclecounter(); } while (0)
 #else
 #define POTRF_T(k) do {} while (0)
+#define POTRF_TW(k) do {} while (0)
 #endif
 
 // Factor + invert the 16 x 16 diagonal block i of T (LDS) given S (its updated value, D layout; only
@@ -787,6 +791,62 @@ __device__ long long g_potrf_t[32];
 // term, so the serial chain is one FMA + one multiply per row (L from LDS by broadcast reads).
 // (A one-MFMA-per-pivot variant -- the rank-1 update as a v_mfma_f64_16x16x4_f64 on the D layout --
 // measured slower: each pivot then waits on a dependent MFMA + readlane, 7.9k vs 5.7k cycles.)
+// X = L^-1 from the registers of Chol16 (lane r: s[c] = L[r][c], c <= r): lane c computes column c,
+// taking L[r][k] from lane r by a DPP row broadcast instead of from LDS (no store / barrier / load
+// round trip; the 120 broadcasts do not depend on the substitution chain)
+template <int K, int R>
+struct Inv16Row {
+  static __device__ __forceinline__ void run(double (&acc)[16], const double (&s)[16]) {
+    acc[R] -= rowbcast<R>(s[K]) * acc[K];
+    Inv16Row<K, R + 1>::run(acc, s);
+  }
+};
+template <int K>
+struct Inv16Row<K, 16> {
+  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16]) {}
+};
+template <int K>
+struct Inv16 {
+  static __device__ __forceinline__ void run(double (&acc)[16], const double (&s)[16], const double (&invd)[16]) {
+    acc[K] *= invd[K];
+    Inv16Row<K, K + 1>::run(acc, s);
+    Inv16<K + 1>::run(acc, s, invd);
+  }
+};
+template <>
+struct Inv16<16> {
+  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16], const double (&)[16]) {}
+};
+
+// diag16 with the inverse taken from registers (Inv16): potrf4_kernel<true> (VIBA_DIAG_INV=dpp)
+__device__ __forceinline__ void diag16_dpp(double* T, double* scratch, double* dinvS, int i, double4_t S, int lane,
+                                           bool& bad) {
+  const int lr = lane & 15, lq = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; r++) scratch[(lq + 4 * r) * 16 + lr] = S[r];  // row-major S[i'][j']
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double s[16], invd[16];
+#pragma unroll
+  for (int c = 0; c < 16; c++) s[c] = scratch[lr * 16 + c];
+  POTRF_TW(15 + 3 * i);
+  Chol16<0>::run(s, invd, lane, bad);
+  POTRF_TW(16 + 3 * i);
+  double acc[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = (r == lr) ? 1.0 : 0.0;
+  Inv16<0>::run(acc, s, invd);
+  POTRF_TW(17 + 3 * i);
+  if (lane < 16) {
+#pragma unroll
+    for (int c = 0; c < 16; c++) T[(16 * i + c) * TS + 16 * i + lane] = (c <= lane) ? s[c] : 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = (r >= lane) ? acc[r] : 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS, int i, double4_t S, int lane,
                                        bool& bad) {
   const int lr = lane & 15, lq = lane >> 4;
@@ -935,6 +995,81 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileLis
   lds_to_global(A, T, TS * TS, lane, 64);
   lds_to_global(dinvG, dinvS, 1024, lane, 64);
   POTRF_T(18);
+}
+
+// The same factorization with four waves, right-looking over the 16-column blocks k: wave w keeps its
+// row block (A_wj^T for j <= w, D layout) in registers.  Wave k factors + inverts its diagonal block
+// (diag16); every wave below then forms L_wk = A_wk Dinv_k^T (4 MFMAs), publishes it in LDS and takes
+// its own diagonal update L_wk L_wk^T from registers, and after a barrier updates its blocks k < j < w
+// with L_jk -- while wave k + 1 is already in diag16.  Between two diag16 the chain is 8 dependent
+// MFMAs (the one-wave left-looking form chains up to 36 of them); the terms are subtracted in the same
+// order as there.  The upper blocks are written as zeros.
+template <bool kDppInv>
+__global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileList, const int32_t* cols,
+                                                     double* dinvAll, const double* fwdB, double* fwdY) {
+  __shared__ double T[TS * TS];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[1024];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  double* A = d.tiles + (int64_t)tileList[blockIdx.x] * TS * TS;
+  double* dinvG = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
+  if (w == 0) POTRF_TW(0);
+  double4_t R[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    if (j < w) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) R[j][r] = A[(16 * j + lq + 4 * r) * TS + 16 * w + lr];
+    } else if (j == w) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) R[j][r] = A[(16 * w + lr) * TS + 16 * w + lq + 4 * r];  // lower part valid
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; r++) T[(16 * j + lq + 4 * r) * TS + 16 * w + lr] = 0.0;
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (w == k) {
+      POTRF_TW(1 + 2 * k);
+      if (kDppInv) diag16_dpp(T, scratch, dinvS, k, R[k], lane, bad);
+      else diag16(T, scratch, dinvS, k, R[k], lane, bad);
+      POTRF_TW(2 + 2 * k);
+    }
+    __syncthreads();
+    if (w == 3) POTRF_TW(9 + k);
+    double4_t Lt = double4_t{0, 0, 0, 0};
+    if (w > k) {
+#pragma unroll
+      for (int s = 0; s < 4; s++) Lt = mfma64(dinvS[k * 256 + (4 * s + lq) * 16 + lr], R[k][s], Lt);
+#pragma unroll
+      for (int r = 0; r < 4; r++) T[(16 * k + lq + 4 * r) * TS + 16 * w + lr] = Lt[r];
+#pragma unroll
+      for (int j = k + 1; j < 4; j++)
+        if (j == w) {
+#pragma unroll
+          for (int s = 0; s < 4; s++) R[j] = mfma64(-Lt[s], Lt[s], R[j]);
+        }
+    }
+    if (k < 2) {
+      __syncthreads();
+#pragma unroll
+      for (int j = k + 1; j < 3; j++)
+        if (j < w) {
+#pragma unroll
+          for (int s = 0; s < 4; s++) R[j] = mfma64(-T[(16 * k + 4 * s + lq) * TS + 16 * j + lr], Lt[s], R[j]);
+        }
+    }
+  }
+  __syncthreads();
+  if (w == 0) POTRF_TW(13);
+  if (bad && lane == 0) atomicOr(d.err, 8);
+  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB, fwdY, lane);
+  lds_to_global(A, T, TS * TS, tid, 256);
+  lds_to_global(dinvG, dinvS, 1024, tid, 256);
+  if (w == 0) POTRF_TW(14);
 }
 
 // X = A L_JJ^-T for target tile target[b] with diagonal tile diag[b] of column cols[b]; wave w =
@@ -1706,7 +1841,20 @@ void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
 // trsm: b_I -= L_IJ y_J for its tile, rows[] = the tile's row I)
 void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st,
                   const double* fwdB, double* fwdY) {
-  if (n > 0) launchK(potrf_kernel, dim3(n), dim3(64), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
+  // VIBA_POTRF_WAVES=1: the one-wave left-looking form; default the four-wave right-looking form, its
+  // diagonal inverses through LDS as in the one-wave form (VIBA_DIAG_INV=dpp: from registers)
+  static const int waves = [] {
+    const char* e = getenv("VIBA_POTRF_WAVES");
+    return e && atoi(e) == 1 ? 1 : 4;
+  }();
+  static const bool dppInv = [] {  // same speed measured; the LDS form needs 213 VGPRs instead of 468
+    const char* e = getenv("VIBA_DIAG_INV");
+    return e && std::string(e) == "dpp";
+  }();
+  if (n <= 0) return;
+  if (waves == 4 && dppInv) launchK(potrf4_kernel<true>, dim3(n), dim3(256), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
+  else if (waves == 4) launchK(potrf4_kernel<false>, dim3(n), dim3(256), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
+  else launchK(potrf_kernel, dim3(n), dim3(64), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
 }
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
                  hipStream_t st, const int32_t* rows, const double* fwdY, double* fwdB) {
