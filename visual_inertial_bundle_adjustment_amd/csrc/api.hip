@@ -1418,8 +1418,13 @@ int doFinalize(vb_handle h) {
       alloc0(&d.Y, lmY[nPts] + 128) || alloc0(&d.yZero, 128) ||  // + the over-read of the Schur gathers
       alloc0(&d.gpNew, nPts * 3) || alloc0(&d.zNew, nPts * 3))
     return VB_E_HIP;
+  std::vector<int64_t> lxChunk;
+  for (int i = 0; i < nRV; i++)
+    for (int64_t b = lxStart[i]; b < lxStart[i + 1]; b += 1024)
+      lxChunk.insert(lxChunk.end(), {i, b, std::min<int64_t>(b + 1024, lxStart[i + 1])});
+  d.nLxChunk = (int64_t)lxChunk.size() / 3;
   if (upload(&d.oxStart, oxStart) || upload(&d.oxObs, oxObs) || upload(&d.oxSlot, oxSlot) ||
-      upload(&d.lxStart, lxStart) || upload(&d.lxLm, lxLm) || upload(&d.lxCol, lxCol))
+      upload(&d.lxStart, lxStart) || upload(&d.lxLm, lxLm) || upload(&d.lxCol, lxCol) || upload(&d.lxChunk, lxChunk))
     return VB_E_HIP;
   if (upload(&d.tileIdx, tileIdx) || alloc0(&d.tiles, (size_t)nTiles * TS * TS)) return VB_E_HIP;
   {
@@ -1876,7 +1881,7 @@ int vb_destroy(vb_handle h) {
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.yZero, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
-                  d.lxStart, d.lxLm, d.lxCol, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
+                  d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,

@@ -171,6 +171,9 @@ struct Dev {
   int64_t* lxStart = nullptr;
   int32_t* lxLm = nullptr;
   int32_t* lxCol = nullptr;
+  // L(X) cut into chunks of <= 1024 landmarks, (X, begin, end) each: the new-RHS pass (reduced_rhs_kernel)
+  int64_t* lxChunk = nullptr;
+  int64_t nLxChunk = 0;
   // Schur assembly work by target tile
   int64_t nTileWorks = 0;
   TileWork* tileWorks = nullptr;

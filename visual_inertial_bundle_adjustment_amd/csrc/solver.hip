@@ -642,45 +642,29 @@ __global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
   *p = *p * (1.0 + lambda) + (addIdentity ? lambda : 0.0);
 }
 
-// gradient-only (mode 0: gRedNew += sum J~^T e~ over this shard's observations) or new reduced RHS
-// (mode 1: rhs = gRedNew - sum Y^T zNew over this shard's landmarks)
-__device__ __forceinline__ bool shard_obs(const Dev& d, int64_t o) {
-  return (o >= d.obB && o < d.obE) || (o >= d.fB && o < d.fE);
-}
-__global__ void __launch_bounds__(256) reduced_grad_kernel(Dev d, int mode) {
+// new reduced RHS (vb_solve_with_new_gradient / vb_assemble_new_rhs): rhs = gRedNew - sum Y^T zNew over this
+// shard's landmarks; rhs starts as a copy of gRedNew, one block per chunk of <= 1024 landmarks of one
+// reduced variable X (the calibration variables see every landmark: one block each took 2.6 ms)
+__global__ void __launch_bounds__(256) reduced_rhs_kernel(Dev d) {
   __shared__ double g[32];
-  const int X1 = blockIdx.x;
+  const int64_t* ch = d.lxChunk + 3 * (int64_t)blockIdx.x;
+  const int X1 = (int)ch[0];
   const int d1 = d.rvDim[X1];
   const int64_t off1 = d.rvOff[X1];
   const int tid = threadIdx.x;
   if (tid < 32) g[tid] = 0.0;
   __syncthreads();
-  if (mode == 0) {
-    for (int64_t idx = d.oxStart[X1] + tid; idx < d.oxStart[X1 + 1]; idx += blockDim.x) {
-      const int64_t o = d.oxObs[idx];
-      if (!shard_obs(d, o)) continue;
-      const int s1 = d.oxSlot[idx];
-      const rec_t* ea = d.Jt + o * kJA;
-      const rec_t* x = jt_plane(d.Jt, d.nObsPad, o, slotPlane(s1));
-      const int st1 = slotStride(s1);
-      for (int j = 0; j < d1; j++) atomicAdd(&g[j], (double)x[j] * ea[kJe] + (double)x[st1 + j] * ea[kJe + 1]);
-    }
-  } else {
-    for (int64_t idx = d.lxStart[X1] + tid; idx < d.lxStart[X1 + 1]; idx += blockDim.x) {
-      const int64_t l = d.lxLm[idx];
-      if (l < d.lmB || l >= d.lmE) continue;
-      const rec_t* y1 = d.Y + d.lmY[l] / 3 + d.lxCol[idx];
-      const int64_t yq = d.nYcol;
-      const double z0 = d.zNew[l * 3], z1 = d.zNew[l * 3 + 1], z2 = d.zNew[l * 3 + 2];
-      for (int j = 0; j < d1; j++)
-        atomicAdd(&g[j], (double)y1[j] * z0 + (double)y1[yq + j] * z1 + (double)y1[2 * yq + j] * z2);
-    }
+  for (int64_t idx = ch[1] + tid; idx < ch[2]; idx += blockDim.x) {
+    const int64_t l = d.lxLm[idx];
+    if (l < d.lmB || l >= d.lmE) continue;
+    const rec_t* y1 = d.Y + d.lmY[l] / 3 + d.lxCol[idx];
+    const int64_t yq = d.nYcol;
+    const double z0 = d.zNew[l * 3], z1 = d.zNew[l * 3 + 1], z2 = d.zNew[l * 3 + 2];
+    for (int j = 0; j < d1; j++)
+      atomicAdd(&g[j], (double)y1[j] * z0 + (double)y1[yq + j] * z1 + (double)y1[2 * yq + j] * z2);
   }
   __syncthreads();
-  if (tid < d1) {
-    if (mode == 0) d.gRedNew[off1 + tid] += g[tid];
-    else d.rhs[off1 + tid] = d.gRedNew[off1 + tid] - g[tid];
-  }
+  if (tid < d1) atomicAdd(&d.rhs[off1 + tid], -g[tid]);
 }
 
 // ------------------------------------------------------------------ tile Cholesky
@@ -1835,7 +1819,8 @@ void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
     if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, 0.0, 1);
     return;
   }
-  if (d.nRV) hipLaunchKernelGGL(reduced_grad_kernel, dim3(d.nRV), dim3(256), 0, st, d, mode);
+  (void)hipMemcpyAsync(d.rhs, d.gRedNew, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, st);
+  if (d.nLxChunk) hipLaunchKernelGGL(reduced_rhs_kernel, dim3((unsigned)d.nLxChunk), dim3(256), 0, st, d);
 }
 // fwdB / fwdY (may be null): the forward solve fused into the factorization (potrf: y_J from b_J;
 // trsm: b_I -= L_IJ y_J for its tile, rows[] = the tile's row I)
