@@ -15,8 +15,12 @@ def wgs(r):
     return g // max(1, w)
 
 
-ks = [(r["Kernel_Name"].split("(")[0].replace("viba::", ""), int(r["Start_Timestamp"]), int(r["End_Timestamp"]), wgs(r))
-      for r in rows]
+def kname(r):
+    n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("viba::", "").split("<")[0]
+    return "potrf_kernel" if n in ("potrf4_kernel", "potrf_trsm_kernel") else n
+
+
+ks = [(kname(r), int(r["Start_Timestamp"]), int(r["End_Timestamp"]), wgs(r)) for r in rows]
 fam = ("fanin_kernel", "potrf_kernel", "trsm_kernel")
 last_di = max(i for i, k in enumerate(ks) if k[0] == "diag_inverse_kernel")
 first = last_di

@@ -35,6 +35,9 @@ void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n
                   const double* fwdB = nullptr, double* fwdY = nullptr);
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
                  hipStream_t st, const int32_t* rows = nullptr, const double* fwdY = nullptr, double* fwdB = nullptr);
+void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, double* dinv, hipStream_t st,
+                       double* fwdB, double* fwdY);
+void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
                          unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st);
@@ -225,7 +228,11 @@ int alloc0(T** dptr, size_t n) {
 // task lists over the same columns (solver.hip fwd/bwd_fanout_kernel).
 struct Sched {
   std::vector<int64_t> lvP, lvT, lvU;
-  std::vector<int64_t> lvUd;        // per level: end of the diagonal targets' fan-in chunks (listed first)
+  // levels factored by one potrf + trsm launch (potrf_trsm_kernel): per level the range of its items
+  // (diagonal tile, column, target, row, writer) in ptfD; the diagonal tiles to copy back from Lscr
+  std::vector<int64_t> lvPF;
+  int32_t *ptfD = nullptr, *ptfDiagD = nullptr;
+  int64_t nPtfDiag = 0;
   std::vector<int64_t> lvF, lvFd;   // factor_level_kernel items per level / diagonal items (padded) per level
   std::vector<int64_t> lvPT, lvPd;  // the same for the potrf + trsm-only items (fusedFactor 2)
   FacItem *facD = nullptr, *ptD = nullptr;
@@ -339,12 +346,8 @@ struct vb_handle_s {
   // the visual kernels, forked after the buffer resets and joined before their first consumer
   hipStream_t st2 = nullptr;
   hipEvent_t evFork = nullptr, evJoin = nullptr;
-  // potrf beside the off-diagonal fan-in (factorSeq): the off-diagonal chunks run on st3
-  hipStream_t st3 = nullptr;
-  hipEvent_t evFanF = nullptr, evFanJ = nullptr;
-  // VIBA_POTRF_OVERLAP=1 (measured no gain: the potrf blocks do not fit beside the fan-in's
-  // workgroups, so they wait for CUs anyway)
-  bool potrfOverlap = false;
+  int64_t ptFuseMax = 256;  // VIBA_PT_FUSE: levels with at most this many off-diagonal tiles run potrf + trsm fused
+  double* lscr = nullptr;   // L_JJ of the fused levels' columns (nT tiles), copied back after the factorization
   // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
   int profFamily = -1;
   std::vector<hipEvent_t> profEv;
@@ -1170,7 +1173,8 @@ int doFinalize(vb_handle h) {
       // level so the launch has ~fanWgs workgroups (>= 4 contributions per chunk: one per wave)
       std::vector<int32_t> pT, pC, tD, tT, tC, tR, fan;
       S.lvP.assign(nLev + 1, 0), S.lvT.assign(nLev + 1, 0), S.lvU.assign(nLev + 1, 0);
-      S.lvUd.clear();
+      S.lvPF.assign(nLev + 1, 0);
+      std::vector<int32_t> ptf, ptfDiag;
       S.lvF.assign(nLev + 1, 0), S.lvFd.assign(nLev, 0), S.lvPT.assign(nLev + 1, 0), S.lvPd.assign(nLev, 0);
       std::vector<FacItem> facItems, ptItems;
       for (int32_t L = 0; L < nLev; L++) {
@@ -1179,20 +1183,6 @@ int doFinalize(vb_handle h) {
           if (tgtSel(J))
             for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
         const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
-        // the diagonal targets' chunks first (they gate the level's potrf, which runs beside the
-        // off-diagonal chunks: factorSeq), cut finer since they sit on the critical path
-        auto chunks = [&](int32_t t, int64_t c) {
-          const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
-          if (m == 0) return;
-          const int64_t nch = (m + c - 1) / c;
-          for (int64_t k = 0; k < nch; k++) {
-            const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
-            fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
-          }
-        };
-        for (int32_t J : cols[L])
-          if (tgtSel(J)) chunks(h->colTilesH[h->colStart[J]], std::min<int64_t>(cs, 8));
-        S.lvUd.push_back((int64_t)fan.size() / 4);
         for (int32_t J : cols[L]) {
           const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
           if (colSel(J)) {
@@ -1201,10 +1191,19 @@ int doFinalize(vb_handle h) {
               tD.push_back(h->colTilesH[c0]), tT.push_back(h->colTilesH[c0 + q]), tC.push_back(J), tR.push_back(h->colRowsH[c0 + q]);
           }
           if (!tgtSel(J)) continue;
-          for (int64_t q = 1; q < n; q++) chunks(h->colTilesH[c0 + q], cs);
+          for (int64_t q = 0; q < n; q++) {
+            const int32_t t = h->colTilesH[c0 + q];
+            const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
+            if (m == 0) continue;
+            const int64_t nch = (m + cs - 1) / cs;
+            for (int64_t k = 0; k < nch; k++) {
+              const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
+              fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
+            }
+          }
         }
         if (fanSort) {  // longest chunks first: the dispatcher hands them out in order (LPT)
-          const size_t u0 = (size_t)S.lvUd[L];
+          const size_t u0 = (size_t)S.lvU[L];
           std::vector<std::array<int32_t, 4>> q((fan.size() / 4) - u0);
           for (size_t i = 0; i < q.size(); i++)
             for (int k = 0; k < 4; k++) q[i][k] = fan[4 * (u0 + i) + k];
@@ -1219,6 +1218,16 @@ int doFinalize(vb_handle h) {
             for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
         }
         S.lvP[L + 1] = (int64_t)pT.size(), S.lvT[L + 1] = (int64_t)tT.size(), S.lvU[L + 1] = (int64_t)fan.size() / 4;
+        if (h->ptFuseMax > 0 && S.lvP[L + 1] > S.lvP[L] && S.lvT[L + 1] - S.lvT[L] <= h->ptFuseMax)
+          for (int32_t J : cols[L]) {
+            if (!colSel(J)) continue;
+            const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+            const int32_t dt = h->colTilesH[c0];
+            if (n == 1) ptf.insert(ptf.end(), {dt, J, -1, -1, 1});
+            for (int64_t q = 1; q < n; q++) ptf.insert(ptf.end(), {dt, J, h->colTilesH[c0 + q], h->colRowsH[c0 + q], q == 1 ? 1 : 0});
+            ptfDiag.insert(ptfDiag.end(), {dt, J});
+          }
+        S.lvPF[L + 1] = (int64_t)ptf.size() / 5;
         // the same level as factor_level_kernel items: every diagonal tile of a factored column first
         // (padded to a multiple of 8), then the off-diagonal tiles and the fan-in-only targets; a
         // factored tile without contributions still gets one item (its potrf / trsm)
@@ -1285,8 +1294,11 @@ int doFinalize(vb_handle h) {
       if (upload(&S.potrfTileD, pT) || upload(&S.potrfColD, pC) || upload(&S.trsmDiagD, tD) ||
           upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.trsmRowD, tR) || upload(&S.updD, fan) ||
           upload(&S.fanPairsD, pairs) || upload(&S.tasksFD, tf) || upload(&S.tasksBD, tb) ||
-          upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.facD, facItems) || upload(&S.ptD, ptItems))
+          upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.facD, facItems) || upload(&S.ptD, ptItems) ||
+          upload(&S.ptfD, ptf) || upload(&S.ptfDiagD, ptfDiag))
         return VB_E_HIP;
+      S.nPtfDiag = (int64_t)ptfDiag.size() / 2;
+      if (S.nPtfDiag && !h->lscr && alloc0(&h->lscr, (size_t)nT * TS * TS)) return VB_E_HIP;
       S.built = true;
       return 0;
     };
@@ -1515,21 +1527,6 @@ bool fwdFused(vb_handle h) {
   return h->fwdInFactor && h->fusedFactor == 0 && h->partWorld <= 1 && !h->sharded && !h->legacySolve;
 }
 
-// level L's fan-in runs as two launches (diagonal targets before the potrf on the main stream, the
-// rest beside them on st3)
-bool splitLevel(vb_handle h, const Sched& S, int32_t L) {
-  return h->fusedFactor == 0 && h->potrfOverlap && S.lvP[L + 1] > S.lvP[L] && S.lvU[L + 1] > S.lvUd[L];
-}
-// fan-in launches per factorization of schedule S
-int64_t faninLaunches(vb_handle h, const Sched& S) {
-  int64_t n = 0;
-  for (int32_t L = 0; L < S.nLevels; L++) {
-    const bool sp = splitLevel(h, S, L);
-    n += (sp ? 1 : 0) + ((sp ? S.lvUd[L] : S.lvU[L + 1]) > S.lvU[L] ? 1 : 0);
-  }
-  return n;
-}
-
 void factorSeq(vb_handle h, const Sched& S) {
   Dev& d = h->d;
   if (h->fusedFactor == 2) {  // per level: fanin_kernel, then one potrf + trsm launch (no fan-in items)
@@ -1566,31 +1563,25 @@ void factorSeq(vb_handle h, const Sched& S) {
   double* fb = fwd ? h->rhsWork : nullptr;
   double* fy = fwd ? h->yvec : nullptr;
   for (int32_t L = 0; L < S.nLevels; L++) {
-    const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L], ud = S.lvUd[L], u1 = S.lvU[L + 1];
-    // the off-diagonal targets' fan-in on st3 while the diagonal targets' fan-in and the potrf run on
-    // the main stream; the trsm waits for both (without potrf work, or with the overlap disabled,
-    // one fan-in launch)
-    const bool split = splitLevel(h, S, L);
-    if (split) {
-      (void)hipEventRecord(h->evFanF, h->st);
-      (void)hipStreamWaitEvent(h->st3, h->evFanF, 0);
-      profBegin(h, KF_GEMM);
-      launch_fanin(d, S.updD + 4 * ud, S.fanPairsD, (int)(u1 - ud), h->st3);
-      profEnd(h, KF_GEMM);
-      (void)hipEventRecord(h->evFanJ, h->st3);
-    }
+    const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
     profBegin(h, KF_GEMM);
-    launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)((split ? ud : u1) - u0), h->st);
+    launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
     profEnd(h, KF_GEMM);
+    if (S.lvPF[L + 1] > S.lvPF[L]) {  // potrf + trsm in one launch
+      profBegin(h, KF_POTRF);
+      launch_potrf_trsm(d, S.ptfD + 5 * S.lvPF[L], (int)(S.lvPF[L + 1] - S.lvPF[L]), h->lscr, h->dinv, h->st, fb, fy);
+      profEnd(h, KF_POTRF);
+      continue;
+    }
     profBegin(h, KF_POTRF);
     launch_potrf(d, S.potrfTileD + p0, S.potrfColD + p0, (int)(S.lvP[L + 1] - p0), h->dinv, h->st, fb, fy);
     profEnd(h, KF_POTRF);
-    if (split) (void)hipStreamWaitEvent(h->st, h->evFanJ, 0);
     profBegin(h, KF_TRSM);
     launch_trsm(d, S.trsmDiagD + t0, S.trsmTargetD + t0, S.trsmColD + t0, (int)(S.lvT[L + 1] - t0), h->dinv, h->st,
                 S.trsmRowD + t0, fy, fb);
     profEnd(h, KF_TRSM);
   }
+  if (S.nPtfDiag) launch_copy_diag(d, S.ptfDiagD, (int)S.nPtfDiag, h->lscr, h->st);
   launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
 }
 
@@ -1855,7 +1846,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   if (const char* e = getenv("VIBA_FUSED_FACTOR")) h->fusedFactor = atoi(e);
   if (const char* e = getenv("VIBA_FWD_IN_FACTOR")) h->fwdInFactor = e[0] != '0';
   if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
-  if (const char* e = getenv("VIBA_POTRF_OVERLAP")) h->potrfOverlap = e[0] == '1';
+  if (const char* e = getenv("VIBA_PT_FUSE")) h->ptFuseMax = atoll(e);
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -1866,9 +1857,6 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming));
-  HIPCHK(hipStreamCreateWithFlags(&h->st3, hipStreamNonBlocking));
-  HIPCHK(hipEventCreateWithFlags(&h->evFanF, hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&h->evFanJ, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -1885,7 +1873,7 @@ int vb_destroy(vb_handle h) {
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
-                  h->rhsWork, h->linv, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
+                  h->rhsWork, h->linv, h->lscr, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
                   h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->facSync,
                   (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise};
   for (void* p : ptrs)
@@ -1908,12 +1896,9 @@ int vb_destroy(vb_handle h) {
   if (h->evFork) hipEventDestroy(h->evFork);
   if (h->evJoin) hipEventDestroy(h->evJoin);
   if (h->st2) hipStreamSynchronize(h->st2), hipStreamDestroy(h->st2);
-  if (h->evFanF) hipEventDestroy(h->evFanF);
-  if (h->evFanJ) hipEventDestroy(h->evFanJ);
-  if (h->st3) hipStreamSynchronize(h->st3), hipStreamDestroy(h->st3);
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
-    void* sp[] = {S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
+    void* sp[] = {S.ptfD, S.ptfDiagD, S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
                   S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD};
     for (void* p : sp)
       if (p) hipFree(p);
@@ -2556,7 +2541,7 @@ int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
   // tiles less the symbolic fill: what the PCG product reads)
   int64_t nS = 0;
   for (uint8_t f : h->tileFill) nS += f ? 0 : 1;
-  out[10] = h->sch[0].built && h->fusedFactor == 0 ? faninLaunches(h, h->sch[0]) : h->nLevels, out[11] = nS;
+  out[10] = h->nLevels, out[11] = nS;
   return 0;
 }
 

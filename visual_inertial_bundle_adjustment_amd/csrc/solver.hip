@@ -930,7 +930,7 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __device__ __forceinline__ void potrf_forward(const Dev& d, const double* T, const double* dinvS, double* sh, int J,
-                                              const double* b, double* y, int lane) {
+                                              const double* b, double* y, int lane, bool store = true) {
   // right-looking by 16-row blocks: lane r keeps b_r; once y_i is known every later row subtracts
   // L(r, block i) y_i, so each block's chain is one 16-term GEMV + one 16-term update
   double br = b[(int64_t)J * TS + lane];
@@ -952,7 +952,7 @@ __device__ __forceinline__ void potrf_forward(const Dev& d, const double* T, con
     }
   }
   const int64_t row = (int64_t)J * TS + lane;
-  y[row] = row < d.nRed ? sh[lane] : 0.0;
+  if (store) y[row] = row < d.nRed ? sh[lane] : 0.0;  // y_J also stays in sh[0, 64)
 }
 
 __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileList, const int32_t* cols, double* dinvAll,
@@ -989,15 +989,10 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileLis
 // MFMAs (the one-wave left-looking form chains up to 36 of them); the terms are subtracted in the same
 // order as there.  The upper blocks are written as zeros.
 template <bool kDppInv>
-__global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileList, const int32_t* cols,
-                                                     double* dinvAll, const double* fwdB, double* fwdY) {
-  __shared__ double T[TS * TS];
-  __shared__ double scratch[256];
-  __shared__ double dinvS[1024];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+__device__ __forceinline__ void potrf4_core(const Dev& d, const double* A, double* T, double* scratch, double* dinvS,
+                                            int tid) {
+  const int lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lq = lane >> 4;
-  double* A = d.tiles + (int64_t)tileList[blockIdx.x] * TS * TS;
-  double* dinvG = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
   if (w == 0) POTRF_TW(0);
   double4_t R[4];
 #pragma unroll
@@ -1050,10 +1045,91 @@ __global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileL
   __syncthreads();
   if (w == 0) POTRF_TW(13);
   if (bad && lane == 0) atomicOr(d.err, 8);
-  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB, fwdY, lane);
+}
+
+template <bool kDppInv>
+__global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileList, const int32_t* cols,
+                                                     double* dinvAll, const double* fwdB, double* fwdY) {
+  __shared__ double T[TS * TS];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[1024];
+  const int tid = threadIdx.x, w = tid >> 6;
+  double* A = d.tiles + (int64_t)tileList[blockIdx.x] * TS * TS;
+  double* dinvG = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
+  potrf4_core<kDppInv>(d, A, T, scratch, dinvS, tid);
+  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB, fwdY, tid & 63);
   lds_to_global(A, T, TS * TS, tid, 256);
   lds_to_global(dinvG, dinvS, 1024, tid, 256);
   if (w == 0) POTRF_TW(14);
+}
+
+// potrf + trsm of a level in ONE launch (the levels with few off-diagonal tiles, where the two launches
+// and the dependency between them cost more than the work): one block per off-diagonal tile (I, J)
+// factors L_JJ itself -- every block of column J computes the identical factor from the untouched A_JJ
+// -- then forms L_IJ = A_IJ L_JJ^-T from LDS (its A_IJ loaded before the factorization).  One block
+// per column (writer) stores L_JJ into the scratch Lscr (A_JJ is still being read by the others; the
+// diagonal tiles are copied back after the last level: copy_diag_kernel) and the inverses into dinv.
+// With the fused forward solve every block also derives y_J (only the writer stores it) for its
+// b_I -= L_IJ y_J.  items: (diagonal tile, column, target tile or -1, target row, writer) per block.
+template <bool kDppInv>
+__global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* items, double* Lscr, double* dinvAll,
+                                                         double* fwdB, double* fwdY) {
+  __shared__ double T[TS * TS];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[1024];
+  const int32_t* it = items + 5 * (int64_t)blockIdx.x;
+  const int32_t diagT = it[0], col = it[1], target = it[2], row = it[3], writer = it[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  double* At = target >= 0 ? d.tiles + (int64_t)target * TS * TS : nullptr;
+  double av[4][4];
+  if (At) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) av[k][r] = At[(16 * k + lq + 4 * r) * TS + 16 * w + lr];
+  }
+  potrf4_core<kDppInv>(d, d.tiles + (int64_t)diagT * TS * TS, T, scratch, dinvS, tid);
+  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, col, fwdB, fwdY, lane, writer != 0);
+  if (writer) {
+    lds_to_global(Lscr + (int64_t)col * TS * TS, T, TS * TS, tid, 256);
+    lds_to_global(dinvAll + (int64_t)col * 1024, dinvS, 1024, tid, 256);
+  }
+  if (!At) return;
+  __syncthreads();  // y_J (scratch[0, 64)) from wave 0
+  double4_t Xt[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    double4_t acc = double4_t{av[k][0], av[k][1], av[k][2], av[k][3]};
+#pragma unroll
+    for (int k2 = 0; k2 < k; k2++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) acc = mfma64(-T[(16 * k2 + 4 * s + lq) * TS + 16 * k + lr], Xt[k2][s], acc);
+    double4_t res = double4_t{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 4; s++) res = mfma64(dinvS[k * 256 + (4 * s + lq) * 16 + lr], acc[s], res);
+    Xt[k] = res;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) At[(16 * k + lq + 4 * r) * TS + 16 * w + lr] = Xt[k][r];
+  if (fwdB) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) v += Xt[k][r] * scratch[16 * k + lq + 4 * r];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lq == 0) atomicAdd(fwdB + (int64_t)row * TS + 16 * w + lr, -v);
+  }
+}
+
+// the diagonal tiles of the fused levels back from Lscr (pairs: diagonal tile, column)
+__global__ void __launch_bounds__(256) copy_diag_kernel(Dev d, const int32_t* pairs, const double* Lscr) {
+  const int32_t t = pairs[2 * blockIdx.x], c = pairs[2 * blockIdx.x + 1];
+  lds_to_global(d.tiles + (int64_t)t * TS * TS, Lscr + (int64_t)c * TS * TS, TS * TS, threadIdx.x, 256);
 }
 
 // X = A L_JJ^-T for target tile target[b] with diagonal tile diag[b] of column cols[b]; wave w =
@@ -1840,6 +1916,16 @@ void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n
   if (waves == 4 && dppInv) launchK(potrf4_kernel<true>, dim3(n), dim3(256), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
   else if (waves == 4) launchK(potrf4_kernel<false>, dim3(n), dim3(256), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
   else launchK(potrf_kernel, dim3(n), dim3(64), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
+}
+void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, double* dinv, hipStream_t st,
+                       double* fwdB, double* fwdY) {
+  static const bool dppInv = getenv("VIBA_DIAG_INV") && std::string(getenv("VIBA_DIAG_INV")) == "dpp";
+  if (n <= 0) return;
+  if (dppInv) launchK(potrf_trsm_kernel<true>, dim3(n), dim3(256), 0, st, d, items, Lscr, dinv, fwdB, fwdY);
+  else launchK(potrf_trsm_kernel<false>, dim3(n), dim3(256), 0, st, d, items, Lscr, dinv, fwdB, fwdY);
+}
+void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(copy_diag_kernel, dim3(n), dim3(256), 0, st, d, pairs, Lscr);
 }
 void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const int32_t* cols, int n, const double* dinv,
                  hipStream_t st, const int32_t* rows, const double* fwdY, double* fwdB) {
