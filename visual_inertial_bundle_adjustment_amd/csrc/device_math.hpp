@@ -246,8 +246,13 @@ DEVI bool project(const double* cam, v3 pc, double uv[2], double Jc[6], double J
     if (WantJ) {
       Jc[0] = p[0] * d00, Jc[1] = 0.0, Jc[2] = p[0] * d02;
       Jc[3] = 0.0, Jc[4] = p[1] * d11, Jc[5] = p[1] * d12;
-      Jp[0] = x, Jp[1] = 0, Jp[2] = 1, Jp[3] = 0;
-      Jp[15] = 0, Jp[16] = y, Jp[17] = 0, Jp[18] = 1;
+      // every entry written, as in the Fisheye624 branch: with only the first four per row the compiler
+      // merged the two branches' stores under selected addresses, which put Jp (and the visual
+      // kernels' 144 B per lane) in scratch
+#pragma unroll
+      for (int i = 0; i < 30; i++) Jp[i] = 0.0;
+      Jp[0] = x, Jp[2] = 1;
+      Jp[16] = y, Jp[18] = 1;
     }
     return true;
   }
