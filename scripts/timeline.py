@@ -18,7 +18,7 @@ for n, dur, t, e in seq[a + 1:b + 1]:
 t0 = out[0][3]
 fan = [0.0, 0]
 for n, dur, c, t, e in out:
-    if n in ("fanin_kernel", "potrf_kernel", "trsm_kernel"):
+    if n.split("<")[0] in ("fanin_kernel", "potrf_kernel", "trsm_kernel", "potrf4_kernel", "potrf_trsm_kernel"):
         fan[0] += dur; fan[1] += c
         continue
     print(f"{(t - t0) / 1e6:8.2f}ms {n:32s} x{c:4d} busy {dur / 1e3:7.3f} ms span {(e - t) / 1e6:7.3f}")

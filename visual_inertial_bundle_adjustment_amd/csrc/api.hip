@@ -24,6 +24,8 @@ namespace viba {
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st);
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
+void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
+void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_rs_build(const Dev& d, hipStream_t st);
 void launch_preint(const Dev& d, const PreintArgs& pa, hipStream_t st);
 void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gObs, const int32_t* gPt, int64_t nG,
@@ -346,6 +348,10 @@ struct vb_handle_s {
   // the visual kernels, forked after the buffer resets and joined before their first consumer
   hipStream_t st2 = nullptr;
   hipEvent_t evFork = nullptr, evJoin = nullptr;
+  // vb_linearize: the reduced system's clear on a stream of its own (stZ), so the small factors'
+  // evaluation (st2) does not queue behind the 2.2 GB memset; their assembly waits for it (evZero)
+  hipStream_t stZ = nullptr;
+  hipEvent_t evZero = nullptr;
   int64_t ptFuseMax = 256;  // VIBA_PT_FUSE: levels with at most this many off-diagonal tiles run potrf + trsm fused
   double* lscr = nullptr;   // L_JJ of the fused levels' columns (nT tiles), copied back after the factorization
   // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
@@ -1857,6 +1863,8 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   for (auto& e : h->ev) HIPCHK(hipEventCreate(&e));
   HIPCHK(hipEventCreateWithFlags(&h->evFork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&h->stZ, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&h->evZero, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -1896,6 +1904,8 @@ int vb_destroy(vb_handle h) {
   if (h->evFork) hipEventDestroy(h->evFork);
   if (h->evJoin) hipEventDestroy(h->evJoin);
   if (h->st2) hipStreamSynchronize(h->st2), hipStreamDestroy(h->st2);
+  if (h->evZero) hipEventDestroy(h->evZero);
+  if (h->stZ) hipStreamSynchronize(h->stZ), hipStreamDestroy(h->stZ);
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
     void* sp[] = {S.ptfD, S.ptfDiagD, S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
@@ -2163,10 +2173,12 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   // the reduced system is cleared and the small factors assembled on the side stream while the visual
   // factors linearize on the main stream (they write only their records and the cost)
   const bool side = smallHere(h, 0);
-  hipStream_t zs = side ? h->st2 : h->st;
+  hipStream_t zs = side ? h->stZ : h->st;
   if (side) {
     HIPCHK(hipEventRecord(h->evFork, h->st));
     HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
+    HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
+    launch_small_eval(d, 0, d.gRed, h->st2);
   }
   if (h->zeroRuns.empty()) {
     HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), zs));
@@ -2177,7 +2189,9 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), zs));
   if (h->isRoot || h->partWorld > 1) launch_pad_diag(d, h->padRowsD, h->nPadRows, zs);
   if (side) {
-    launch_small(d, 0, d.gRed, h->st2);
+    HIPCHK(hipEventRecord(h->evZero, h->stZ));
+    HIPCHK(hipStreamWaitEvent(h->st2, h->evZero, 0));
+    launch_small_assemble(d, 0, d.gRed, h->st2);
     HIPCHK(hipEventRecord(h->evJoin, h->st2));
   }
   visualLinShard(h, update_cache, dont_retry_failed);

@@ -400,13 +400,44 @@ __device__ void inertial_eval(const double* c, const double* calib, const ImuIdx
                               const se3& Tn, v3 vn, v3 g, SmallEval& E, const int cols[5]) {
   const int n = jac.size;
   const double dt = c[10];
-  double dc[23];
-  imu_boxminus(calib, c + 11 + 207 + 81, jac, dc);
+  // corr = J_calib * boxMinus(calib, calib at preintegration): the error-state entries in the
+  // ImuJacInd order (bias g / a, scale g / a, nonorth g / a, time offsets), enabled blocks only, each
+  // consumed as it is formed (a compacted boxMinus array indexed at run time lived in scratch)
   double corr[9];
-  for (int i = 0; i < 9; i++) {
-    double s = 0;
-    for (int j = 0; j < n; j++) s += c[11 + j * 9 + i] * dc[j];
-    corr[i] = s;
+#pragma unroll
+  for (int i = 0; i < 9; i++) corr[i] = 0.0;
+  {
+    const double* r = c + 11 + 207 + 81;
+    const double* Jc = c + 11;
+    auto take = [&](double v) {
+#pragma unroll
+      for (int i = 0; i < 9; i++) corr[i] += Jc[i] * v;
+      Jc += 9;
+    };
+    if (jac.gB >= 0)
+#pragma unroll
+      for (int i = 0; i < 3; i++) take(calib[6 + i] - r[6 + i]);
+    if (jac.aB >= 0)
+#pragma unroll
+      for (int i = 0; i < 3; i++) take(calib[9 + i] - r[9 + i]);
+    if (jac.gS >= 0)
+#pragma unroll
+      for (int i = 0; i < 3; i++) take(1.0 / calib[i] - 1.0 / r[i]);
+    if (jac.aS >= 0)
+#pragma unroll
+      for (int i = 0; i < 3; i++) take(1.0 / calib[3 + i] - 1.0 / r[3 + i]);
+    if (jac.gN >= 0) {
+      constexpr int kG[6] = {3, 6, 1, 7, 2, 5};  // col-major (0,1) (0,2) (1,0) (1,2) (2,0) (2,1)
+#pragma unroll
+      for (int i = 0; i < 6; i++) take(calib[12 + kG[i]] - r[12 + kG[i]]);
+    }
+    if (jac.aN >= 0) {
+      constexpr int kA[3] = {3, 6, 7};  // (0,1) (0,2) (1,2)
+#pragma unroll
+      for (int i = 0; i < 3; i++) take(calib[21 + kA[i]] - r[21 + kA[i]]);
+    }
+    if (jac.rT >= 0) take(calib[31] - r[31]);
+    if (jac.gaT >= 0) take((calib[30] - calib[31]) - (r[30] - r[31]));
   }
   q4 Rc = qexp(mk(-corr[0], -corr[1], -corr[2]));
   q4 cR = qmul(Rc, qinv(q4{c[0], c[1], c[2], c[3]}));
@@ -572,12 +603,13 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
     SmallEval E;
     const int64_t slot = d.sf[FK].stage + k;
     E.J = (double(*)[kMaxCols])(d.sJ + slot * kSmallJ);
-    const int nv = kNV[FK];
+    constexpr int nv = (FK == 0) ? 5 : (FK == 1) ? 6 : (FK == 2) ? 9 : (FK == 3) ? 10 : (FK <= 8) ? 2 : 1;  // kNV
     const int32_t* vi = a.vars + k * nv;
     const double* c = a.consts + k * a.nc;
     // column layout: every non-gravity slot gets columns (also constant ones: simpler eval)
     int colc = 0;
     E.nslot = nv;
+#pragma unroll
     for (int s = 0; s < nv; s++) {
       const int kind = kFK[FK][s], h = vi[s];
       if (kind == 8 || h < 0) {
@@ -720,18 +752,23 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
       }
     }
     // whitening of the residual by a square root U of the precision (P = U^T U, row-major m x m);
-    // the Jacobian is whitened by small_assemble_kernel
-    const int m = E.m;
+    // the Jacobian is whitened by small_assemble_kernel.  m is the kind's residual size (E.m), a
+    // compile-time bound so E.e stays in registers
+    constexpr int m = mRows;
     if (whiten) {
-      double te[kMaxM];
+      double te[m];
+#pragma unroll
       for (int i = 0; i < m; i++) {
         double s = 0;
+#pragma unroll
         for (int q = 0; q < m; q++) s += U[i * m + q] * E.e[q];
         te[i] = s;
       }
+#pragma unroll
       for (int i = 0; i < m; i++) E.e[i] = te[i];
     }
     double sq = 0;
+#pragma unroll
     for (int i = 0; i < m; i++) sq += E.e[i] * E.e[i];
     double rho, drho;
     if (useImuLoss) huber_jet2(d.imu.a, d.imu.b, d.imu.k2, d.imu.h, sq, rho, drho);
@@ -742,9 +779,11 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
       acc[0] = 0.5 * rho;
       double* se = d.sE + slot * kSmallE;
       se[0] = drho;
+#pragma unroll
       for (int i = 0; i < m; i++) se[1 + i] = E.e[i];
       int32_t* mt = d.sMeta + slot * kSmallMeta;
       mt[0] = m, mt[1] = colc, mt[2] = nv, mt[3] = whiten ? (int32_t)(U - a.consts) : -1, mt[4] = FK;
+#pragma unroll
       for (int s = 0; s < nv; s++) mt[5 + s] = E.red[s], mt[15 + s] = E.col[s], mt[25 + s] = E.dim[s];
     }
   }
@@ -758,26 +797,34 @@ struct SmallLaunch {
   int32_t first[15];
   int32_t countCost;  // the root counts the small factors' cost (partitioned: every rank evaluates)
 };
+// kinds [LO, HI] per launch: the IMU kinds (1-3) get a kernel of their own, so their register
+// allocation is not the union with the priors' and random walks' paths
+template <int FK, int LO, int HI>
+__device__ __forceinline__ double small_case(const Dev& d, const SmallLaunch& L, int fk, int64_t k) {
+  if constexpr (FK < LO || FK > HI) return 0.0;
+  else return fk == FK ? small_eval<FK>(d, L.a[FK], k) : 0.0;
+}
+template <int LO, int HI>
 __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallLaunch L) {
-  const int b = blockIdx.x;
-  int fk = 1;
-  while (fk < 13 && b >= L.first[fk + 1]) fk++;
+  const int b = blockIdx.x + L.first[LO];
+  int fk = LO;
+  while (fk < HI && b >= L.first[fk + 1]) fk++;
   const int64_t k = (int64_t)(b - L.first[fk]) * 64 + threadIdx.x;
   double acc[1] = {0.0};
   switch (fk) {
-    case 1: acc[0] = small_eval<1>(d, L.a[1], k); break;
-    case 2: acc[0] = small_eval<2>(d, L.a[2], k); break;
-    case 3: acc[0] = small_eval<3>(d, L.a[3], k); break;
-    case 4: acc[0] = small_eval<4>(d, L.a[4], k); break;
-    case 5: acc[0] = small_eval<5>(d, L.a[5], k); break;
-    case 6: acc[0] = small_eval<6>(d, L.a[6], k); break;
-    case 7: acc[0] = small_eval<7>(d, L.a[7], k); break;
-    case 8: acc[0] = small_eval<8>(d, L.a[8], k); break;
-    case 9: acc[0] = small_eval<9>(d, L.a[9], k); break;
-    case 10: acc[0] = small_eval<10>(d, L.a[10], k); break;
-    case 11: acc[0] = small_eval<11>(d, L.a[11], k); break;
-    case 12: acc[0] = small_eval<12>(d, L.a[12], k); break;
-    default: acc[0] = small_eval<13>(d, L.a[13], k); break;
+    case 1: acc[0] = small_case<1, LO, HI>(d, L, fk, k); break;
+    case 2: acc[0] = small_case<2, LO, HI>(d, L, fk, k); break;
+    case 3: acc[0] = small_case<3, LO, HI>(d, L, fk, k); break;
+    case 4: acc[0] = small_case<4, LO, HI>(d, L, fk, k); break;
+    case 5: acc[0] = small_case<5, LO, HI>(d, L, fk, k); break;
+    case 6: acc[0] = small_case<6, LO, HI>(d, L, fk, k); break;
+    case 7: acc[0] = small_case<7, LO, HI>(d, L, fk, k); break;
+    case 8: acc[0] = small_case<8, LO, HI>(d, L, fk, k); break;
+    case 9: acc[0] = small_case<9, LO, HI>(d, L, fk, k); break;
+    case 10: acc[0] = small_case<10, LO, HI>(d, L, fk, k); break;
+    case 11: acc[0] = small_case<11, LO, HI>(d, L, fk, k); break;
+    case 12: acc[0] = small_case<12, LO, HI>(d, L, fk, k); break;
+    default: acc[0] = small_case<13, LO, HI>(d, L, fk, k); break;
   }
   if (!L.countCost) acc[0] = 0.0;
   block_sum_atomic<1>(acc, d.red + (L.a[1].mode == 2 ? 1 : 0));
@@ -1063,11 +1110,17 @@ void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st) {
   }
   L.first[14] = nb;
   L.countCost = d.root;
-  if (nb > 0) hipLaunchKernelGGL(small_kernel, dim3((unsigned)nb), dim3(64), 0, st, d, L);
+  const int32_t nImu = L.first[4] - L.first[1], nRest = L.first[14] - L.first[4];
+  if (nImu > 0) hipLaunchKernelGGL((small_kernel<1, 3>), dim3((unsigned)nImu), dim3(64), 0, st, d, L);
+  if (nRest > 0) hipLaunchKernelGGL((small_kernel<4, 13>), dim3((unsigned)nRest), dim3(64), 0, st, d, L);
 }
 
+void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st) {
   launch_small_eval(d, mode, gOut, st);
+  launch_small_assemble(d, mode, gOut, st);
+}
+void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st) {
   if (mode == 2 || d.nSmallStage <= 0) return;
   // three launches by residual size: IMU kinds 1-3 (9 rows), omega priors (3), the rest (<= 23); the
   // staging slots run kind by kind
