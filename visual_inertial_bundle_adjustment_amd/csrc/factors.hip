@@ -676,46 +676,63 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
       for (int i = 0; i < 3; i++) E.J[i][E.col[0] + i] = 1.0 / sig;
       E.e[0] = r.x, E.e[1] = r.y, E.e[2] = r.z;
     } else if (FK == 5 || FK == 10) {  // imu calib RW / prior (residual padded to 23)
+      // rows in the canonical error-state order (a disabled block leaves zero rows: J^T J and J^T e
+      // do not depend on the row order), columns / weights at the compact index j -- every register
+      // index static (a compacted residual array indexed at run time lived in scratch)
       E.m = 23;
-      const int n = d.jac.size;
-      double dd[23];
-      for (int i = 0; i < 23; i++) E.e[i] = 0.0, dd[i] = 0.0;
-      if (FK == 5) {
-        imu_boxminus(d.var[6] + (int64_t)vi[1] * 32, d.var[6] + (int64_t)vi[0] * 32, d.jac, dd);
-        for (int i = 0; i < n; i++) {
-          E.e[i] = dd[i] * c[i];
-          E.J[i][E.col[0] + i] = -c[i];
-          E.J[i][E.col[1] + i] = c[i];
+      const double* v = d.var[6] + (int64_t)vi[FK == 5 ? 1 : 0] * 32;
+      const double* r = FK == 5 ? d.var[6] + (int64_t)vi[0] * 32 : c;
+      const ImuIdx& jc = d.jac;
+      const bool on[8] = {jc.gB >= 0, jc.aB >= 0, jc.gS >= 0, jc.aS >= 0, jc.gN >= 0, jc.aN >= 0, jc.rT >= 0, jc.gaT >= 0};
+      constexpr int kBlk[23] = {0, 0, 0, 1, 1, 1, 2, 2, 2, 3, 3, 3, 4, 4, 4, 4, 4, 4, 5, 5, 5, 6, 7};
+      constexpr int kNo[9] = {3, 6, 1, 7, 2, 5, 3, 6, 7};  // gN (col-major), then aN
+      int j = 0;
+#pragma unroll
+      for (int q = 0; q < 23; q++) {
+        E.e[q] = 0.0;
+        if (!on[kBlk[q]]) continue;
+        double dv;
+        if (q < 3) dv = v[6 + q] - r[6 + q];
+        else if (q < 6) dv = v[9 + q - 3] - r[9 + q - 3];
+        else if (q < 9) dv = 1.0 / v[q - 6] - 1.0 / r[q - 6];
+        else if (q < 12) dv = 1.0 / v[3 + q - 9] - 1.0 / r[3 + q - 9];
+        else if (q < 18) dv = v[12 + kNo[q - 12]] - r[12 + kNo[q - 12]];
+        else if (q < 21) dv = v[21 + kNo[q - 12]] - r[21 + kNo[q - 12]];
+        else if (q == 21) dv = v[31] - r[31];
+        else dv = (v[30] - v[31]) - (r[30] - r[31]);
+        if (FK == 5) {
+          E.e[q] = dv * c[j];
+          E.J[q][E.col[0] + j] = -c[j];
+          E.J[q][E.col[1] + j] = c[j];
+        } else {
+          const double sq = sqrt(c[32 + j]);
+          E.e[q] = dv * sq;
+          E.J[q][E.col[0] + j] = sq;
         }
-      } else {
-        imu_boxminus(d.var[6] + (int64_t)vi[0] * 32, c, d.jac, dd);
-        for (int i = 0; i < n; i++) {
-          const double sq = sqrt(c[32 + i]);
-          E.e[i] = dd[i] * sq;
-          E.J[i][E.col[0] + i] = sq;
-        }
+        j++;
       }
     } else if (FK == 6 || FK == 11) {  // cam intrinsics RW / prior (residual padded to 17)
+      // rows: projection parameter q (q < np), 15 readout, 16 time offset (as above: static indices)
       E.m = 17;
-      for (int i = 0; i < 17; i++) E.e[i] = 0.0;
       const double* v = d.var[4] + (int64_t)vi[FK == 6 ? 1 : 0] * 24;
       const double* b = FK == 6 ? d.var[4] + (int64_t)vi[0] * 24 : c;
       const int np = (int)v[1];
-      double dd[17];
-      int i = 0;
-      for (; i < np; i++) dd[i] = v[9 + i] - b[9 + i];
-      if (v[7] != 0.0) dd[i++] = v[5] - b[5];
-      if (v[8] != 0.0) dd[i++] = v[6] - b[6];
-      const int nt = i;
-      for (int j = 0; j < nt; j++) {
+      int j = 0;
+#pragma unroll
+      for (int q = 0; q < 17; q++) {
+        E.e[q] = 0.0;
+        const bool on = q < 15 ? q < np : q == 15 ? v[7] != 0.0 : v[8] != 0.0;
+        if (!on) continue;
+        const double dv = q < 15 ? v[9 + q] - b[9 + q] : q == 15 ? v[5] - b[5] : v[6] - b[6];
         const double sq = FK == 6 ? c[j] : sqrt(c[24 + j]);
-        E.e[j] = dd[j] * sq;
+        E.e[q] = dv * sq;
         if (FK == 6) {
-          E.J[j][E.col[0] + j] = -sq;
-          E.J[j][E.col[1] + j] = sq;
+          E.J[q][E.col[0] + j] = -sq;
+          E.J[q][E.col[1] + j] = sq;
         } else {
-          E.J[j][E.col[0] + j] = sq;
+          E.J[q][E.col[0] + j] = sq;
         }
+        j++;
       }
     } else {  // SE3 RW (7, 8), pose prior (9), SE3 priors (12, 13)
       E.m = 6;
