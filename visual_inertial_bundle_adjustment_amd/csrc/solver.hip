@@ -646,25 +646,29 @@ __global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
 // shard's landmarks; rhs starts as a copy of gRedNew, one block per chunk of <= 1024 landmarks of one
 // reduced variable X (the calibration variables see every landmark: one block each took 2.6 ms)
 __global__ void __launch_bounds__(256) reduced_rhs_kernel(Dev d) {
-  __shared__ double g[32];
+  __shared__ double g[4][32];
   const int64_t* ch = d.lxChunk + 3 * (int64_t)blockIdx.x;
   const int X1 = (int)ch[0];
   const int d1 = d.rvDim[X1];
   const int64_t off1 = d.rvOff[X1];
-  const int tid = threadIdx.x;
-  if (tid < 32) g[tid] = 0.0;
-  __syncthreads();
-  for (int64_t idx = ch[1] + tid; idx < ch[2]; idx += blockDim.x) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // lanes = (landmark slot, column j): P = d1 rounded up to a power of two lanes per landmark, so a
+  // wave reads 64 / P landmarks' panel rows at once (runs of d1 doubles per plane) instead of one
+  // landmark's 3 d1 values per lane
+  const int P = d1 <= 4 ? 4 : d1 <= 8 ? 8 : d1 <= 16 ? 16 : 32;
+  const int S = 64 / P, slot = lane / P, j = lane % P;
+  const int64_t yq = d.nYcol;
+  double acc = 0.0;
+  for (int64_t idx = ch[1] + wave * S + slot; idx < ch[2]; idx += 4 * S) {
     const int64_t l = d.lxLm[idx];
-    if (l < d.lmB || l >= d.lmE) continue;
-    const rec_t* y1 = d.Y + d.lmY[l] / 3 + d.lxCol[idx];
-    const int64_t yq = d.nYcol;
-    const double z0 = d.zNew[l * 3], z1 = d.zNew[l * 3 + 1], z2 = d.zNew[l * 3 + 2];
-    for (int j = 0; j < d1; j++)
-      atomicAdd(&g[j], (double)y1[j] * z0 + (double)y1[yq + j] * z1 + (double)y1[2 * yq + j] * z2);
+    if (j >= d1 || l < d.lmB || l >= d.lmE) continue;
+    const rec_t* y1 = d.Y + d.lmY[l] / 3 + d.lxCol[idx] + j;
+    acc += (double)y1[0] * d.zNew[l * 3] + (double)y1[yq] * d.zNew[l * 3 + 1] + (double)y1[2 * yq] * d.zNew[l * 3 + 2];
   }
+  for (int o = P; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);  // over the landmark slots
+  if (lane < P && lane < d1) g[wave][lane] = acc;
   __syncthreads();
-  if (tid < d1) atomicAdd(&d.rhs[off1 + tid], -g[tid]);
+  if (tid < d1) atomicAdd(&d.rhs[off1 + tid], -(g[0][tid] + g[1][tid] + g[2][tid] + g[3][tid]));
 }
 
 // ------------------------------------------------------------------ tile Cholesky
