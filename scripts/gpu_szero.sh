@@ -1,0 +1,10 @@
+#!/bin/bash
+# coalesced staging zeroing in the small-factor kernels: parity, bench x2, kernel stats
+set -o pipefail
+mkdir -p gpurun_out
+O=gpurun_out/szero
+timeout -k 10 900 python -u -m pytest tests/test_parity_gpu.py tests/test_parity_configs.py tests/test_preint.py tests/test_covariances.py tests/test_distributed_gpu.py -x -q -m gpu --timeout 300 --timeout-method thread > ${O}_pytest.log 2>&1; rc=$?; tail -2 ${O}_pytest.log; [ $rc -eq 0 ] || exit $rc
+for i in 1 2; do timeout -k 10 300 python bench.py --no-cpu-baseline > ${O}_$i.json 2>${O}_$i.log || exit $?
+python -c "import json;d=json.load(open('${O}_$i.json'));print(round(d['value'],2), d['phases_ms'])"; done
+bash scripts/gpu_kstats.sh szero > ${O}_kstats.txt 2>&1 || exit $?
+grep -E "small" ${O}_kstats.txt

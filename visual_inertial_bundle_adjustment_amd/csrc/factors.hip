@@ -599,6 +599,21 @@ __constant__ int kNV[14] = {5, 6, 9, 10, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1};
 template <int FK>
 __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, int64_t k) {
   double acc[1] = {0.0};
+  constexpr int mRows = (FK >= 1 && FK <= 3) ? 9 : FK == 4 ? 3 : (FK == 5 || FK == 10) ? 23 : (FK == 6 || FK == 11) ? 17 : 6;
+  if (a.mode != 2) {
+    // the wave's 64 staging slots (consecutive factors) zeroed over their first mRows rows with the
+    // lanes on consecutive 16 B: one factor's rows zeroed per lane made every store instruction 64
+    // scattered 8-byte writes
+    const int lane = threadIdx.x & 63;
+    const int64_t k0 = k - lane, ns = a.n - k0 < 64 ? a.n - k0 : 64;
+    typedef double zd2 __attribute__((ext_vector_type(2)));
+    for (int64_t q = 0; q < ns; q++) {
+      zd2* base = (zd2*)(d.sJ + (d.sf[FK].stage + k0 + q) * kSmallJ);
+      for (int e = lane; e < mRows * kMaxCols / 2; e += 64) base[e] = zd2{0.0, 0.0};
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // before the lanes' own Jacobian stores
+    __builtin_amdgcn_wave_barrier();
+  }
   if (k < a.n) {
     SmallEval E;
     const int64_t slot = d.sf[FK].stage + k;
@@ -621,9 +636,6 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
       colc += E.dim[s];
       E.red[s] = d.redOf[kind][h];
     }
-    constexpr int mRows = (FK >= 1 && FK <= 3) ? 9 : FK == 4 ? 3 : (FK == 5 || FK == 10) ? 23 : (FK == 6 || FK == 11) ? 17 : 6;
-    for (int i = 0; i < mRows; i++)
-      for (int j = 0; j < colc; j++) E.J[i][j] = 0.0;
     bool whiten = false;
     const double* U = nullptr;
     bool useImuLoss = false;
