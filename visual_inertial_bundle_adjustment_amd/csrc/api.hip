@@ -25,7 +25,7 @@ void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo,
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
-void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st);
+void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st, int part = 3);
 void launch_rs_build(const Dev& d, hipStream_t st);
 void launch_preint(const Dev& d, const PreintArgs& pa, hipStream_t st);
 void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gObs, const int32_t* gPt, int64_t nG,
@@ -351,7 +351,7 @@ struct vb_handle_s {
   // vb_linearize: the reduced system's clear on a stream of its own (stZ), so the small factors'
   // evaluation (st2) does not queue behind the 2.2 GB memset; their assembly waits for it (evZero)
   hipStream_t stZ = nullptr;
-  hipEvent_t evZero = nullptr;
+  hipEvent_t evZero = nullptr, evSmallE = nullptr, evZJoin = nullptr;
   int64_t ptFuseMax = 256;  // VIBA_PT_FUSE: levels with at most this many off-diagonal tiles run potrf + trsm fused
   double* lscr = nullptr;   // L_JJ of the fused levels' columns (nT tiles), copied back after the factorization
   // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
@@ -1865,6 +1865,8 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipEventCreateWithFlags(&h->evJoin, hipEventDisableTiming));
   HIPCHK(hipStreamCreateWithFlags(&h->stZ, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->evZero, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evSmallE, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evZJoin, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -1905,6 +1907,8 @@ int vb_destroy(vb_handle h) {
   if (h->evJoin) hipEventDestroy(h->evJoin);
   if (h->st2) hipStreamSynchronize(h->st2), hipStreamDestroy(h->st2);
   if (h->evZero) hipEventDestroy(h->evZero);
+  if (h->evSmallE) hipEventDestroy(h->evSmallE);
+  if (h->evZJoin) hipEventDestroy(h->evZJoin);
   if (h->stZ) hipStreamSynchronize(h->stZ), hipStreamDestroy(h->stZ);
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
@@ -2189,13 +2193,20 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), zs));
   if (h->isRoot || h->partWorld > 1) launch_pad_diag(d, h->padRowsD, h->nPadRows, zs);
   if (side) {
+    // the IMU kinds' assembly on st2, the other kinds' on stZ after the clear: both wait for the clear
+    // and the evaluation
     HIPCHK(hipEventRecord(h->evZero, h->stZ));
+    HIPCHK(hipEventRecord(h->evSmallE, h->st2));
     HIPCHK(hipStreamWaitEvent(h->st2, h->evZero, 0));
-    launch_small_assemble(d, 0, d.gRed, h->st2);
+    HIPCHK(hipStreamWaitEvent(h->stZ, h->evSmallE, 0));
+    launch_small_assemble(d, 0, d.gRed, h->st2, 1);
+    launch_small_assemble(d, 0, d.gRed, h->stZ, 2);
     HIPCHK(hipEventRecord(h->evJoin, h->st2));
+    HIPCHK(hipEventRecord(h->evZJoin, h->stZ));
   }
   visualLinShard(h, update_cache, dont_retry_failed);
   joinSmall(h);
+  if (side) HIPCHK(hipStreamWaitEvent(h->st, h->evZJoin, 0));
   HIPCHK(hipEventRecord(h->ev[1], h->st));
   double c = 0;
   if (int rc = readRed(h, &c, 0, 1)) return rc;

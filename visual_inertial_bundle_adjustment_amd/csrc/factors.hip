@@ -1144,21 +1144,22 @@ void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st) {
   if (nRest > 0) hipLaunchKernelGGL((small_kernel<4, 13>), dim3((unsigned)nRest), dim3(64), 0, st, d, L);
 }
 
-void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st);
+void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st, int part = 3);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st) {
   launch_small_eval(d, mode, gOut, st);
   launch_small_assemble(d, mode, gOut, st);
 }
-void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st) {
+// part bit 0: the IMU kinds' launch, bit 1: the omega priors' and the rest's launches
+void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st, int part) {
   if (mode == 2 || d.nSmallStage <= 0) return;
   // three launches by residual size: IMU kinds 1-3 (9 rows), omega priors (3), the rest (<= 23); the
   // staging slots run kind by kind
   const int64_t a = d.sf[1].stage, b = d.sf[4].stage, c = d.sf[5].stage, e = d.nSmallStage;
-  if (b > a)
+  if (b > a && (part & 1))
     launchK(small_assemble_kernel<9>, dim3((unsigned)((b - a + 3) / 4)), dim3(256), 0, st, d, mode, gOut, a, b);
-  if (c > b)
+  if (c > b && (part & 2))
     hipLaunchKernelGGL(small_assemble_kernel<3>, dim3((unsigned)((c - b + 3) / 4)), dim3(256), 0, st, d, mode, gOut, b, c);
-  if (e > c)
+  if (e > c && (part & 2))
     hipLaunchKernelGGL(small_assemble_kernel<kMaxM>, dim3((unsigned)((e - c + 3) / 4)), dim3(256), 0, st, d, mode, gOut,
                        c, e);
 }
