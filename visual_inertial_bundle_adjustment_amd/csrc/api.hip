@@ -591,6 +591,13 @@ int doFinalize(vb_handle h) {
   std::vector<int> tdims(nRV);
   for (int r = 0; r < nRV; r++) tdims[r] = tdimOf(red[r].first, red[r].second);
   int64_t leafDims = 1024;
+  // cut: the thinnest separator -- the left variables coupled across the cut, or the right ones --
+  // among the cuts within +-cutWin of the part's median (config C: 954k -> 701k tile contributions,
+  // 110 -> 89 levels against the median cut with left separators; wider windows unbalance the parts:
+  // 0.1: 746k, 0.25: 880k).  VIBA_ND_CUTWIN=0: the median cut; VIBA_ND_SEPRIGHT=0: left separators only
+  double cutWin = 0.05;
+  if (const char* e = getenv("VIBA_ND_CUTWIN")) cutWin = std::max(0.0, std::min(0.45, atof(e)));
+  const bool sepRight = !(getenv("VIBA_ND_SEPRIGHT") && atoi(getenv("VIBA_ND_SEPRIGHT")) == 0);
   if (const char* e = getenv("VIBA_ND_LEAF")) leafDims = std::max<int64_t>(64, atoll(e));
   if (getenv("VIBA_ND_OFF")) leafDims = INT64_MAX;
   std::vector<int> nord;             // final order (registration indices)
@@ -620,14 +627,43 @@ int doFinalize(vb_handle h) {
     size_t k = 0;
     while (k < vs.size() && acc + tdims[vs[k]] <= dims / 2) acc += tdims[vs[k++]];
     if (k == 0 || k >= vs.size()) return emit(vs, false);
-    const int cut = tp[vs[k]];
-    std::vector<int> L, R(vs.begin() + k, vs.end()), S;
-    int64_t sd = 0;
-    for (size_t i = 0; i < k; i++) {
-      if (hiP[vs[i]] >= cut) S.push_back(vs[i]), sd += tdims[vs[i]];
-      else L.push_back(vs[i]);
+    bool right = false;
+    if (cutWin > 0.0) {
+      const size_t w = (size_t)(cutWin * (double)vs.size());
+      const size_t k0 = k > w + 1 ? k - w : 1, k1 = std::min(vs.size() - 1, k + w);
+      int64_t best = INT64_MAX;
+      size_t bk = k;
+      bool br = false;
+      for (size_t c = k0; c <= k1; c++) {
+        const int ct = tp[vs[c]];
+        int64_t sl = 0, sr = 0;
+        for (size_t i = 0; i < c; i++)
+          if (hiP[vs[i]] >= ct) sl += tdims[vs[i]];
+        if (sepRight)
+          for (size_t i = c; i < vs.size(); i++)
+            if (loP[vs[i]] < ct) sr += tdims[vs[i]];
+        if (sl < best) best = sl, bk = c, br = false;
+        if (sepRight && sr < best) best = sr, bk = c, br = true;
+      }
+      k = bk, right = br;
     }
-    if (L.empty() || 2 * sd > dims) return emit(vs, false);  // no useful separator
+    const int cut = tp[vs[k]];
+    std::vector<int> L, R, S;
+    int64_t sd = 0;
+    if (!right) {  // separator: the left variables coupled across the cut
+      R.assign(vs.begin() + k, vs.end());
+      for (size_t i = 0; i < k; i++) {
+        if (hiP[vs[i]] >= cut) S.push_back(vs[i]), sd += tdims[vs[i]];
+        else L.push_back(vs[i]);
+      }
+    } else {  // the right variables coupled across it
+      L.assign(vs.begin(), vs.begin() + k);
+      for (size_t i = k; i < vs.size(); i++) {
+        if (loP[vs[i]] < cut) S.push_back(vs[i]), sd += tdims[vs[i]];
+        else R.push_back(vs[i]);
+      }
+    }
+    if (L.empty() || R.empty() || 2 * sd > dims) return emit(vs, false);  // no useful separator
     dissect(L, depth + 1, 2 * sub, own);
     dissect(R, depth + 1, 2 * sub + 1, own);
     emit(S, true);
