@@ -147,8 +147,8 @@ def test_rolling_shutter_out_of_range_is_an_error():
 def test_full_size_properties_config_C():
     """Config C (10k rigs / 300k landmarks / 6M obs) through size-independent properties:
     linearize cost == cost pass at the same point; model reduction > 0; accepted step lowers the
-    cost; backup/restore restores the variables bit-exactly (the cost to the last ulp: its
-    reduction uses atomics)."""
+    cost; backup/restore restores the variables bit-exactly (the cost to 1e-13 relative: it is an fp64
+    atomic sum of 6M terms whose order changes run to run -- measured up to 1.3e-14)."""
     g, p = make(hip(), "C")
     c0 = g.linearize(True, False)
     c_pass, _ = g.cost(False)
@@ -162,7 +162,7 @@ def test_full_size_properties_config_C():
     assert c1 < c0 and st[1] < 0.03 * st[0]
     g.restore()
     c_back, _ = g.cost(False)
-    assert abs(c_back - c_pass) <= 1e-14 * c_pass
+    assert abs(c_back - c_pass) <= 1e-13 * c_pass
     for a, k in zip(v0, (1, 4)):
         assert np.array_equal(a, g.get_vars(k))
 
