@@ -24,7 +24,7 @@ ks = [(kname(r), int(r["Start_Timestamp"]), int(r["End_Timestamp"]), wgs(r)) for
 fam = ("fanin_kernel", "potrf_kernel", "trsm_kernel")
 last_di = max(i for i, k in enumerate(ks) if k[0] == "diag_inverse_kernel")
 first = last_di
-while first > 0 and ks[first - 1][0] in fam:
+while first > 0 and (ks[first - 1][0] in fam or ks[first - 1][0] == "copy_diag_kernel"):
     first -= 1
 seg = ks[first:last_di + 1]
 levels, cur = [], {}
