@@ -730,7 +730,7 @@ struct Chol16 {
     bad |= !(piv > 0.0);
     const double y = rsqrt_nr(piv);
     invd[C] = y;
-    const double lc = ((lane & 15) == C) ? piv * y : s[C] * y;
+    const double lc = s[C] * y;  // lane C holds the pivot itself: L_CC = piv * y
     s[C] = lc;
     Upd16<C, C + 1>::run(s, lc);
     Chol16<C + 1>::run(s, invd, lane, bad);
@@ -830,7 +830,7 @@ __device__ __forceinline__ void diag16_dpp(double* T, double* scratch, double* d
 #pragma unroll
     for (int c = 0; c < 16; c++) T[(16 * i + c) * TS + 16 * i + lane] = (c <= lane) ? s[c] : 0.0;
 #pragma unroll
-    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = (r >= lane) ? acc[r] : 0.0;
+    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = acc[r];  // rows above the lane stay +0.0
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -868,7 +868,7 @@ __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS
   }
   if (lane < 16) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = (r >= lane) ? acc[r] : 0.0;
+    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = acc[r];  // rows above the lane stay +0.0
   }
   __builtin_amdgcn_wave_barrier();
 }
