@@ -23,6 +23,7 @@ namespace viba {
 // kernels (factors.hip / solver.hip)
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st);
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
+void launch_fold_red(const Dev& d, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st, int part = 3);
@@ -1535,7 +1536,7 @@ int doFinalize(vb_handle h) {
         upload(&d.rsN, cnt))
       return VB_E_HIP;
   }
-  if (alloc0(&d.red, 64) || alloc0(&d.err, 4)) return VB_E_HIP;
+  if (alloc0(&d.red, 64) || alloc0(&d.redS, 64 * 8) || alloc0(&d.err, 4)) return VB_E_HIP;
   h->finalized = true;
   return 0;
 }
@@ -1561,6 +1562,7 @@ void visualLinShard(vb_handle h, int updateCache, int dontRetry) {
   launch_visual_lin(d, updateCache, dontRetry, d.obB, d.obE, h->st);
   launch_visual_lin(d, updateCache, dontRetry, d.fB, d.fE, h->st);
   profEnd(h, KF_VISUAL_LIN);
+  launch_fold_red(d, h->st);
 }
 void visualCostShard(vb_handle h, int comparable) {
   const Dev& d = h->d;
@@ -1568,6 +1570,7 @@ void visualCostShard(vb_handle h, int comparable) {
   launch_visual_cost(d, comparable, d.obB, d.obE, h->st);
   launch_visual_cost(d, comparable, d.fB, d.fE, h->st);
   profEnd(h, KF_VISUAL_COST);
+  launch_fold_red(d, h->st);
 }
 
 // vb_damp_factor_solve's forward solve runs inside the factorization (potrf_forward / trsm_kernel)
@@ -1923,7 +1926,7 @@ int vb_destroy(vb_handle h) {
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.yZero, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
-                  d.rsCalib, d.red, d.err, h->colTilesD,
+                  d.rsCalib, d.red, d.redS, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->lscr, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
                   h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->facSync,

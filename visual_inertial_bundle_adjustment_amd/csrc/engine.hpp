@@ -218,6 +218,9 @@ struct Dev {
   int32_t rsGravVar = 0;
   // scratch for reductions
   double* red = nullptr;  // 64 doubles
+  // the visual kernels' cost sums striped over 64 slots of 8 (slot blockIdx & 63): one atomic target
+  // per cost word serialised ~90k atomics in L2; fold_red_kernel adds them into red[0..8) and clears them
+  double* redS = nullptr;
   int32_t* err = nullptr;  // error flags
   // landmark shard of this handle (multi-GPU; the whole problem on a single GPU): landmarks
   // [lmB, lmE), their observations [obB, obE), constant-point observations [fB, fE) (all of

@@ -313,7 +313,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   double x = acc[0];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
-  if (lane == 0 && x != 0.0) atomicAdd(d.red + 0, x);
+  if (lane == 0 && x != 0.0) atomicAdd(d.redS + (blockIdx.x & 63) * 8 + 0, x);
 }
 
 // cost pass: red[1] += cost, red[2..4] += stats (numTotal, numInvalid, numPrevInvalid)
@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(256) visual_cost_kernel(Dev d, int comparable,
       acc[0] = 0.5 * huber_val(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s);
     }
   }
-  block_sum_atomic<4>(acc, d.red + 1);
+  block_sum_atomic<4>(acc, d.redS + (blockIdx.x & 63) * 8 + 1);
 }
 
 // ------------------------------------------------------------------ small factors
@@ -1121,6 +1121,16 @@ void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo,
   launchK(visual_lin_kernel, dim3((unsigned)((n + kVisBlock - 1) / kVisBlock)), dim3(kVisBlock), 0, st, d, updateCache,
           dontRetry, lo, hi);
 }
+// red[k] += sum of the 64 stripes of redS[., k] (atomically: the small factors add into red beside), and
+// the stripes cleared for the next launch
+__global__ void fold_red_kernel(Dev d) {
+  const int k = threadIdx.x;
+  if (k >= 8) return;
+  double s = 0.0;
+  for (int i = 0; i < 64; i++) s += d.redS[i * 8 + k], d.redS[i * 8 + k] = 0.0;
+  if (s != 0.0) atomicAdd(d.red + k, s);
+}
+void launch_fold_red(const Dev& d, hipStream_t st) { hipLaunchKernelGGL(fold_red_kernel, dim3(1), dim3(64), 0, st, d); }
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
   const int64_t n = hi - lo;
