@@ -221,7 +221,8 @@ def main():
     # roofline of the profiled kernel family (average launch duration from HIP events on the engine
     # stream, algorithmic work from the symbolic structure)
     avg_ms = kms / max(1, launches)
-    if args.profile_family < 0:  # nothing profiled (the factorization runs from its HIP graph)
+    if args.profile_family < 0 or launches == 0 or kms <= 0:
+        # nothing event-timed (the factorization ran from its HIP graph, or the family never launched)
         roof = None
     elif args.profile_family == KF_GEMM:
         # st[6] tile-pair contributions per factorization (2 * 64^3 flops each), st[10] fan-in launches

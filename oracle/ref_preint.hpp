@@ -235,7 +235,9 @@ inline PreIntResult computePreIntegration(const ImuJacInd& ji, const std::vector
     rvp2J = Mat(9, nc);
     setBlock(rvp2J, 0, 9, mul(PJ, measJ));
     if (es) setBlock(rvp2J, 0, 15, mul(PJ, calibJ));
-    if (newA && ji.gaT >= 0) {
+    // the reference tests `jacInd.gyroAccelTimeOffsetIdx()` for truth (PreIntegration.cpp:198,213): an
+    // unestimated offset (-1) writes column 14 (raw accel z), an offset at index 0 is never written
+    if (newA && ji.gaT != 0) {
       V3 dG = g - prevG, dA = a - prevA;
       if (newG) {
         V3 bG, bA, fG, fA;

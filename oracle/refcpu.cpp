@@ -2055,6 +2055,23 @@ void ref_mi_boxplus(const double* b, const double* delta, double* out) {
   r.dt = B.dt;
   packRvp(r, out);
 }
+// integrate(gyro, accel, dt, &paramJac) (MotionIntegral.cpp:162-226): RVP + 9 x 6 Jacobian, row-major
+void ref_mi_integrate_jac(const double* gyro, const double* accel, double dt, double* out, double* jac96) {
+  Mat PJ;
+  packRvp(integrateJac(v3(gyro[0], gyro[1], gyro[2]), v3(accel[0], accel[1], accel[2]), dt, PJ), out);
+  for (int i = 0; i < 9; i++)
+    for (int j = 0; j < 6; j++) jac96[i * 6 + j] = PJ(i, j);
+}
+// combineJacs(a, b, aJac, bJac, cJac) (MotionIntegral.cpp:52-75) for 9 x 6 Jacobians, row-major
+void ref_mi_combine_jacs(const double* a, const double* b, const double* aJ96, const double* bJ96, double* out,
+                         double* cJ96) {
+  Mat aJ(9, 6), bJ(9, 6), cJ;
+  for (int i = 0; i < 9; i++)
+    for (int j = 0; j < 6; j++) aJ(i, j) = aJ96[i * 6 + j], bJ(i, j) = bJ96[i * 6 + j];
+  packRvp(combineJacs(unpackRvp(a), unpackRvp(b), aJ, bJ, cJ), out);
+  for (int i = 0; i < 9; i++)
+    for (int j = 0; j < 6; j++) cJ96[i * 6 + j] = cJ(i, j);
+}
 }  // extern "C"
 
 // ---------------------------------------------------------------- landmark shards (test of the

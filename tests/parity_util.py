@@ -98,7 +98,7 @@ def make_failing(p, n_behind=30, n_edge=60, edge_depth=2e-4, seed=11):
 SPRING_X0 = (-2.0, -1.0, 0.0, 0.5, 1.5, 2.5)
 
 
-def make_spring_chain(engine_cls, x0=SPRING_X0, spring=1.0):
+def make_spring_chain(engine_cls, x0=SPRING_X0, spring=1.0, const=None):
     """TestOptimizer.Simple (lib/small_thing/tests/TestOptimizer.cpp:22-50) restated with the
     engine's own factor kinds: each point x_i is parameter 0 of a Linear camera-intrinsics variable
     holding v_i = x_i - i * spring, and the spring y - x - spring becomes the additive intrinsics
@@ -110,7 +110,7 @@ def make_spring_chain(engine_cls, x0=SPRING_X0, spring=1.0):
     cams[:, 0], cams[:, 1], cams[:, 2], cams[:, 3] = 0, 4, 640, 480
     cams[:, 9] = [x - i * spring for i, x in enumerate(x0)]
     e = engine_cls()
-    e.set_vars(VAR_CAM_INTR, cams)
+    e.set_vars(VAR_CAM_INTR, cams, None if const is None else np.asarray(const, np.uint8))
     consts = np.zeros((n - 1, 17))
     consts[:, :4] = 1.0
     e.add_factors(F_RW_CAM_INTR, np.array([[i, i + 1] for i in range(n - 1)]), None, consts)

@@ -42,7 +42,7 @@ class MI:
     def __init__(self):
         self.lib = load()
         for n in ("ref_mi_integrate", "ref_mi_combine", "ref_mi_uncombine_left", "ref_mi_differentiate",
-                  "ref_mi_boxminus", "ref_mi_boxplus"):
+                  "ref_mi_boxminus", "ref_mi_boxplus", "ref_mi_integrate_jac", "ref_mi_combine_jacs"):
             getattr(self.lib, n).restype = None
         self.lib.ref_mi_integrate.argtypes = [_dp, _dp, C.c_double, _dp]
 
@@ -69,6 +69,17 @@ class MI:
 
     def boxplus(self, b, d):
         return self._bin("ref_mi_boxplus", b, d, 11)
+
+    def integrate_jac(self, g, a, dt):
+        out, J = _arr(11), _arr(54)
+        g, a = np.ascontiguousarray(g, float), np.ascontiguousarray(a, float)
+        self.lib.ref_mi_integrate_jac(_p(g), _p(a), C.c_double(dt), out.ctypes.data_as(_dp), J.ctypes.data_as(_dp))
+        return out, J.reshape(9, 6)
+
+    def combine_jacs(self, a, b, aJ, bJ):
+        out, J = _arr(11), _arr(54)
+        self.lib.ref_mi_combine_jacs(_p(a), _p(b), _p(aJ), _p(bJ), out.ctypes.data_as(_dp), J.ctypes.data_as(_dp))
+        return out, J.reshape(9, 6)
 
     def differentiate(self, rvp):
         out = _arr(9)
@@ -145,12 +156,71 @@ def test_mi_small_steps(mi):  # TestMotionIntegral.SmallSteps (fewer cases: ctyp
         assert np.linalg.norm(mi.boxminus(acc, mi.integrate(g, a, 1.0))) < 1e-10
 
 
+def _integrate_num_jac(mi, g, a, dt, eps=1e-7):
+    """integrateNumJac (TestMotionIntegral.cpp:129-145): forward differences of boxMinus over gyro, accel."""
+    base = mi.integrate(g, a, dt)
+    J = np.zeros((9, 6))
+    for i in range(6):
+        gp, ap = np.array(g, float), np.array(a, float)
+        if i < 3:
+            gp[i] += eps
+        else:
+            ap[i - 3] += eps
+        J[:, i] = mi.boxminus(mi.integrate(gp, ap, dt), base) / eps
+    return J
+
+
+def test_mi_jacobian(mi):  # TestMotionIntegral.Jacobian (TestMotionIntegral.cpp:147-160): |numJ - anJ| < 1e-7
+    rng = np.random.default_rng(42)
+    worst = 0.0
+    for _ in range(100):
+        g, a, t1 = rng.normal(size=3), rng.normal(size=3), rng.uniform(0.1, 0.9)
+        _, anJ = mi.integrate_jac(g, a, t1)
+        worst = max(worst, np.linalg.norm(_integrate_num_jac(mi, g, a, t1) - anJ))
+    assert worst < 1e-7, worst
+
+
+def test_mi_jacobian_small_angle(mi):  # the same check in integrate's th < 1e-3 series branch
+    rng = np.random.default_rng(7)
+    for _ in range(20):
+        g, a, t1 = rng.normal(size=3) * 1e-4, rng.normal(size=3), rng.uniform(0.1, 0.9)
+        _, anJ = mi.integrate_jac(g, a, t1)
+        assert np.linalg.norm(_integrate_num_jac(mi, g, a, t1) - anJ) < 1e-7
+
+
+def test_mi_combine_jacobian(mi):  # TestMotionIntegral.CombineJacobian (:162-175): |cJ - dJ| < 1e-10
+    rng = np.random.default_rng(42)
+    for _ in range(100):
+        g, a, t1 = rng.normal(size=3), rng.normal(size=3), rng.uniform(0.1, 0.9)
+        ra, aJ = mi.integrate_jac(g, a, t1)
+        rb, bJ = mi.integrate_jac(g, a, 1.0 - t1)
+        rc, cJ = mi.integrate_jac(g, a, 1.0)
+        rd, dJ = mi.combine_jacs(ra, rb, aJ, bJ)
+        assert np.linalg.norm(cJ - dJ) < 1e-10
+        assert np.linalg.norm(mi.boxminus(rd, rc)) < 1e-10
+
+
 def test_spring_chain_oracle():  # TestOptimizer.Simple
     e = make_spring_chain(RefEngine)
     s = e.optimize()
     x = spring_positions(e)
     assert np.all(np.abs(np.diff(x) - 1.0) < 1e-8), x
     assert s.final_cost < 1e-12 and s.num_iterations >= 1
+
+
+def test_const_in_factor_oracle():
+    """TestOptimizer.ConstInFactor (TestDynamicVars.cpp:58-86): the spring chain whose factor takes its
+    variables as fixed-size const inputs.  Every factor kind here has fixed sizes, so the restatement
+    adds what a const input means to the solver: the first point is a constant variable (skipped in the
+    gradient / Hessian, Variable.h:225 kConstantVar), the others must settle 1 apart from it (1e-8) and
+    the constant one must not move at all."""
+    from parity_util import SPRING_X0
+    e = make_spring_chain(RefEngine, const=[1] + [0] * (len(SPRING_X0) - 1))
+    e.optimize()
+    x = spring_positions(e)
+    assert x[0] == SPRING_X0[0]
+    assert np.all(np.abs(np.diff(x) - 1.0) < 1e-8), x
+    assert np.all(np.abs(x - (SPRING_X0[0] + np.arange(len(x)))) < 1e-8)
 
 
 # ------------------------------------------------------------------ finite-difference Jacobians

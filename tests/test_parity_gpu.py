@@ -103,6 +103,19 @@ def test_spring_chain_no_landmarks():  # TestOptimizer.Simple restated; empty po
     assert np.all(np.abs(np.diff(x) - 1.0) < 1e-8), x
 
 
+def test_const_in_factor_gpu():  # TestOptimizer.ConstInFactor restated (test_oracle_kat.py), on the GPU
+    from parity_util import SPRING_X0
+    from oracle.refcpu import RefEngine
+    const = [1] + [0] * (len(SPRING_X0) - 1)
+    e = make_spring_chain(hip(), const=const)
+    r = make_spring_chain(RefEngine, const=const)
+    s, sr = e.optimize(), r.optimize()
+    x, xr = spring_positions(e), spring_positions(r)
+    assert x[0] == SPRING_X0[0]
+    assert np.all(np.abs(np.diff(x) - 1.0) < 1e-8), x
+    assert np.abs(x - xr).max() < 1e-10 and s.num_iterations == sr.num_iterations
+
+
 @pytest.mark.parametrize("mask", [0x03, 0x0F | 0x40])
 def test_imu_calib_subsets(mask):  # ImuCalibrationJacobianIndices with options switched off
     g, _ = make(hip(), "miniB", imu_calib_options=mask)

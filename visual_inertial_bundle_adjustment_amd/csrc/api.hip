@@ -636,16 +636,33 @@ int doFinalize(vb_handle h) {
       double best = 1e300;
       size_t bk = k;
       bool br = false;
+      // separator widths of every candidate cut c (vs ascends in tp): sl(c) = dims of the i < c with
+      // hiP >= tp(c), sr(c) = dims of the i >= c with loP < tp(c); two sweeps over Fenwick trees keyed
+      // by time position, O(|vs| log nRV) per part instead of a rescan per candidate
+      const size_t nc = k1 - k0 + 1;
+      std::vector<int64_t> slC(nc, 0), srC(nc, 0), bit(nRV + 1, 0);
+      auto bitAdd = [&](int pos, int64_t v) { for (int x = std::min(pos, nRV - 1) + 1; x <= nRV; x += x & -x) bit[x] += v; };
+      auto bitSum = [&](int pos) { int64_t r = 0; for (int x = pos; x > 0; x -= x & -x) r += bit[x]; return r; };  // keys < pos
+      {
+        int64_t tot = 0;
+        for (size_t i = 0; i < k0; i++) bitAdd(hiP[vs[i]], tdims[vs[i]]), tot += tdims[vs[i]];
+        for (size_t c = k0; c <= k1; c++) {
+          slC[c - k0] = tot - bitSum(tp[vs[c]]);
+          bitAdd(hiP[vs[c]], tdims[vs[c]]), tot += tdims[vs[c]];
+        }
+      }
+      if (sepRight) {
+        std::fill(bit.begin(), bit.end(), 0);
+        for (size_t i = vs.size(); i-- > k1 + 1;) bitAdd(loP[vs[i]], tdims[vs[i]]);
+        for (size_t c = k1 + 1; c-- > k0;) {
+          bitAdd(loP[vs[c]], tdims[vs[c]]);
+          srC[c - k0] = bitSum(tp[vs[c]]);
+        }
+      }
       int64_t accC = 0;
       for (size_t i = 0; i < k0; i++) accC += tdims[vs[i]];
       for (size_t c = k0; c <= k1; accC += tdims[vs[c]], c++) {
-        const int ct = tp[vs[c]];
-        int64_t sl = 0, sr = 0;
-        for (size_t i = 0; i < c; i++)
-          if (hiP[vs[i]] >= ct) sl += tdims[vs[i]];
-        if (sepRight)
-          for (size_t i = c; i < vs.size(); i++)
-            if (loP[vs[i]] < ct) sr += tdims[vs[i]];
+        const int64_t sl = slC[c - k0], sr = srC[c - k0];
         const double pen = cutBal * (double)std::llabs(2 * accC - dims) * 0.5;  // imbalance, in dims
         if (sl + pen < best) best = sl + pen, bk = c, br = false;
         if (sepRight && sr + pen < best) best = sr + pen, bk = c, br = true;

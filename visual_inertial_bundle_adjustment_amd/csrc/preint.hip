@@ -202,6 +202,7 @@ __global__ void __launch_bounds__(64) preint_kernel(Dev d, PreintArgs pa) {
   // this lane's column role and which calibration block its column belongs to
   const bool isJ = lane < es, isFG = lane >= kLaneFG && lane < kLaneFG + 3, isFA = lane >= kLaneFA && lane < kLaneFA + 3;
   const bool isC = lane >= kLaneCov && lane < kLaneCov + 9;
+  const int gaLane = J.gaT > 0 ? J.gaT : J.gaT < 0 ? kLaneFA + 2 : -1;
   double x[9];
 #pragma unroll
   for (int r = 0; r < 9; r++) x[r] = 0.0;
@@ -268,16 +269,6 @@ __global__ void __launch_bounds__(64) preint_kernel(Dev d, PreintArgs pa) {
         for (int k = 0; k < 6; k++) s += PJ[i][k] * cj[k];
         b[i] = s;
       }
-      if (newA && lane == J.gaT) {
-        v3 dG = sub(g, prevG), dA = sub(a, prevA);
-        if (newG) {
-          const v3 fG = sub(mvr(cG, gRaw), bg), fA = sub(mvr(cA, prevRawA), ba);
-          const v3 bG = sub(mvr(cG, prevRawG), bg), bA = sub(mvr(cA, aRaw), ba);
-          dG = scl(0.5, add(sub(bG, prevG), sub(g, fG)));
-          dA = scl(0.5, add(sub(bA, prevA), sub(a, fA)));
-        }
-        drvp_left(r, dG, dA, b);
-      }
     } else if (isFG || isFA) {
       const int j = isFG ? lane - kLaneFG : lane - kLaneFA;
       const int k0 = isFG ? 0 : 3;
@@ -291,6 +282,20 @@ __global__ void __launch_bounds__(64) preint_kernel(Dev d, PreintArgs pa) {
     } else {
 #pragma unroll
       for (int i = 0; i < 9; i++) b[i] = 0.0;
+    }
+    // the accel-boundary column rvp2Jac.col(15 + gyroAccelTimeOffsetIdx()) under the reference's guard
+    // `transitionToNewAccelMeas && jacInd.gyroAccelTimeOffsetIdx()` (PreIntegration.cpp:198,213): the
+    // index is tested for truth, so an unestimated offset (-1) overwrites column 14 (raw accel z, fromA
+    // lane 2) and an offset at index 0 is never written
+    if (newA && lane == gaLane) {
+      v3 dG = sub(g, prevG), dA = sub(a, prevA);
+      if (newG) {
+        const v3 fG = sub(mvr(cG, gRaw), bg), fA = sub(mvr(cA, prevRawA), ba);
+        const v3 bG = sub(mvr(cG, prevRawG), bg), bA = sub(mvr(cA, aRaw), ba);
+        dG = scl(0.5, add(sub(bG, prevG), sub(g, fG)));
+        dA = scl(0.5, add(sub(bA, prevA), sub(a, fA)));
+      }
+      drvp_left(r, dG, dA, b);
     }
     prevA = a, prevG = g, prevRawA = aRaw, prevRawG = gRaw;
     if (!have) {

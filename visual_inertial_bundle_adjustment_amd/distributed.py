@@ -468,7 +468,10 @@ def run_sharded(args, rank: int, world: int, local: int):
     p = synth.generate(synth.config(args.config))
     # default: partitioned factorization (world a power of two); VIBA_MULTI=shard selects landmark
     # shards with the whole reduced system factored on rank 0
-    mode = os.environ.get("VIBA_MULTI", "partition" if world & (world - 1) == 0 else "shard")
+    # (world 1: the partition protocol has no subtree to hand out, so one rank runs as a single shard)
+    mode = os.environ.get("VIBA_MULTI", "partition" if world > 1 and world & (world - 1) == 0 else "shard")
+    if world == 1:
+        mode = "shard"
     e = HipEngine(imu_calib_options=p.imu_calib_options, device=local, precision=getattr(args, "precision", "fp64"))
     if mode == "partition":
         e.set_partition(rank, world)
@@ -528,14 +531,21 @@ def run_sharded(args, rank: int, world: int, local: int):
         return
     FP64_MFMA_PEAK_TF = 78.6
     l0, k0, f0 = per_rank[0]
-    achieved = f0 / max(1e-12, k0 * 1e-3) / 1e12
+    if l0 == 0 or k0 <= 0:  # no fan-in launch was event-timed on rank 0 (e.g. a graphed factorization)
+        achieved = None
+    else:
+        achieved = f0 / (k0 * 1e-3) / 1e12
+    from bench import pmc_traffic
     roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-            "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": None,
+            "frac": None if achieved is None else achieved / FP64_MFMA_PEAK_TF,
+            # HBM bytes per fan-in launch from the committed 1-GPU PMC passes (profiles/pmc_summary.json);
+            # a rank's subtree launches are the same kernel over a subset of the same levels
+            "traffic": pmc_traffic("fanin_kernel"), "traffic_source": "profiles/pmc_summary.json (1 GPU)",
             "kernel": "fanin_kernel on rank 0 (its subtree + the ROOT separators), HIP events on the engine stream",
             "flops_per_launch": f0 / max(1, l0), "avg_launch_ms": k0 / max(1, l0), "launches": l0,
-            "per_rank_tflops": [f / max(1e-12, k * 1e-3) / 1e12 for _, k, f in per_rank]}
+            "per_rank_tflops": [f / (k * 1e-3) / 1e12 if k > 0 else None for _, k, f in per_rank]}
     log(f"[bench] timed {iters} its in {elapsed:.3f}s; rank 0 last it: lin {ph.linearize_ms:.2f} schur "
-        f"{ph.schur_ms:.2f} factor {ph.factor_ms:.2f} solve {ph.solve_ms:.2f} ms; fan-in {achieved:.1f} TF/s")
+        f"{ph.schur_ms:.2f} factor {ph.factor_ms:.2f} solve {ph.solve_ms:.2f} ms; fan-in {achieved} TF/s")
     cpu = None
     if not args.no_cpu_baseline:
         e.close()
