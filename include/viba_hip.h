@@ -236,6 +236,21 @@ int vb_set_rs_rigs(vb_handle h, int32_t n_tables, const int64_t* midpoint_us, co
  * every iteration, as ark_vi_ba's preStepCallback.  VB_E_RANGE when the IMU data does not cover an
  * interval (the reference throws in enumIntegrationSteps, PreIntegration.cpp:16-61). */
 int vb_update_rs_tables(vb_handle h);
+/* SingleSessionProblem::T_bodyImu_world_atImageRow (viba/problem/VisualFactor.cpp:303-327) for a batch of
+ * observations, as SingleSessionAdapter::initPointsFromObservations needs it before the problem exists
+ * (Triangulation.cpp:122-123,184-185 with kModelRollingShutter, after updateRollingShutterData,
+ * SingleSessionAdapter.cpp:59,64).  Stateless (no handle): the tables of n_rs rigs are built on the device
+ * from the IMU-0 stream (RollingShutterData::compute with table t's IMU calibration model rs_calib32[32 t..]
+ * and gravity4), then observation i (rig obs_rig[i], camera record obs_cam[i] of cams24, image row
+ * obs_row[i]) gets T_midImu_imuAtT^-1 T_bodyImu_world of its rig (rig_pose7, rig_vel3, table rig_rs[r] or
+ * -1) when its camera is rolling-shutter or time-offset, else the rig pose; out_pose7: 7 doubles each.
+ * VB_E_RANGE: IMU data not covering a table, or a row time outside it (the reference throws);
+ * VB_E_ARG: a rolling-shutter camera on a rig without a table (findOrDie). */
+int vb_rs_row_poses(int64_t n_imu, const int64_t* imu_t_ns, const double* imu_gyro, const double* imu_accel,
+                    int32_t n_rs, const int64_t* rs_mid_us, const int64_t* rs_half_us, const double* rs_calib32,
+                    const double* gravity4, int64_t n_rigs, const double* rig_pose7, const double* rig_vel3,
+                    const int32_t* rig_rs, int64_t n_cams, const double* cams24, int64_t n_obs,
+                    const int32_t* obs_rig, const int32_t* obs_cam, const double* obs_row, double* out_pose7);
 /* download table t: sample count, samples (11 doubles each, NULL to skip) and interpolants (9 each) */
 int vb_get_rs_table(vb_handle h, int32_t t, int32_t* n_samples, double* samples, double* interp);
 /* --recompute-preint (viba/single_session/InertialFactors.cpp:19-70,

@@ -35,6 +35,7 @@
 #include <unordered_map>
 #include "ref_factors.hpp"
 #include "ref_preint.hpp"
+#include "ref_triang.hpp"
 
 using namespace refcpu;
 
@@ -2918,6 +2919,69 @@ int ref_preint_cov_kat(int q, int nSamples, double* out9, int64_t* added) {
   } catch (const std::exception& e) {
     g_err = e.what();
     return -5;
+  }
+  return 0;
+}
+}  // extern "C"
+
+// ================================================================== session set-up: triangulation
+// The oracle forms of vb_rs_row_poses (include/viba_hip.h; T_bodyImu_world_atImageRow over tables from
+// RollingShutterData::compute) and of libviba_host's vbh_triangulate (initPointsFromObservations ->
+// triangulatePoint), same arguments; ref_triang.hpp cites the reference lines.
+extern "C" {
+int ref_rs_row_poses(int64_t n_imu, const int64_t* imu_t_ns, const double* imu_gyro, const double* imu_accel,
+                     int32_t n_rs, const int64_t* rs_mid_us, const int64_t* rs_half_us, const double* rs_calib32,
+                     const double* gravity4, int64_t n_rigs, const double* rig_pose7, const double* rig_vel3,
+                     const int32_t* rig_rs, int64_t n_cams, const double* cams24, int64_t n_obs, const int32_t* obs_rig,
+                     const int32_t* obs_cam, const double* obs_row, double* out_pose7) {
+  try {
+    std::vector<ImuMeas> meas((size_t)n_imu);
+    for (int64_t i = 0; i < n_imu; i++)
+      meas[i] = {imu_t_ns[i], v3(imu_gyro[3 * i], imu_gyro[3 * i + 1], imu_gyro[3 * i + 2]),
+                 v3(imu_accel[3 * i], imu_accel[3 * i + 1], imu_accel[3 * i + 2])};
+    std::vector<RSTable> rs((size_t)n_rs);
+    for (int32_t t = 0; t < n_rs; t++) {
+      ImuModel m;
+      std::copy(rs_calib32 + 32 * (int64_t)t, rs_calib32 + 32 * (int64_t)t + 32, m.d);
+      rs_compute(rs[t], meas, m, rs_mid_us[t], rs_half_us[t], v3(gravity4[0], gravity4[1], gravity4[2]));
+    }
+    for (int64_t i = 0; i < n_obs; i++) {
+      const int32_t r = obs_rig[i];
+      if (r < 0 || r >= n_rigs || obs_cam[i] < 0 || obs_cam[i] >= n_cams) return (g_err = "bad observation", -1);
+      const SE3 Tbw = SE3::fromData(rig_pose7 + 7 * (int64_t)r);
+      const double* vw = rig_vel3 + 3 * (int64_t)r;
+      const CamModel cam = CamModel::fromData(cams24 + 24 * (int64_t)obs_cam[i]);
+      const RSTable* tab = rig_rs[r] >= 0 ? &rs[rig_rs[r]] : nullptr;
+      if ((cam.isRollingShutter() || cam.hasTimeOffset()) && !tab) return (g_err = "rig without rolling-shutter data", -1);
+      ref_triang::bodyImuWorldAtImageRow(Tbw, v3(vw[0], vw[1], vw[2]), cam, tab, obs_row[i]).toData(out_pose7 + 7 * i);
+    }
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -5;
+  }
+  return 0;
+}
+
+int ref_triangulate(int64_t nPts, const int64_t* start, const int32_t* seed, const double* Tcw, const int32_t* camIdx,
+                    const double* cams, const double* uv, const double* sqrtH, double* point, uint8_t* ok,
+                    uint8_t* inlier) {
+  for (int64_t p = 0; p < nPts; p++) {
+    const int64_t b = start[p], e = start[p + 1];
+    std::vector<ref_triang::TObs> obs;
+    for (int64_t i = b; i < e; i++) {
+      ref_triang::TObs o;
+      o.T_cam_world = SE3::fromData(Tcw + 7 * i);
+      o.cam = CamModel::fromData(cams + 24 * (int64_t)camIdx[i]);
+      o.uv[0] = uv[2 * i], o.uv[1] = uv[2 * i + 1];
+      for (int k = 0; k < 4; k++) o.sqrtH[k] = sqrtH[4 * i + k];
+      obs.push_back(o);
+    }
+    V3 pt = v3(0, 0, 0);
+    std::vector<uint8_t> inl;
+    const bool good = ref_triang::triangulate(obs, seed[p], pt, inl);
+    ok[p] = good ? 1 : 0;
+    for (int k = 0; k < 3; k++) point[3 * p + k] = good ? pt[k] : 0.0;
+    for (int64_t i = b; i < e; i++) inlier[i] = good ? inl[i - b] : 0;
   }
   return 0;
 }

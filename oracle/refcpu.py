@@ -23,7 +23,8 @@ P = C.c_void_p
 
 def build_oracle(force: bool = False) -> str:
     """Compile the oracle (g++, no external deps) into oracle/_ref/."""
-    src = [os.path.join(HERE, f) for f in ("refcpu.cpp", "ref_factors.hpp", "ref_math.hpp", "ref_preint.hpp")]
+    src = [os.path.join(HERE, f) for f in ("refcpu.cpp", "ref_factors.hpp", "ref_math.hpp", "ref_preint.hpp",
+                                                "ref_triang.hpp")]
     if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(s)
                                                    for s in src):
         return LIB
@@ -238,3 +239,28 @@ def preint_cov_kat(q: int, n_samples: int = 250_000):
     if lib.ref_preint_cov_kat(q, n_samples, out, C.byref(n)):
         raise _err(lib)
     return np.array(out[:]), n.value
+
+
+def rs_row_poses(*args):
+    """The oracle's T_bodyImu_world_atImageRow over its own RollingShutterData::compute tables
+    (ref_rs_row_poses; same arguments as engine.rs_row_poses)."""
+    from visual_inertial_bundle_adjustment_amd.engine import rs_row_poses as call
+    return call(*args, lib=load(), name="ref_rs_row_poses")
+
+
+def triangulate(start, seeds, Tcw, camvar, cams, uv, sqrt_h):
+    """The oracle's triangulatePoint over every track (ref_triangulate; arguments of libviba_host's
+    vbh_triangulate).  Returns (points (n, 3), ok (n,), inlier flags per observation)."""
+    lib = load()
+    start, seeds = np.ascontiguousarray(start, np.int64), np.ascontiguousarray(seeds, np.int32)
+    Tcw, cams = np.ascontiguousarray(Tcw, np.float64), np.ascontiguousarray(cams, np.float64)
+    camvar = np.ascontiguousarray(camvar, np.int32)
+    uv, sqrt_h = np.ascontiguousarray(uv, np.float64), np.ascontiguousarray(sqrt_h, np.float64)
+    n = len(start) - 1
+    pts, ok, inl = np.zeros((n, 3)), np.zeros(n, np.uint8), np.zeros(int(start[-1]), np.uint8)
+    f = lib.ref_triangulate
+    f.argtypes = [C.c_int64] + [P] * 10
+    f.restype = C.c_int
+    ptr = lambda a: a.ctypes.data_as(P)
+    f(n, ptr(start), ptr(seeds), ptr(Tcw), ptr(camvar), ptr(cams), ptr(uv), ptr(sqrt_h), ptr(pts), ptr(ok), ptr(inl))
+    return pts, ok, inl

@@ -3,7 +3,11 @@ emitted by the synthetic generator (visual_inertial_bundle_adjustment_amd.synth.
 session_small.npz: the oracle's one LM step and 8-iteration optimize on the problem the session
 adapter builds from that folder (the stored reference of tests/test_session.py).
 
-    python tests/golden/make_session.py
+    python tests/golden/make_session.py            (folder + npz)
+    python tests/golden/make_session.py --npz-only (npz from the committed folder)
+
+The adapter triangulates with the oracle's image-row poses (oracle.refcpu.rs_row_poses), so the stored
+step needs no GPU.
 
 The folder is data only: 55 rigs at 10 Hz (two 5 s calibration windows), 200 landmarks, an Aria-like rig
 (rolling-shutter RGB + two global-shutter SLAM cameras, two IMUs), IMU samples at 10 significant digits.
@@ -31,11 +35,13 @@ CONFIG = dict(n_kf=55, n_lm=200)
 
 
 def main():
-    p = synth.generate(synth.config("miniB", **CONFIG))
-    if os.path.exists(FOLDER):
-        shutil.rmtree(FOLDER)
-    synth.write_session(p, FOLDER, imu_digits=10)
-    q = adapter.build_problem(session.SessionData.load(FOLDER))
+    from oracle.refcpu import rs_row_poses
+    if "--npz-only" not in sys.argv:
+        p = synth.generate(synth.config("miniB", **CONFIG))
+        if os.path.exists(FOLDER):
+            shutil.rmtree(FOLDER)
+        synth.write_session(p, FOLDER, imu_digits=10)
+    q = adapter.build_problem(session.SessionData.load(FOLDER), row_poses=rs_row_poses)
     e = adapter.load_into(RefEngine(reproj_loss=q.reproj_loss, imu_loss=q.imu_loss,
                                     imu_calib_options=q.imu_calib_options), q)
     o = one_step(e)

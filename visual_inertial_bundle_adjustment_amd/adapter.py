@@ -186,8 +186,11 @@ def compensated_gyro_at_end(stream, model, t0_us: int, t1_us: int) -> np.ndarray
 
 
 class SessionAdapter:
-    def __init__(self, sd: SessionData, matcher: Matcher, settings: InitSettings | None = None):
+    def __init__(self, sd: SessionData, matcher: Matcher, settings: InitSettings | None = None, row_poses=None):
         self.sd, self.m, self.s = sd, matcher, settings or InitSettings()
+        # T_bodyImu_world_atImageRow provider for the triangulation: the device (engine.rs_row_poses,
+        # vb_rs_row_poses) unless a caller passes another implementation with the same arguments
+        self.row_poses = row_poses
         self.n_cam = len(sd.slam_camera_serials)
         self.n_imu = len(sd.slam_imu_labels)
 
@@ -309,8 +312,13 @@ class SessionAdapter:
         rig = m.obs_to_rig[flat] - r0 if len(flat) else np.zeros(0, np.int64)
         cam = obs.camera_index[flat].astype(np.int64) if len(flat) else np.zeros(0, np.int64)
         camvar = np.array([p.cam_var(int(r), int(c)) for r, c in zip(rig, cam)], np.int32)
-        Tcw = np.array([se3_mul(p.vars[5][cv], p.vars[1][r]) for cv, r in zip(camvar, rig)]).reshape(-1, 7)
         uv = np.ascontiguousarray(obs.uv[flat]).reshape(-1, 2)
+        # kModelRollingShutter (Triangulation.h:43): rays and refinements use the rig pose at the
+        # observation's image row, T_bodyImu_world_atImageRow (Triangulation.cpp:122-123,184-185), from
+        # the rolling-shutter tables updateRollingShutterData builds first (SingleSessionAdapter.cpp:59,64)
+        self.row_pose_inputs = (rig, camvar, uv[:, 1].copy())
+        Tbw_row = self._row_poses(p, rig, camvar, uv[:, 1])
+        Tcw = np.array([se3_mul(p.vars[5][cv], Tbw_row[i]) for i, cv in enumerate(camvar)]).reshape(-1, 7)
         sh = np.ascontiguousarray(obs.sqrt_h[flat]).reshape(-1, 4)
         cams = np.ascontiguousarray(p.vars[4])
         pts = np.zeros((len(tracks), 3))
@@ -319,8 +327,12 @@ class SessionAdapter:
         seeds = np.array(seeds, np.int32)
         lib = load_host_lib()
         ptr = lambda a: a.ctypes.data_as(C.c_void_p)
-        lib.vbh_triangulate(len(tracks), ptr(start), ptr(seeds), ptr(np.ascontiguousarray(Tcw)), ptr(camvar), ptr(cams),
+        Tcw = np.ascontiguousarray(Tcw)
+        lib.vbh_triangulate(len(tracks), ptr(start), ptr(seeds), ptr(Tcw), ptr(camvar), ptr(cams),
                             ptr(uv), ptr(sh), ptr(pts), ptr(ok), ptr(inl))
+        # kept for the parity tests (tests/test_session.py against the oracle's triangulatePoint)
+        self.triangulation = {"inputs": (start, seeds, Tcw, camvar, cams, uv, sh), "points": pts, "ok": ok,
+                              "inliers": inl}
         keep = np.flatnonzero(ok)
         p.triangulated = len(keep)
         p.point_ids = np.array(pids, np.int64)[keep]
@@ -339,6 +351,22 @@ class SessionAdapter:
                 fi.append(int(self.rs_table[r]) if rs else -1)
                 fc.append((uv[j, 0], uv[j, 1], *sh[j]))
         self.visual = (np.array(fv, np.int32).reshape(-1, 5), np.array(fi, np.int32), np.array(fc).reshape(-1, 6))
+
+    def _row_pose_args(self, p: SessionProblem, rig, camvar, row) -> tuple:
+        """arguments of engine.rs_row_poses: the IMU-0 stream, the rigs' rolling-shutter intervals with
+        their IMU calibration models and gravity, the rigs, the cameras, the observations"""
+        has_rs = p.rs_mid is not None and len(p.rs_mid) > 0
+        e64, e3 = np.zeros(0, np.int64), np.zeros((0, 3))
+        return (p.imu_t if has_rs else e64, p.imu_gyro if has_rs else e3, p.imu_accel if has_rs else e3,
+                p.rs_mid if has_rs else e64, p.rs_half if has_rs else e64,
+                p.vars[6][p.rs_calib] if has_rs else np.zeros((0, 32)), p.vars[8][0], p.vars[1], p.vars[2],
+                self.rs_table, p.vars[4], rig, camvar, row)
+
+    def _row_poses(self, p: SessionProblem, rig, camvar, row) -> np.ndarray:
+        fn = self.row_poses
+        if fn is None:
+            from .engine import rs_row_poses as fn
+        return fn(*self._row_pose_args(p, rig, camvar, row))
 
     # ------------------------------------------------------------------ inertial factors + omega priors
     def _inertial(self, p: SessionProblem):
@@ -545,9 +573,11 @@ class SessionAdapter:
         return p
 
 
-def build_problem(sd: SessionData, matcher: Matcher | None = None, settings: InitSettings | None = None) -> SessionProblem:
-    """SessionData -> SessionProblem (ark_vi_ba main_AriaKit_ViBa.cpp:49-63)."""
-    return SessionAdapter(sd, matcher or Matcher.build(sd), settings).problem()
+def build_problem(sd: SessionData, matcher: Matcher | None = None, settings: InitSettings | None = None,
+                  row_poses=None) -> SessionProblem:
+    """SessionData -> SessionProblem (ark_vi_ba main_AriaKit_ViBa.cpp:49-63).  row_poses: the
+    T_bodyImu_world_atImageRow provider of the triangulation (default: the device, vb_rs_row_poses)."""
+    return SessionAdapter(sd, matcher or Matcher.build(sd), settings, row_poses).problem()
 
 
 def load_into(engine, p: SessionProblem, finalize: bool = True, recompute_preint: bool | None = None):

@@ -28,6 +28,9 @@ void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st, int part = 3);
 void launch_rs_build(const Dev& d, hipStream_t st);
+void launch_rs_row_poses(const Dev& d, int64_t n, const int32_t* obsRig, const int32_t* obsCam, const double* obsRow,
+                         const double* rigPose, const double* rigVel, const int32_t* rigRS, const double* cams,
+                         double* out, hipStream_t st);
 void launch_preint(const Dev& d, const PreintArgs& pa, hipStream_t st);
 void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gObs, const int32_t* gPt, int64_t nG,
                           double* backups, double* acc, hipStream_t st);
@@ -2939,6 +2942,92 @@ int vb_share_x(vb_handle h, double** xred, int64_t* len) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- rolling-shutter row poses (session set-up)
+// SingleSessionAdapter::initPointsFromObservations triangulates with T_bodyImu_world_atImageRow
+// (Triangulation.cpp:122-123,184-185, kModelRollingShutter = true, Triangulation.h:43) after
+// updateRollingShutterData (SingleSessionAdapter.cpp:59,64).  Stateless: builds the tables of the given
+// rigs on the device (rs_build_kernel, the per-iteration rebuild's kernel) and evaluates every
+// observation's row pose (rs_row_pose_kernel), then frees everything.  Errors as the reference's
+// throws / aborts: VB_E_RANGE (IMU data do not cover a table, or a row time outside its table),
+// VB_E_ARG (a rolling-shutter camera on a rig without a table).
+extern "C" int vb_rs_row_poses(int64_t n_imu, const int64_t* imu_t_ns, const double* imu_gyro, const double* imu_accel,
+                               int32_t n_rs, const int64_t* rs_mid_us, const int64_t* rs_half_us, const double* rs_calib32,
+                               const double* gravity4, int64_t n_rigs, const double* rig_pose7, const double* rig_vel3,
+                               const int32_t* rig_rs, int64_t n_cams, const double* cams24, int64_t n_obs,
+                               const int32_t* obs_rig, const int32_t* obs_cam, const double* obs_row, double* out_pose7) {
+  if (n_imu < 0 || n_rs < 0 || n_rigs < 0 || n_cams < 0 || n_obs < 0 || (n_obs && (!obs_rig || !obs_cam || !obs_row ||
+      !out_pose7 || !rig_pose7 || !rig_vel3 || !rig_rs || !cams24)) || (n_rs && (!imu_t_ns || !imu_gyro || !imu_accel ||
+      !rs_mid_us || !rs_half_us || !rs_calib32 || !gravity4)))
+    return fail(VB_E_ARG, "bad vb_rs_row_poses arguments");
+  for (int64_t i = 0; i < n_obs; i++)
+    if (obs_rig[i] < 0 || obs_rig[i] >= n_rigs || obs_cam[i] < 0 || obs_cam[i] >= n_cams)
+      return fail(VB_E_ARG, "vb_rs_row_poses: observation with an unknown rig or camera");
+  for (int64_t r = 0; r < n_rigs; r++)
+    if (rig_rs[r] >= n_rs) return fail(VB_E_ARG, "vb_rs_row_poses: unknown rolling-shutter table");
+  for (int64_t i = 1; i < n_imu; i++)
+    if (imu_t_ns[i] <= imu_t_ns[i - 1]) return fail(VB_E_ARG, "IMU timestamps must increase");
+  if (n_obs == 0) return 0;
+  std::vector<void*> mem;
+  auto freeAll = [&] { for (void* p : mem) (void)hipFree(p); };
+  auto up = [&](auto** dst, const auto* src, size_t n) -> bool {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(*src)) != hipSuccess) return false;
+    mem.push_back(p);
+    *dst = (std::remove_cv_t<std::remove_reference_t<decltype(**dst)>>*)p;
+    return n == 0 || hipMemcpy(p, src, n * sizeof(*src), hipMemcpyHostToDevice) == hipSuccess;
+  };
+  auto zero = [&](auto** dst, size_t n) -> bool {
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(**dst)) != hipSuccess) return false;
+    mem.push_back(p);
+    *dst = (std::remove_reference_t<decltype(*dst)>)p;
+    return hipMemset(p, 0, std::max<size_t>(n, 1) * sizeof(**dst)) == hipSuccess;
+  };
+  Dev d{};
+  // tables: capacity as vb_finalize sizes them (the samples of [mid - half, mid + half] +- 20 ms, + 4)
+  std::vector<int64_t> off(n_rs + 1, 0);
+  std::vector<double> v((size_t)n_imu * 6);
+  for (int64_t i = 0; i < n_imu; i++)
+    for (int k = 0; k < 3; k++) v[6 * i + k] = imu_gyro[3 * i + k], v[6 * i + 3 + k] = imu_accel[3 * i + k];
+  for (int32_t t = 0; t < n_rs; t++) {
+    const int64_t kWidenNs = 20000000;
+    const int64_t a = (rs_mid_us[t] - rs_half_us[t]) * 1000 - kWidenNs, b = (rs_mid_us[t] + rs_half_us[t]) * 1000 + kWidenNs;
+    off[t + 1] = off[t] + (std::upper_bound(imu_t_ns, imu_t_ns + n_imu, b) - std::lower_bound(imu_t_ns, imu_t_ns + n_imu, a)) + 4;
+  }
+  std::vector<int32_t> calibIdx(n_rs);
+  std::iota(calibIdx.begin(), calibIdx.end(), 0);
+  int32_t *oRig = nullptr, *oCam = nullptr, *rRS = nullptr;
+  double *oRow = nullptr, *rPose = nullptr, *rVel = nullptr, *cams = nullptr, *out = nullptr;
+  bool ok = zero(&d.err, 4) && up(&oRig, obs_rig, n_obs) && up(&oCam, obs_cam, n_obs) && up(&oRow, obs_row, n_obs) &&
+            up(&rPose, rig_pose7, n_rigs * 7) && up(&rVel, rig_vel3, n_rigs * 3) && up(&rRS, rig_rs, n_rigs) &&
+            up(&cams, cams24, n_cams * 24) && zero(&out, n_obs * 7);
+  if (ok && n_rs) {
+    d.nRS = n_rs, d.nImu = n_imu, d.rsGravVar = 0;
+    ok = up(&d.imuT, imu_t_ns, n_imu) && up(&d.imuV, v.data(), v.size()) && up(&d.rsMid, rs_mid_us, n_rs) &&
+         up(&d.rsHalf, rs_half_us, n_rs) && up(&d.rsCalib, calibIdx.data(), n_rs) &&
+         up(&d.var[6], rs_calib32, (size_t)n_rs * 32) && up(&d.var[8], gravity4, 4) && up(&d.rsOff, off.data(), off.size()) &&
+         zero(&d.rsS, off[n_rs] * 11) && zero(&d.rsI, (off[n_rs] - n_rs) * 9) && zero(&d.rsG, (size_t)n_rs * 3) &&
+         zero(&d.rsN, n_rs);
+  }
+  if (!ok) {
+    freeAll();
+    return fail(VB_E_HIP, "vb_rs_row_poses: device allocation / copy failed");
+  }
+  if (n_rs) launch_rs_build(d, nullptr);
+  launch_rs_row_poses(d, n_obs, oRig, oCam, oRow, rPose, rVel, rRS, cams, out, nullptr);
+  int32_t e[2] = {0, 0};
+  const bool okRun = hipDeviceSynchronize() == hipSuccess && hipMemcpy(e, d.err, sizeof(e), hipMemcpyDeviceToHost) == hipSuccess &&
+                     hipMemcpy(out_pose7, out, (size_t)n_obs * 7 * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+  freeAll();
+  if (!okRun) return fail(VB_E_HIP, "vb_rs_row_poses: kernel failed");
+  if (e[1] & 1) return fail(VB_E_RANGE, "enumIntegrationSteps: IMU measurements do not cover a rolling-shutter interval");
+  if (e[1] & 2) return fail(VB_E_NUMERIC, "RollingShutterData::compute: non-increasing sample times");
+  if (e[1] & 4) return fail(VB_E_STATE, "internal: rolling-shutter table capacity exceeded");
+  if (e[0] & 2) return fail(VB_E_ARG, "T_bodyImu_world_atImageRow: rolling-shutter camera on a rig without a table");
+  if (e[0] & 1) return fail(VB_E_RANGE, "RollingShutterData::getEstimate: image-row time outside the table");
+  return 0;
+}
 
 // ---------------------------------------------------------------- kernel micro-benchmark (tuning aid)
 // Times one launch of a factorization kernel on scratch tiles (random SPD diagonal tile, random

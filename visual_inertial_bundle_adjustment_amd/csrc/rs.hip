@@ -152,7 +152,53 @@ __global__ void __launch_bounds__(64) rs_build_kernel(Dev d) {
   d.rsN[t] = cnt;
 }
 
+// SingleSessionProblem::T_bodyImu_world_atImageRow (viba/problem/VisualFactor.cpp:303-327), one lane per
+// observation: a rolling-shutter or time-offset camera looks the rig's table up at the row's time
+// (getEstimate without velocities) and returns T_midImu_imuAtT^-1 T_bodyImu_world, any other camera the
+// rig pose.  Inputs per observation: rig, camera record; per rig: pose (7), velocity (3), table (-1: none).
+// err bit 1: time outside the table (the reference throws), bit 2: a rolling-shutter camera on a rig
+// without a table (findOrDie aborts).
+__global__ void __launch_bounds__(256) rs_row_pose_kernel(Dev d, int64_t n, const int32_t* obsRig, const int32_t* obsCam,
+                                                          const double* obsRow, const double* rigPose,
+                                                          const double* rigVel, const int32_t* rigRS,
+                                                          const double* cams, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int32_t r = obsRig[i];
+  const double* cam = cams + (int64_t)obsCam[i] * 24;
+  const se3 Tbw = se3_load(rigPose + (int64_t)r * 7);
+  se3 T = Tbw;
+  // isRollingShutter() || hasTimeOffset() of the camera record (include/viba_hip.h VB_CAM_DATA)
+  if (cam[4] != 0.0 || cam[6] != 0.0 || cam[7] != 0.0 || cam[8] != 0.0) {
+    const int t = rigRS[r];
+    if (t < 0) {
+      atomicOr(d.err, 2);
+    } else {
+      const double tpf = obsRow[i] / cam[3] - 0.5;
+      const double ro = cam[4] != 0.0 ? cam[5] : 0.0;
+      const double dt = ro * tpf - cam[6];
+      const int64_t s0 = d.rsOff[t];
+      const double* vp = rigVel + (int64_t)r * 3;
+      bool oor = false;
+      const se3 TmidAtT = rs_estimate(d.rsS + s0 * 11, d.rsI + (s0 - t) * 9, d.rsN[t], d.rsG + 3 * t, dt,
+                                      mk(vp[0], vp[1], vp[2]), qinv(se3_inv(Tbw).R), &oor);
+      if (oor) atomicOr(d.err, 1);
+      else T = se3_mul(se3_inv(TmidAtT), Tbw);
+    }
+  }
+  double* o = out + i * 7;
+  o[0] = T.R.x, o[1] = T.R.y, o[2] = T.R.z, o[3] = T.R.w, o[4] = T.t.x, o[5] = T.t.y, o[6] = T.t.z;
+}
+
 }  // namespace
+
+void launch_rs_row_poses(const Dev& d, int64_t n, const int32_t* obsRig, const int32_t* obsCam, const double* obsRow,
+                         const double* rigPose, const double* rigVel, const int32_t* rigRS, const double* cams,
+                         double* out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(rs_row_pose_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, n, obsRig, obsCam,
+                     obsRow, rigPose, rigVel, rigRS, cams, out);
+}
 
 void launch_rs_build(const Dev& d, hipStream_t st) {
   if (d.nRS <= 0 || !d.rsMid) return;

@@ -525,6 +525,250 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
   }
 }
 
+// The same assembly with the K-row bookkeeping taken out of the k-loop (schur_run3_kernel, default):
+// before a task, the wave writes one (I-side, J-side) element offset per K row into an LDS table --
+// row kr = 3 e + q of the task's landmarks -> q * nYcol + the entry's first panel column in tile I / J
+// (+ 16 a0 on the J side), rows past the task's landmarks -> the zero pad behind the panels.  A k-step
+// is then one broadcast ds_read_b64 of its row's offsets, two 64-bit address adds and the NR + NBI
+// gathers at immediate offsets, one step ahead of the MFMAs (schur_run2's per-step landmark / plane
+// advance, bounds select and plane-base select were ~20 VALU + 17 SALU per MFMA: DESIGN.md §8).
+#ifndef VIBA_SCHUR_ASMLD
+#define VIBA_SCHUR_ASMLD 1
+#endif
+// one gather of an 8-B (fp64) / 4-B (fp32) operand at an immediate byte offset I * STRIDE, as inline asm
+// (invisible to hipcc's waitcnt pass: the caller waits with vm_wait and pins the destination)
+template <int STRIDE>
+__device__ __forceinline__ void gather_asm(double& dst, const double* p, int i) {
+  switch (i) {
+    case 0: asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
+    case 1: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
+    case 2: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
+    default: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
+  }
+}
+template <int STRIDE>
+__device__ __forceinline__ void gather_asm(float& dst, const float* p, int i) {
+  switch (i) {
+    case 0: asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
+    case 1: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
+    case 2: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
+    default: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
+  }
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NBI, int NR, int DA0>
+__device__ __forceinline__ void schur_task3(const Dev& d, const uint2* rowOff, int nks, int a0r, int l4, int l15,
+                                            const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
+  // DA0 >= 0: diagonal tile, block row a0 = DA0 known at compile time, so the lower-triangle test of
+  // each block is static (a runtime a0 put a scalar branch in front of every MFMA)
+  constexpr bool DIAG = DA0 >= 0;
+  const int a0 = DIAG ? DA0 : a0r;
+  hacc4_t acc[NR][NBI];
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int b = 0; b < NBI; b++) acc[i][b] = hacc4_t{0, 0, 0, 0};
+  const rec_t* Y = d.Y + l15;
+#if VIBA_SCHUR_ASMLD
+  // the gathers as inline-asm loads, counted by hand: hipcc's own waitcnt pass cannot follow the two
+  // register sets around the loop's back edge and waited for the step just issued (vmcnt(0) before the
+  // current step's MFMAs), which left every gather's latency exposed.  Each set is pinned after its
+  // wait ("+v"), so nothing reads it early (cdna_hip_programming.md §5.7 item 1, form ii).
+  constexpr int kN = NR + NBI;
+  auto ld = [&](int ks, rec_t (&av)[NR], rec_t (&bv)[NBI]) {
+    const uint2 o = rowOff[4 * ks + l4];
+    const rec_t* pJ = Y + o.y;
+    const rec_t* pI = Y + o.x;
+#pragma unroll
+    for (int i = 0; i < NR; i++) gather_asm<16 * sizeof(rec_t)>(av[i], pJ, i);
+#pragma unroll
+    for (int b = 0; b < NBI; b++) gather_asm<16 * sizeof(rec_t)>(bv[b], pI, b);
+  };
+  auto pin = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
+#pragma unroll
+    for (int i = 0; i < NR; i++) asm volatile("" : "+v"(av[i]));
+#pragma unroll
+    for (int b = 0; b < NBI; b++) asm volatile("" : "+v"(bv[b]));
+  };
+#else
+  constexpr int kN = 0;
+  auto ld = [&](int ks, rec_t (&av)[NR], rec_t (&bv)[NBI]) {
+    const uint2 o = rowOff[4 * ks + l4];
+    const rec_t* pJ = Y + o.y;
+    const rec_t* pI = Y + o.x;
+#pragma unroll
+    for (int i = 0; i < NR; i++) av[i] = pJ[16 * i];
+#pragma unroll
+    for (int b = 0; b < NBI; b++) bv[b] = pI[16 * b];
+  };
+  auto pin = [&](rec_t (&)[NR], rec_t (&)[NBI]) {};
+#endif
+  auto mm = [&](const rec_t (&av)[NR], const rec_t (&bv)[NBI]) {
+#pragma unroll
+    for (int i = 0; i < NR; i++)
+#pragma unroll
+      for (int b = 0; b < NBI; b++)
+        if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
+  };
+  rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
+  ld(0, a0v, b0v);
+  for (int ks = 0; ks < nks; ks += 2) {
+    if (ks + 1 < nks) {
+      ld(ks + 1, a1v, b1v);
+      vm_wait<kN>();  // step ks's set landed (step ks + 1's stays in flight)
+    } else {
+      vm_wait<0>();
+    }
+    pin(a0v, b0v);
+    mm(a0v, b0v);
+    if (ks + 1 < nks) {
+      if (ks + 2 < nks) {
+        ld(ks + 2, a0v, b0v);
+        vm_wait<kN>();
+      } else {
+        vm_wait<0>();
+      }
+      pin(a1v, b1v);
+      mm(a1v, b1v);
+    }
+  }
+  int colT[NBI];
+#pragma unroll
+  for (int b = 0; b < NBI; b++) {
+    const int n = 16 * b + l15;
+    colT[b] = n < nI ? posI[n] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q;
+      if (m >= nJ) continue;
+      double* Cr = C + posJ[m] * TS;
+#pragma unroll
+      for (int b = 0; b < NBI; b++)
+        if ((!DIAG || a0 + i <= b) && colT[b] >= 0) atomicAdd(Cr + colT[b], -(double)acc[i][b][q]);
+    }
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run3_kernel(Dev d, double lambda) {
+  __shared__ double C[TS * TS];
+  __shared__ uint32_t ecol[256][2];
+  __shared__ int16_t runStart[258];
+  __shared__ uint8_t posW[4][2][TS];
+  __shared__ uint2 rowTab[4][4 * ((3 * kCh + 3) / 4)];
+  __shared__ double rq[TS];
+  __shared__ int nRunsS;
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
+  const TileWork wk = d.tileWorks[w];
+  const bool diag = wk.I == wk.J;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int cnt = wk.count;
+  const TileEnt* ents = d.tileEnts + wk.start;
+  if (tid < cnt) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
+  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
+  if (tid < TS) rq[tid] = 0.0;
+  __syncthreads();
+  if (wave == 0) {
+    int n = 0;
+    for (int e0 = 0; e0 < cnt; e0 += 64) {
+      const int e = e0 + lane;
+      const bool st = e < cnt && (e == 0 || ents[e].maskI != ents[e - 1].maskI || ents[e].maskJ != ents[e - 1].maskJ);
+      const uint64_t b = __ballot(st);
+      if (st) runStart[n + __popcll(b & ((1ull << lane) - 1))] = (int16_t)e;
+      n += __popcll(b);
+    }
+    if (lane == 0) runStart[n] = (int16_t)cnt, nRunsS = n;
+  }
+  __syncthreads();
+  const int nRuns = nRunsS;
+  uint8_t* posI = posW[wave][0];
+  uint8_t* posJ = posW[wave][1];
+  uint2* rt = rowTab[wave];
+  const uint32_t pq = (uint32_t)d.nYcol, zeroOff = 3u * (uint32_t)d.nYcol;  // the 128 zeros behind the planes
+  int task = 0;
+  for (int r = 0; r < nRuns; r++) {
+    const int e0 = runStart[r], e1 = runStart[r + 1];
+    const uint64_t mI = uniform64(ents[e0].maskI), mJ = diag ? mI : uniform64(ents[e0].maskJ);
+    const int nI = __popcll(mI), nJ = __popcll(mJ);
+    const int nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4, nbR = (nbJ + kTR - 1) / kTR;
+    const int nch = (e1 - e0 + kCh - 1) / kCh;
+    const int nTask = nch * nbR;
+    bool mapped = false;
+    for (int t = 0; t < nTask; t++, task++) {
+      if ((task & 3) != wave) continue;
+      if (!mapped) {
+        if ((mI >> lane) & 1) posI[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
+        if ((mJ >> lane) & 1) posJ[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
+        mapped = true;
+      }
+      const int ch = t / nbR, a0 = kTR * (t - ch * nbR);
+      const int c0 = e0 + ch * kCh, nl = min(kCh, e1 - c0), rows = 3 * nl, nks = (rows + 3) >> 2;
+      __builtin_amdgcn_wave_barrier();  // the previous task's readers of rt are done
+      if (lane < 4 * nks) {
+        uint2 o = make_uint2(zeroOff, zeroOff);
+        if (lane < rows) {
+          const int e = c0 + lane / 3, q = lane - 3 * (lane / 3);
+          const uint32_t base = (uint32_t)q * pq;
+          o = make_uint2(base + ecol[e][0], base + ecol[e][1] + 16u * (uint32_t)a0);
+        }
+        rt[lane] = o;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int nr = min(kTR, nbJ - a0);
+      static_assert(kTR == 2, "schur_run3_kernel's diagonal cases assume two block rows per task");
+      // off-diagonal: (NBI, NR); diagonal (nbI == nbJ): (NBI, a0), NR = min(2, NBI - a0)
+      const int sel = diag ? 16 + (nbI - 1) * 2 + (a0 >> 1) : ((nbI - 1) * 2 + (nr - 1));
+      switch (sel) {
+#define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
+  case (NBI - 1) * 2 + (NR - 1):                                                                      \
+    schur_task3<NBI, NR, -1>(d, rt, nks, a0, l4, l15, posI, posJ, nI, nJ, C);                         \
+    break;
+#define VIBA_SCHUR_DCASE(NBI, A0)                                                                     \
+  case 16 + (NBI - 1) * 2 + (A0 >> 1):                                                                \
+    schur_task3<NBI, (NBI - A0 < 2 ? NBI - A0 : 2), A0>(d, rt, nks, a0, l4, l15, posI, posJ, nI, nJ, C); \
+    break;
+        VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(2, 2)
+        VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 1) VIBA_SCHUR_CASE(4, 2)
+        VIBA_SCHUR_DCASE(1, 0) VIBA_SCHUR_DCASE(2, 0) VIBA_SCHUR_DCASE(3, 0) VIBA_SCHUR_DCASE(3, 2)
+        VIBA_SCHUR_DCASE(4, 0) VIBA_SCHUR_DCASE(4, 2)
+#undef VIBA_SCHUR_CASE
+#undef VIBA_SCHUR_DCASE
+        default: break;
+      }
+      if (diag && a0 == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
+        double racc = 0.0;
+        for (int e = c0; e < c0 + nl; e++) {
+          const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
+          const double* zz = d.z + 3 * (int64_t)ents[e].lm;
+          racc += (double)y[0] * zz[0] + (double)y[d.nYcol] * zz[1] + (double)y[2 * d.nYcol] * zz[2];
+        }
+        atomicAdd(&rq[posI[lane]], -racc);
+      }
+    }
+    if (mapped) __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
+  if (wk.kind) {
+    for (int i = tid; i < TS * TS; i += 256)
+      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else {
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
+  }
+  if (diag && tid < TS) {
+    const int64_t row = (int64_t)wk.I * TS + tid;
+    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
+  }
+}
+
 // Direct visual terms by observation group (observations sharing their reduced blocks: one rig, one
 // camera).  Per group: H = sum_o J~_o^T J~_o over the 32 columns [pose 6 | extr 6 | intr <= 17 |
 // vel 3] and g = sum_o J~_o^T e~_o, on v_mfma_f64_16x16x4_f64 (K = the group's residual rows, 4 per
@@ -1908,7 +2152,12 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
   if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
-  if (d.nTileWorks) launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+  // VIBA_SCHUR_V=2: the previous form with the K-row bookkeeping inside the k-loop
+  static const int v = getenv("VIBA_SCHUR_V") ? atoi(getenv("VIBA_SCHUR_V")) : 3;
+  if (d.nTileWorks) {
+    if (v == 2) launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else launchK(schur_run3_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+  }
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {

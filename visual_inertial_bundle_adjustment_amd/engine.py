@@ -77,6 +77,35 @@ def _arr(a, dtype):
     return np.ascontiguousarray(a, dtype=dtype)
 
 
+def rs_row_poses(imu_t, imu_gyro, imu_accel, rs_mid, rs_half, rs_calib, gravity, rig_pose, rig_vel, rig_rs, cams,
+                 obs_rig, obs_cam, obs_row, lib=None, name="vb_rs_row_poses"):
+    """SingleSessionProblem::T_bodyImu_world_atImageRow (viba/problem/VisualFactor.cpp:303-327) of every
+    observation (rig obs_rig[i], camera record obs_cam[i] of cams, image row obs_row[i]), with the rolling-
+    shutter tables of the rigs built from the IMU-0 stream first (vb_rs_row_poses, include/viba_hip.h; on
+    the device).  rs_calib: (n_rs, 32) IMU calibration model per table; rig_rs: table of each rig or -1.
+    Returns (n_obs, 7) poses.  `lib` / `name` select another library with the same entry (the oracle)."""
+    if lib is None:
+        from ._lib import load_hip_lib
+        lib = load_hip_lib()
+    i64, i32, f64 = (lambda a: _arr(a, np.int64)), (lambda a: _arr(a, np.int32)), (lambda a: _arr(a, np.float64))
+    it, ig, ia = i64(imu_t), f64(imu_gyro).reshape(-1, 3), f64(imu_accel).reshape(-1, 3)
+    rm, rh, rc, g = i64(rs_mid), i64(rs_half), f64(rs_calib).reshape(-1, 32), f64(gravity).reshape(4)
+    rp, rv, rr = f64(rig_pose).reshape(-1, 7), f64(rig_vel).reshape(-1, 3), i32(rig_rs)
+    cm, orr, oc, ow = f64(cams).reshape(-1, 24), i32(obs_rig), i32(obs_cam), f64(obs_row)
+    out = np.zeros((len(orr), 7))
+    f = getattr(lib, name)
+    f.restype = C.c_int
+    f.argtypes = [C.c_int64, P, P, P, C.c_int32, P, P, P, P, C.c_int64, P, P, P, C.c_int64, P, C.c_int64, P, P, P, P]
+    ptr = lambda a: a.ctypes.data_as(P)
+    rc_ = f(len(it), ptr(it), ptr(ig), ptr(ia), len(rm), ptr(rm), ptr(rh), ptr(rc), ptr(g), len(rp), ptr(rp), ptr(rv),
+            ptr(rr), len(cm), ptr(cm), len(orr), ptr(orr), ptr(oc), ptr(ow), ptr(out))
+    if rc_ != 0:
+        err = getattr(lib, name.split("_")[0] + "_last_error")
+        err.restype = C.c_char_p
+        raise VbError(rc_, err().decode())
+    return out
+
+
 class CEngineBase:
     """Shared ctypes plumbing for engines exposing the vb_* function family under a prefix."""
 

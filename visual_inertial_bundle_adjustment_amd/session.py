@@ -350,8 +350,12 @@ def read_point_observations(path) -> PointObservations:
     """PointObservationReader::read (PointObservationReader.cpp:19-47)."""
     c = _read_columns(path, OBSERVATION_COLUMNS, (np.int64, np.int64, np.int32) + (np.float64,) * 6)
     n = len(c[0])
-    return PointObservations(c[0], c[1], c[2], np.stack([c[3], c[4]], axis=1).reshape(n, 2),
-                             np.stack(c[5:9], axis=1).reshape(n, 2, 2))
+    # PointObservation holds the projection and its sqrt information as Eigen::Vector2f / Matrix2f
+    # (interfaces/ark/point_observation/PointObservation.h:22-23): the reader rounds them to fp32, and
+    # every later use casts those values to double (VisualFactors.cpp:35-36, Triangulation.cpp:139-140)
+    f32 = [np.asarray(x, np.float64).astype(np.float32).astype(np.float64) for x in c[3:9]]
+    return PointObservations(c[0], c[1], c[2], np.stack([f32[0], f32[1]], axis=1).reshape(n, 2),
+                             np.stack(f32[2:6], axis=1).reshape(n, 2, 2))
 
 
 def write_point_observations(path, obs: PointObservations):
