@@ -99,3 +99,74 @@ def test_covariances_gpu_match_oracle(which):
     # the LM state is rebuilt by the next iteration
     s = g.optimize(Settings.default(max_num_iterations=2))
     assert s.num_iterations == 2
+
+
+def _all_blocks(p):
+    """every rig block (pose, velocity, omega) and every calibration variable: the whole request of
+    SingleSessionProblem::computeCovariances"""
+    omega = len(p.fivals[4]) > 0
+    blocks = [[(1, r), (2, r)] + ([(3, r)] if omega else []) for r in range(len(p.const[1]))]
+    for kind in (4, 5, 6, 7):
+        blocks += [[(kind, h)] for h in range(len(p.const[kind])) if not p.const[kind][h]]
+    return blocks
+
+
+def _solved(e, blocks, monkeypatch):
+    """the same blocks by one reduced solve per column (VIBA_COV_SOLVES=1)"""
+    monkeypatch.setenv("VIBA_COV_SOLVES", "1")
+    try:
+        return e.compute_covariances(blocks)
+    finally:
+        monkeypatch.delenv("VIBA_COV_SOLVES")
+
+
+@pytest.mark.gpu
+def test_selected_inversion_matches_column_solves_miniB(monkeypatch):
+    """The selected inversion (csrc/selinv.hip) against one reduced solve per column on miniB, every
+    rig and calibration block, plus joint blocks of far-apart rigs (off the factor's tile pattern: they
+    take the per-column solves inside the same call)."""
+    from parity_util import rel
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    g, p = make(HipEngine, "miniB")
+    g.optimize(Settings.default(max_num_iterations=3))
+    n = len(p.const[1])
+    blocks = _all_blocks(p) + [[(1, 0), (1, n - 1)], [(1, 3), (2, n // 2), (4, 0)]]
+    ci, li = g.compute_covariances(blocks)
+    cs, ls = _solved(g, blocks, monkeypatch)
+    assert li == ls
+    worst = max(rel(a, b) for a, b in zip(ci, cs))
+    print(f"miniB: {len(blocks)} blocks, selected inversion vs column solves {worst:.2e}")
+    assert worst < 1e-8
+    for c in ci:
+        assert np.allclose(c, c.T, rtol=0, atol=1e-10 * np.abs(c).max())
+
+
+@pytest.mark.gpu
+def test_selected_inversion_config_C_all_rigs(monkeypatch):
+    """SingleSessionProblem::computeCovariances' whole request at config C (10k rig blocks of pose +
+    velocity + omega, every calibration variable) in one call, in seconds; 40 sampled blocks against the
+    per-column solves."""
+    import time
+
+    from parity_util import rel
+    from visual_inertial_bundle_adjustment_amd import synth
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    p = synth.generate(synth.config("C"))
+    g = HipEngine(imu_calib_options=p.imu_calib_options)
+    synth.load_into(g, p)
+    blocks = _all_blocks(p)
+    g.synchronize()
+    t = time.perf_counter()
+    ci, _ = g.compute_covariances(blocks)
+    dt = time.perf_counter() - t
+    print(f"config C: {len(blocks)} covariance blocks in {dt:.2f} s")
+    assert dt < 20.0
+    rng = np.random.default_rng(5)
+    pick = sorted(rng.choice(len(blocks), size=40, replace=False))
+    cs, _ = _solved(g, [blocks[i] for i in pick], monkeypatch)
+    worst = max(rel(ci[i], c) for i, c in zip(pick, cs))
+    print(f"config C: sampled blocks vs column solves {worst:.2e}")
+    assert worst < 1e-8
+    for c in ci[::97]:
+        assert np.linalg.eigvalsh(0.5 * (c + c.T)).min() > 0
+    g.close()

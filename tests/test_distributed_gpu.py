@@ -1,6 +1,10 @@
 """Landmark-sharded LM on the HIP engine: two processes (each a shard, both on cuda:0, gloo with
 host staging instead of RCCL on this one-GPU test box) reproduce the single-GPU vb_optimize run and the
-CPU oracle's: same iterations, costs to 1e-9, variables to 1e-7 (summation order across shards differs)."""
+CPU oracle's: same iterations, costs to 1e-9, variables to 1e-7 (summation order across shards differs).
+
+Also: the partitioned factorization at config-B size (2k rigs / 60k landmarks / 1.19M observations), and
+config E (the mixed-precision build, libviba_hip_mixed.so) through the partitioned controller against the
+single-GPU mixed engine and the fp64 oracle at config E's stated tolerance."""
 from __future__ import annotations
 
 import os
@@ -19,7 +23,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, which, its, out_dir, mode="shard"):
+def _worker(rank, world, port, which, its, out_dir, mode="shard", precision="fp64"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "tests")]
@@ -31,12 +35,12 @@ def _worker(rank, world, port, which, its, out_dir, mode="shard"):
     from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    if mode == "partition":
+    if mode == "partition" and which == "miniB":
         os.environ["VIBA_ND_LEAF"] = "128"  # miniB is small: finer dissection so 4 ranks get subtrees
     dist.init_process_group("gloo", rank=rank, world_size=world)
     p = synth.generate(synth.config(which))
     lb, le = shard_bounds(p, world)[rank]
-    e = HipEngine(imu_calib_options=p.imu_calib_options, device=0)
+    e = HipEngine(imu_calib_options=p.imu_calib_options, device=0, precision=precision)
     if mode == "partition":
         e.set_partition(rank, world)
         cls = PartitionedOptimizer
@@ -54,23 +58,43 @@ def _worker(rank, world, port, which, its, out_dir, mode="shard"):
     dist.destroy_process_group()
 
 
-def _check_against_single(tmp_path, world, which, its):
-    """every rank against the single-GPU engine AND the CPU oracle (oracle/refcpu) on the same inputs"""
+# tolerances per (engine the ranks run, reference engine): (final cost, variables) relative
+_TOL = {("fp64", "fp64"): (1e-9, 1e-7),
+        # config E: the ranks' and the single GPU's fp32 Schur products differ in summation order only
+        ("mixed", "mixed"): (1e-8, 1e-5),
+        # config E against the fp64 oracle (test_parity_configs: step 1e-3, cost after a step 1e-6)
+        ("mixed", "fp64"): (1e-6, 1e-3)}
+
+
+def _check_against_single(tmp_path, world, which, its, precision="fp64"):
+    """every rank against the single-GPU engine (same precision) AND the CPU oracle (oracle/refcpu,
+    fp64) on the same inputs"""
     from oracle.refcpu import RefEngine
-    from parity_util import make, rel
+    from parity_util import oracle_threads, rel
+    from visual_inertial_bundle_adjustment_amd import synth
     from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
     r = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
+    p = synth.generate(synth.config(which))
     for cls in (HipEngine, RefEngine):
-        e, _ = make(cls, which)
+        if cls is HipEngine:
+            e, ref_prec = HipEngine(imu_calib_options=p.imu_calib_options, precision=precision), precision
+        else:
+            e, ref_prec = RefEngine(imu_calib_options=p.imu_calib_options), "fp64"
+            e.set_threads(oracle_threads())
+        synth.load_into(e, p)
         s = e.optimize(Settings.default(max_num_iterations=its))
+        cost_tol, var_tol = _TOL[(precision, ref_prec)]
         for k in range(world):
             assert int(r[k]["iters"]) == s.num_iterations, cls
             assert abs(float(r[k]["initial"]) - s.initial_cost) <= 1e-11 * s.initial_cost, cls
-            assert abs(float(r[k]["final"]) - s.final_cost) <= 1e-9 * s.final_cost, cls
+            assert abs(float(r[k]["final"]) - s.final_cost) <= cost_tol * s.final_cost, \
+                (cls, float(r[k]["final"]), s.final_cost)
             for kind in range(1, 8):
                 ref = e.get_vars(kind)
                 if len(ref):
-                    assert rel(r[k][f"v{kind}"], ref) < 1e-7, (cls, kind)
+                    assert rel(r[k][f"v{kind}"], ref) < var_tol, (cls, kind, rel(r[k][f"v{kind}"], ref))
+        if hasattr(e, "close"):
+            e.close()
 
 
 @pytest.mark.parametrize("which,its", [("miniB", 8)])
@@ -90,3 +114,22 @@ def test_partitioned_factorization_matches_single_gpu(world, tmp_path):
     part = [np.load(tmp_path / f"rank{k}.npz")["part"] for k in range(world)]
     assert sum(q[0] > 0 for q in part) >= 2, part  # subtrees factored on several ranks
     assert part[0][1] > 0 and part[0][3] > 0, part[0]  # and rank 0 the ROOT separators
+
+
+def test_partitioned_factorization_config_B_size(tmp_path):
+    """The partitioned controller (2 ranks) at config-B size: 2k rigs, 60k landmarks, 1.19M observations,
+    the default nested-dissection leaves; against the single GPU and the oracle over 3 iterations."""
+    world, which, its = 2, "B", 3
+    mp.spawn(_worker, args=(world, _free_port(), which, its, str(tmp_path), "partition"), nprocs=world, join=True)
+    _check_against_single(tmp_path, world, which, its)
+    part = [np.load(tmp_path / f"rank{k}.npz")["part"] for k in range(world)]
+    assert all(q[0] > 0 for q in part), part
+
+
+@pytest.mark.parametrize("mode", ["partition", "shard"])
+def test_config_E_multi_process(mode, tmp_path):
+    """Config E (mixed build) through both multi-process controllers on miniB: the single-GPU mixed
+    engine's trajectory, and the fp64 oracle's within config E's stated tolerance."""
+    world, which, its = 2, "miniB", 6
+    mp.spawn(_worker, args=(world, _free_port(), which, its, str(tmp_path), mode, "mixed"), nprocs=world, join=True)
+    _check_against_single(tmp_path, world, which, its, precision="mixed")

@@ -110,6 +110,34 @@ def test_config_E_on_B_against_fp64_oracle():
 
 
 @pytest.mark.gpu
+def test_config_E_full_C_against_fp64_engine():
+    """Config E at the benchmarked size (config C: 10k rigs, 300k landmarks, 5.94M observations): one LM
+    step of the mixed build against the fp64 HIP engine (itself oracle-pinned on the C slice and on B).
+    Stated tolerance as on B: costs 1e-10, gradient 1e-6, step 1e-3 max-abs and 1e-4 L2 relative, the
+    cost after the step 1e-6, the model reduction 1e-4 (measured at r02k: step L2 3.9e-6)."""
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    p = synth.generate(synth.config("C"))
+    out = {}
+    for prec in ("fp64", "mixed"):
+        e = HipEngine(imu_calib_options=p.imu_calib_options, precision=prec)
+        synth.load_into(e, p, rs_device=True)
+        out[prec] = one_step(e)
+        e.close()
+    og, orf = out["mixed"], out["fp64"]
+    assert abs(og["cost0"] - orf["cost0"]) <= 1e-10 * orf["cost0"]
+    gm = max(rel(og["grad"][k], orf["grad"][k]) for k in range(NUM_VAR_KINDS - 1) if orf["grad"][k].size)
+    sm = max(rel(og["step"][k], orf["step"][k]) for k in range(NUM_VAR_KINDS - 1) if orf["step"][k].size)
+    s64 = np.concatenate([s.ravel() for s in orf["step"]])
+    smx = np.concatenate([s.ravel() for s in og["step"]])
+    l2 = float(np.linalg.norm(smx - s64) / np.linalg.norm(s64))
+    print(f"config E on C vs fp64 engine: gradient {gm:.2e}, step max {sm:.2e}, step L2 {l2:.2e}, cost1 "
+          f"{abs(og['cost1'] - orf['cost1']) / orf['cost1']:.2e}")
+    assert gm < 1e-6 and sm < 1e-3 and l2 < 1e-4
+    assert abs(og["cost1"] - orf["cost1"]) <= 1e-6 * orf["cost1"]
+    assert abs(og["model_red"] - orf["model_red"]) <= 1e-4 * orf["model_red"]
+
+
+@pytest.mark.gpu
 def test_failing_factors_one_step_matches_oracle():
     """CostStats {numTotal, numInvalid, numPrevInvalid} and the comparable cost with cached costs of
     newly failing factors (Factor.h:390-417) after one step, the -1 ResultCache of factors failing at

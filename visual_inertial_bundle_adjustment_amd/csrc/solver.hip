@@ -2152,8 +2152,9 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
   if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
-  // VIBA_SCHUR_V=2: the previous form with the K-row bookkeeping inside the k-loop
-  static const int v = getenv("VIBA_SCHUR_V") ? atoi(getenv("VIBA_SCHUR_V")) : 3;
+  // VIBA_SCHUR_V=3: the K-row offsets from an LDS table with hand-counted gathers (schur_run3_kernel);
+  // measured r03a on config C: Schur phase 6.50 ms against 6.15 for schur_run2 (the default)
+  static const int v = getenv("VIBA_SCHUR_V") ? atoi(getenv("VIBA_SCHUR_V")) : 2;
   if (d.nTileWorks) {
     if (v == 2) launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
     else launchK(schur_run3_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
