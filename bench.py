@@ -28,7 +28,7 @@ sys.path.insert(0, ROOT)
 # kernel families of vb_profile_kernel
 KF_VISUAL_LIN, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACKSUB, KF_COST, KF_SMALL, KF_TRSM, \
     KF_SYMV = range(12)
-SOLVERS = {"direct": 0, "pcg-trivial": 1, "pcg-jacobi": 2, "pcg-gauss-seidel": 3}
+SOLVERS = {"direct": 0, "pcg-trivial": 1, "pcg-jacobi": 2, "pcg-gauss-seidel": 3, "pcg-lower-prec": 4}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix peak (spec)
 # what v_mfma_f64_16x16x4_f64 sustains on this chip with independent accumulators and no memory traffic
@@ -152,7 +152,7 @@ def main():
                          "iteration (ark_vi_ba's preStepCallback); host: fixed precomputed tables")
     ap.add_argument("--solver", choices=tuple(SOLVERS), default="direct",
                     help="reduced-system solver (Optimizer::Settings solverType): the tile Cholesky, or PCG with "
-                         "the identity / block-Jacobi / block-Gauss-Seidel preconditioner")
+                         "the identity / block-Jacobi / block-Gauss-Seidel / fp32-Cholesky preconditioner")
     ap.add_argument("--pcg-iterations", type=int, default=40, help="pcgMaxIterations (Optimizer.h:44)")
     ap.add_argument("--pcg-residual", type=float, default=1e-10, help="pcgDesiredResidual (Optimizer.h:45)")
     ap.add_argument("--recompute-preint", action="store_true",

@@ -310,8 +310,10 @@ int vb_solve_with_new_gradient(vb_handle h);
  * with the preconditioners of Preconditioner.h: identity, block Jacobi over the parameter blocks, and
  * block Gauss-Seidel (the pseudo-factor -- diagonal blocks factored, off-diagonal blocks scaled, no
  * updates -- here over the 64 x 64 tiles of this library's reduced ordering, as BaSpaCho's is over
- * its supernodes).  The lower-precision-factor preconditioner is not built (VB_E_UNSUPPORTED).  Single
- * handle only: VB_E_UNSUPPORTED on a landmark shard or a partitioned rank.  Any time after vb_create. */
+ * its supernodes), and LowerPrecSolvePrecond (Preconditioner.h:166-246: S cast to fp32 and factored by
+ * the tile Cholesky's schedule in fp32, the diagonal raised and the factor redone while it holds a
+ * non-finite value; applied by fp32 triangular solves).  Single handle only: VB_E_UNSUPPORTED on a
+ * landmark shard or a partitioned rank.  Any time after vb_create. */
 #define VB_SOLVER_DIRECT 0
 #define VB_SOLVER_PCG_TRIVIAL 1
 #define VB_SOLVER_PCG_JACOBI 2

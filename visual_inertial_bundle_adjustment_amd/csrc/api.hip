@@ -80,6 +80,18 @@ void launch_selinv_level(double* tiles, const int32_t* tileIdx, int32_t nT, cons
                          const int32_t* uItems, int nU, const int32_t* zItems, int nZ, const int32_t* dItems, int nD,
                          hipStream_t st);
 void launch_gather(const double* src, const int64_t* idx, int64_t n, double* out, hipStream_t st);
+void launch_lp_cast(const double* in, float* out, int64_t n, hipStream_t st);
+void launch_lp_uncast(const float* in, double* out, int64_t n, hipStream_t st);
+void launch_lp_damp(float* t32, const int32_t* tileIdx, int32_t nT, const int64_t* rvOff, const int32_t* rvDim,
+                    int64_t nRV, float eps, hipStream_t st);
+void launch_lp_factor_level(float* t32, const int32_t* work, int nWork, const int32_t* pairs, const int32_t* diag,
+                            const int32_t* cols, int nDiag, const int32_t* targets, const int32_t* tcols, int nTrsm,
+                            float* linv, hipStream_t st);
+void launch_lp_nonfinite(const float* x, int64_t n, int32_t* flag, hipStream_t st);
+void launch_lp_fwd_level(const float* t32, const int32_t* cols, int nCols, const int32_t* targets, const int32_t* tcols,
+                         const int32_t* trows, int nTrsm, const float* linv, float* t, hipStream_t st);
+void launch_lp_bwd_level(const float* t32, const int64_t* colStart, const int32_t* colTiles, const int32_t* colRows,
+                         const int32_t* cols, int nCols, const float* linv, float* t, hipStream_t st);
 }  // namespace viba
 
 using namespace viba;
@@ -346,6 +358,8 @@ struct vb_handle_s {
   int64_t nSymv = 0;
   double *pcgR = nullptr, *pcgZ = nullptr, *pcgP = nullptr, *pcgAp = nullptr, *pcgB = nullptr;
   double *jacL = nullptr, *tilesGS = nullptr;  // Jacobi block factors / Gauss-Seidel pseudo-factor
+  // LowerPrecSolvePrecond (lowprec.hip): fp32 factor tiles, fp32 diagonal-tile inverses, fp32 vector
+  float *lpTiles = nullptr, *lpLinv = nullptr, *lpT = nullptr;
   // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
   hipGraphExec_t solveGraph = nullptr;
   bool useGraphs = true;
@@ -1784,7 +1798,61 @@ int pcgPrepare(vb_handle h) {
   if (h->solverType == VB_SOLVER_PCG_JACOBI && !h->jacL && alloc0(&h->jacL, nPad * 32)) return VB_E_HIP;
   if (h->solverType == VB_SOLVER_PCG_GAUSS_SEIDEL && !h->tilesGS && alloc0(&h->tilesGS, d.nTiles * TS * TS))
     return VB_E_HIP;
+  if (h->solverType == VB_SOLVER_PCG_LOWER_PREC && !h->lpTiles &&
+      (alloc0(&h->lpTiles, d.nTiles * TS * TS) || alloc0(&h->lpLinv, (size_t)d.nT * TS * TS) || alloc0(&h->lpT, nPad)))
+    return VB_E_HIP;
   return 0;
+}
+
+// LowerPrecSolvePrecond::init (Preconditioner.h:180-213): S cast to fp32 and factored by the direct
+// solver's tile schedule in fp32 (lowprec.hip); while the factor holds a non-finite value (the
+// reference sums it), redo it from S with the diagonal raised: epsilon 0, then 1e-8, then x3 per attempt
+int lpInit(vb_handle h) {
+  Dev& d = h->d;
+  const Sched& S = h->sch[0];
+  const int64_t nEl = d.nTiles * TS * TS;
+  float eps = 0.0f;
+  for (int attempt = 0; attempt < 200; attempt++) {
+    launch_lp_cast(d.tiles, h->lpTiles, nEl, h->st);
+    if (eps > 0) {
+      launch_lp_damp(h->lpTiles, d.tileIdx, d.nT, d.rvOff, d.rvDim, d.nRV, eps, h->st);
+      eps *= 3.0f;
+    } else {
+      eps = 1e-8f;
+    }
+    for (int32_t L = 0; L < S.nLevels; L++) {
+      const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
+      launch_lp_factor_level(h->lpTiles, S.updD + 4 * u0, (int)(S.lvU[L + 1] - u0), S.fanPairsD, S.potrfTileD + p0,
+                             S.potrfColD + p0, (int)(S.lvP[L + 1] - p0), S.trsmTargetD + t0, S.trsmColD + t0,
+                             (int)(S.lvT[L + 1] - t0), h->lpLinv, h->st);
+    }
+    HIPCHK(hipMemsetAsync(d.err + 3, 0, sizeof(int32_t), h->st));  // err[3]: a non-finite factor entry
+    launch_lp_nonfinite(h->lpTiles, nEl, d.err + 3, h->st);
+    int32_t bad = 0;
+    HIPCHK(hipMemcpyAsync(&bad, d.err + 3, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    if (!bad) return 0;
+  }
+  return fail(VB_E_NUMERIC, "LowerPrecSolvePrecond: the fp32 factor keeps breaking down");
+}
+
+// LowerPrecSolvePrecond::operator() (Preconditioner.h:215-237): z = (L L^T)^-1 r in fp32
+void lpApply(vb_handle h, const double* r, double* z) {
+  Dev& d = h->d;
+  const Sched& S = h->sch[0];
+  const int64_t n = (int64_t)d.nT * TS;
+  launch_lp_cast(r, h->lpT, n, h->st);
+  for (int32_t L = 0; L < S.nLevels; L++) {
+    const int64_t p0 = S.lvP[L], t0 = S.lvT[L];
+    launch_lp_fwd_level(h->lpTiles, S.potrfColD + p0, (int)(S.lvP[L + 1] - p0), S.trsmTargetD + t0, S.trsmColD + t0,
+                        S.trsmRowD + t0, (int)(S.lvT[L + 1] - t0), h->lpLinv, h->lpT, h->st);
+  }
+  for (int32_t L = S.nLevels - 1; L >= 0; L--) {
+    const int64_t p0 = S.lvP[L];
+    launch_lp_bwd_level(h->lpTiles, h->colStartD, h->colTilesD, h->colRowsD, S.potrfColD + p0, (int)(S.lvP[L + 1] - p0),
+                        h->lpLinv, h->lpT, h->st);
+  }
+  launch_lp_uncast(h->lpT, z, n, h->st);
 }
 
 // Preconditioner::init on the assembled (damped) S
@@ -1804,6 +1872,8 @@ int precondInit(vb_handle h) {
     launch_potrf(g, S.potrfTileD, S.potrfColD, (int)S.lvP[S.nLevels], h->dinv, h->st);
     launch_trsm(g, S.trsmDiagD, S.trsmTargetD, S.trsmColD, (int)S.lvT[S.nLevels], h->dinv, h->st);
     launch_diag_inverse(g, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
+  } else if (h->solverType == VB_SOLVER_PCG_LOWER_PREC) {
+    return lpInit(h);
   }
   return 0;
 }
@@ -1820,6 +1890,10 @@ int precondApply(vb_handle h, const double* r, double* z) {
     launch_solve_fanout(g, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD, h->rowTilesD,
                         h->rowColD, h->linv, h->pcgB, h->yvec, z, h->solveFlags, h->numCUs * solveWgPerCU(), h->st, 3,
                         nullptr, 0);
+    return 0;
+  }
+  if (h->solverType == VB_SOLVER_PCG_LOWER_PREC) {
+    lpApply(h, r, z);
     return 0;
   }
   HIPCHK(hipMemcpyAsync(z, r, bytes, hipMemcpyDeviceToDevice, h->st));
@@ -1954,7 +2028,7 @@ int vb_destroy(vb_handle h) {
                   d.rsCalib, d.red, d.redS, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->lscr, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
-                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->facSync,
+                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->lpTiles, h->lpLinv, h->lpT, h->facSync,
                   (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -2370,8 +2444,6 @@ int vb_solve_with_new_gradient(vb_handle h) {
 int vb_set_solver(vb_handle h, int solver_type, int pcg_max_iterations, double pcg_desired_residual) {
   if (!h) return fail(VB_E_ARG, "null handle");
   if (solver_type < VB_SOLVER_DIRECT || solver_type > VB_SOLVER_PCG_LOWER_PREC) return fail(VB_E_ARG, "unknown solver type");
-  if (solver_type == VB_SOLVER_PCG_LOWER_PREC)
-    return fail(VB_E_UNSUPPORTED, "LowerPrecSolvePrecond is not built (use VB_SOLVER_PCG_GAUSS_SEIDEL or the direct solver)");
   if (solver_type != VB_SOLVER_DIRECT && (h->partWorld > 1 || h->sharded))
     return fail(VB_E_UNSUPPORTED, "the PCG solvers run on a single handle (no landmark shards, no partition)");
   if (pcg_max_iterations < 1) return fail(VB_E_ARG, "pcg_max_iterations must be >= 1");
