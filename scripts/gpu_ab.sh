@@ -1,14 +1,21 @@
 #!/bin/bash
-# A/B bench of the in-tree build against alternative library builds (VIBA_LIB_DIR); optional GPU
-# parity tests first (set TESTS=1).  args: lib dirs under visual_inertial_bundle_adjustment_amd/
+# A/B of library builds and environment switches on the default bench (config C, no CPU baseline):
+#   gpu_ab.sh TAG [--test "pytest -k expr"] SPEC...   SPEC = libdir[:VAR=v,VAR2=w]  (libdir under the package)
+# stops at the first failing step
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-if [ -n "$TESTS" ]; then
-  timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_pytest.log 2>&1 || { tail -30 gpurun_out/ab_pytest.log; exit 1; }
-  tail -2 gpurun_out/ab_pytest.log
+TAG=$1; shift
+if [ "$1" = "--test" ]; then
+  timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 300 --timeout-method thread -k "$2" > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.log; exit 1; }
+  tail -1 gpurun_out/${TAG}_pytest.log
+  shift 2
 fi
-for L in lib "$@" lib; do
-  VIBA_LIB_DIR=$GRAFT_REPO_ROOT/visual_inertial_bundle_adjustment_amd/$L timeout -k 10 200 python bench.py --no-cpu-baseline --steps 5 --warmup 2 > gpurun_out/ab_$L.json 2> gpurun_out/ab_$L.log || exit 1
-  echo "$L: $(grep timed gpurun_out/ab_$L.log)"
+i=0
+for spec in "$@"; do
+  lib=${spec%%:*}; envs=""
+  [ "$spec" != "$lib" ] && envs=${spec#*:}
+  env VIBA_LIB_DIR=$GRAFT_REPO_ROOT/visual_inertial_bundle_adjustment_amd/$lib ${envs//,/ } timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/${TAG}_b$i.json 2> gpurun_out/${TAG}_b$i.log || { tail -5 gpurun_out/${TAG}_b$i.log; exit 1; }
+  echo "$spec: $(python -c "import json;d=json.load(open('gpurun_out/${TAG}_b$i.json'));p=d['phases_ms'];print(round(d['value'],2), {k: p[k] for k in ('linearize_ms','schur_ms','factor_ms','solve_ms','cost_ms')})")"
+  i=$((i+1))
 done

@@ -1069,6 +1069,7 @@ int doFinalize(vb_handle h) {
       auto blocks16 = [](uint64_t m) { int n = 0; for (int b = 0; b < 4; b++) n += ((m >> (16 * b)) & 0xffff) ? 1 : 0; return n; };
       double cur = 0, grp = 0, dense = 0, useful = 0, grpTile = 0;
       int64_t gsz[6] = {0, 0, 0, 0, 0, 0};
+      double shp[5][5] = {}, shpE[5][5] = {};
       int64_t nGrp = 0;
       for (int64_t t = 0; t < nTiles; t++) {
         std::vector<std::pair<std::pair<uint64_t, uint64_t>, int>> sig;
@@ -1086,6 +1087,11 @@ int doFinalize(vb_handle h) {
           grp += std::ceil(3.0 * (j - i) / 4.0) * std::ceil(nI / 16.0) * std::ceil(nJ / 16.0);
           grpTile += std::ceil(3.0 * (j - i) / 4.0) * blocks16(sig[i].first.first) * blocks16(sig[i].first.second);
           gsz[std::min<size_t>(5, j - i <= 1 ? 0 : j - i <= 3 ? 1 : j - i <= 7 ? 2 : j - i <= 15 ? 3 : j - i <= 63 ? 4 : 5)] += j - i;
+          {  // MFMAs by compact shape (nbI, nbJ)
+            const int bi = (nI + 15) / 16, bj = (nJ + 15) / 16;
+            shp[bi][bj] += std::ceil(3.0 * (j - i) / 4.0) * bi * bj;
+            shpE[bi][bj] += (double)(j - i);
+          }
           nGrp++;
           i = j;
         }
@@ -1113,6 +1119,10 @@ int doFinalize(vb_handle h) {
       fprintf(stderr, "[schur stats] identical-mask groups in tile coordinates (dense K) %.3g; entries in groups of "
               "1 / 2-3 / 4-7 / 8-15 / 16-63 / 64+: %lld %lld %lld %lld %lld %lld\n", grpTile, (long long)gsz[0],
               (long long)gsz[1], (long long)gsz[2], (long long)gsz[3], (long long)gsz[4], (long long)gsz[5]);
+      for (int bi = 1; bi <= 4; bi++)
+        for (int bj = 1; bj <= 4; bj++)
+          if (shpE[bi][bj] > 0)
+            fprintf(stderr, "[schur stats] compact blocks %d x %d: entries %.3g, MFMAs %.3g\n", bi, bj, shpE[bi][bj], shp[bi][bj]);
     }
     // entries of a tile in runs of identical (maskI, maskJ) (solver.hip schur_run2_kernel), by
     // landmark within a run
@@ -1179,6 +1189,59 @@ int doFinalize(vb_handle h) {
         }
       }
     for (TileWork& w : works) w.kind = itemsPerTile[w.tile] > 1 ? 1 : 0;
+    // per item: its runs of identical (maskI, maskJ) and its tasks (run, chunk of <= kSchurCh landmarks,
+    // kSchurTR compact block rows), dealt to the 4 waves longest-first by an MFMA + gather cost model and
+    // kept in (run, chunk) order per wave, so a wave rebuilds its row maps only when its run changes
+    // (schur_run4_kernel: no run scan, no per-run global mask reads, balanced waves)
+    std::vector<uint64_t> runsH;
+    std::vector<uint32_t> tasksH;
+    for (TileWork& w : works) {
+      const bool diag = w.I == w.J;
+      std::vector<int> rs;
+      for (int e = 0; e < w.count; e++) {
+        const TileEnt& a = ents[w.start + e];
+        if (e == 0 || a.maskI != ents[w.start + e - 1].maskI || a.maskJ != ents[w.start + e - 1].maskJ) rs.push_back(e);
+      }
+      rs.push_back(w.count);
+      w.runFirst = (int32_t)(runsH.size() / 2), w.nRuns = (uint16_t)(rs.size() - 1);
+      struct Tk {
+        uint32_t code;
+        double cost;
+      };
+      std::vector<Tk> tl;
+      for (size_t r = 0; r + 1 < rs.size(); r++) {
+        const uint64_t mI = ents[w.start + rs[r]].maskI, mJ = diag ? mI : ents[w.start + rs[r]].maskJ;
+        runsH.push_back(mI), runsH.push_back(mJ);
+        const int nbI = (__builtin_popcountll(mI) + 15) / 16, nbJ = (__builtin_popcountll(mJ) + 15) / 16;
+        for (int c0 = rs[r]; c0 < rs[r + 1]; c0 += kSchurCh)
+          for (int a0 = 0; a0 < nbJ; a0 += kSchurTR) {
+            const int nl = std::min(kSchurCh, rs[r + 1] - c0), nr = std::min(kSchurTR, nbJ - a0);
+            const int nks = (3 * nl + 3) / 4;
+            int mf = 0;
+            for (int i = 0; i < nr; i++)
+              for (int b = 0; b < nbI; b++) mf += (!diag || a0 + i <= b) ? 1 : 0;
+            const double cost = nks * (16.0 * mf + 3.0 * (nr + nbI)) + 6.0 * mf + 24.0 + (diag && a0 == 0 ? 6.0 * nl : 0.0);
+            tl.push_back({(uint32_t)r | ((uint32_t)c0 << 8) | ((uint32_t)nl << 16) | ((uint32_t)a0 << 21), cost});
+          }
+      }
+      std::stable_sort(tl.begin(), tl.end(), [](const Tk& a, const Tk& b) { return a.cost > b.cost; });
+      std::vector<uint32_t> per[4];
+      double load[4] = {0, 0, 0, 0};
+      for (const Tk& t : tl) {
+        const int k = (int)(std::min_element(load, load + 4) - load);
+        load[k] += t.cost, per[k].push_back(t.code);
+      }
+      w.taskFirst = (int32_t)tasksH.size();
+      for (int k = 0; k < 4; k++) {
+        std::sort(per[k].begin(), per[k].end(), [](uint32_t a, uint32_t b) {
+          return (a & 0xffffu) != (b & 0xffffu) ? (a & 0xffffu) < (b & 0xffffu) : a < b;  // run, chunk, row
+        });
+        w.wOff[k] = (uint16_t)(tasksH.size() - w.taskFirst);
+        tasksH.insert(tasksH.end(), per[k].begin(), per[k].end());
+      }
+      w.wOff[4] = (uint16_t)(tasksH.size() - w.taskFirst);
+    }
+    if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH)) return VB_E_HIP;
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
     d.nTileWorks = (int64_t)works.size();
     h->nTileEnt = (int64_t)ents.size(), h->nObEnt = d.nGroups;
@@ -2023,7 +2086,7 @@ int vb_destroy(vb_handle h) {
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.yZero, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
-                  d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
+                  d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.schurRuns, d.schurTasks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.redS, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,

@@ -120,7 +120,14 @@ struct TileWork {
   int32_t tile, I, J, count;  // count <= 256 landmark entries
   int64_t start;              // into tileEnts
   int32_t kind, pad;          // kind 1: the tile is split over several items (atomic epilogue)
+  // schur_run4_kernel: the item's runs of identical (maskI, maskJ) at schurRuns[runFirst ..) and its
+  // tasks at schurTasks[taskFirst ..), wave w's at [wOff[w], wOff[w + 1])
+  int32_t runFirst, taskFirst;
+  uint16_t nRuns, wOff[5];
 };
+// one task of schur_run4_kernel (32 bits): run (8) | first entry of its landmark chunk (8) | landmarks
+// (5) | first compact block row (2); built at finalize with kSchurCh landmarks x kSchurTR block rows
+constexpr int kSchurCh = 16, kSchurTR = 2;
 
 struct Dev {
   // variables
@@ -177,6 +184,8 @@ struct Dev {
   // Schur assembly work by target tile
   int64_t nTileWorks = 0;
   TileWork* tileWorks = nullptr;
+  uint64_t* schurRuns = nullptr;   // per run: maskI, maskJ
+  uint32_t* schurTasks = nullptr;
   TileEnt* tileEnts = nullptr;
   int32_t* tileObs = nullptr;  // (unused: direct terms go through the observation groups)
   // direct visual terms by observation group (observations sharing their 4 reduced blocks: one rig,

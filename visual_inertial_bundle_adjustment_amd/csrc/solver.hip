@@ -358,6 +358,11 @@ constexpr int kTR = VIBA_SCHUR_TR;  // compact block rows per task (1 or 2)
 #define VIBA_SCHUR_PF 1
 #endif
 constexpr int kPF = VIBA_SCHUR_PF;  // k-steps of operand gathers in flight
+// schur_run2's gathers: 0 compiler-scheduled loads; 1 or 2 sets of hand-counted inline-asm loads in
+// flight ahead of the MFMAs
+#ifndef VIBA_SCHUR_PFD
+#define VIBA_SCHUR_PFD 0
+#endif
 
 // One task's K loop: acc[i][b] += A_i^T B_b over the dense K rows (3 per landmark) of landmarks
 // c0 .. c0 + rows / 3, A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block
@@ -366,6 +371,115 @@ constexpr int kPF = VIBA_SCHUR_PF;  // k-steps of operand gathers in flight
 // from the landmark's first panel column in tile J / I.  Columns past nJ / nI load neighbouring
 // panel data into accumulator rows / columns that are never stored; K rows past `rows` read the zero
 // pad.  The next step's gathers are issued before the current step's MFMAs.
+#ifndef VIBA_SCHUR_ASMLD
+#define VIBA_SCHUR_ASMLD 1
+#endif
+// one gather of an 8-B (fp64) / 4-B (fp32) operand at an immediate byte offset I * STRIDE, as inline asm
+// (invisible to hipcc's waitcnt pass: the caller waits with vm_wait and pins the destination)
+template <int STRIDE>
+__device__ __forceinline__ void gather_asm(double& dst, const double* p, int i) {
+  switch (i) {
+    case 0: asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
+    case 1: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
+    case 2: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
+    default: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
+  }
+}
+template <int STRIDE>
+__device__ __forceinline__ void gather_asm(float& dst, const float* p, int i) {
+  switch (i) {
+    case 0: asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
+    case 1: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
+    case 2: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
+    default: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
+  }
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// C -= acc of one task through the run's compact -> tile row maps.  VIBA_SCHUR_EPI=1 (default): every
+// map entry of the task read up front (one LDS wait), the adds predicated; 0: the map read per
+// accumulator row inside a branch (a wait per row)
+#ifndef VIBA_SCHUR_EPI
+#define VIBA_SCHUR_EPI 1
+#endif
+template <int NBI, int NR, bool DIAG>
+__device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], int a0, int l4, int l15,
+                                               const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
+  int colT[NBI];
+#if VIBA_SCHUR_EPI
+  int rowT[NR][4];
+#pragma unroll
+  for (int b = 0; b < NBI; b++) colT[b] = posI[min(16 * b + l15, TS - 1)];
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) rowT[i][q] = posJ[min(16 * (a0 + i) + kAccL4 * l4 + kAccR * q, TS - 1)];
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool mv = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q < nJ;
+#pragma unroll
+      for (int b = 0; b < NBI; b++)
+        if ((!DIAG || a0 + i <= b) && mv && 16 * b + l15 < nI) atomicAdd(C + rowT[i][q] * TS + colT[b], -(double)acc[i][b][q]);
+    }
+#else
+#pragma unroll
+  for (int b = 0; b < NBI; b++) {
+    const int n = 16 * b + l15;
+    colT[b] = n < nI ? posI[n] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q;
+      if (m >= nJ) continue;
+      double* Cr = C + posJ[m] * TS;
+#pragma unroll
+      for (int b = 0; b < NBI; b++)
+        if ((!DIAG || a0 + i <= b) && colT[b] >= 0) atomicAdd(Cr + colT[b], -(double)acc[i][b][q]);
+    }
+#endif
+}
+
+// rhs -= Y^T z over a chunk's landmarks (diagonal tiles), lanes over the run's compact I columns.
+// VIBA_SCHUR_RHS=1 (default): four landmarks' loads in flight per step; 0: one landmark at a time
+#ifndef VIBA_SCHUR_RHS
+#define VIBA_SCHUR_RHS 1
+#endif
+__device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2], const TileEnt* ents, int c0, int nl,
+                                          int lane, const uint8_t* posI, double* rq) {
+  const int64_t pq = d.nYcol;
+  double racc = 0.0;
+#if VIBA_SCHUR_RHS
+  int e = c0;
+  for (; e + 4 <= c0 + nl; e += 4) {
+    double y[4][3], z[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const rec_t* yp = d.Y + (int64_t)ecol[e + u][0] + lane;
+      const double* zz = d.z + 3 * (int64_t)ents[e + u].lm;
+#pragma unroll
+      for (int q = 0; q < 3; q++) y[u][q] = (double)yp[q * pq], z[u][q] = zz[q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) racc += y[u][0] * z[u][0] + y[u][1] * z[u][1] + y[u][2] * z[u][2];
+  }
+  for (; e < c0 + nl; e++) {
+#else
+  for (int e = c0; e < c0 + nl; e++) {
+#endif
+    const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
+    const double* zz = d.z + 3 * (int64_t)ents[e].lm;
+    racc += (double)y[0] * zz[0] + (double)y[pq] * zz[1] + (double)y[2 * pq] * zz[2];
+  }
+  atomicAdd(&rq[posI[lane]], -racc);
+}
+
 template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0, int rows, int a0, int l4, int l15,
                                            const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
@@ -399,6 +513,77 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
       for (int b = 0; b < NBI; b++)
         if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
   };
+#if VIBA_SCHUR_PFD > 0
+  // the gathers as inline-asm loads counted by hand (hipcc's waitcnt pass put a vmcnt(0) in front of
+  // every step's MFMAs, so the loads issued a step ahead were waited for at once): VIBA_SCHUR_PFD sets
+  // of gathers in flight while a step's MFMAs run
+  constexpr int kN = NR + NBI;
+  auto lda = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
+    const bool kv = kr < rows;
+    const uint2 c = ec[kv ? e : c0];
+    const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
+    const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
+    const rec_t* pI = kv ? base + c.x : zp;
+#pragma unroll
+    for (int i = 0; i < NR; i++) gather_asm<16 * sizeof(rec_t)>(av[i], pJ, i);
+#pragma unroll
+    for (int b = 0; b < NBI; b++) gather_asm<16 * sizeof(rec_t)>(bv[b], pI, b);
+    kr += 4, e += 1, q += 1;
+    if (q == 3) q = 0, e += 1;
+  };
+  auto pin = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
+#pragma unroll
+    for (int i = 0; i < NR; i++) asm volatile("" : "+v"(av[i]));
+#pragma unroll
+    for (int b = 0; b < NBI; b++) asm volatile("" : "+v"(bv[b]));
+  };
+#if VIBA_SCHUR_PFD == 1
+  rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
+  lda(a0v, b0v);
+  for (int ks = 0; ks < nks; ks += 2) {
+    if (ks + 1 < nks) {
+      lda(a1v, b1v);
+      vm_wait<kN>();
+    } else {
+      vm_wait<0>();
+    }
+    pin(a0v, b0v);
+    mm(a0v, b0v);
+    if (ks + 1 < nks) {
+      if (ks + 2 < nks) {
+        lda(a0v, b0v);
+        vm_wait<kN>();
+      } else {
+        vm_wait<0>();
+      }
+      pin(a1v, b1v);
+      mm(a1v, b1v);
+    }
+  }
+#else
+  rec_t av[3][NR], bv[3][NBI];
+  lda(av[0], bv[0]);
+  if (1 < nks) lda(av[1], bv[1]);
+  // step k uses set k % 3; before its MFMAs step k + 2 is issued, then all but the two newest sets land
+  auto step = [&](int k, rec_t (&a)[NR], rec_t (&b)[NBI], rec_t (&an)[NR], rec_t (&bn)[NBI]) {
+    if (k + 2 < nks) {
+      lda(an, bn);
+      vm_wait<2 * kN>();
+    } else if (k + 1 < nks) {
+      vm_wait<kN>();
+    } else {
+      vm_wait<0>();
+    }
+    pin(a, b);
+    mm(a, b);
+  };
+  for (int ks = 0; ks < nks; ks += 3) {
+    step(ks, av[0], bv[0], av[2], bv[2]);
+    if (ks + 1 < nks) step(ks + 1, av[1], bv[1], av[0], bv[0]);
+    if (ks + 2 < nks) step(ks + 2, av[2], bv[2], av[1], bv[1]);
+  }
+#endif
+#else
   rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
   ld(a0v, b0v);
   for (int ks = 0; ks < nks; ks += 2) {
@@ -407,33 +592,31 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     if (ks + 2 < nks) ld(a0v, b0v);
     if (ks + 1 < nks) mm(a1v, b1v);
   }
+#endif
   // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
-  int colT[NBI];
-#pragma unroll
-  for (int b = 0; b < NBI; b++) {
-    const int n = 16 * b + l15;
-    colT[b] = n < nI ? posI[n] : -1;
-  }
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q;
-      if (m >= nJ) continue;
-      double* Cr = C + posJ[m] * TS;
-#pragma unroll
-      for (int b = 0; b < NBI; b++)
-        if ((!DIAG || a0 + i <= b) && colT[b] >= 0) atomicAdd(Cr + colT[b], -(double)acc[i][b][q]);
-    }
+  schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run2_kernel(Dev d, double lambda) {
+#ifndef VIBA_SCHUR_WPE
+#define VIBA_SCHUR_WPE 4
+#endif
+// diagnostic build (-DVIBA_SCHUR_TIMING): per-wave cycle sums of schur_run2's phases (s_memtime), read by
+// vb_debug_schur_times: 0 setup, 1 run scan, 2 tasks (3 of them k-loops + epilogues, 4 rhs), 5 wait at
+// the final barrier, 6 write-back, 7 waves
+#ifdef VIBA_SCHUR_TIMING
+__device__ unsigned long long g_schur_t[8];
+#define SCHUR_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
+#else
+#define SCHUR_T(x)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_SCHUR_WPE, VIBA_SCHUR_WPE))) schur_run2_kernel(Dev d, double lambda) {
   __shared__ double C[TS * TS];
   __shared__ uint32_t ecol[256][2];  // the entries' first panel columns (colI, colJ); the rest from global
   __shared__ int16_t runStart[258];
   __shared__ uint8_t posW[4][2][TS];
   __shared__ double rq[TS];
   __shared__ int nRunsS;
+  SCHUR_T(t0);
   const int64_t w = xcd_block(blockIdx.x, gridDim.x);
   const TileWork wk = d.tileWorks[w];
   const bool diag = wk.I == wk.J;
@@ -445,6 +628,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
   for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
   if (tid < TS) rq[tid] = 0.0;
   __syncthreads();
+  SCHUR_T(t1);
   if (wave == 0) {
     int n = 0;
     for (int e0 = 0; e0 < cnt; e0 += 64) {
@@ -457,6 +641,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
     if (lane == 0) runStart[n] = (int16_t)cnt, nRunsS = n;
   }
   __syncthreads();
+  SCHUR_T(t2);
+#ifdef VIBA_SCHUR_TIMING
+  unsigned long long tk = 0, tr = 0;
+#endif
   const int nRuns = nRunsS;
   uint8_t* posI = posW[wave][0];
   uint8_t* posJ = posW[wave][1];
@@ -486,6 +674,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
       // tile): no per-MFMA predicates, gathers at immediate offsets from per-step base pointers
       const int nr = min(kTR, nbJ - a0);
       const int sel = ((nbI - 1) * 2 + (nr - 1)) * 2 + (diag ? 1 : 0);
+      SCHUR_T(ta);
       switch (sel) {
 #define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
   case ((NBI - 1) * 2 + (NR - 1)) * 2:                                                                \
@@ -499,17 +688,113 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
 #undef VIBA_SCHUR_CASE
         default: break;
       }
-      if (diag && a0 == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
-        double racc = 0.0;
-        for (int e = c0; e < c0 + nl; e++) {
-          const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
-          const double* zz = d.z + 3 * (int64_t)ents[e].lm;
-          racc += (double)y[0] * zz[0] + (double)y[d.nYcol] * zz[1] + (double)y[2 * d.nYcol] * zz[2];
-        }
-        atomicAdd(&rq[posI[lane]], -racc);
-      }
+      SCHUR_T(tb);
+      if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
+#ifdef VIBA_SCHUR_TIMING
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      SCHUR_T(tc);
+      tk += tb - ta, tr += tc - tb;
+#endif
     }
     if (mapped) __builtin_amdgcn_wave_barrier();  // the maps are rewritten by this wave's next run
+  }
+  SCHUR_T(t3);
+  __syncthreads();
+  SCHUR_T(t4);
+  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
+  if (wk.kind) {
+    for (int i = tid; i < TS * TS; i += 256)
+      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else {
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
+  }
+  if (diag && tid < TS) {
+    const int64_t row = (int64_t)wk.I * TS + tid;
+    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
+  }
+#ifdef VIBA_SCHUR_TIMING
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  SCHUR_T(t5);
+  if (lane == 0) {
+    atomicAdd(&g_schur_t[0], t1 - t0);
+    atomicAdd(&g_schur_t[1], t2 - t1);
+    atomicAdd(&g_schur_t[2], t3 - t2);
+    atomicAdd(&g_schur_t[3], tk);
+    atomicAdd(&g_schur_t[4], tr);
+    atomicAdd(&g_schur_t[5], t4 - t3);
+    atomicAdd(&g_schur_t[6], t5 - t4);
+    atomicAdd(&g_schur_t[7], 1ull);
+  }
+#endif
+}
+
+// schur_run2's assembly with its per-item bookkeeping moved to finalize (api.hip): the item's runs
+// (masks) and tasks come precomputed, the tasks dealt to the waves longest-first (TileWork::wOff), so
+// the kernel has no run scan (wave 0 reading every entry's masks from global), no per-run global mask
+// reads by every wave, no skipping over other waves' tasks, and balanced waves at the final barrier
+// (measured in a -DVIBA_SCHUR_TIMING build of schur_run2 on config C: 5 % run scan, ~29 % task
+// bookkeeping outside the k-loops, 7.6 % waiting at the final barrier).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_SCHUR_WPE, VIBA_SCHUR_WPE))) schur_run4_kernel(Dev d, double lambda) {
+  static_assert(kCh == kSchurCh && kTR == kSchurTR, "finalize's task shapes (engine.hpp) and the kernel's");
+  __shared__ double C[TS * TS];
+  __shared__ uint32_t ecol[256][2];
+  __shared__ uint64_t rmask[256][2];
+  __shared__ uint8_t posW[4][2][TS];
+  __shared__ double rq[TS];
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
+  const TileWork* wp = d.tileWorks + w;  // fields read in place (a by-value copy went to scratch:
+  const TileWork wk = *wp;                 // wOff is indexed by the wave)
+  const bool diag = wk.I == wk.J;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int cnt = wk.count;
+  const TileEnt* ents = d.tileEnts + wk.start;
+  if (tid < cnt) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
+  if (tid < wk.nRuns) {
+    const uint64_t* rm = d.schurRuns + 2 * ((int64_t)wk.runFirst + tid);
+    rmask[tid][0] = rm[0], rmask[tid][1] = rm[1];
+  }
+  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
+  if (tid < TS) rq[tid] = 0.0;
+  __syncthreads();
+  uint8_t* posI = posW[wave][0];
+  uint8_t* posJ = posW[wave][1];
+  const uint2* ec2 = reinterpret_cast<const uint2*>(&ecol[0][0]);
+  const uint32_t* tasks = d.schurTasks + wk.taskFirst;
+  const int t0 = wp->wOff[wave], t1 = wp->wOff[wave + 1];
+  int cur = -1;
+  for (int t = t0; t < t1; t++) {
+    const uint32_t code = __builtin_amdgcn_readfirstlane(tasks[t]);
+    const int r = code & 255, c0 = (code >> 8) & 255, nl = (code >> 16) & 31, a0 = (code >> 21) & 3;
+    const uint64_t mI = uniform64(rmask[r][0]), mJ = uniform64(rmask[r][1]);
+    const int nI = __popcll(mI), nJ = __popcll(mJ);
+    const int nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4;
+    if (r != cur) {  // the run's compact -> tile row maps (wave-private)
+      __builtin_amdgcn_wave_barrier();  // the previous run's readers are done
+      if ((mI >> lane) & 1) posI[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
+      if ((mJ >> lane) & 1) posJ[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      cur = r;
+    }
+    const int rows = 3 * nl;
+    const int nr = min(kTR, nbJ - a0);
+    const int sel = ((nbI - 1) * 2 + (nr - 1)) * 2 + (diag ? 1 : 0);
+    switch (sel) {
+#define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
+  case ((NBI - 1) * 2 + (NR - 1)) * 2:                                                                \
+    schur_task<NBI, NR, false>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                 \
+    break;                                                                                            \
+  case ((NBI - 1) * 2 + (NR - 1)) * 2 + 1:                                                            \
+    schur_task<NBI, NR, true>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                  \
+    break;
+      VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(2, 2)
+      VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 1) VIBA_SCHUR_CASE(4, 2)
+#undef VIBA_SCHUR_CASE
+      default: break;
+    }
+    if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
   }
   __syncthreads();
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
@@ -532,34 +817,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
 // is then one broadcast ds_read_b64 of its row's offsets, two 64-bit address adds and the NR + NBI
 // gathers at immediate offsets, one step ahead of the MFMAs (schur_run2's per-step landmark / plane
 // advance, bounds select and plane-base select were ~20 VALU + 17 SALU per MFMA: DESIGN.md §8).
-#ifndef VIBA_SCHUR_ASMLD
-#define VIBA_SCHUR_ASMLD 1
-#endif
-// one gather of an 8-B (fp64) / 4-B (fp32) operand at an immediate byte offset I * STRIDE, as inline asm
-// (invisible to hipcc's waitcnt pass: the caller waits with vm_wait and pins the destination)
-template <int STRIDE>
-__device__ __forceinline__ void gather_asm(double& dst, const double* p, int i) {
-  switch (i) {
-    case 0: asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
-    case 1: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
-    case 2: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
-    default: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
-  }
-}
-template <int STRIDE>
-__device__ __forceinline__ void gather_asm(float& dst, const float* p, int i) {
-  switch (i) {
-    case 0: asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
-    case 1: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
-    case 2: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
-    default: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
-  }
-}
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 template <int NBI, int NR, int DA0>
 __device__ __forceinline__ void schur_task3(const Dev& d, const uint2* rowOff, int nks, int a0r, int l4, int l15,
                                             const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
@@ -636,23 +893,7 @@ __device__ __forceinline__ void schur_task3(const Dev& d, const uint2* rowOff, i
       mm(a1v, b1v);
     }
   }
-  int colT[NBI];
-#pragma unroll
-  for (int b = 0; b < NBI; b++) {
-    const int n = 16 * b + l15;
-    colT[b] = n < nI ? posI[n] : -1;
-  }
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q;
-      if (m >= nJ) continue;
-      double* Cr = C + posJ[m] * TS;
-#pragma unroll
-      for (int b = 0; b < NBI; b++)
-        if ((!DIAG || a0 + i <= b) && colT[b] >= 0) atomicAdd(Cr + colT[b], -(double)acc[i][b][q]);
-    }
+  schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run3_kernel(Dev d, double lambda) {
@@ -743,15 +984,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
 #undef VIBA_SCHUR_DCASE
         default: break;
       }
-      if (diag && a0 == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
-        double racc = 0.0;
-        for (int e = c0; e < c0 + nl; e++) {
-          const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
-          const double* zz = d.z + 3 * (int64_t)ents[e].lm;
-          racc += (double)y[0] * zz[0] + (double)y[d.nYcol] * zz[1] + (double)y[2 * d.nYcol] * zz[2];
-        }
-        atomicAdd(&rq[posI[lane]], -racc);
-      }
+      if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
     }
     if (mapped) __builtin_amdgcn_wave_barrier();
   }
@@ -2152,12 +2385,14 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
   if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
-  // VIBA_SCHUR_V=3: the K-row offsets from an LDS table with hand-counted gathers (schur_run3_kernel);
-  // measured r03a on config C: Schur phase 6.50 ms against 6.15 for schur_run2 (the default)
-  static const int v = getenv("VIBA_SCHUR_V") ? atoi(getenv("VIBA_SCHUR_V")) : 2;
+  // VIBA_SCHUR_V: 4 (default) precomputed runs and balanced tasks (schur_run4_kernel); 2 the run scan in
+  // the kernel (schur_run2_kernel); 3 schur_run2 with the K-row offsets from an LDS table and hand-counted
+  // gathers (schur_run3_kernel; measured r03a on config C: Schur phase 6.50 ms against 6.15 for run2)
+  static const int v = getenv("VIBA_SCHUR_V") ? atoi(getenv("VIBA_SCHUR_V")) : 4;
   if (d.nTileWorks) {
     if (v == 2) launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else launchK(schur_run3_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else if (v == 3) launchK(schur_run3_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else launchK(schur_run4_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
   }
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
@@ -2280,5 +2515,16 @@ void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, h
 #ifdef VIBA_POTRF_TIMING
 extern "C" int vb_debug_potrf_times(long long* out32) {
   return hipMemcpyFromSymbol(out32, HIP_SYMBOL(viba::g_potrf_t), 32 * sizeof(long long)) == hipSuccess ? 0 : -3;
+}
+#endif
+
+#ifdef VIBA_SCHUR_TIMING
+extern "C" int vb_debug_schur_times(unsigned long long* out8, int reset) {
+  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(viba::g_schur_t), 8 * sizeof(unsigned long long)) != hipSuccess) return -3;
+  if (reset) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(viba::g_schur_t), z, sizeof(z)) != hipSuccess) return -3;
+  }
+  return 0;
 }
 #endif
