@@ -1221,7 +1221,7 @@ int doFinalize(vb_handle h) {
             for (int i = 0; i < nr; i++)
               for (int b = 0; b < nbI; b++) mf += (!diag || a0 + i <= b) ? 1 : 0;
             const double cost = nks * (16.0 * mf + 3.0 * (nr + nbI)) + 6.0 * mf + 24.0 + (diag && a0 == 0 ? 6.0 * nl : 0.0);
-            tl.push_back({(uint32_t)r | ((uint32_t)c0 << 8) | ((uint32_t)nl << 16) | ((uint32_t)a0 << 21), cost});
+            tl.push_back({(uint32_t)r | ((uint32_t)c0 << 8) | ((uint32_t)nl << 16) | ((uint32_t)a0 << 22), cost});
           }
       }
       std::stable_sort(tl.begin(), tl.end(), [](const Tk& a, const Tk& b) { return a.cost > b.cost; });

@@ -126,8 +126,14 @@ struct TileWork {
   uint16_t nRuns, wOff[5];
 };
 // one task of schur_run4_kernel (32 bits): run (8) | first entry of its landmark chunk (8) | landmarks
-// (5) | first compact block row (2); built at finalize with kSchurCh landmarks x kSchurTR block rows
-constexpr int kSchurCh = 16, kSchurTR = 2;
+// (6) | first compact block row (2); built at finalize with kSchurCh landmarks x kSchurTR block rows
+#ifndef VIBA_SCHUR_CH
+#define VIBA_SCHUR_CH 16
+#endif
+#ifndef VIBA_SCHUR_TR
+#define VIBA_SCHUR_TR 2
+#endif
+constexpr int kSchurCh = VIBA_SCHUR_CH, kSchurTR = VIBA_SCHUR_TR;
 
 struct Dev {
   // variables

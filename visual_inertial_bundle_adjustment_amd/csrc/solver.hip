@@ -363,6 +363,9 @@ constexpr int kPF = VIBA_SCHUR_PF;  // k-steps of operand gathers in flight
 #ifndef VIBA_SCHUR_PFD
 #define VIBA_SCHUR_PFD 0
 #endif
+#ifndef VIBA_SCHUR_EXPT
+#define VIBA_SCHUR_EXPT 0
+#endif
 
 // One task's K loop: acc[i][b] += A_i^T B_b over the dense K rows (3 per landmark) of landmarks
 // c0 .. c0 + rows / 3, A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block
@@ -495,7 +498,12 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
   int kr = l4, e = c0 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
   auto ld = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
     const bool kv = kr < rows;
+#if VIBA_SCHUR_EXPT == 1
+    // diagnostic build: every gather inside the first 4096 panel columns (L2-resident), results garbage
+    const uint2 c = make_uint2(ec[kv ? e : c0].x & 4095u, ec[kv ? e : c0].y & 4095u);
+#else
     const uint2 c = ec[kv ? e : c0];
+#endif
     const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
     const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
     const rec_t* pI = kv ? base + c.x : zp;
@@ -507,11 +515,19 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     if (q == 3) q = 0, e += 1;
   };
   auto mm = [&](const rec_t (&av)[NR], const rec_t (&bv)[NBI]) {
+#if VIBA_SCHUR_EXPT == 2
+    // diagnostic build: no MFMAs (the operands are still consumed), results garbage
+#pragma unroll
+    for (int i = 0; i < NR; i++)
+#pragma unroll
+      for (int b = 0; b < NBI; b++) acc[i][b][0] += av[i] + bv[b];
+#else
 #pragma unroll
     for (int i = 0; i < NR; i++)
 #pragma unroll
       for (int b = 0; b < NBI; b++)
         if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
+#endif
   };
 #if VIBA_SCHUR_PFD > 0
   // the gathers as inline-asm loads counted by hand (hipcc's waitcnt pass put a vmcnt(0) in front of
@@ -741,6 +757,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
   __shared__ uint64_t rmask[256][2];
   __shared__ uint8_t posW[4][2][TS];
   __shared__ double rq[TS];
+  SCHUR_T(t0);
   const int64_t w = xcd_block(blockIdx.x, gridDim.x);
   const TileWork* wp = d.tileWorks + w;  // fields read in place (a by-value copy went to scratch:
   const TileWork wk = *wp;                 // wOff is indexed by the wave)
@@ -757,15 +774,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
   for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
   if (tid < TS) rq[tid] = 0.0;
   __syncthreads();
+  SCHUR_T(t1);
+  SCHUR_T(t2);
+#ifdef VIBA_SCHUR_TIMING
+  unsigned long long tk = 0, tr = 0;
+#endif
   uint8_t* posI = posW[wave][0];
   uint8_t* posJ = posW[wave][1];
   const uint2* ec2 = reinterpret_cast<const uint2*>(&ecol[0][0]);
   const uint32_t* tasks = d.schurTasks + wk.taskFirst;
-  const int t0 = wp->wOff[wave], t1 = wp->wOff[wave + 1];
+  const int tBeg = wp->wOff[wave], tEnd = wp->wOff[wave + 1];
   int cur = -1;
-  for (int t = t0; t < t1; t++) {
+  for (int t = tBeg; t < tEnd; t++) {
     const uint32_t code = __builtin_amdgcn_readfirstlane(tasks[t]);
-    const int r = code & 255, c0 = (code >> 8) & 255, nl = (code >> 16) & 31, a0 = (code >> 21) & 3;
+    const int r = code & 255, c0 = (code >> 8) & 255, nl = (code >> 16) & 63, a0 = (code >> 22) & 3;
     const uint64_t mI = uniform64(rmask[r][0]), mJ = uniform64(rmask[r][1]);
     const int nI = __popcll(mI), nJ = __popcll(mJ);
     const int nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4;
@@ -781,6 +803,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
     const int rows = 3 * nl;
     const int nr = min(kTR, nbJ - a0);
     const int sel = ((nbI - 1) * 2 + (nr - 1)) * 2 + (diag ? 1 : 0);
+    SCHUR_T(ta);
     switch (sel) {
 #define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
   case ((NBI - 1) * 2 + (NR - 1)) * 2:                                                                \
@@ -794,9 +817,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
 #undef VIBA_SCHUR_CASE
       default: break;
     }
+#ifdef VIBA_SCHUR_TIMING
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+    SCHUR_T(tb);
     if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
+#ifdef VIBA_SCHUR_TIMING
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    SCHUR_T(tc);
+    tk += tb - ta, tr += tc - tb;
+#endif
   }
+  SCHUR_T(t3);
   __syncthreads();
+  SCHUR_T(t4);
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
   if (wk.kind) {
     for (int i = tid; i < TS * TS; i += 256)
@@ -808,6 +842,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
     const int64_t row = (int64_t)wk.I * TS + tid;
     if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
   }
+#ifdef VIBA_SCHUR_TIMING
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  SCHUR_T(t5);
+  if (lane == 0) {
+    atomicAdd(&g_schur_t[0], t1 - t0);
+    atomicAdd(&g_schur_t[1], t2 - t1);
+    atomicAdd(&g_schur_t[2], t3 - t2);
+    atomicAdd(&g_schur_t[3], tk);
+    atomicAdd(&g_schur_t[4], tr);
+    atomicAdd(&g_schur_t[5], t4 - t3);
+    atomicAdd(&g_schur_t[6], t5 - t4);
+    atomicAdd(&g_schur_t[7], 1ull);
+  }
+#endif
 }
 
 // The same assembly with the K-row bookkeeping taken out of the k-loop (schur_run3_kernel, default):
