@@ -366,7 +366,7 @@ struct vb_handle_s {
   // state
   bool linearized = false, factored = false;
   vb_phase_times times{};
-  hipEvent_t ev[10];
+  hipEvent_t ev[12];
   // side stream: the small (non-visual) factor kernels -- few waves, latency-bound -- run beside
   // the visual kernels, forked after the buffer resets and joined before their first consumer
   hipStream_t st2 = nullptr;
@@ -1194,7 +1194,7 @@ int doFinalize(vb_handle h) {
     // kept in (run, chunk) order per wave, so a wave rebuilds its row maps only when its run changes
     // (schur_run4_kernel: no run scan, no per-run global mask reads, balanced waves)
     std::vector<uint64_t> runsH;
-    std::vector<uint32_t> tasksH;
+    std::vector<uint32_t> tasksH, chunksH;
     for (TileWork& w : works) {
       const bool diag = w.I == w.J;
       std::vector<int> rs;
@@ -1209,6 +1209,11 @@ int doFinalize(vb_handle h) {
         double cost;
       };
       std::vector<Tk> tl;
+      w.chunkFirst = (int32_t)chunksH.size();
+      for (size_t r = 0; r + 1 < rs.size(); r++)
+        for (int c0 = rs[r]; c0 < rs[r + 1]; c0 += kSchurCh5)
+          chunksH.push_back((uint32_t)r | ((uint32_t)c0 << 8) | ((uint32_t)std::min(kSchurCh5, rs[r + 1] - c0) << 16));
+      w.nChunks = (uint16_t)(chunksH.size() - w.chunkFirst);
       for (size_t r = 0; r + 1 < rs.size(); r++) {
         const uint64_t mI = ents[w.start + rs[r]].maskI, mJ = diag ? mI : ents[w.start + rs[r]].maskJ;
         runsH.push_back(mI), runsH.push_back(mJ);
@@ -1241,7 +1246,7 @@ int doFinalize(vb_handle h) {
       }
       w.wOff[4] = (uint16_t)(tasksH.size() - w.taskFirst);
     }
-    if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH)) return VB_E_HIP;
+    if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH) || upload(&d.schurChunks, chunksH)) return VB_E_HIP;
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
     d.nTileWorks = (int64_t)works.size();
     h->nTileEnt = (int64_t)ents.size(), h->nObEnt = d.nGroups;
@@ -2086,7 +2091,7 @@ int vb_destroy(vb_handle h) {
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.yZero, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
-                  d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.schurRuns, d.schurTasks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
+                  d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.schurRuns, d.schurTasks, d.schurChunks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.redS, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
@@ -2375,8 +2380,8 @@ int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_
   return 0;
 }
 
-int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* cost) {
-  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_linearize before vb_finalize");
+// vb_linearize's device work, no host read (cost in red[0], errors in err)
+int linearizeEnqueue(vb_handle h, int update_cache, int dont_retry_failed) {
   Dev& d = h->d;
   HIPCHK(hipEventRecord(h->ev[0], h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
@@ -2415,6 +2420,12 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   joinSmall(h);
   if (side) HIPCHK(hipStreamWaitEvent(h->st, h->evZJoin, 0));
   HIPCHK(hipEventRecord(h->ev[1], h->st));
+  return 0;
+}
+
+int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* cost) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_linearize before vb_finalize");
+  if (int rc = linearizeEnqueue(h, update_cache, dont_retry_failed)) return rc;
   double c = 0;
   if (int rc = readRed(h, &c, 0, 1)) return rc;
   if (int rc = checkErr(h)) return rc;
@@ -2425,10 +2436,11 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   return 0;
 }
 
-int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reduction) {
-  if (!h || !h->linearized) return fail(VB_E_STATE, "vb_damp_factor_solve needs a fresh vb_linearize");
+// vb_damp_factor_solve's device work (model dot in red[16]); clearErr = false keeps the linearization's
+// error bits for one check at the end of the iteration (vb_optimize)
+int dampFactorSolveEnqueue(vb_handle h, double lambda, bool clearErr) {
   Dev& d = h->d;
-  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  if (clearErr) HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   HIPCHK(hipEventRecord(h->ev[2], h->st));
   profBegin(h, KF_LANDMARK);
   launch_landmark(d, lambda, 0, d.lmB, d.lmE, h->st);
@@ -2456,6 +2468,12 @@ int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reductio
   }
   backSubstitute(h, 0);
   HIPCHK(hipEventRecord(h->ev[5], h->st));
+  return 0;
+}
+
+int vb_damp_factor_solve(vb_handle h, double lambda, double* model_cost_reduction) {
+  if (!h || !h->linearized) return fail(VB_E_STATE, "vb_damp_factor_solve needs a fresh vb_linearize");
+  if (int rc = dampFactorSolveEnqueue(h, lambda, true)) return rc;
   double dotv = 0;
   if (int rc = readRed(h, &dotv, 16, 1)) return rc;
   if (int rc = checkErr(h)) return rc;
@@ -2730,13 +2748,18 @@ int vb_scale_step(vb_handle h, double f) {
   return 0;
 }
 
-int vb_apply_step_raw(vb_handle h, int which, double raw[3]) {
-  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+// box-plus of the step (red[8..10]: the raw step ratios), bracketed by events e0 / e1
+int applyStepEnqueue(vb_handle h, int which, int e0, int e1) {
   Dev& d = h->d;
-  HIPCHK(hipEventRecord(h->ev[6], h->st));
+  HIPCHK(hipEventRecord(h->ev[e0], h->st));
   HIPCHK(hipMemsetAsync(d.red + 8, 0, 3 * sizeof(double), h->st));
   launch_boxplus(d, which ? d.subRed : d.stepRed, which ? d.subPt : d.stepPt, h->st);
-  HIPCHK(hipEventRecord(h->ev[7], h->st));
+  HIPCHK(hipEventRecord(h->ev[e1], h->st));
+  return 0;
+}
+int vb_apply_step_raw(vb_handle h, int which, double raw[3]) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  if (int rc = applyStepEnqueue(h, which, 6, 7)) return rc;
   double r[3];
   if (int rc = readRed(h, r, 8, 3)) return rc;
   h->times.step_ms = elapsed(h->ev[6], h->ev[7]);
@@ -2752,26 +2775,34 @@ int vb_apply_step(vb_handle h, int which, double ratios[3]) {
 }
 int64_t vb_num_params(vb_handle h) { return h ? h->nParams : -1; }
 
-int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
-  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+// the cost pass (red[1..4]: cost and CostStats), bracketed by ev[6] / ev[7]
+int costEnqueue(vb_handle h, int comparable, bool clearErr) {
   Dev& d = h->d;
   HIPCHK(hipEventRecord(h->ev[6], h->st));
   HIPCHK(hipMemsetAsync(d.red + 1, 0, 4 * sizeof(double), h->st));
-  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  if (clearErr) HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   forkSmall(h, 2, nullptr);
   visualCostShard(h, comparable);
   joinSmall(h);
   HIPCHK(hipEventRecord(h->ev[7], h->st));
+  return 0;
+}
+void costStats(vb_handle h, const double* r, double* cost, vb_cost_stats* stats) {
+  int64_t nSmall = 0;
+  if (h->isRoot)
+    for (int k = 1; k < 14; k++) nSmall += h->d.sf[k].n;
+  if (cost) *cost = r[0];
+  if (stats) stats->num_total = (int64_t)std::llround(r[1]) + nSmall, stats->num_invalid = std::llround(r[2]),
+             stats->num_prev_invalid = std::llround(r[3]);
+}
+int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
+  if (int rc = costEnqueue(h, comparable, true)) return rc;
   double r[4];
   if (int rc = readRed(h, r, 1, 4)) return rc;
   if (int rc = checkErr(h)) return rc;
   h->times.cost_ms = elapsed(h->ev[6], h->ev[7]);
-  int64_t nSmall = 0;
-  if (h->isRoot)
-    for (int k = 1; k < 14; k++) nSmall += d.sf[k].n;
-  if (cost) *cost = r[0];
-  if (stats) stats->num_total = (int64_t)std::llround(r[1]) + nSmall, stats->num_invalid = std::llround(r[2]),
-             stats->num_prev_invalid = std::llround(r[3]);
+  costStats(h, r, cost, stats);
   return 0;
 }
 
@@ -2917,12 +2948,32 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     const bool preint = h->recomputePreint && h->pi.n > 0;
     if ((h->rsDevice || preint) && (rc = rsUpdateAsync(h, h->rsDevice, preint))) return rc;
     if (pre) pre(it, user);
-    double prevCost;
-    if ((rc = vb_linearize(h, 1, dontRetry, &prevCost))) return rc;
+    // linearize, damp + eliminate + factor + solve, backup, box-plus and the cost pass queued back to back;
+    // the host reads their scalars (costs, CostStats, model reduction, step ratios) and errors once,
+    // after the cost pass: none of them changes what the queued work does
+    double prevCost, modelRed, ratios[3], newCost;
+    vb_cost_stats st;
+    if ((rc = linearizeEnqueue(h, 1, dontRetry)) || (rc = dampFactorSolveEnqueue(h, damping, false)) ||
+        (rc = vb_backup(h)) || (rc = applyStepEnqueue(h, 0, 10, 11)) || (rc = costEnqueue(h, 1, false)))
+      return rc;
+    {
+      double r[17];
+      if ((rc = readRed(h, r, 0, 17)) || (rc = checkErr(h))) return rc;
+      prevCost = r[0], modelRed = 0.5 * r[16];
+      const double n = (double)std::max<int64_t>(1, h->nParams);
+      ratios[0] = r[8], ratios[1] = std::sqrt(r[9] / n), ratios[2] = r[10] / n;
+      costStats(h, r + 1, &newCost, &st);
+      h->times.linearize_ms = elapsed(h->ev[0], h->ev[1]);
+      if (h->rsTimed) h->times.rs_update_ms = elapsed(h->ev[8], h->ev[9]), h->rsTimed = false;
+      h->times.schur_ms = elapsed(h->ev[2], h->ev[3]);
+      h->times.factor_ms = elapsed(h->ev[3], h->ev[4]);
+      h->times.solve_ms = elapsed(h->ev[4], h->ev[5]);
+      h->times.step_ms = elapsed(h->ev[10], h->ev[11]);
+      h->times.cost_ms = elapsed(h->ev[6], h->ev[7]);
+      h->linearized = false, h->factored = true;
+    }
     finalCost = prevCost;
     if (it == 0) initialCost = prevCost;
-    double modelRed;
-    if ((rc = vb_damp_factor_solve(h, damping, &modelRed))) return rc;
     if (it == h->faultNegModelRedIt) modelRed = -modelRed;  // test fault injection
     if (modelRed < 0) {
       // Optimizer.cpp:835-854: the reference re-linearizes into `hess` at the same point (the caches
@@ -2933,12 +2984,6 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
       // factor (tests/test_parity_configs.py forces this branch).
       damping *= s.damping_adjust_on_fail;
     }
-    if ((rc = vb_backup(h))) return rc;
-    double ratios[3];
-    if ((rc = vb_apply_step(h, 0, ratios))) return rc;
-    vb_cost_stats st;
-    double newCost;
-    if ((rc = vb_cost(h, 1, &newCost, &st))) return rc;
     double costRed = prevCost - newCost;
     const double ratioRedToCost = costRed / newCost;
     double ratioRedToExp = costRed / modelRed;

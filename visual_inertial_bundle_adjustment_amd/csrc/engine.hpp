@@ -124,6 +124,10 @@ struct TileWork {
   // tasks at schurTasks[taskFirst ..), wave w's at [wOff[w], wOff[w + 1])
   int32_t runFirst, taskFirst;
   uint16_t nRuns, wOff[5];
+  // schur_run5_kernel: the item's landmark chunks (run | first entry << 8 | landmarks << 16, at most
+  // kSchurCh5 landmarks each) at schurChunks[chunkFirst ..)
+  int32_t chunkFirst;
+  uint16_t nChunks, pad2;
 };
 // one task of schur_run4_kernel (32 bits): run (8) | first entry of its landmark chunk (8) | landmarks
 // (6) | first compact block row (2); built at finalize with kSchurCh landmarks x kSchurTR block rows
@@ -134,6 +138,10 @@ struct TileWork {
 #define VIBA_SCHUR_TR 2
 #endif
 constexpr int kSchurCh = VIBA_SCHUR_CH, kSchurTR = VIBA_SCHUR_TR;
+#ifndef VIBA_SCHUR_CH5
+#define VIBA_SCHUR_CH5 12
+#endif
+constexpr int kSchurCh5 = VIBA_SCHUR_CH5;
 
 struct Dev {
   // variables
@@ -192,6 +200,7 @@ struct Dev {
   TileWork* tileWorks = nullptr;
   uint64_t* schurRuns = nullptr;   // per run: maskI, maskJ
   uint32_t* schurTasks = nullptr;
+  uint32_t* schurChunks = nullptr;
   TileEnt* tileEnts = nullptr;
   int32_t* tileObs = nullptr;  // (unused: direct terms go through the observation groups)
   // direct visual terms by observation group (observations sharing their 4 reduced blocks: one rig,

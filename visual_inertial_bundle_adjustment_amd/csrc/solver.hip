@@ -858,6 +858,147 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
 #endif
 }
 
+// Schur assembly with the operands staged in LDS (schur_run5_kernel): the workgroup walks its item's
+// landmark chunks (<= kSchurCh5 landmarks of one run, api.hip); per chunk all 256 threads gather the
+// chunk's compact panel rows -- K = 3 rows per landmark, 16 columns per block, the I-side blocks and (off
+// the diagonal) the J-side blocks -- into LDS with every load in flight at once, then the four waves
+// run the chunk's MFMAs from LDS.  A wave owns output blocks of the run (up to four; shapes with fewer
+// than four blocks split the k-steps two or four ways), and its accumulators persist over the run's
+// chunks: the compact -> tile scatter into the LDS tile (LDS atomics) happens once per run, not once per
+// task.  Two workgroups per CU (77 KB of LDS each): one stages while the other multiplies.  Diagonal
+// tiles also form rhs -= Y^T z from the staged I-side rows.
+constexpr int kCh5 = kSchurCh5;
+constexpr int kK5 = ((3 * kCh5 + 3) / 4) * 4;  // staged K rows per chunk (the MFMA's K = 4 steps)
+constexpr int kSB5 = kK5 * 16;                  // elements per staged 16-column block
+
+__global__ void __launch_bounds__(256, 2) schur_run5_kernel(Dev d, double lambda) {
+  __shared__ double C[TS * TS];
+  __shared__ rec_t stg[8 * kSB5];
+  __shared__ uint32_t ecol[256][2];
+  __shared__ uint64_t rmask[256][2];
+  __shared__ uint8_t posIs[TS], posJs[TS];
+  __shared__ double rq[TS];
+  __shared__ double zst[kK5];
+  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
+  const TileWork* wp = d.tileWorks + w;
+  const TileWork wk = *wp;
+  const bool diag = wk.I == wk.J;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const TileEnt* ents = d.tileEnts + wk.start;
+  if (tid < wk.count) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
+  if (tid < wk.nRuns) {
+    const uint64_t* rm = d.schurRuns + 2 * ((int64_t)wk.runFirst + tid);
+    rmask[tid][0] = rm[0], rmask[tid][1] = rm[1];
+  }
+  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
+  if (tid < TS) rq[tid] = 0.0;
+  const uint32_t* chunks = d.schurChunks + wk.chunkFirst;
+  const int64_t pq = d.nYcol;
+  // the wave's units of the current run: output block (ui, ub), k-steps [p nks / P, (p + 1) nks / P)
+  int nu = 0, ui[4] = {0, 0, 0, 0}, ub[4] = {0, 0, 0, 0}, up[4] = {0, 0, 0, 0}, P = 1;
+  hacc4_t acc[4];
+  int cur = -1, nI = 0, nJ = 0, nbI = 0, nbJ = 0;
+  auto flush = [&]() {  // C -= the wave's accumulated blocks of the current run (LDS atomics)
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      if (m >= nu) break;
+      const int n = 16 * ub[m] + l15;
+      const int colT = posIs[min(n, TS - 1)];
+      int rowT[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) rowT[q] = posJs[min(16 * ui[m] + kAccL4 * l4 + kAccR * q, TS - 1)];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (n < nI && 16 * ui[m] + kAccL4 * l4 + kAccR * q < nJ) atomicAdd(&C[rowT[q] * TS + colT], -(double)acc[m][q]);
+    }
+  };
+  for (int ci = 0; ci < wk.nChunks; ci++) {
+    const uint32_t code = __builtin_amdgcn_readfirstlane(chunks[ci]);
+    const int r = code & 255, c0 = (code >> 8) & 255, nl = (code >> 16) & 63;
+    if (r != cur && cur >= 0) flush();
+    __syncthreads();  // flushes, the previous chunk's MFMAs and rhs are done with the maps and the stage
+    if (r != cur) {
+      const uint64_t mI = uniform64(rmask[r][0]), mJ = diag ? mI : uniform64(rmask[r][1]);
+      nI = __popcll(mI), nJ = __popcll(mJ), nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4;
+      if (wave == 0) {
+        if ((mI >> lane) & 1) posIs[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
+        if ((mJ >> lane) & 1) posJs[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
+      }
+      // the run's output blocks (row-major; diagonal tiles: b >= i), split over the waves
+      int nblk = 0;
+      for (int i = 0; i < nbJ; i++) nblk += diag ? nbI - i : nbI;
+      P = nblk >= 4 ? 1 : nblk == 1 ? 4 : 2;
+      nu = 0;
+      for (int u = wave; u < nblk * P && nu < 4; u += 4) {
+        int j = u % nblk, i = 0;
+        while (j >= (diag ? nbI - i : nbI)) j -= diag ? nbI - i : nbI, i++;
+        ui[nu] = i, ub[nu] = diag ? i + j : j, up[nu] = u / nblk, nu++;
+      }
+#pragma unroll
+      for (int m = 0; m < 4; m++) acc[m] = hacc4_t{0, 0, 0, 0};
+      cur = r;
+    }
+    // stage the chunk: row-block rb = (side-block sb, K row kr) holds 16 doubles of plane q of landmark
+    // c0 + kr / 3 from its first panel column in tile I (sb < nbI) or J; rows past the landmarks zero
+    const int nsb = diag ? nbI : nbI + nbJ, total = nsb * kK5, K = 3 * nl;
+    {
+      const int l16 = tid & 15, rb0 = tid >> 4;
+      constexpr int kU = (8 * kK5 + 15) / 16;
+      rec_t v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const int rb = rb0 + 16 * u, sb = rb / kK5, kr = rb - sb * kK5;
+        v[u] = rec_t(0);
+        if (rb < total && kr < K) {
+          const int e = c0 + kr / 3, q = kr - 3 * (kr / 3);
+          const uint32_t col = sb < nbI ? ecol[e][0] + 16u * sb : ecol[e][1] + 16u * (sb - nbI);
+          v[u] = d.Y[q * pq + col + l16];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const int rb = rb0 + 16 * u;
+        if (rb < total) stg[rb * 16 + l16] = v[u];
+      }
+      if (diag && tid < kK5) zst[tid] = tid < K ? d.z[3 * (int64_t)ents[c0 + tid / 3].lm + tid % 3] : 0.0;
+    }
+    __syncthreads();
+    const int nks = (K + 3) >> 2;
+    const rec_t* sI = stg;
+    const rec_t* sJ = diag ? stg : stg + nbI * kSB5;
+    int klo[4], khi[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) klo[m] = up[m] * nks / P, khi[m] = (up[m] + 1) * nks / P;
+    for (int ks = 0; ks < nks; ks++) {
+      const int row = (4 * ks + l4) * 16 + l15;
+#pragma unroll
+      for (int m = 0; m < 4; m++)
+        if (m < nu && ks >= klo[m] && ks < khi[m])
+          acc[m] = mfma_h(sJ[ui[m] * kSB5 + row], sI[ub[m] * kSB5 + row], acc[m]);
+    }
+    if (diag && wave == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
+      const rec_t* y = sI + (lane >> 4) * kSB5 + (lane & 15);
+      double racc = 0.0;
+      for (int kr = 0; kr < K; kr++) racc += (double)y[kr * 16] * zst[kr];
+      atomicAdd(&rq[posIs[lane]], -racc);
+    }
+  }
+  if (cur >= 0) flush();
+  __syncthreads();
+  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
+  if (wk.kind) {
+    for (int i = tid; i < TS * TS; i += 256)
+      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else {
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
+  }
+  if (diag && tid < TS) {
+    const int64_t row = (int64_t)wk.I * TS + tid;
+    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
+  }
+}
+
 // The same assembly with the K-row bookkeeping taken out of the k-loop (schur_run3_kernel, default):
 // before a task, the wave writes one (I-side, J-side) element offset per K row into an LDS table --
 // row kr = 3 e + q of the task's landmarks -> q * nYcol + the entry's first panel column in tile I / J
@@ -2440,6 +2581,7 @@ void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) 
   if (d.nTileWorks) {
     if (v == 2) launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
     else if (v == 3) launchK(schur_run3_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
+    else if (v == 5) launchK(schur_run5_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
     else launchK(schur_run4_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
   }
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
