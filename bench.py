@@ -70,13 +70,15 @@ def host_threads() -> tuple[int, int]:
     return max(1, min(nproc, share)), nproc
 
 
-def cpu_baseline(p, name: str = "C", steps: int = 1, recompute_preint: bool = False):
+def cpu_baseline(p, name: str = "C", steps: int = 1, recompute_preint: bool = False, warmup: int = 0):
     """The CPU baseline of BASELINE.md, measured on the FULL workload (no slice, no extrapolation):
     oracle/refcpu (this repository's restatement of the reference path: factor functors, the LM loop,
-    point elimination + blocked Cholesky) runs `steps` iterations of Optimizer::optimize on the same
-    generated problem, at 8 threads (the reference's numThreads default, Optimizer.h:42 /
-    Settings.h:87) and at the host's thread count.  Each run starts from the same variables.  Reports
-    iterations/s per thread count and the last iteration's phase split."""
+    point elimination + blocked Cholesky) runs `warmup` untimed iterations (as the GPU bench does, so the
+    timed iteration starts from the same kind of state as the GPU's), then times `steps` iterations of
+    Optimizer::optimize on the same generated problem, at 8 threads (the reference's numThreads default,
+    Optimizer.h:42 / Settings.h:87) and at the host's thread count.  Each timed run starts from the
+    variables after the warmup.  Reports iterations/s per thread count and the last iteration's phase
+    split."""
     from oracle.refcpu import RefEngine
     from visual_inertial_bundle_adjustment_amd import synth
     from visual_inertial_bundle_adjustment_amd.engine import Settings
@@ -86,6 +88,12 @@ def cpu_baseline(p, name: str = "C", steps: int = 1, recompute_preint: bool = Fa
     log(f"[bench] cpu baseline: oracle loaded in {time.perf_counter() - t:.1f}s")
     nthr, nproc = host_threads()
     runs = {}
+    if warmup:
+        e.set_threads(nthr)
+        t = time.perf_counter()
+        e.optimize(Settings.default(max_num_iterations=warmup, stop_if_no_improvement_for=10**6,
+                                    distance_from_troubled_iteration=0))
+        log(f"[bench] cpu baseline: {warmup} warmup iteration(s) in {time.perf_counter() - t:.1f}s")
     e.backup()
     for th in sorted({8, nthr}):
         e.restore()
@@ -103,7 +111,8 @@ def cpu_baseline(p, name: str = "C", steps: int = 1, recompute_preint: bool = Fa
     return {"value": runs[best]["value"], "unit": "LM iterations/s", "cores": best, "kind": "port",
             "nproc": nproc, "threads": {str(k): v for k, v in runs.items()},
             "sample": f"{steps} full LM iteration(s) of oracle/refcpu on the whole config-{name} problem "
-                      f"({p.num_obs} obs), measured at 8 threads and at {nthr} (nproc {nproc}); value = the faster"}
+                      f"({p.num_obs} obs) after {warmup} untimed warmup iteration(s), measured at 8 threads and at "
+                      f"{nthr} (nproc {nproc}); value = the faster"}
 
 
 def mixed_vs_fp64(p, device, rs_device):
@@ -268,7 +277,7 @@ def main():
     if not args.no_cpu_baseline:
         e.close()  # free the device before the host run
         try:
-            cpu = cpu_baseline(p, args.config, recompute_preint=args.recompute_preint)
+            cpu = cpu_baseline(p, args.config, recompute_preint=args.recompute_preint, warmup=args.warmup)
         except Exception as ex:  # the baseline must never hide the GPU number
             log(f"[bench] cpu baseline failed: {ex}")
     out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,

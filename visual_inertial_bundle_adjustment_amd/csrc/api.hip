@@ -337,6 +337,8 @@ struct vb_handle_s {
   // the forward solve of vb_damp_factor_solve rides the factorization's potrf / trsm launches (single
   // handle, 3-launch levels); VIBA_FWD_IN_FACTOR=0 keeps the separate fan-out forward solve
   bool fwdInFactor = true;
+  // a factorization without a solve to follow (vb_compute_covariances): no fused forward solve, eager
+  bool factorOnly = false;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool sharded = false;  // vb_set_landmark_shard called
@@ -1717,7 +1719,7 @@ void factorSeq(vb_handle h, const Sched& S) {
     return;
   }
   // the forward solve of rhsWork into yvec, fused (schedule 0 of a single handle only)
-  const bool fwd = fwdFused(h) && &S == &h->sch[0];
+  const bool fwd = fwdFused(h) && &S == &h->sch[0] && !h->factorOnly;
   double* fb = fwd ? h->rhsWork : nullptr;
   double* fy = fwd ? h->yvec : nullptr;
   for (int32_t L = 0; L < S.nLevels; L++) {
@@ -1782,7 +1784,7 @@ int factorReduced(vb_handle h, int which = 0) {
   const bool prof = h->profFamily == KF_POTRF || h->profFamily == KF_GEMM || h->profFamily == KF_TRSM;
   // (a profiled family runs launch by launch: its per-launch events, recorded as event nodes inside
   // a graph, cost as much as the graph saves -- measured)
-  if (!h->useGraphs || prof) {
+  if (!h->useGraphs || prof || h->factorOnly) {
     factorSeq(h, S);
     return 0;
   }
@@ -2623,7 +2625,10 @@ int vb_compute_covariances(vb_handle h, double damping, int64_t n_blocks, const 
     launch_landmark(d, lam, 0, d.lmB, d.lmE, h->st);
     HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
     launch_schur(d, lam, 1, h->st);
-    if (int rc = factorReduced(h)) return rc;
+    h->factorOnly = true;  // (the fused forward solve would run on a stale right-hand side)
+    const int frc = factorReduced(h);
+    h->factorOnly = false;
+    if (frc) return frc;
     int32_t e = 0;
     HIPCHK(hipMemcpyAsync(&e, d.err, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));

@@ -551,7 +551,7 @@ def run_sharded(args, rank: int, world: int, local: int):
         e.close()
         try:
             from bench import cpu_baseline
-            cpu = cpu_baseline(p, args.config)
+            cpu = cpu_baseline(p, args.config, warmup=args.warmup)
         except Exception as ex:  # the baseline must never hide the GPU number
             log(f"[bench] cpu baseline failed: {ex}")
     out = {"metric": "LM iterations/sec on 10k-pose/300k-landmark VI-BA", "value": iters / elapsed,
