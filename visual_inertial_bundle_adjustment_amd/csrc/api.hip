@@ -36,6 +36,9 @@ void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gO
                           double* backups, double* acc, hipStream_t st);
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st);
 void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st);
+void launch_damp(const Dev& d, double lambda, int addIdentity, hipStream_t st);
+void launch_groups(const Dev& d, double lambda, hipStream_t st);
+void launch_schur_products(const Dev& d, double lambda, hipStream_t st);
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st);
 void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st,
                   const double* fwdB = nullptr, double* fwdY = nullptr);
@@ -80,6 +83,7 @@ void launch_selinv_level(double* tiles, const int32_t* tileIdx, int32_t nT, cons
                          const int32_t* uItems, int nU, const int32_t* zItems, int nZ, const int32_t* dItems, int nD,
                          hipStream_t st);
 void launch_gather(const double* src, const int64_t* idx, int64_t n, double* out, hipStream_t st);
+void launch_zero_tiles(double* tiles, const int32_t* list, int64_t n, hipStream_t st);
 void launch_lp_cast(const double* in, float* out, int64_t n, hipStream_t st);
 void launch_lp_uncast(const float* in, double* out, int64_t n, hipStream_t st);
 void launch_lp_damp(float* t32, const int32_t* tileIdx, int32_t nT, const int64_t* rvOff, const int32_t* rvDim,
@@ -339,6 +343,9 @@ struct vb_handle_s {
   bool fwdInFactor = true;
   // a factorization without a solve to follow (vb_compute_covariances): no fused forward solve, eager
   bool factorOnly = false;
+  // tiles the linearization clears (single handle): every tile but those one Schur item stores whole
+  int32_t* clearTilesD = nullptr;
+  int64_t nClear = 0;
   // shard
   int64_t lmBegin = 0, lmEnd = -1;
   bool sharded = false;  // vb_set_landmark_shard called
@@ -957,7 +964,7 @@ int doFinalize(vb_handle h) {
     const int64_t c0 = h->rvOff[b] / TS, c1 = (h->rvOff[b] + h->rvDim[b] - 1) / TS;
     for (int64_t I = r0; I <= r1; I++)
       for (int64_t J = c0; J <= c1; J++)
-        if (I >= J) pat[I * nT + J] = 1;
+        if (I >= J) pat[I * nT + J] = 3;  // 3: written by a direct term (damping, visual groups, small factors)
   };
   for (int i = 0; i < nRV; i++) coupleBlocks(i, i);
   for (int64_t o = 0; o < nObs; o++)
@@ -980,7 +987,10 @@ int doFinalize(vb_handle h) {
     std::sort(tl.begin(), tl.end());
     tl.erase(std::unique(tl.begin(), tl.end()), tl.end());
     for (size_t a = 0; a < tl.size(); a++)
-      for (size_t b = 0; b <= a; b++) pat[tl[a] * nT + tl[b]] = 1;
+      for (size_t b = 0; b <= a; b++) {
+        uint8_t& q = pat[tl[a] * nT + tl[b]];
+        q = q ? q : 1;  // 1: landmark (Schur) terms only
+      }
   }
   for (int fk = 1; fk < 14; fk++) {
     const int nv = kNumVars[fk];
@@ -1008,6 +1018,7 @@ int doFinalize(vb_handle h) {
   }
   std::vector<int32_t> tileIdx((size_t)nT * nT, -1);
   h->tileFill.clear();
+  std::vector<uint8_t> tileDirect;  // per tile: a direct term (not only landmark products) writes it
   h->colStart.assign(nT + 1, 0);
   h->colTilesH.clear(), h->colRowsH.clear();
   int64_t nTiles = 0;
@@ -1016,6 +1027,7 @@ int doFinalize(vb_handle h) {
       if (I == J || pat[(size_t)I * nT + J]) {
         tileIdx[(size_t)I * nT + J] = (int32_t)nTiles;
         h->tileFill.push_back(I != J && pat[(size_t)I * nT + J] == 2 ? 1 : 0);
+        tileDirect.push_back(I == J || pat[(size_t)I * nT + J] == 3 ? 1 : 0);
         h->colTilesH.push_back((int32_t)nTiles++);
         h->colRowsH.push_back(I);
       }
@@ -1191,6 +1203,24 @@ int doFinalize(vb_handle h) {
         }
       }
     for (TileWork& w : works) w.kind = itemsPerTile[w.tile] > 1 ? 1 : 0;
+    // a tile written by exactly one Schur item and by no direct term is stored whole by that item (kind
+    // 2: no read of the tile) and left out of the clear in vb_linearize (single handle; shards and
+    // partitions clear their tile ranges and add); the clear covers the rest, by tile list
+    if (!h->sharded && h->partWorld <= 1) {
+      std::vector<int32_t> clr;
+      for (TileWork& w : works)
+        if (w.kind == 0 && !tileDirect[w.tile]) w.kind = 2;
+      std::vector<uint8_t> stored(nTiles, 0);
+      for (const TileWork& w : works)
+        if (w.kind == 2) stored[w.tile] = 1;
+      for (int64_t t = 0; t < nTiles; t++)
+        if (!stored[t]) clr.push_back((int32_t)t);
+      h->nClear = (int64_t)clr.size();
+      if (getenv("VIBA_SCHUR_STATS"))
+        fprintf(stderr, "[schur stats] tiles %lld: %lld stored whole by one Schur item, %lld cleared\n", (long long)nTiles,
+                (long long)(nTiles - h->nClear), (long long)h->nClear);
+      if (upload(&h->clearTilesD, clr)) return VB_E_HIP;
+    }
     // per item: its runs of identical (maskI, maskJ) and its tasks (run, chunk of <= kSchurCh landmarks,
     // kSchurTR compact block rows), dealt to the 4 waves longest-first by an MFMA + gather cost model and
     // kept in (run, chunk) order per wave, so a wave rebuilds its row maps only when its run changes
@@ -2098,7 +2128,7 @@ int vb_destroy(vb_handle h) {
                   d.rsCalib, d.red, d.redS, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->lscr, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
-                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->lpTiles, h->lpLinv, h->lpT, h->facSync,
+                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->lpTiles, h->lpLinv, h->lpT, h->clearTilesD, h->facSync,
                   (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -2398,7 +2428,9 @@ int linearizeEnqueue(vb_handle h, int update_cache, int dont_retry_failed) {
     HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
     launch_small_eval(d, 0, d.gRed, h->st2);
   }
-  if (h->zeroRuns.empty()) {
+  if (h->clearTilesD) {  // the tiles no Schur item stores whole
+    launch_zero_tiles(d.tiles, h->clearTilesD, h->nClear, zs);
+  } else if (h->zeroRuns.empty()) {
     HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), zs));
   } else {  // partitioned: colStart runs are tile-store index ranges (tiles stored column by column)
     for (const auto& r : h->zeroRuns)
@@ -2444,13 +2476,27 @@ int dampFactorSolveEnqueue(vb_handle h, double lambda, bool clearErr) {
   Dev& d = h->d;
   if (clearErr) HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
   HIPCHK(hipEventRecord(h->ev[2], h->st));
+  // the observation-group Gram blocks on the side stream beside the landmark elimination (both stream
+  // records from HBM; neither reads what the other writes), joined before the tile products
+  // (VIBA_GROUPS_SIDE=0: in line)
+  static const bool groupsSide = !(getenv("VIBA_GROUPS_SIDE") && atoi(getenv("VIBA_GROUPS_SIDE")) == 0);
+  const int addId = (h->isRoot || h->partWorld > 1) ? 1 : 0;
+  launch_damp(d, lambda, addId, h->st);
+  if (groupsSide) {
+    HIPCHK(hipEventRecord(h->evFork, h->st));
+    HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
+    launch_groups(d, lambda, h->st2);
+    HIPCHK(hipEventRecord(h->evJoin, h->st2));
+  }
   profBegin(h, KF_LANDMARK);
   launch_landmark(d, lambda, 0, d.lmB, d.lmE, h->st);
   profEnd(h, KF_LANDMARK);
   HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
+  if (groupsSide) HIPCHK(hipStreamWaitEvent(h->st, h->evJoin, 0));
+  else launch_groups(d, lambda, h->st);
   profBegin(h, KF_SCHUR);
-    launch_schur(d, lambda, (h->isRoot || h->partWorld > 1) ? 1 : 0, h->st);
-    profEnd(h, KF_SCHUR);
+  launch_schur_products(d, lambda, h->st);
+  profEnd(h, KF_SCHUR);
   HIPCHK(hipEventRecord(h->ev[3], h->st));
   const bool fused = !pcgMode(h) && fwdFused(h);
   if (fused)  // the factorization runs the forward solve of rhsWork (into yvec)

@@ -119,7 +119,8 @@ struct FacItem {
 struct TileWork {
   int32_t tile, I, J, count;  // count <= 256 landmark entries
   int64_t start;              // into tileEnts
-  int32_t kind, pad;          // kind 1: the tile is split over several items (atomic epilogue)
+  int32_t kind, pad;          // kind 0: adds into the tile; 1: the tile is split over several items (atomic
+                              // epilogue); 2: the item is the tile's only writer (a plain store, no clear)
   // schur_run4_kernel: the item's runs of identical (maskI, maskJ) at schurRuns[runFirst ..) and its
   // tasks at schurTasks[taskFirst ..), wave w's at [wOff[w], wOff[w + 1])
   int32_t runFirst, taskFirst;

@@ -20,6 +20,7 @@ namespace viba {
 namespace {
 using namespace tmma;
 typedef Acc<double>::type acc_t;
+typedef double double2_t __attribute__((ext_vector_type(2)));
 
 // U_q = L_IJ L_JJ^-1 for item q = (L slot, J): one workgroup per off-diagonal tile of the level
 __global__ void __launch_bounds__(256) selinv_u_kernel(const double* tiles, const int32_t* items, const double* linv,
@@ -84,6 +85,12 @@ __global__ void __launch_bounds__(256) selinv_diag_kernel(double* tiles, const i
   tile_store<double>(tiles + (int64_t)tileIdx[(int64_t)J * nT + J] * TS * TS, 1.0, wave, lane, acc);
 }
 
+__global__ void __launch_bounds__(256) zero_tiles_kernel(double* tiles, const int32_t* list) {
+  double2_t* t = reinterpret_cast<double2_t*>(tiles + (int64_t)list[blockIdx.x] * TS * TS);
+#pragma unroll
+  for (int i = threadIdx.x; i < TS * TS / 2; i += 256) t[i] = double2_t{0.0, 0.0};
+}
+
 __global__ void gather_kernel(const double* src, const int64_t* idx, int64_t n, double* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = src[idx[i]];
@@ -99,6 +106,11 @@ void launch_selinv_level(double* tiles, const int32_t* tileIdx, int32_t nT, cons
   if (nD)
     hipLaunchKernelGGL(selinv_diag_kernel, dim3(nD), dim3(256), 0, st, tiles, tileIdx, nT, dItems, colStart, colTiles,
                        linv, U);
+}
+
+// the linearization's clear of the reduced system (api.hip vb_linearize): the listed tiles only
+void launch_zero_tiles(double* tiles, const int32_t* list, int64_t n, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(zero_tiles_kernel, dim3((unsigned)n), dim3(256), 0, st, tiles, list);
 }
 
 void launch_gather(const double* src, const int64_t* idx, int64_t n, double* out, hipStream_t st) {

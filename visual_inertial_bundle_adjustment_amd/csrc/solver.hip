@@ -412,6 +412,16 @@ template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], int a0, int l4, int l15,
                                                const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
   int colT[NBI];
+#if VIBA_SCHUR_EXPT == 3
+  // diagnostic build: no scatter into C (the accumulators are still consumed), results garbage
+  double sink = 0.0;
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int b = 0; b < NBI; b++) sink += acc[i][b][0] + acc[i][b][3];
+  if (sink == 12345.678) C[l15] = sink;
+  return;
+#endif
 #if VIBA_SCHUR_EPI
   int rowT[NR][4];
 #pragma unroll
@@ -456,6 +466,9 @@ __device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], in
 #endif
 __device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2], const TileEnt* ents, int c0, int nl,
                                           int lane, const uint8_t* posI, double* rq) {
+#if VIBA_SCHUR_EXPT == 4
+  return;  // diagnostic build: no rhs
+#endif
   const int64_t pq = d.nYcol;
   double racc = 0.0;
 #if VIBA_SCHUR_RHS
@@ -599,6 +612,9 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     if (ks + 2 < nks) step(ks + 2, av[2], bv[2], av[1], bv[1]);
   }
 #endif
+#elif VIBA_SCHUR_EXPT == 5
+  // diagnostic build: no k-loop (no gathers, no MFMAs), results garbage
+  if (nks < 0) acc[0][0][0] = 1.0;
 #else
   rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
   ld(a0v, b0v);
@@ -718,9 +734,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
   __syncthreads();
   SCHUR_T(t4);
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind) {
+  if (wk.kind == 1) {
     for (int i = tid; i < TS * TS; i += 256)
       if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
   } else {
     for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
   }
@@ -832,9 +850,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
   __syncthreads();
   SCHUR_T(t4);
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind) {
+  if (wk.kind == 1) {
     for (int i = tid; i < TS * TS; i += 256)
       if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
   } else {
     for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
   }
@@ -987,9 +1007,11 @@ __global__ void __launch_bounds__(256, 2) schur_run5_kernel(Dev d, double lambda
   if (cur >= 0) flush();
   __syncthreads();
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind) {
+  if (wk.kind == 1) {
     for (int i = tid; i < TS * TS; i += 256)
       if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
   } else {
     for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
   }
@@ -1179,9 +1201,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
   }
   __syncthreads();
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind) {
+  if (wk.kind == 1) {
     for (int i = tid; i < TS * TS; i += 256)
       if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
+  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
+    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
   } else {
     for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
   }
@@ -1925,16 +1949,33 @@ typedef __attribute__((address_space(1))) unsigned int guint;
 
 // Fan-in accumulation of contributions [start, start + count) of one target: acc = sum L_IK L_JK^T over
 // the wave's 32 x 32 quadrant (ring in `stg`; every wave passes a barrier per stage, so all waves call it)
+#ifndef VIBA_FAN_MFMA4
+#define VIBA_FAN_MFMA4 0
+#endif
+#if VIBA_FAN_MFMA4
+typedef double fan_acc_t[2][8];
+#else
+typedef double4_t fan_acc_t[2][2];
+#endif
 __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, int32_t start, int32_t count,
-                                            double* stg, int wave, int lane, double4_t (&acc)[2][2]) {
+                                            double* stg, int wave, int lane, fan_acc_t& accOut) {
   static_assert(kGlds * (kFanRing - 1) <= 63 && kFanRing <= 8 && kFanRing >= 3, "vmcnt range");
   const int l15 = lane & 15, l4 = lane >> 4;
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
   const int32_t nst = (TS / kFanK) * count;
+#if VIBA_FAN_MFMA4
+  fan_acc_t& acc4 = accOut;
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc4[a][c] = 0.0;
+#else
+  fan_acc_t& acc = accOut;
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
+#endif
 #if VIBA_FAN_LATE
   // issue-after-barrier: kFanRing - 1 stages in flight; stage s + R - 1 goes into the buffer of stage
   // s - 1, whose readers all passed this iteration's barrier
@@ -1965,6 +2006,25 @@ __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, 
 #endif
     const double* bk = stg + (s % kFanRing) * kStage;
     const double* bi = bk + kFanK * TS;
+#if VIBA_FAN_MFMA4
+    // v_mfma_f64_4x4x4_4b: D_i[b][j] = sum_k A(lane 16k + 4i + b) B(lane 16k + 4i + j), D_i[b][j] at lane
+    // 16b + 4i + j (profiles/r02_mfma4_layout.txt).  A of row group g is the 16x16x4 A operand (lane ->
+    // y row yb + 16g + (lane & 15), k = lane >> 4); B of column group c is x column xb + 4c + (lane & 3)
+    // for every i (a broadcast read).  16 instructions of 512 flops per k-step, 16 accumulators.
+#pragma unroll
+    for (int t0 = 0; t0 < kFanK; t0 += 4) {
+      const int t = t0 + l4, rot = (t & 1) * 16;
+      double av[2], bv[8];
+#pragma unroll
+      for (int a = 0; a < 2; a++) av[a] = bk[t * TS + ((pb + a * 16 + l15 + rot) & 63)];
+#pragma unroll
+      for (int c = 0; c < 8; c++) bv[c] = bi[t * TS + ((qb + 4 * c + (lane & 3) + rot) & 63)];
+#pragma unroll
+      for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int c = 0; c < 8; c++) acc4[a][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[a], bv[c], acc4[a][c], 0, 0, 0);
+    }
+#else
 #pragma unroll
     for (int t0 = 0; t0 < kFanK; t0 += 4) {
       const int t = t0 + l4, rot = (t & 1) * 16;
@@ -1978,12 +2038,37 @@ __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, 
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
     }
+#endif
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // C -= acc (the wave's quadrant): agent-scope fp64 atomics when the target's list is split over
 // several workgroups, else a read-modify-write with all 16 loads in flight before the stores
+#if VIBA_FAN_MFMA4
+// C -= acc4 (the wave's quadrant in the 4x4x4_4b output map: row x = qb + 4c + (lane & 3), column
+// y = pb + 16a + 4 ((lane >> 2) & 3) + (lane >> 4))
+__device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const fan_acc_t& acc4) {
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  double* Cw = C + (pb + 4 * ((lane >> 2) & 3) + (lane >> 4)) * TS + qb + (lane & 3);
+  if (atomic) {
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int c = 0; c < 8; c++) atomicAdd(Cw + 16 * a * TS + 4 * c, -acc4[a][c]);
+  } else {
+    double v[2][8];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int c = 0; c < 8; c++) v[a][c] = Cw[16 * a * TS + 4 * c];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int c = 0; c < 8; c++) Cw[16 * a * TS + 4 * c] = v[a][c] - acc4[a][c];
+  }
+}
+#else
 __device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const double4_t (&acc)[2][2]) {
   const int l15 = lane & 15, l4 = lane >> 4;
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
@@ -2011,12 +2096,13 @@ __device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, in
         for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + b * 16] = v[a][b][r] - acc[a][b][r];
   }
 }
+#endif
 
 __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
   __shared__ double stg[kFanRing * kStage];
   const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double4_t acc[2][2];
+  fan_acc_t acc;
   fanin_accum(d, pairs, wk[1], wk[2], stg, wave, lane, acc);
   fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
 }
@@ -2062,7 +2148,7 @@ __global__ void __launch_bounds__(256, 3) factor_level_kernel(Dev d, const FacIt
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* C = d.tiles + (int64_t)it.target * TS * TS;
   if (it.count > 0) {
-    double4_t acc[2][2];
+    fan_acc_t acc;
     fanin_accum(d, pairs, it.first, it.count, stg, wave, lane, acc);
     fanin_store(C, it.nch > 1, wave, lane, acc);
   }
@@ -2570,10 +2656,23 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
     launchK(landmark_kernel, dim3(blocks(hi - lo, 4)), dim3(256), 0, st, d, lambda, mode, lo, hi);
   }
 }
-// S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry)
-void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
+// S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry), in
+// three parts: the damping of the assembled direct terms (a read-modify-write of the diagonal, so it
+// precedes the observation-group atomics), the observation-group Gram blocks (independent of the
+// landmark elimination: vb_damp_factor_solve runs them on the side stream beside it), the tile products
+void launch_damp(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
   if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
+}
+void launch_groups(const Dev& d, double lambda, hipStream_t st) {
   if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
+}
+void launch_schur_products(const Dev& d, double lambda, hipStream_t st);
+void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
+  launch_damp(d, lambda, addIdentity, st);
+  launch_groups(d, lambda, st);
+  launch_schur_products(d, lambda, st);
+}
+void launch_schur_products(const Dev& d, double lambda, hipStream_t st) {
   // VIBA_SCHUR_V: 4 (default) precomputed runs and balanced tasks (schur_run4_kernel); 2 the run scan in
   // the kernel (schur_run2_kernel); 3 schur_run2 with the K-row offsets from an LDS table and hand-counted
   // gathers (schur_run3_kernel; measured r03a on config C: Schur phase 6.50 ms against 6.15 for run2)
