@@ -49,6 +49,56 @@ __global__ void __launch_bounds__(256) mfma_clock(double* out, int iters, unsign
   if (blockIdx.x == 0 && threadIdx.x == 0) clk[0] = c1 - c0, clk[1] = r1 - r0;
 }
 
+
+// the split-K register-blocked form of the fan-in: 8 A x 8 B operands, 64 accumulators per wave; LDS=1
+// re-reads the 16 operands from LDS every iteration (16 ds_read_b64 per 64 instructions)
+template <int LDSRD>
+__global__ void __launch_bounds__(256) mfma4_outer(double* out, int iters) {
+  __shared__ double sh[4 * 16 * 64];
+  double* my = sh + (threadIdx.x >> 6) * 1024;
+  for (int i = threadIdx.x & 63; i < 1024; i += 64) my[i] = i * 1e-6;
+  __syncthreads();
+  double acc[64];
+  for (int i = 0; i < 64; i++) acc[i] = 0;
+  double av[8], bv[8];
+  const int lane = threadIdx.x & 63;
+  for (int i = 0; i < 8; i++) av[i] = my[i * 64 + lane], bv[i] = my[512 + i * 64 + lane];
+  for (int it = 0; it < iters; it++) {
+    if (LDSRD) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) av[i] = my[((i + it) & 7) * 64 + lane], bv[i] = my[512 + ((i + it) & 7) * 64 + lane];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int c = 0; c < 8; c++) acc[r * 8 + c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], bv[c], acc[r * 8 + c], 0, 0, 0);
+  }
+  double s = 0;
+  for (int i = 0; i < 64; i++) s += acc[i];
+  if (s == 12345.0) out[0] = s;
+}
+
+template <int LDSRD>
+void runOuter(int blocksPerCU, int iters) {
+  int ncu = 0;
+  hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
+  double* out;
+  hipMalloc(&out, 8);
+  const int grid = ncu * blocksPerCU;
+  hipLaunchKernelGGL(mfma4_outer<LDSRD>, dim3(grid), dim3(256), 0, 0, out, iters);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0), hipEventCreate(&e1);
+  hipEventRecord(e0);
+  hipLaunchKernelGGL(mfma4_outer<LDSRD>, dim3(grid), dim3(256), 0, 0, out, iters);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  const double flops = (double)grid * 4 * iters * 64 * 512.0;
+  printf("4x4x4 outer 8x8 lds=%d %d WG/CU: %.1f TFLOP/s\n", LDSRD, blocksPerCU, flops / (ms * 1e-3) / 1e12);
+  hipFree(out);
+}
+
 template <int NACC>
 void run4(int blocksPerCU, int iters) {
   int ncu = 0;
@@ -96,6 +146,8 @@ int main() {
   for (int b : {1, 2}) run<16>(b, 5000);
   for (int b : {2, 4}) run<8>(b, 40000);
   for (int b : {2, 4}) run4<8>(b, 40000);
+  for (int b : {1, 2, 3}) runOuter<0>(b, 5000);
+  for (int b : {1, 2, 3}) runOuter<1>(b, 5000);
   int ncu = 0;
   hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
   double* out;

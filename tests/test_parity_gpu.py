@@ -72,6 +72,22 @@ def test_fused_factor_levels_match_oracle(mode, monkeypatch):
     assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
 
 
+@pytest.mark.parametrize("bins", ["7", "768"])
+def test_streamed_fanin_matches_oracle(bins, monkeypatch):
+    """The streamed fan-in (VIBA_FAN_STREAM bins per level, solver.hip fanin_stream_kernel: the LDS ring
+    runs on across a bin's items, every item ends in atomics): one LM step and a 6-iteration optimize on
+    miniB against the oracle; 7 bins put many items of different targets into one workgroup."""
+    monkeypatch.setenv("VIBA_FAN_STREAM", bins)
+    g, _ = make(hip(), "miniB")
+    r, _ = make(RefEngine, "miniB")
+    assert_step_parity(one_step(g), one_step(r))
+    from visual_inertial_bundle_adjustment_amd.engine import Settings
+    s = Settings.default(max_num_iterations=6)
+    sg, sr = g.optimize(s), r.optimize(s)
+    assert sg.num_iterations == sr.num_iterations
+    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
+
+
 @pytest.mark.parametrize("which", ["A", "miniB"])
 def test_optimize_trajectory_matches_oracle(which):
     g, _ = make(hip(), which)

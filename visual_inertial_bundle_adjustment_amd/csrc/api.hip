@@ -48,6 +48,8 @@ void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, 
                        double* fwdB, double* fwdY);
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
+void launch_fanin_stream(const Dev& d, const int32_t* work, const int32_t* bins, const int32_t* pairs, int nBins,
+                         hipStream_t st);
 void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
                          unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st);
 void launch_bump_epoch(unsigned* epoch, hipStream_t st);
@@ -255,6 +257,11 @@ int alloc0(T** dptr, size_t n) {
 // task lists over the same columns (solver.hip fwd/bwd_fanout_kernel).
 struct Sched {
   std::vector<int64_t> lvP, lvT, lvU;
+  // streamed fan-in (fanStream): per level the bins' item ranges (nBins + 1 offsets relative to the
+  // level's first item, from lvB[L] in binD) and the bin count
+  std::vector<int64_t> lvB;
+  std::vector<int32_t> lvNB;
+  int32_t* binD = nullptr;
   // levels factored by one potrf + trsm launch (potrf_trsm_kernel): per level the range of its items
   // (diagonal tile, column, target, row, writer) in ptfD; the diagonal tiles to copy back from Lscr
   std::vector<int64_t> lvPF;
@@ -384,6 +391,7 @@ struct vb_handle_s {
   // evaluation (st2) does not queue behind the 2.2 GB memset; their assembly waits for it (evZero)
   hipStream_t stZ = nullptr;
   hipEvent_t evZero = nullptr, evSmallE = nullptr, evZJoin = nullptr;
+  int64_t fanStream = 0;    // VIBA_FAN_STREAM: fan-in bins per launch for the streamed fan-in (0: one workgroup per item)
   int64_t ptFuseMax = 256;  // VIBA_PT_FUSE: levels with at most this many off-diagonal tiles run potrf + trsm fused
   double* lscr = nullptr;   // L_JJ of the fused levels' columns (nT tiles), copied back after the factorization
   // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
@@ -1365,6 +1373,8 @@ int doFinalize(vb_handle h) {
       std::vector<int32_t> ptf, ptfDiag;
       S.lvF.assign(nLev + 1, 0), S.lvFd.assign(nLev, 0), S.lvPT.assign(nLev + 1, 0), S.lvPd.assign(nLev, 0);
       std::vector<FacItem> facItems, ptItems;
+      std::vector<int32_t> binsH;
+      S.lvB.assign(nLev + 1, 0), S.lvNB.assign(nLev, 0);
       for (int32_t L = 0; L < nLev; L++) {
         int64_t total = 0;
         for (int32_t J : cols[L])
@@ -1404,6 +1414,41 @@ int doFinalize(vb_handle h) {
           }
           for (size_t i = 0; i < q.size(); i++)
             for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
+        }
+        if (h->fanStream > 0) {
+          // bins of the streamed fan-in: the level's items cut into 8 contiguous ranges (one per XCD, so a
+          // column's targets share that XCD's L2, as the per-item launch's xcd_block order does), each
+          // dealt longest-first to the least-loaded of its XCD's bins (b % 8 == x); weight = stages + 2
+          // (the item's start and atomics); the items are then laid out bin by bin
+          const size_t u0 = (size_t)S.lvU[L], nq = fan.size() / 4 - u0;
+          const int32_t nb = (int32_t)std::min<int64_t>((int64_t)nq, h->fanStream);
+          std::vector<std::vector<int32_t>> bin(nb);
+          std::vector<int64_t> load(nb, 0);
+          for (int32_t x = 0, q0 = 0; x < 8; x++) {
+            const int32_t len = (int32_t)(nq / 8 + ((size_t)x < nq % 8 ? 1 : 0));
+            std::vector<int32_t> ord(len);
+            for (int32_t i = 0; i < len; i++) ord[i] = q0 + i;
+            std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return fan[4 * (u0 + a) + 2] > fan[4 * (u0 + b) + 2]; });
+            for (int32_t i : ord) {
+              int32_t best = -1;
+              for (int32_t b = x % nb; b < nb; b += 8)
+                if (best < 0 || load[b] < load[best]) best = b;
+              if (best < 0) best = (int32_t)(i % nb);  // fewer bins than XCDs
+              bin[best].push_back(i), load[best] += 4 * (int64_t)fan[4 * (u0 + i) + 2] + 2;
+            }
+            q0 += len;
+          }
+          std::vector<int32_t> q(fan.begin() + 4 * u0, fan.end());
+          size_t w = 4 * u0;
+          binsH.push_back(0);
+          for (int32_t b = 0; b < nb; b++) {
+            for (int32_t i : bin[b])
+              for (int k = 0; k < 4; k++) fan[w++] = q[4 * (size_t)i + k];
+            binsH.push_back((int32_t)((w - 4 * u0) / 4));
+          }
+          S.lvNB[L] = nb, S.lvB[L + 1] = (int64_t)binsH.size();
+        } else {
+          S.lvB[L + 1] = S.lvB[L];
         }
         S.lvP[L + 1] = (int64_t)pT.size(), S.lvT[L + 1] = (int64_t)tT.size(), S.lvU[L + 1] = (int64_t)fan.size() / 4;
         if (h->ptFuseMax > 0 && S.lvP[L + 1] > S.lvP[L] && S.lvT[L + 1] - S.lvT[L] <= h->ptFuseMax)
@@ -1483,7 +1528,7 @@ int doFinalize(vb_handle h) {
           upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.trsmRowD, tR) || upload(&S.updD, fan) ||
           upload(&S.fanPairsD, pairs) || upload(&S.tasksFD, tf) || upload(&S.tasksBD, tb) ||
           upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.facD, facItems) || upload(&S.ptD, ptItems) ||
-          upload(&S.ptfD, ptf) || upload(&S.ptfDiagD, ptfDiag))
+          upload(&S.ptfD, ptf) || upload(&S.ptfDiagD, ptfDiag) || upload(&S.binD, binsH))
         return VB_E_HIP;
       S.nPtfDiag = (int64_t)ptfDiag.size() / 2;
       if (S.nPtfDiag && !h->lscr && alloc0(&h->lscr, (size_t)nT * TS * TS)) return VB_E_HIP;
@@ -1755,7 +1800,10 @@ void factorSeq(vb_handle h, const Sched& S) {
   for (int32_t L = 0; L < S.nLevels; L++) {
     const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
     profBegin(h, KF_GEMM);
-    launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
+    if (S.lvNB.size() && S.lvNB[L] > 0)
+      launch_fanin_stream(d, S.updD + 4 * u0, S.binD + S.lvB[L], S.fanPairsD, S.lvNB[L], h->st);
+    else
+      launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
     profEnd(h, KF_GEMM);
     if (S.lvPF[L + 1] > S.lvPF[L]) {  // potrf + trsm in one launch
       profBegin(h, KF_POTRF);
@@ -2097,6 +2145,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   if (const char* e = getenv("VIBA_FWD_IN_FACTOR")) h->fwdInFactor = e[0] != '0';
   if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
   if (const char* e = getenv("VIBA_PT_FUSE")) h->ptFuseMax = atoll(e);
+  if (const char* e = getenv("VIBA_FAN_STREAM")) h->fanStream = std::max<int64_t>(0, atoll(e));
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2157,7 +2206,7 @@ int vb_destroy(vb_handle h) {
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
     void* sp[] = {S.ptfD, S.ptfDiagD, S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
-                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD};
+                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD, S.binD};
     for (void* p : sp)
       if (p) hipFree(p);
     if (S.graph) hipGraphExecDestroy(S.graph);

@@ -1917,7 +1917,15 @@ __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagLis
 constexpr int kFanK = VIBA_FAN_K;          // columns per stage
 constexpr int kFanRing = VIBA_FAN_RING;    // stages in the LDS ring (kFanRing - 2 in flight)
 constexpr int kStage = 2 * kFanK * TS;     // doubles per stage: [L_JK, L_IK][kFanK columns][64 rows]
-constexpr int kGlds = kStage / 128 / 4;    // global_load_lds per wave per stage (1 KB = 128 doubles each)
+#ifndef VIBA_FAN_MFMA4
+#define VIBA_FAN_MFMA4 0
+#endif
+constexpr int kFanWaves = VIBA_FAN_MFMA4 == 3 ? 8 : 4;  // waves per fan-in workgroup
+constexpr int kGlds = kStage / 128 / kFanWaves;          // global_load_lds per wave per stage (1 KB = 128 doubles each)
+// LDS row rotation of stage column t (rows stored at (row + rot) & 63): odd columns by 16, so a half-wave
+// reading two columns of one row range hits all 64 banks; the split-K 4x4x4 form (VIBA_FAN_MFMA4 == 2)
+// reads 4 row groups x 4 column quads x 2 columns per half-wave, so the quads are rotated by 4 more each
+__device__ __forceinline__ int fan_rot(int t) { return 16 * (t & 1) + (VIBA_FAN_MFMA4 >= 2 ? 4 * ((t >> 2) & 3) : 0); }
 
 __device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, int32_t start, int s, double* buf,
                                             int wave, int lane) {
@@ -1933,10 +1941,10 @@ __device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, 
   const int64_t tk = pc[2 * c + 1], ti = pc[2 * c];
 #endif
   const int hi = lane >> 5;
-  const int row = (2 * (lane & 31) - 16 * hi) & 63;
 #pragma unroll
   for (int j = 0; j < kGlds; j++) {
     const int i = wave * kGlds + j, tile = i / (kFanK / 2), cp = i % (kFanK / 2);  // 1 KB = 2 columns each
+    const int row = (2 * (lane & 31) - fan_rot(2 * cp + hi)) & 63;
     const double* src = d.tiles + (tile ? ti : tk) * TS * TS + (int64_t)(k0 + 2 * cp + hi) * TS + row;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(buf + tile * kFanK * TS + cp * 2 * TS),
@@ -1949,10 +1957,11 @@ typedef __attribute__((address_space(1))) unsigned int guint;
 
 // Fan-in accumulation of contributions [start, start + count) of one target: acc = sum L_IK L_JK^T over
 // the wave's 32 x 32 quadrant (ring in `stg`; every wave passes a barrier per stage, so all waves call it)
-#ifndef VIBA_FAN_MFMA4
-#define VIBA_FAN_MFMA4 0
-#endif
-#if VIBA_FAN_MFMA4
+#if VIBA_FAN_MFMA4 == 3
+typedef double fan_acc_t[8][4];
+#elif VIBA_FAN_MFMA4 == 2
+typedef double fan_acc_t[8][8];
+#elif VIBA_FAN_MFMA4
 typedef double fan_acc_t[2][8];
 #else
 typedef double4_t fan_acc_t[2][2];
@@ -1961,9 +1970,23 @@ __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, 
                                             double* stg, int wave, int lane, fan_acc_t& accOut) {
   static_assert(kGlds * (kFanRing - 1) <= 63 && kFanRing <= 8 && kFanRing >= 3, "vmcnt range");
   const int l15 = lane & 15, l4 = lane >> 4;
+#if VIBA_FAN_MFMA4 == 3
+  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;  // eight 32 x 16 strips
+#else
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+#endif
   const int32_t nst = (TS / kFanK) * count;
-#if VIBA_FAN_MFMA4
+#if VIBA_FAN_MFMA4 >= 2
+  fan_acc_t& acc4 = accOut;
+#pragma unroll
+  for (int r = 0; r < 8; r++)
+#pragma unroll
+    for (int c = 0; c < (VIBA_FAN_MFMA4 == 3 ? 4 : 8); c++) acc4[r][c] = 0.0;
+  // operand lane map of the split-K form: lane 16 k' + 4 i + e reads stage column t = 4 i + k', row group
+  // member e (see below)
+  const int tq = 4 * ((lane >> 2) & 3) + (lane >> 4);
+  const int offA = tq * TS, rowA = pb + (lane & 3) + fan_rot(tq), rowB = qb + (lane & 3) + fan_rot(tq);
+#elif VIBA_FAN_MFMA4
   fan_acc_t& acc4 = accOut;
 #pragma unroll
   for (int a = 0; a < 2; a++)
@@ -2006,7 +2029,43 @@ __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, 
 #endif
     const double* bk = stg + (s % kFanRing) * kStage;
     const double* bi = bk + kFanK * TS;
-#if VIBA_FAN_MFMA4
+#if VIBA_FAN_MFMA4 == 3
+    // the split-K form on a 32 x 16 strip per wave (8 waves): 8 + 4 operand reads, 32 instructions
+    {
+      double av[8], bv[4];
+#pragma unroll
+      for (int r = 0; r < 8; r++) av[r] = bk[offA + ((rowA + 4 * r) & 63)];
+#pragma unroll
+      for (int c = 0; c < 4; c++) bv[c] = bi[offA + ((rowB + 4 * c) & 63)];
+#ifdef VIBA_FAN_NOMMA  // measurement build: the operand reads without the products
+#pragma unroll
+      for (int r = 0; r < 8; r++) acc4[r][r & 3] += av[r] * bv[r & 3];
+#else
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) acc4[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], bv[c], acc4[r][c], 0, 0, 0);
+#endif
+    }
+#elif VIBA_FAN_MFMA4 == 2
+    // split-K v_mfma_f64_4x4x4_4b: D_i[b][j] = sum_k' A(lane 16k' + 4i + b) B(lane 16k' + 4i + j) at lane
+    // 16b + 4i + j (profiles/r02_mfma4_layout.txt).  Block i takes the stage's columns 4i .. 4i + 3, so
+    // every block of one instruction adds into the same 4 x 4 piece of the quadrant and the blocks are
+    // summed once per target (fanin_store).  Row group r of the wave's 32 rows and column group c of its
+    // 32 columns: 8 + 8 operand reads feed 64 independent instructions (the 16x16x4 form's read count
+    // per flop), 64 accumulators.
+    {
+      double av[8], bv[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++) av[r] = bk[offA + ((rowA + 4 * r) & 63)];
+#pragma unroll
+      for (int c = 0; c < 8; c++) bv[c] = bi[offA + ((rowB + 4 * c) & 63)];
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+#pragma unroll
+        for (int c = 0; c < 8; c++) acc4[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], bv[c], acc4[r][c], 0, 0, 0);
+    }
+#elif VIBA_FAN_MFMA4
     // v_mfma_f64_4x4x4_4b: D_i[b][j] = sum_k A(lane 16k + 4i + b) B(lane 16k + 4i + j), D_i[b][j] at lane
     // 16b + 4i + j (profiles/r02_mfma4_layout.txt).  A of row group g is the 16x16x4 A operand (lane ->
     // y row yb + 16g + (lane & 15), k = lane >> 4); B of column group c is x column xb + 4c + (lane & 3)
@@ -2033,10 +2092,15 @@ __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, 
       for (int a = 0; a < 2; a++) av[a] = bk[t * TS + ((pb + a * 16 + l15 + rot) & 63)];
 #pragma unroll
       for (int b = 0; b < 2; b++) bv[b] = bi[t * TS + ((qb + b * 16 + l15 + rot) & 63)];
+#ifdef VIBA_FAN_NOMMA  // measurement build: the operand reads without the products
+#pragma unroll
+      for (int a = 0; a < 2; a++) acc[a][a][0] += av[a] * bv[a];
+#else
 #pragma unroll
       for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
+#endif
     }
 #endif
     __builtin_amdgcn_sched_barrier(0);
@@ -2045,7 +2109,57 @@ __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, 
 
 // C -= acc (the wave's quadrant): agent-scope fp64 atomics when the target's list is split over
 // several workgroups, else a read-modify-write with all 16 loads in flight before the stores
-#if VIBA_FAN_MFMA4
+#if VIBA_FAN_MFMA4 >= 2
+__device__ __forceinline__ double swz_xor8(double v) {
+  const int2 w = __builtin_bit_cast(int2, v);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_ds_swizzle(w.x, 0x201f), __builtin_amdgcn_ds_swizzle(w.y, 0x201f)));
+}
+__device__ __forceinline__ double swz_xor4(double v) {
+  const int2 w = __builtin_bit_cast(int2, v);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_ds_swizzle(w.x, 0x101f), __builtin_amdgcn_ds_swizzle(w.y, 0x101f)));
+}
+// C -= the split-K accumulators: acc[r][c] at lane 16b + 4i + j holds block i's part of C(q = qb + 4c + j,
+// p = pb + 4r + b).  The four blocks (lane bits 2-3) are summed by a reduce-scatter over the column
+// quads 4c1 .. 4c1 + 3: lane i keeps the sum of quad 4c1 + i, so each lane ends with 16 values at
+// q = qb + 16 c1 + (lane & 15), p = pb + 4r + (lane >> 4) -- the 16x16x4 form's store map
+__device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const fan_acc_t& acc4) {
+#if VIBA_FAN_MFMA4 == 3
+  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;
+  constexpr int kC1 = 1;
+#else
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  constexpr int kC1 = 2;
+#endif
+  const bool h2 = (lane & 8) != 0, h1 = (lane & 4) != 0;
+  double v[8][2];
+#pragma unroll
+  for (int r = 0; r < 8; r++)
+#pragma unroll
+    for (int c1 = 0; c1 < kC1; c1++) {
+      const double* g = acc4[r] + 4 * c1;
+      const double k0 = (h2 ? g[2] : g[0]) + swz_xor8(h2 ? g[0] : g[2]);
+      const double k1 = (h2 ? g[3] : g[1]) + swz_xor8(h2 ? g[1] : g[3]);
+      v[r][c1] = (h1 ? k1 : k0) + swz_xor4(h1 ? k0 : k1);
+    }
+  double* Cw = C + (pb + (lane >> 4)) * TS + qb + (lane & 15);
+  if (atomic) {
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int c1 = 0; c1 < kC1; c1++) atomicAdd(Cw + 4 * r * TS + 16 * c1, -v[r][c1]);
+  } else {
+    double o[8][2];
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int c1 = 0; c1 < kC1; c1++) o[r][c1] = Cw[4 * r * TS + 16 * c1];
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int c1 = 0; c1 < kC1; c1++) Cw[4 * r * TS + 16 * c1] = o[r][c1] - v[r][c1];
+  }
+}
+#elif VIBA_FAN_MFMA4
 // C -= acc4 (the wave's quadrant in the 4x4x4_4b output map: row x = qb + 4c + (lane & 3), column
 // y = pb + 16a + 4 ((lane >> 2) & 3) + (lane >> 4))
 __device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const fan_acc_t& acc4) {
@@ -2098,7 +2212,7 @@ __device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, in
 }
 #endif
 
-__global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
+__global__ void __launch_bounds__(kFanWaves * 64) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
   __shared__ double stg[kFanRing * kStage];
   const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2106,6 +2220,111 @@ __global__ void __launch_bounds__(256) fanin_kernel(Dev d, const int32_t* work, 
   fanin_accum(d, pairs, wk[1], wk[2], stg, wave, lane, acc);
   fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
 }
+
+// Streamed fan-in: one workgroup per bin of a level's work items (host-balanced, XCD-placed: bin b runs
+// on XCD b % 8), the LDS ring running on across the bin's items, so each item's first stages are in
+// flight while the previous item computes and stores (fanin_kernel refills the ring from empty for
+// every item).  Every item ends in agent-scope atomics (a single-writer target receives exactly one add
+// per element, so its result is that of the plain read-modify-write); their 16 vector-memory
+// operations per wave are younger than the stages issued before them, which the counted waits add in
+// (s_waitcnt vmcnt counts loads, stores, atomics and LDS-DMA together, in issue order).  Items hold at
+// least TS / kFanK stages, so at most one item end falls between a stage's issue and its use.
+__device__ __forceinline__ void fan_zero(fan_acc_t& acc) {
+#if VIBA_FAN_MFMA4
+  for (auto& row : acc)
+    for (auto& v : row) v = 0.0;
+#else
+#pragma unroll
+  for (int a = 0; a < 2; a++)
+#pragma unroll
+    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
+#endif
+}
+
+__device__ __forceinline__ void fan_stage(const double* bk, int wave, int lane, fan_acc_t& acc) {
+  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
+  const double* bi = bk + kFanK * TS;
+#if VIBA_FAN_MFMA4 == 2
+  const int tq = 4 * ((lane >> 2) & 3) + (lane >> 4);
+  const int offA = tq * TS, rowA = pb + (lane & 3) + fan_rot(tq), rowB = qb + (lane & 3) + fan_rot(tq);
+  double av[8], bv[8];
+#pragma unroll
+  for (int r = 0; r < 8; r++) av[r] = bk[offA + ((rowA + 4 * r) & 63)];
+#pragma unroll
+  for (int c = 0; c < 8; c++) bv[c] = bi[offA + ((rowB + 4 * c) & 63)];
+#pragma unroll
+  for (int r = 0; r < 8; r++)
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], bv[c], acc[r][c], 0, 0, 0);
+#elif VIBA_FAN_MFMA4 == 0
+  const int l15 = lane & 15, l4 = lane >> 4;
+#pragma unroll
+  for (int t0 = 0; t0 < kFanK; t0 += 4) {
+    const int t = t0 + l4, rot = fan_rot(t);
+    double av[2], bv[2];
+#pragma unroll
+    for (int a = 0; a < 2; a++) av[a] = bk[t * TS + ((pb + a * 16 + l15 + rot) & 63)];
+#pragma unroll
+    for (int b = 0; b < 2; b++) bv[b] = bi[t * TS + ((qb + b * 16 + l15 + rot) & 63)];
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+      for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
+  }
+#endif
+}
+
+#if VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2
+__global__ void __launch_bounds__(256) fanin_stream_kernel(Dev d, const int32_t* work, const int32_t* bins,
+                                                           const int32_t* pairs) {
+  static_assert(kGlds * (kFanRing - 2) + 16 <= 63 && kFanRing >= 3 && kFanRing <= 5, "vmcnt range");
+  static_assert(VIBA_FAN_LATE, "issue-after-barrier ring");
+  __shared__ double stg[kFanRing * kStage];
+  typedef const __attribute__((address_space(4))) int32_t cint;
+  cint* wk = (cint*)work;
+  cint* bn = (cint*)bins;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int32_t i0 = bn[blockIdx.x], i1 = bn[blockIdx.x + 1];
+  constexpr int kAhead = kFanRing - 1, kSt = TS / kFanK;
+  int32_t iI = i0, sI = 0, nI = i0 < i1 ? kSt * wk[4 * i0 + 2] : 0, issued = 0;
+  auto issueNext = [&]() {
+    fanin_issue(d, pairs, wk[4 * iI + 1], sI, stg + (issued % kFanRing) * kStage, wave, lane);
+    issued++;
+    if (++sI == nI) {
+      iI++, sI = 0;
+      nI = iI < i1 ? kSt * wk[4 * iI + 2] : 0;
+    }
+  };
+  for (int k = 0; k < kAhead && iI < i1; k++) issueNext();
+  int32_t g = 0, epiIssued = 0;  // stages below epiIssued were issued before the last item's atomics
+  for (int32_t it = i0; it < i1; it++) {
+    fan_acc_t acc;
+    fan_zero(acc);
+    const int32_t nst = kSt * wk[4 * it + 2];
+    for (int32_t s = 0; s < nst; s++, g++) {
+      // stage g landed: younger than it are the later stages issued so far and, if an item ended since
+      // its issue, that item's 16 atomics
+      switch (2 * min(kAhead - 1, issued - 1 - g) + (g < epiIssued ? 1 : 0)) {
+#define VIBA_FAN_WAIT(c) \
+  case c: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGlds * ((c) >> 1) + 16 * ((c) & 1)) : "memory"); break;
+        VIBA_FAN_WAIT(1) VIBA_FAN_WAIT(2) VIBA_FAN_WAIT(3) VIBA_FAN_WAIT(4) VIBA_FAN_WAIT(5) VIBA_FAN_WAIT(6)
+        VIBA_FAN_WAIT(7)
+#undef VIBA_FAN_WAIT
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      }
+      __builtin_amdgcn_s_barrier();  // ... and every other wave's; the ring buffer of stage g - 1 is free
+      __builtin_amdgcn_sched_barrier(0);
+      if (iI < i1) issueNext();
+      __builtin_amdgcn_sched_barrier(0);
+      fan_stage(stg + (g % kFanRing) * kStage, wave, lane, acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    fanin_store(d.tiles + (int64_t)wk[4 * it] * TS * TS, true, wave, lane, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    epiIssued = issued;
+  }
+}
+#endif
 
 // One elimination level of the tile Cholesky in ONE launch (fan-in + potrf + trsm; the 3-launch form is
 // fanin_kernel / potrf_kernel / trsm_kernel).  Item b (FacItem, 8 int32): fan-in of `count`
@@ -2148,9 +2367,14 @@ __global__ void __launch_bounds__(256, 3) factor_level_kernel(Dev d, const FacIt
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double* C = d.tiles + (int64_t)it.target * TS * TS;
   if (it.count > 0) {
+#if VIBA_FAN_MFMA4 == 3  // the 8-wave fan-in has no fused-level form
+    if (tid == 0) atomicOr(d.err, 16);
+    return;
+#else
     fan_acc_t acc;
     fanin_accum(d, pairs, it.first, it.count, stg, wave, lane, acc);
     fanin_store(C, it.nch > 1, wave, lane, acc);
+#endif
   }
   if (it.kind == 0) return;
   // this workgroup's part of the target is out; is the tile complete?
@@ -2750,7 +2974,15 @@ void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, cons
 }
 
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
-  if (n > 0) launchK(fanin_kernel, dim3(n), dim3(256), 0, st, d, work, pairs);
+  if (n > 0) launchK(fanin_kernel, dim3(n), dim3(kFanWaves * 64), 0, st, d, work, pairs);
+}
+void launch_fanin_stream(const Dev& d, const int32_t* work, const int32_t* bins, const int32_t* pairs, int nBins,
+                         hipStream_t st) {
+#if VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2
+  if (nBins > 0) launchK(fanin_stream_kernel, dim3(nBins), dim3(256), 0, st, d, work, bins, pairs);
+#else
+  (void)d, (void)work, (void)bins, (void)pairs, (void)nBins, (void)st;
+#endif
 }
 void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
                          unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st) {
