@@ -141,6 +141,23 @@ def mixed_vs_fp64(p, device, rs_device):
             "cost_after_step": {"fp64": c164, "mixed": c1mx}, "cost_before": c0}
 
 
+def banded_contributions(p, device, rs_device, precision):
+    """Tile-pair contributions of the reduced system's Cholesky in the time order (VIBA_ND_OFF: the
+    symbolic analysis without the nested dissection), from a second handle that is only finalized."""
+    from visual_inertial_bundle_adjustment_amd import synth
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine
+    os.environ["VIBA_ND_OFF"] = "1"
+    try:
+        eb = HipEngine(imu_calib_options=p.imu_calib_options, device=device, precision=precision)
+        try:
+            synth.load_into(eb, p, rs_device=rs_device)
+            return int(eb.problem_stats()[6])
+        finally:
+            eb.close()
+    finally:
+        del os.environ["VIBA_ND_OFF"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,6 +181,9 @@ def main():
                          "the identity / block-Jacobi / block-Gauss-Seidel / fp32-Cholesky preconditioner")
     ap.add_argument("--pcg-iterations", type=int, default=40, help="pcgMaxIterations (Optimizer.h:44)")
     ap.add_argument("--pcg-residual", type=float, default=1e-10, help="pcgDesiredResidual (Optimizer.h:45)")
+    ap.add_argument("--no-banded-count", action="store_true",
+                    help="skip the symbolic analysis of the time-ordered (banded) reduced system that prices the "
+                         "factorization against the banded flop count")
     ap.add_argument("--recompute-preint", action="store_true",
                     help="ark_vi_ba --recompute-preint: every iteration re-preintegrates every inertial factor "
                          "from the IMU stream on the device (preint.hip)")
@@ -273,9 +293,25 @@ def main():
                                "last_relative_residual": res}
         log(f"[bench] last PCG solve: {it} iterations, relative residual {res:.3g}")
     out_extra["phases_ms"] = {k: round(getattr(ph, k), 3) for k, _ in ph._fields_}
+    e.close()  # free the device before the banded analysis and the host run
+    if roof is not None and args.profile_family == KF_GEMM and not args.no_banded_count:
+        # the factorization against two flop counts: the nested-dissection order's (what runs) and the
+        # time order's (the band the reference's supernodal solver would see without our reordering)
+        t = time.perf_counter()
+        try:
+            banded = banded_contributions(p, local, args.rs_tables == "device", args.precision)
+            nd_gf, band_gf = st[6] * 2.0 * 64 ** 3 / 1e9, banded * 2.0 * 64 ** 3 / 1e9
+            roof["factor"] = {"factor_ms": ph.factor_ms, "contributions_nd": int(st[6]),
+                              "contributions_banded": int(banded), "gflop_nd": nd_gf, "gflop_banded": band_gf,
+                              "tflops_nd": nd_gf / ph.factor_ms, "tflops_banded": band_gf / ph.factor_ms,
+                              "frac_nd": nd_gf / ph.factor_ms / FP64_MFMA_PEAK_TF,
+                              "frac_banded": band_gf / ph.factor_ms / FP64_MFMA_PEAK_TF}
+            log(f"[bench] banded analysis {time.perf_counter() - t:.1f}s: {banded} contributions "
+                f"(nested dissection {st[6]})")
+        except Exception as ex:
+            log(f"[bench] banded analysis failed: {ex}")
     cpu = None
     if not args.no_cpu_baseline:
-        e.close()  # free the device before the host run
         try:
             cpu = cpu_baseline(p, args.config, recompute_preint=args.recompute_preint, warmup=args.warmup)
         except Exception as ex:  # the baseline must never hide the GPU number
