@@ -88,6 +88,21 @@ def test_streamed_fanin_matches_oracle(bins, monkeypatch):
     assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
 
 
+def test_paired_fanin_matches_oracle(monkeypatch):
+    """The paired fan-in (VIBA_FAN_PAIR, solver.hip fanin_pair_kernel: two targets of one column with the
+    same source list stage L_JK once; split-K-by-2 v_mfma_f64_4x4x4_4b): one LM step and a 6-iteration
+    optimize on miniB against the oracle."""
+    monkeypatch.setenv("VIBA_FAN_PAIR", "1")
+    g, _ = make(hip(), "miniB")
+    r, _ = make(RefEngine, "miniB")
+    assert_step_parity(one_step(g), one_step(r))
+    from visual_inertial_bundle_adjustment_amd.engine import Settings
+    s = Settings.default(max_num_iterations=6)
+    sg, sr = g.optimize(s), r.optimize(s)
+    assert sg.num_iterations == sr.num_iterations
+    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
+
+
 @pytest.mark.parametrize("which", ["A", "miniB"])
 def test_optimize_trajectory_matches_oracle(which):
     g, _ = make(hip(), which)

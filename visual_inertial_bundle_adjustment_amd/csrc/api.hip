@@ -14,6 +14,7 @@
 #include <numeric>
 #include <string>
 #include <unordered_map>
+#include <map>
 #include <vector>
 
 #include "../../include/viba_hip.h"
@@ -50,6 +51,7 @@ void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* L
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_fanin_stream(const Dev& d, const int32_t* work, const int32_t* bins, const int32_t* pairs, int nBins,
                          hipStream_t st);
+void launch_fanin_pair(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
                          unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st);
 void launch_bump_epoch(unsigned* epoch, hipStream_t st);
@@ -262,6 +264,10 @@ struct Sched {
   std::vector<int64_t> lvB;
   std::vector<int32_t> lvNB;
   int32_t* binD = nullptr;
+  // paired fan-in (fanPair): per level the range of its 8-int items (target pairs of identical source
+  // lists, or single targets) in fanPD
+  std::vector<int64_t> lvU2;
+  int32_t* fanPD = nullptr;
   // levels factored by one potrf + trsm launch (potrf_trsm_kernel): per level the range of its items
   // (diagonal tile, column, target, row, writer) in ptfD; the diagonal tiles to copy back from Lscr
   std::vector<int64_t> lvPF;
@@ -391,6 +397,7 @@ struct vb_handle_s {
   // evaluation (st2) does not queue behind the 2.2 GB memset; their assembly waits for it (evZero)
   hipStream_t stZ = nullptr;
   hipEvent_t evZero = nullptr, evSmallE = nullptr, evZJoin = nullptr;
+  bool fanPair = false;      // VIBA_FAN_PAIR=1: paired fan-in (solver.hip fanin_pair_kernel)
   int64_t fanStream = 0;    // VIBA_FAN_STREAM: fan-in bins per launch for the streamed fan-in (0: one workgroup per item)
   int64_t ptFuseMax = 256;  // VIBA_PT_FUSE: levels with at most this many off-diagonal tiles run potrf + trsm fused
   double* lscr = nullptr;   // L_JJ of the fused levels' columns (nT tiles), copied back after the factorization
@@ -1373,8 +1380,38 @@ int doFinalize(vb_handle h) {
       std::vector<int32_t> ptf, ptfDiag;
       S.lvF.assign(nLev + 1, 0), S.lvFd.assign(nLev, 0), S.lvPT.assign(nLev + 1, 0), S.lvPd.assign(nLev, 0);
       std::vector<FacItem> facItems, ptItems;
-      std::vector<int32_t> binsH;
-      S.lvB.assign(nLev + 1, 0), S.lvNB.assign(nLev, 0);
+      if (getenv("VIBA_FAN_STATS")) {
+        // operand sharing among one column's fan-in targets: targets (I, J) whose lists hold the same
+        // source columns K (the same L_JK tiles) could stage L_JK once for all of them
+        int64_t C = 0, Cdiag = 0, st1 = 0, stAll = 0, st2 = 0, st4 = 0, nGrp = 0, inGrp = 0;
+        for (int32_t J = 0; J < nT; J++) {
+          if (!tgtSel(J)) continue;
+          std::map<std::vector<int32_t>, int64_t> groups;
+          for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
+            const int32_t t = h->colTilesH[c];
+            const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
+            if (m == 0) continue;
+            C += m;
+            if (h->colRowsH[c] == J) Cdiag += m;
+            std::vector<int32_t> key(m);
+            for (int64_t i = 0; i < m; i++) key[i] = pairs[2 * (b + i) + 1];
+            std::sort(key.begin(), key.end());
+            groups[key]++;
+          }
+          for (auto& [key, g] : groups) {
+            const int64_t m = (int64_t)key.size();
+            st1 += 2 * m * g, stAll += m * (g + 1);
+            st2 += m * (g + (g + 1) / 2), st4 += m * (g + (g + 3) / 4);
+            if (g > 1) nGrp++, inGrp += g * m;
+          }
+        }
+        fprintf(stderr, "[viba] fan-in sharing: %lld contributions (%lld into diagonal targets), %lld in %lld groups of "
+                "identical source lists; staged tiles single %lld, shared by pairs %.3f, by quads %.3f, by whole groups %.3f\n",
+                (long long)C, (long long)Cdiag, (long long)inGrp, (long long)nGrp, (long long)st1, (double)st2 / st1,
+                (double)st4 / st1, (double)stAll / st1);
+      }
+      std::vector<int32_t> binsH, fanP;
+      S.lvB.assign(nLev + 1, 0), S.lvNB.assign(nLev, 0), S.lvU2.assign(nLev + 1, 0);
       for (int32_t L = 0; L < nLev; L++) {
         int64_t total = 0;
         for (int32_t J : cols[L])
@@ -1415,6 +1452,49 @@ int doFinalize(vb_handle h) {
           for (size_t i = 0; i < q.size(); i++)
             for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
         }
+        if (h->fanPair) {
+          // the paired fan-in's items: per column, the targets grouped by their (ordered) source lists --
+          // the counting sort appends sources in one global order, so equal sets are equal sequences --
+          // paired within each group, chunked like the single items; longest first per XCD range
+          const size_t p0 = fanP.size() / 8;
+          for (int32_t J : cols[L]) {
+            if (!tgtSel(J)) continue;
+            const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
+            std::map<std::vector<int32_t>, std::vector<int32_t>> grp;
+            for (int64_t q = 0; q < n; q++) {
+              const int32_t t = h->colTilesH[c0 + q];
+              const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
+              if (m == 0) continue;
+              std::vector<int32_t> key(m);
+              for (int64_t i = 0; i < m; i++) key[i] = pairs[2 * (b + i) + 1];
+              grp[key].push_back(t);
+            }
+            for (auto& [key, mem] : grp) {
+              const int64_t m = (int64_t)key.size(), nch = (m + cs - 1) / cs;
+              for (size_t a = 0; a < mem.size(); a += 2) {
+                const int32_t t1 = mem[a], t2 = a + 1 < mem.size() ? mem[a + 1] : -1;
+                for (int64_t k = 0; k < nch; k++) {
+                  const int64_t s0 = m * k / nch, s1 = m * (k + 1) / nch;
+                  fanP.insert(fanP.end(), {t1, t2, (int32_t)(ccnt[t1] + s0), (int32_t)(t2 >= 0 ? ccnt[t2] + s0 : ccnt[t1] + s0),
+                                           (int32_t)(s1 - s0), nch > 1 ? 1 : 0, 0, 0});
+                }
+              }
+            }
+          }
+          const size_t nq = fanP.size() / 8 - p0, qq = nq / 8, rr = nq % 8;
+          std::vector<std::array<int32_t, 8>> q(nq);
+          for (size_t i = 0; i < nq; i++)
+            for (int k = 0; k < 8; k++) q[i][k] = fanP[8 * (p0 + i) + k];
+          auto wt = [](const std::array<int32_t, 8>& a) { return (int64_t)a[4] * (a[1] >= 0 ? 3 : 2); };
+          for (size_t x = 0, b0 = 0; x < 8; x++) {
+            const size_t len = qq + (x < rr ? 1 : 0);
+            std::stable_sort(q.begin() + b0, q.begin() + b0 + len, [&](const auto& a, const auto& b) { return wt(a) > wt(b); });
+            b0 += len;
+          }
+          for (size_t i = 0; i < nq; i++)
+            for (int k = 0; k < 8; k++) fanP[8 * (p0 + i) + k] = q[i][k];
+        }
+        S.lvU2[L + 1] = (int64_t)fanP.size() / 8;
         if (h->fanStream > 0) {
           // bins of the streamed fan-in: the level's items cut into 8 contiguous ranges (one per XCD, so a
           // column's targets share that XCD's L2, as the per-item launch's xcd_block order does), each
@@ -1528,7 +1608,7 @@ int doFinalize(vb_handle h) {
           upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.trsmRowD, tR) || upload(&S.updD, fan) ||
           upload(&S.fanPairsD, pairs) || upload(&S.tasksFD, tf) || upload(&S.tasksBD, tb) ||
           upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.facD, facItems) || upload(&S.ptD, ptItems) ||
-          upload(&S.ptfD, ptf) || upload(&S.ptfDiagD, ptfDiag) || upload(&S.binD, binsH))
+          upload(&S.ptfD, ptf) || upload(&S.ptfDiagD, ptfDiag) || upload(&S.binD, binsH) || upload(&S.fanPD, fanP))
         return VB_E_HIP;
       S.nPtfDiag = (int64_t)ptfDiag.size() / 2;
       if (S.nPtfDiag && !h->lscr && alloc0(&h->lscr, (size_t)nT * TS * TS)) return VB_E_HIP;
@@ -1800,7 +1880,9 @@ void factorSeq(vb_handle h, const Sched& S) {
   for (int32_t L = 0; L < S.nLevels; L++) {
     const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
     profBegin(h, KF_GEMM);
-    if (S.lvNB.size() && S.lvNB[L] > 0)
+    if (h->fanPair && S.lvU2.size())
+      launch_fanin_pair(d, S.fanPD + 8 * S.lvU2[L], S.fanPairsD, (int)(S.lvU2[L + 1] - S.lvU2[L]), h->st);
+    else if (S.lvNB.size() && S.lvNB[L] > 0)
       launch_fanin_stream(d, S.updD + 4 * u0, S.binD + S.lvB[L], S.fanPairsD, S.lvNB[L], h->st);
     else
       launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
@@ -2146,6 +2228,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
   if (const char* e = getenv("VIBA_PT_FUSE")) h->ptFuseMax = atoll(e);
   if (const char* e = getenv("VIBA_FAN_STREAM")) h->fanStream = std::max<int64_t>(0, atoll(e));
+  if (const char* e = getenv("VIBA_FAN_PAIR")) h->fanPair = atoi(e) != 0;
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2206,7 +2289,7 @@ int vb_destroy(vb_handle h) {
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
     void* sp[] = {S.ptfD, S.ptfDiagD, S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
-                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD, S.binD};
+                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD, S.binD, S.fanPD};
     for (void* p : sp)
       if (p) hipFree(p);
     if (S.graph) hipGraphExecDestroy(S.graph);

@@ -2326,6 +2326,155 @@ __global__ void __launch_bounds__(256) fanin_stream_kernel(Dev d, const int32_t*
 }
 #endif
 
+// Paired fan-in (VIBA_FAN_PAIR): two targets (I1, J), (I2, J) of one column whose contribution lists
+// hold the same source columns K, in the same order (api.hip pairs them within the groups of identical
+// lists: 580k of config C's 701k contributions), stage L_JK once: 3 tiles per 2 products instead of 4,
+// and the product runs on v_mfma_f64_4x4x4_4b in a split-K-by-2 form that keeps the accumulators small
+// enough for two targets.  Eight waves; wave w owns the 32 x 16 strip p in [32 (w & 1), +32), q in
+// [16 (w >> 1), +16) of both targets.  A stage is 16 columns = two k-steps of 8; in a k-step, block i of
+// an instruction takes row group 2r + (i >> 1) and columns 4 (i & 1) .. 4 (i & 1) + 3 of the k-step, so
+// blocks i and i ^ 1 add two partials of one 4 x 4 piece (summed once per target by one swizzle) and
+// blocks 0 / 2 read the same B column group (one address, a broadcast).  Per k-step and wave: 4 A and
+// 4 + 4 B operand reads feed 32 instructions of 512 flops.  Items (8 int32): t1, t2 (< 0: one target),
+// first1, first2, count, atomic.
+constexpr int kPairWaves = 8;
+constexpr int kPRing = 3;
+constexpr int kPStage = 3 * kFanK * TS;  // [L_JK, L_I1K, L_I2K][kFanK columns][64 rows]
+__device__ __forceinline__ int pair_rot(int t) { return 16 * ((t >> 2) & 1) + 8 * (t & 1); }
+
+template <int NT>  // tiles staged per stage: 3 (pair) or 2 (single target)
+__device__ __forceinline__ void pair_issue(const Dev& d, const int32_t* pairs, int32_t f1, int32_t f2, int s,
+                                           double* buf, int wave, int lane) {
+  constexpr int kG = NT * kFanK / 2 / kPairWaves;  // 1 KB loads per wave per stage
+  const int64_t c = s / (TS / kFanK);
+  const int k0 = (s % (TS / kFanK)) * kFanK;
+  const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
+  const int64_t tk = pc[2 * (f1 + c) + 1], t1 = pc[2 * (f1 + c)], t2 = NT == 3 ? pc[2 * (f2 + c)] : 0;
+  const int hi = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < kG; j++) {
+    const int i = wave * kG + j, tile = i / (kFanK / 2), cp = i % (kFanK / 2);
+    const int row = (2 * (lane & 31) - pair_rot(2 * cp + hi)) & 63;
+    const int64_t tt = tile == 0 ? tk : tile == 1 ? t1 : t2;
+    const double* src = d.tiles + tt * TS * TS + (int64_t)(k0 + 2 * cp + hi) * TS + row;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(buf + tile * kFanK * TS + cp * 2 * TS),
+                                     16, 0, 0);
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void pair_accum(const Dev& d, const int32_t* pairs, int32_t f1, int32_t f2, int32_t count,
+                                           double* stg, int wave, int lane, double (&a1)[4][4], double (&a2)[4][4]) {
+  constexpr int kG = NT * kFanK / 2 / kPairWaves;
+  constexpr int kAhead = kPRing - 1;
+  static_assert(kG * kAhead <= 63 && kFanK == 16, "pair ring");
+  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;
+  const int kq = lane >> 4, i = (lane >> 2) & 3, e = lane & 3;
+  const int rowA = pb + 4 * (i >> 1) + e, colB = qb + e;
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) a1[r][c] = 0.0, a2[r][c] = 0.0;
+  const int32_t nst = (TS / kFanK) * count;
+  for (int s = 0; s < kAhead && s < nst; s++) pair_issue<NT>(d, pairs, f1, f2, s, stg + s * kPStage, wave, lane);
+  for (int s = 0; s < nst; s++) {
+    switch (min(kAhead - 1, nst - 1 - s)) {
+      case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kG) : "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + kAhead < nst) pair_issue<NT>(d, pairs, f1, f2, s + kAhead, stg + ((s + kAhead) % kPRing) * kPStage, wave, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    const double* bk = stg + (s % kPRing) * kPStage;
+#pragma unroll
+    for (int ks = 0; ks < 2; ks++) {
+      const int t = 8 * ks + 4 * (i & 1) + kq, rt = pair_rot(t);
+      const double* ak = bk + t * TS;
+      double av[4], b1[4], b2[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) av[r] = ak[(rowA + 8 * r + rt) & 63];
+#pragma unroll
+      for (int c = 0; c < 4; c++) b1[c] = ak[kFanK * TS + ((colB + 4 * c + rt) & 63)];
+      if (NT == 3) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) b2[c] = ak[2 * kFanK * TS + ((colB + 4 * c + rt) & 63)];
+      }
+#ifdef VIBA_FAN_NOMMA  // measurement build: the operand reads without the products
+#pragma unroll
+      for (int r = 0; r < 4; r++) a1[r][r] += av[r] * b1[r] + (NT == 3 ? b2[r] : 0.0);
+#else
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) a1[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], b1[c], a1[r][c], 0, 0, 0);
+      if (NT == 3) {
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) a2[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], b2[c], a2[r][c], 0, 0, 0);
+      }
+#endif
+      __builtin_amdgcn_sched_barrier(0);  // one k-step's operands live at a time (4 waves per SIMD)
+    }
+  }
+}
+
+__device__ __forceinline__ double pair_swz_xor4(double v) {
+  const int2 w = __builtin_bit_cast(int2, v);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_ds_swizzle(w.x, 0x101f), __builtin_amdgcn_ds_swizzle(w.y, 0x101f)));
+}
+
+// C -= acc: acc[r][c] at lane 16b + 4i + j is the partial (columns 4 (i & 1) ..) of C(q = qb + 4c + j,
+// p = pb + 4 (2r + (i >> 1)) + b); the two partials (lane bit 2) are summed by a reduce-scatter over
+// column-group pairs, so lane keeps q = qb + 8 c1 + (lane & 7), p = pb + 8r + 4 ((lane >> 3) & 1) + (lane >> 4)
+__device__ __forceinline__ void pair_store(double* C, bool atomic, int wave, int lane, const double (&acc)[4][4]) {
+  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;
+  const bool kh = (lane & 4) != 0;
+  double v[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+#pragma unroll
+    for (int c1 = 0; c1 < 2; c1++) {
+      const double g0 = acc[r][2 * c1], g1 = acc[r][2 * c1 + 1];
+      v[r][c1] = (kh ? g1 : g0) + pair_swz_xor4(kh ? g0 : g1);
+    }
+  double* Cw = C + (pb + 4 * ((lane >> 3) & 1) + (lane >> 4)) * TS + qb + (lane & 7);
+  if (atomic) {
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c1 = 0; c1 < 2; c1++) atomicAdd(Cw + 8 * r * TS + 8 * c1, -v[r][c1]);
+  } else {
+    double o[4][2];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c1 = 0; c1 < 2; c1++) o[r][c1] = Cw[8 * r * TS + 8 * c1];
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int c1 = 0; c1 < 2; c1++) Cw[8 * r * TS + 8 * c1] = o[r][c1] - v[r][c1];
+  }
+}
+
+__global__ void __launch_bounds__(kPairWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
+fanin_pair_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
+  __shared__ double stg[kPRing * kPStage];
+  const int32_t* wk = work + 8 * xcd_block(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double a1[4][4], a2[4][4];
+  if (wk[1] >= 0) {
+    pair_accum<3>(d, pairs, wk[2], wk[3], wk[4], stg, wave, lane, a1, a2);
+    pair_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[5] != 0, wave, lane, a1);
+    pair_store(d.tiles + (int64_t)wk[1] * TS * TS, wk[5] != 0, wave, lane, a2);
+  } else {
+    pair_accum<2>(d, pairs, wk[2], wk[2], wk[4], stg, wave, lane, a1, a2);
+    pair_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[5] != 0, wave, lane, a1);
+  }
+}
+
 // One elimination level of the tile Cholesky in ONE launch (fan-in + potrf + trsm; the 3-launch form is
 // fanin_kernel / potrf_kernel / trsm_kernel).  Item b (FacItem, 8 int32): fan-in of `count`
 // contributions into `target` -- its list may be split over `nch` items (atomics + an arrival ticket
@@ -2975,6 +3124,9 @@ void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, cons
 
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
   if (n > 0) launchK(fanin_kernel, dim3(n), dim3(kFanWaves * 64), 0, st, d, work, pairs);
+}
+void launch_fanin_pair(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
+  if (n > 0) launchK(fanin_pair_kernel, dim3(n), dim3(kPairWaves * 64), 0, st, d, work, pairs);
 }
 void launch_fanin_stream(const Dev& d, const int32_t* work, const int32_t* bins, const int32_t* pairs, int nBins,
                          hipStream_t st) {
