@@ -1730,6 +1730,18 @@ int doFinalize(vb_handle h) {
     }
   }
   if (upload(&d.obCostOrder, costOrder)) return VB_E_HIP;
+  {
+    std::vector<int32_t> pack((size_t)nObs * 8);
+    std::vector<double> cp((size_t)nObs * 6);
+    for (int64_t i = 0; i < nObs; i++) {
+      const int32_t o = costOrder[i];
+      int32_t* q = &pack[(size_t)i * 8];
+      q[0] = o, q[1] = obPt[o], q[2] = obPose[o], q[3] = obExtr[o], q[4] = obIntr[o], q[5] = obRS[o], q[6] = obVel[o];
+      q[7] = (obRed[(size_t)o * 4 + kSlotIntr] >= 0 ? 1 : 0) | (obRed[(size_t)o * 4 + kSlotVel] >= 0 ? 2 : 0);
+      for (int k = 0; k < 6; k++) cp[(size_t)i * 6 + k] = obC[(size_t)o * 6 + k];
+    }
+    if (upload(&d.obPack, pack) || upload(&d.obCP, cp)) return VB_E_HIP;
+  }
   if (upload(&d.obPose, obPose) || upload(&d.obExtr, obExtr) || upload(&d.obIntr, obIntr) ||
       upload(&d.obVel, obVel) || upload(&d.obRS, obRS) || upload(&d.obPt, obPt) || upload(&d.obRed, obRed) ||
       upload(&d.obCol, obCol) || upload(&d.obC, obC))
@@ -2252,7 +2264,7 @@ int vb_destroy(vb_handle h) {
   hipSetDevice(h->cfg.device);
   hipStreamSynchronize(h->st);
   Dev& d = h->d;
-  void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPose, d.obExtr, d.obIntr, d.obVel,
+  void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPack, d.obCP, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.yZero, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
                   d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.schurRuns, d.schurTasks, d.schurChunks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,

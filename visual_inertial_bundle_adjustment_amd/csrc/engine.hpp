@@ -164,6 +164,11 @@ struct Dev {
           *obRS = nullptr, *obPt = nullptr;
   int32_t* obRed = nullptr;  // 4 per obs
   int32_t* obCostOrder = nullptr;  // visual_cost_kernel's order: per observation range, global shutter first
+  // per position of obCostOrder, the visual kernels' inputs gathered once at finalize: (o, point, pose,
+  // extrinsics, intrinsics, rs, velocity, flags: 1 intrinsics estimated, 2 velocity estimated) and the
+  // observation's 6 doubles, so a lane's first loads are two coalesced 16 B reads, not an index chain
+  int32_t* obPack = nullptr;  // 8 per position
+  double* obCP = nullptr;     // 6 per position
   int32_t* obCol = nullptr;  // 4 per obs (column offset in the landmark's Y panel, -1)
   double* obC = nullptr;     // 6 per obs
   double* cache = nullptr;   // ResultCache per obs

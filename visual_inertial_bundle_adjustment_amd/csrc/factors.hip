@@ -218,7 +218,9 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   const int nrec = (int)max<int64_t>(0, min<int64_t>(64, hi - ob));
   // the observation of this lane: the range in obCostOrder (global shutter first), so a wave takes one
   // evaluation path; its record still goes to the observation's own slot
-  const int32_t o = lane < nrec ? d.obCostOrder[ob + lane] : 0;
+  int4 pa = make_int4(0, 0, 0, 0), pb = make_int4(0, 0, 0, 0);
+  if (lane < nrec) pa = reinterpret_cast<const int4*>(d.obPack)[2 * (ob + lane)], pb = reinterpret_cast<const int4*>(d.obPack)[2 * (ob + lane) + 1];
+  const int32_t o = pa.x;
   double* S = stage[wave];
   double acc[1] = {0.0};
   VisOut v;
@@ -232,23 +234,21 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
     if (dontRetry && c0 < 0.0) {
       ok = false;
     } else {
-      const double* obsC = d.obC + o * 6;
-      const int pt = d.obPt[o];
-      const double* Xp = d.var[0] + (int64_t)pt * 3;
+      const double* obsC = d.obCP + (ob + lane) * 6;
+      const double* Xp = d.var[0] + (int64_t)pa.y * 3;
       v3 X = mk(Xp[0], Xp[1], Xp[2]);
-      se3 Tbw = se3_load(d.var[1] + (int64_t)d.obPose[o] * 7);
-      se3 Tcb = se3_load(d.var[5] + (int64_t)d.obExtr[o] * 7);
-      const double* cam = d.var[4] + (int64_t)d.obIntr[o] * 24;
-      const int rs = d.obRS[o];
+      se3 Tbw = se3_load(d.var[1] + (int64_t)pa.z * 7);
+      se3 Tcb = se3_load(d.var[5] + (int64_t)pa.w * 7);
+      const double* cam = d.var[4] + (int64_t)pb.x * 24;
+      const int rs = pb.y;
       if (rs < 0) {
         ok = vis_eval<true>(obsC, X, Tbw, Tcb, cam, v);
 #pragma unroll
         for (int i = 0; i < 6; i++) v.Jvel[i] = 0.0;
       } else {
-        const double* vp = d.var[2] + (int64_t)d.obVel[o] * 3;
-        const int32_t* red = d.obRed + o * 4;
-        ok = rs_eval<true>(d, obsC, rs, X, Tbw, Tcb, cam, mk(vp[0], vp[1], vp[2]), red[kSlotIntr] >= 0,
-                           red[kSlotVel] >= 0, v, &oor);
+        const double* vp = d.var[2] + (int64_t)pb.z * 3;
+        ok = rs_eval<true>(d, obsC, rs, X, Tbw, Tcb, cam, mk(vp[0], vp[1], vp[2]), (pb.w & 1) != 0,
+                           (pb.w & 2) != 0, v, &oor);
         if (oor) atomicOr(d.err, 1);
       }
       if (!ok && (updateCache || dontRetry)) d.cache[o] = -1.0;
@@ -321,22 +321,23 @@ __global__ void __launch_bounds__(256) visual_cost_kernel(Dev d, int comparable,
   const int64_t i = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   if (i < hi) {
-    const int64_t o = d.obCostOrder[i];  // a permutation of [lo, hi): global shutter first
+    // position i of obCostOrder (a permutation of [lo, hi): global shutter first), packed (Dev::obPack)
+    const int4 pa = reinterpret_cast<const int4*>(d.obPack)[2 * i], pb = reinterpret_cast<const int4*>(d.obPack)[2 * i + 1];
+    const int64_t o = pa.x;
     VisOut v;
     v.Jintr = nullptr;
     bool oor = false, ok;
-    const double* obsC = d.obC + o * 6;
-    const int pt = d.obPt[o];
-    const double* Xp = d.var[0] + (int64_t)pt * 3;
+    const double* obsC = d.obCP + i * 6;
+    const double* Xp = d.var[0] + (int64_t)pa.y * 3;
     v3 X = mk(Xp[0], Xp[1], Xp[2]);
-    se3 Tbw = se3_load(d.var[1] + (int64_t)d.obPose[o] * 7);
-    se3 Tcb = se3_load(d.var[5] + (int64_t)d.obExtr[o] * 7);
-    const double* cam = d.var[4] + (int64_t)d.obIntr[o] * 24;
-    const int rs = d.obRS[o];
+    se3 Tbw = se3_load(d.var[1] + (int64_t)pa.z * 7);
+    se3 Tcb = se3_load(d.var[5] + (int64_t)pa.w * 7);
+    const double* cam = d.var[4] + (int64_t)pb.x * 24;
+    const int rs = pb.y;
     if (rs < 0) {
       ok = vis_eval<false>(obsC, X, Tbw, Tcb, cam, v);
     } else {
-      const double* vp = d.var[2] + (int64_t)d.obVel[o] * 3;
+      const double* vp = d.var[2] + (int64_t)pb.z * 3;
       ok = rs_eval<false>(d, obsC, rs, X, Tbw, Tcb, cam, mk(vp[0], vp[1], vp[2]), false, false, v, &oor);
       if (oor) atomicOr(d.err, 1);
     }
