@@ -2274,7 +2274,7 @@ __device__ __forceinline__ void fan_stage(const double* bk, int wave, int lane, 
 #endif
 }
 
-#if VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2
+#if (VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2) && VIBA_FAN_RING <= 5 && VIBA_FAN_LATE
 __global__ void __launch_bounds__(256) fanin_stream_kernel(Dev d, const int32_t* work, const int32_t* bins,
                                                            const int32_t* pairs) {
   static_assert(kGlds * (kFanRing - 2) + 16 <= 63 && kFanRing >= 3 && kFanRing <= 5, "vmcnt range");
@@ -2338,27 +2338,28 @@ __global__ void __launch_bounds__(256) fanin_stream_kernel(Dev d, const int32_t*
 // 4 + 4 B operand reads feed 32 instructions of 512 flops.  Items (8 int32): t1, t2 (< 0: one target),
 // first1, first2, count, atomic.
 constexpr int kPairWaves = 8;
+constexpr int kPK = 16;  // columns per stage (the single fan-in's kFanK may be rebuilt otherwise)
 constexpr int kPRing = 3;
-constexpr int kPStage = 3 * kFanK * TS;  // [L_JK, L_I1K, L_I2K][kFanK columns][64 rows]
+constexpr int kPStage = 3 * kPK * TS;  // [L_JK, L_I1K, L_I2K][kPK columns][64 rows]
 __device__ __forceinline__ int pair_rot(int t) { return 16 * ((t >> 2) & 1) + 8 * (t & 1); }
 
 template <int NT>  // tiles staged per stage: 3 (pair) or 2 (single target)
 __device__ __forceinline__ void pair_issue(const Dev& d, const int32_t* pairs, int32_t f1, int32_t f2, int s,
                                            double* buf, int wave, int lane) {
-  constexpr int kG = NT * kFanK / 2 / kPairWaves;  // 1 KB loads per wave per stage
-  const int64_t c = s / (TS / kFanK);
-  const int k0 = (s % (TS / kFanK)) * kFanK;
+  constexpr int kG = NT * kPK / 2 / kPairWaves;  // 1 KB loads per wave per stage
+  const int64_t c = s / (TS / kPK);
+  const int k0 = (s % (TS / kPK)) * kPK;
   const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
   const int64_t tk = pc[2 * (f1 + c) + 1], t1 = pc[2 * (f1 + c)], t2 = NT == 3 ? pc[2 * (f2 + c)] : 0;
   const int hi = lane >> 5;
 #pragma unroll
   for (int j = 0; j < kG; j++) {
-    const int i = wave * kG + j, tile = i / (kFanK / 2), cp = i % (kFanK / 2);
+    const int i = wave * kG + j, tile = i / (kPK / 2), cp = i % (kPK / 2);
     const int row = (2 * (lane & 31) - pair_rot(2 * cp + hi)) & 63;
     const int64_t tt = tile == 0 ? tk : tile == 1 ? t1 : t2;
     const double* src = d.tiles + tt * TS * TS + (int64_t)(k0 + 2 * cp + hi) * TS + row;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(buf + tile * kFanK * TS + cp * 2 * TS),
+                                     (__attribute__((address_space(3))) void*)(buf + tile * kPK * TS + cp * 2 * TS),
                                      16, 0, 0);
   }
 }
@@ -2366,9 +2367,9 @@ __device__ __forceinline__ void pair_issue(const Dev& d, const int32_t* pairs, i
 template <int NT>
 __device__ __forceinline__ void pair_accum(const Dev& d, const int32_t* pairs, int32_t f1, int32_t f2, int32_t count,
                                            double* stg, int wave, int lane, double (&a1)[4][4], double (&a2)[4][4]) {
-  constexpr int kG = NT * kFanK / 2 / kPairWaves;
+  constexpr int kG = NT * kPK / 2 / kPairWaves;
   constexpr int kAhead = kPRing - 1;
-  static_assert(kG * kAhead <= 63 && kFanK == 16, "pair ring");
+  static_assert(kG * kAhead <= 63, "pair ring");
   const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;
   const int kq = lane >> 4, i = (lane >> 2) & 3, e = lane & 3;
   const int rowA = pb + 4 * (i >> 1) + e, colB = qb + e;
@@ -2376,7 +2377,7 @@ __device__ __forceinline__ void pair_accum(const Dev& d, const int32_t* pairs, i
   for (int r = 0; r < 4; r++)
 #pragma unroll
     for (int c = 0; c < 4; c++) a1[r][c] = 0.0, a2[r][c] = 0.0;
-  const int32_t nst = (TS / kFanK) * count;
+  const int32_t nst = (TS / kPK) * count;
   for (int s = 0; s < kAhead && s < nst; s++) pair_issue<NT>(d, pairs, f1, f2, s, stg + s * kPStage, wave, lane);
   for (int s = 0; s < nst; s++) {
     switch (min(kAhead - 1, nst - 1 - s)) {
@@ -2396,10 +2397,10 @@ __device__ __forceinline__ void pair_accum(const Dev& d, const int32_t* pairs, i
 #pragma unroll
       for (int r = 0; r < 4; r++) av[r] = ak[(rowA + 8 * r + rt) & 63];
 #pragma unroll
-      for (int c = 0; c < 4; c++) b1[c] = ak[kFanK * TS + ((colB + 4 * c + rt) & 63)];
+      for (int c = 0; c < 4; c++) b1[c] = ak[kPK * TS + ((colB + 4 * c + rt) & 63)];
       if (NT == 3) {
 #pragma unroll
-        for (int c = 0; c < 4; c++) b2[c] = ak[2 * kFanK * TS + ((colB + 4 * c + rt) & 63)];
+        for (int c = 0; c < 4; c++) b2[c] = ak[2 * kPK * TS + ((colB + 4 * c + rt) & 63)];
       }
 #ifdef VIBA_FAN_NOMMA  // measurement build: the operand reads without the products
 #pragma unroll
@@ -3130,7 +3131,7 @@ void launch_fanin_pair(const Dev& d, const int32_t* work, const int32_t* pairs, 
 }
 void launch_fanin_stream(const Dev& d, const int32_t* work, const int32_t* bins, const int32_t* pairs, int nBins,
                          hipStream_t st) {
-#if VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2
+#if (VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2) && VIBA_FAN_RING <= 5 && VIBA_FAN_LATE
   if (nBins > 0) launchK(fanin_stream_kernel, dim3(nBins), dim3(256), 0, st, d, work, bins, pairs);
 #else
   (void)d, (void)work, (void)bins, (void)pairs, (void)nBins, (void)st;
