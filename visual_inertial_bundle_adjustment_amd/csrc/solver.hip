@@ -2743,6 +2743,13 @@ __device__ __forceinline__ void add_agent(double* p, double v) {
   __hip_atomic_fetch_add((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// lane r's value of x in every lane (r a compile-time constant in the unrolled GEMVs): two
+// v_readlane_b32 into SGPRs, the FMA then reads the scalar operand -- no LDS crossbar round trip
+__device__ __forceinline__ double bcast_lane(double x, int r) {
+  const int2 w = __builtin_bit_cast(int2, x);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(w.x, r), __builtin_amdgcn_readlane(w.y, r)));
+}
+
 __global__ void __launch_bounds__(256) fwd_fanout_kernel(Dev d, const int32_t* tasks, int64_t nTask,
                                                          const int32_t* colTiles, const int32_t* colRows,
                                                          const int32_t* expect, const double* linv, double* b,
@@ -2761,7 +2768,7 @@ __global__ void __launch_bounds__(256) fwd_fanout_kernel(Dev d, const int32_t* t
       const double bk = ld_sc1(b + row);
       double v = 0.0;
 #pragma unroll
-      for (int q = 0; q < TS; q++) v += a[q] * __shfl(bk, q, 64);
+      for (int q = 0; q < TS; q++) v += a[q] * bcast_lane(bk, q);
       publish(y + row, row < d.nRed ? v : 0.0, true, ready + K, lane);
     } else {
       const int I = colRows[c];
@@ -2773,7 +2780,7 @@ __global__ void __launch_bounds__(256) fwd_fanout_kernel(Dev d, const int32_t* t
       const double yk = ld_sc1(y + (int64_t)K * TS + lane);
       double v = 0.0;
 #pragma unroll
-      for (int q = 0; q < TS; q++) v += a[q] * __shfl(yk, q, 64);
+      for (int q = 0; q < TS; q++) v += a[q] * bcast_lane(yk, q);
       add_agent(b + (int64_t)I * TS + lane, -v);
       count_up(cnt + I, lane);
     }
@@ -2798,7 +2805,7 @@ __global__ void __launch_bounds__(256) bwd_fanout_kernel(Dev d, const int32_t* t
       const double tj = ld_sc1(yv + row);
       double v = 0.0;
 #pragma unroll
-      for (int r = 0; r < TS; r++) v += a[r] * __shfl(tj, r, 64);
+      for (int r = 0; r < TS; r++) v += a[r] * bcast_lane(tj, r);
       publish(x + row, row < d.nRed ? v : 0.0, true, ready + J, lane);
     } else {
       const int K = rowCol[c];
@@ -2810,7 +2817,7 @@ __global__ void __launch_bounds__(256) bwd_fanout_kernel(Dev d, const int32_t* t
       const double xj = ld_sc1(x + (int64_t)J * TS + lane);
       double v = 0.0;
 #pragma unroll
-      for (int r = 0; r < TS; r++) v += a[r] * __shfl(xj, r, 64);
+      for (int r = 0; r < TS; r++) v += a[r] * bcast_lane(xj, r);
       add_agent(yv + (int64_t)K * TS + lane, -v);
       count_up(cnt + K, lane);
     }
