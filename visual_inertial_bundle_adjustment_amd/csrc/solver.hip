@@ -2698,7 +2698,7 @@ __device__ __forceinline__ bool wait_flag(unsigned* flag, int lane, int32_t* err
     }
     if (v != 1u) atomicOr(err, 16);
   }
-  v = __shfl(v, 0, 64);
+  v = (unsigned)__builtin_amdgcn_readlane((int)v, 0);  // lane 0 polled
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keep the payload loads below the poll
   return v == 1u;
 }
@@ -2731,7 +2731,7 @@ __device__ __forceinline__ bool wait_count(unsigned* c, unsigned expect, int lan
     }
     if (v < expect) atomicOr(err, 16);
   }
-  v = __shfl(v, 0, 64);
+  v = (unsigned)__builtin_amdgcn_readlane((int)v, 0);  // lane 0 polled
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return v >= expect;
 }
