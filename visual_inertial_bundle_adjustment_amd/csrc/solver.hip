@@ -52,10 +52,24 @@ __device__ inline int rv_dim(const Dev& d, int r) { return d.rvDim[r]; }
 //   mode 0: lanes over the Y panel columns: W(:, c) = sum over the observation slots of the column's
 //   block of Jp^T J_x(:, j), Y(:, c) = L^-1 W(:, c) (no atomics: each column has one owner)
 //   mode 1: gradient only into gpNew
+// all-lane sum: within each 16-lane row by DPP (quad swaps, then row rotations by 4 and 8), the four
+// row sums by v_readlane -- VALU-local, no LDS-crossbar ds_bpermute round trips
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const int2 w = __builtin_bit_cast(int2, x);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_update_dpp(0, w.x, kCtrl, 0xf, 0xf, false),
+                                              __builtin_amdgcn_update_dpp(0, w.y, kCtrl, 0xf, 0xf, false)));
+}
+__device__ __forceinline__ double lane_f64(double x, int l) {
+  const int2 w = __builtin_bit_cast(int2, x);
+  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(w.x, l), __builtin_amdgcn_readlane(w.y, l)));
+}
 __device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-  return x;
+  x += dpp_f64<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+  x += dpp_f64<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+  x += dpp_f64<0x124>(x);  // row_ror:4
+  x += dpp_f64<0x128>(x);  // row_ror:8
+  return (lane_f64(x, 0) + lane_f64(x, 16)) + (lane_f64(x, 32) + lane_f64(x, 48));
 }
 
 __device__ __forceinline__ void landmark_eliminate(const Dev& d, double lambda, int mode, int64_t l) {
