@@ -258,8 +258,16 @@ def main():
         # per factorization
         per_launch = st[6] * 2.0 * 64 ** 3 / max(1, st[10])
         achieved = per_launch / (avg_ms * 1e-3) / 1e12
+        # compulsory HBM bytes of one launch: within a level every contribution's L_IK is a distinct
+        # tile (a column K has at most one ancestor column per level) and every L_JK is also the
+        # I-side tile of the diagonal contribution (J, J, K), so the operands are pairs x 32 KB; each
+        # target tile is read and written once (st[5] tiles over the launches bounds the targets)
+        compulsory = (st[6] * 64 * 64 * 8 + st[5] * 2 * 64 * 64 * 8) / max(1, st[10])
+        traffic = pmc_traffic("fanin_kernel")
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": pmc_traffic("fanin_kernel"),
+                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": traffic,
+                "compulsory_bytes_per_launch": compulsory,
+                "traffic_over_compulsory": traffic / compulsory if traffic else None,
                 "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
                           "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
                 "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches,
