@@ -648,8 +648,14 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
       const double* gd = d.var[8] + (int64_t)vi[nv - 1] * 4;
       v3 g = mk(gd[0], gd[1], gd[2]);
       const double* calib = d.var[6] + (int64_t)vi[0] * 32;
+      // the cost pass (mode 2) forms the residual only: every Jacobian block is skipped (a block with
+      // column < 0 is not formed), which halves the IMU kinds' serial chain per lane
+      const bool wantJ = a.mode != 2;
       if (FK == 1) {
         int cols[5] = {E.col[0], E.col[1], E.col[2], E.col[3], E.col[4]};
+        if (!wantJ)
+#pragma unroll
+          for (int q = 0; q < 5; q++) cols[q] = -1;
         inertial_eval(c, calib, d.jac, se3_load(d.var[1] + (int64_t)vi[1] * 7), mk3(d.var[2], vi[2]),
                       se3_load(d.var[1] + (int64_t)vi[3] * 7), mk3(d.var[2], vi[4]), g, E, cols);
       } else {
@@ -666,9 +672,14 @@ __device__ __forceinline__ double small_eval(const Dev& d, const SmallArgs& a, i
         // primary-factor blocks in scratch columns after the slot columns
         const int sc = colc;  // pT 6, pV 3, nT 6, nV 3 => 18 scratch columns
         int cols[5] = {E.col[0], sc, sc + 6, sc + 9, sc + 15};
+        if (!wantJ)
+#pragma unroll
+          for (int q = 0; q < 5; q++) cols[q] = -1;
         inertial_eval(c, calib, d.jac, ps.T_iw, ps.vw, ns.T_iw, ns.vw, g, E, cols);
-        sec_compose(ps, pO, pE, E.J, sc, sc + 6, E.col[spT], E.col[spV], E.col[spO], E.col[spE], false);
-        sec_compose(ns, nO, nE, E.J, sc + 9, sc + 15, E.col[snT], E.col[snV], E.col[snO], E.col[snE], !split);
+        if (wantJ) {
+          sec_compose(ps, pO, pE, E.J, sc, sc + 6, E.col[spT], E.col[spV], E.col[spO], E.col[spE], false);
+          sec_compose(ns, nO, nE, E.J, sc + 9, sc + 15, E.col[snT], E.col[snV], E.col[snO], E.col[snE], !split);
+        }
       }
     } else if (FK == 4) {  // omega prior
       E.m = 3;
