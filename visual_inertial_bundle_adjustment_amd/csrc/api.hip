@@ -405,6 +405,7 @@ struct vb_handle_s {
   int profFamily = -1;
   std::vector<hipEvent_t> profEv;
   size_t profUsed = 0;
+  size_t profDone = 0;  // leading profEv entries known complete, harvested after the next enqueue
   int64_t profLaunches = 0;
   double profMs = 0.0;
 };
@@ -441,14 +442,32 @@ void profHarvest(vb_handle h) {
     h->profMs += ms;
     h->profLaunches++;
   }
-  h->profUsed = 0;
+  h->profUsed = 0, h->profDone = 0;
+}
+// harvest the first n entries (complete at the last stream sync) after the next iteration's work is
+// queued, so the host reads the event times while the device runs instead of between two iterations;
+// the entries still pending move to the front
+void profHarvestPrefix(vb_handle h, size_t n) {
+  if (h->profFamily < 0 || n == 0 || n > h->profUsed) return;
+  for (size_t i = 0; i < n; i += 2) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, h->profEv[i], h->profEv[i + 1]);
+    h->profMs += ms;
+    h->profLaunches++;
+  }
+  std::rotate(h->profEv.begin(), h->profEv.begin() + n, h->profEv.begin() + h->profUsed);
+  h->profUsed -= n, h->profDone = 0;
 }
 
 int checkRsErr(vb_handle h, int32_t e);
+int errFromWords(vb_handle h, const int32_t* ee);
 int checkErr(vb_handle h) {
   int32_t ee[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(ee, h->d.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
+  return errFromWords(h, ee);
+}
+int errFromWords(vb_handle h, const int32_t* ee) {
   const int32_t e = ee[0];
   if (int rc = checkRsErr(h, ee[1])) return rc;
   if (e & 1) return fail(VB_E_RANGE, "RollingShutterData::getEstimate: out of range");
@@ -474,6 +493,16 @@ int readRed(vb_handle h, double* out, int i0, int n) {
   HIPCHK(hipStreamSynchronize(h->st));
   profHarvest(h);
   return 0;
+}
+// vb_optimize's one read per iteration: the scalars red[0, n) and the error words in one stream sync;
+// the profiled events stay for profHarvestPrefix after the next enqueue
+int readRedErr(vb_handle h, double* out, int n) {
+  int32_t ee[2] = {0, 0};
+  HIPCHK(hipMemcpyAsync(out, h->d.red, n * sizeof(double), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipMemcpyAsync(ee, h->d.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+  HIPCHK(hipStreamSynchronize(h->st));
+  h->profDone = h->profUsed;
+  return errFromWords(h, ee);
 }
 
 int doFinalize(vb_handle h) {
@@ -3082,7 +3111,7 @@ void* vb_stream(vb_handle h) { return h ? (void*)h->st : nullptr; }
 int vb_profile_kernel(vb_handle h, int family) {
   if (!h || family < -1 || family >= KF_COUNT) return fail(VB_E_ARG, "bad kernel family");
   profHarvest(h);
-  h->profFamily = family, h->profLaunches = 0, h->profMs = 0.0, h->profUsed = 0;
+  h->profFamily = family, h->profLaunches = 0, h->profMs = 0.0, h->profUsed = 0, h->profDone = 0;
   return 0;
 }
 int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms) {
@@ -3151,9 +3180,10 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     if ((rc = linearizeEnqueue(h, 1, dontRetry)) || (rc = dampFactorSolveEnqueue(h, damping, false)) ||
         (rc = vb_backup(h)) || (rc = applyStepEnqueue(h, 0, 10, 11)) || (rc = costEnqueue(h, 1, false)))
       return rc;
+    profHarvestPrefix(h, h->profDone);  // the previous iteration's event times, read while this one runs
     {
       double r[17];
-      if ((rc = readRed(h, r, 0, 17)) || (rc = checkErr(h))) return rc;
+      if ((rc = readRedErr(h, r, 17))) return rc;
       prevCost = r[0], modelRed = 0.5 * r[16];
       const double n = (double)std::max<int64_t>(1, h->nParams);
       ratios[0] = r[8], ratios[1] = std::sqrt(r[9] / n), ratios[2] = r[10] / n;
