@@ -55,54 +55,6 @@ def test_one_lm_step_matches_oracle(which):
     assert_step_parity(one_step(g), one_step(r))
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
-def test_fused_factor_levels_match_oracle(mode, monkeypatch):
-    """The alternative level forms of the tile Cholesky (VIBA_FUSED_FACTOR, api.hip factorSeq): 1 = one
-    factor_level_kernel launch per level (fan-in, potrf and trsm with in-kernel hand-offs), 2 = fan-in
-    launch + one potrf/trsm launch.  One LM step and a 6-iteration optimize on miniB (the second
-    exercises graph replays: the hand-off flags carry a per-factorization epoch) against the oracle."""
-    monkeypatch.setenv("VIBA_FUSED_FACTOR", mode)
-    g, _ = make(hip(), "miniB")
-    r, _ = make(RefEngine, "miniB")
-    assert_step_parity(one_step(g), one_step(r))
-    from visual_inertial_bundle_adjustment_amd.engine import Settings
-    s = Settings.default(max_num_iterations=6)
-    sg, sr = g.optimize(s), r.optimize(s)
-    assert sg.num_iterations == sr.num_iterations
-    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
-
-
-@pytest.mark.parametrize("bins", ["7", "768"])
-def test_streamed_fanin_matches_oracle(bins, monkeypatch):
-    """The streamed fan-in (VIBA_FAN_STREAM bins per level, solver.hip fanin_stream_kernel: the LDS ring
-    runs on across a bin's items, every item ends in atomics): one LM step and a 6-iteration optimize on
-    miniB against the oracle; 7 bins put many items of different targets into one workgroup."""
-    monkeypatch.setenv("VIBA_FAN_STREAM", bins)
-    g, _ = make(hip(), "miniB")
-    r, _ = make(RefEngine, "miniB")
-    assert_step_parity(one_step(g), one_step(r))
-    from visual_inertial_bundle_adjustment_amd.engine import Settings
-    s = Settings.default(max_num_iterations=6)
-    sg, sr = g.optimize(s), r.optimize(s)
-    assert sg.num_iterations == sr.num_iterations
-    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
-
-
-def test_paired_fanin_matches_oracle(monkeypatch):
-    """The paired fan-in (VIBA_FAN_PAIR, solver.hip fanin_pair_kernel: two targets of one column with the
-    same source list stage L_JK once; split-K-by-2 v_mfma_f64_4x4x4_4b): one LM step and a 6-iteration
-    optimize on miniB against the oracle."""
-    monkeypatch.setenv("VIBA_FAN_PAIR", "1")
-    g, _ = make(hip(), "miniB")
-    r, _ = make(RefEngine, "miniB")
-    assert_step_parity(one_step(g), one_step(r))
-    from visual_inertial_bundle_adjustment_amd.engine import Settings
-    s = Settings.default(max_num_iterations=6)
-    sg, sr = g.optimize(s), r.optimize(s)
-    assert sg.num_iterations == sr.num_iterations
-    assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
-
-
 @pytest.mark.parametrize("which", ["A", "miniB"])
 def test_optimize_trajectory_matches_oracle(which):
     g, _ = make(hip(), which)

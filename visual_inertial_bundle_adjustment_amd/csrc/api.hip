@@ -49,12 +49,6 @@ void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, 
                        double* fwdB, double* fwdY);
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
-void launch_fanin_stream(const Dev& d, const int32_t* work, const int32_t* bins, const int32_t* pairs, int nBins,
-                         hipStream_t st);
-void launch_fanin_pair(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
-void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
-                         unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st);
-void launch_bump_epoch(unsigned* epoch, hipStream_t st);
 void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
                       double* y, const double* stop, hipStream_t st);
 void launch_jacobi_init(const Dev& d, double* jac, hipStream_t st);
@@ -69,10 +63,6 @@ void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, cons
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st);
 void launch_chunk_copy(double* base, const int32_t* idx, int64_t n, int chunk, double* buf, int mode, hipStream_t st);
 void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st);
-void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
-                double* b, double* x, hipStream_t st);
-void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
-                double* t, double* x, hipStream_t st);
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st);
 void launch_solve_fanout(const Dev& d, const int32_t* tasksF, int64_t nF, const int32_t* tasksB, int64_t nB,
                          const int32_t* expF, const int32_t* expB, const int32_t* colTiles, const int32_t* colRows,
@@ -259,23 +249,11 @@ int alloc0(T** dptr, size_t n) {
 // task lists over the same columns (solver.hip fwd/bwd_fanout_kernel).
 struct Sched {
   std::vector<int64_t> lvP, lvT, lvU;
-  // streamed fan-in (fanStream): per level the bins' item ranges (nBins + 1 offsets relative to the
-  // level's first item, from lvB[L] in binD) and the bin count
-  std::vector<int64_t> lvB;
-  std::vector<int32_t> lvNB;
-  int32_t* binD = nullptr;
-  // paired fan-in (fanPair): per level the range of its 8-int items (target pairs of identical source
-  // lists, or single targets) in fanPD
-  std::vector<int64_t> lvU2;
-  int32_t* fanPD = nullptr;
   // levels factored by one potrf + trsm launch (potrf_trsm_kernel): per level the range of its items
   // (diagonal tile, column, target, row, writer) in ptfD; the diagonal tiles to copy back from Lscr
   std::vector<int64_t> lvPF;
   int32_t *ptfD = nullptr, *ptfDiagD = nullptr;
   int64_t nPtfDiag = 0;
-  std::vector<int64_t> lvF, lvFd;   // factor_level_kernel items per level / diagonal items (padded) per level
-  std::vector<int64_t> lvPT, lvPd;  // the same for the potrf + trsm-only items (fusedFactor 2)
-  FacItem *facD = nullptr, *ptD = nullptr;
   int32_t nLevels = 0;
   int64_t nPairs = 0;
   int32_t *potrfTileD = nullptr, *potrfColD = nullptr, *trsmDiagD = nullptr, *trsmTargetD = nullptr,
@@ -345,15 +323,7 @@ struct vb_handle_s {
   int64_t *colStartD = nullptr, *rowStartD = nullptr;
   unsigned* solveFlags = nullptr;
   int numCUs = 256;
-  bool legacySolve = false;  // VIBA_SOLVE_LEGACY=1: one launch pair per tile column
   double *dinv = nullptr, *yvec = nullptr, *rhsWork = nullptr, *linv = nullptr;
-  unsigned* facSync = nullptr;  // factor_level_kernel: per-tile arrival tickets, per-column flags, epoch
-  // VIBA_FUSED_FACTOR: 0 (default) fanin / potrf / trsm launches per level; 1 one factor_level_kernel
-  // launch per level; 2 fanin + one potrf/trsm launch.  Measured on config C (r02): 14.5 / 20.1 / 15.2 ms
-  int fusedFactor = 0;
-  // the forward solve of vb_damp_factor_solve rides the factorization's potrf / trsm launches (single
-  // handle, 3-launch levels); VIBA_FWD_IN_FACTOR=0 keeps the separate fan-out forward solve
-  bool fwdInFactor = true;
   // a factorization without a solve to follow (vb_compute_covariances): no fused forward solve, eager
   bool factorOnly = false;
   // tiles the linearization clears (single handle): every tile but those one Schur item stores whole
@@ -382,8 +352,7 @@ struct vb_handle_s {
   double *jacL = nullptr, *tilesGS = nullptr;  // Jacobi block factors / Gauss-Seidel pseudo-factor
   // LowerPrecSolvePrecond (lowprec.hip): fp32 factor tiles, fp32 diagonal-tile inverses, fp32 vector
   float *lpTiles = nullptr, *lpLinv = nullptr, *lpT = nullptr;
-  // captured launch sequences (tile factorization, reduced solve rhsWork -> xRed)
-  hipGraphExec_t solveGraph = nullptr;
+  // the tile factorization's launches, captured into a HIP graph per schedule (VIBA_NO_GRAPHS=1: eager)
   bool useGraphs = true;
   // state
   bool linearized = false, factored = false;
@@ -397,9 +366,7 @@ struct vb_handle_s {
   // evaluation (st2) does not queue behind the 2.2 GB memset; their assembly waits for it (evZero)
   hipStream_t stZ = nullptr;
   hipEvent_t evZero = nullptr, evSmallE = nullptr, evZJoin = nullptr;
-  bool fanPair = false;      // VIBA_FAN_PAIR=1: paired fan-in (solver.hip fanin_pair_kernel)
-  int64_t fanStream = 0;    // VIBA_FAN_STREAM: fan-in bins per launch for the streamed fan-in (0: one workgroup per item)
-  int64_t ptFuseMax = 256;  // VIBA_PT_FUSE: levels with at most this many off-diagonal tiles run potrf + trsm fused
+  int64_t ptFuseMax = 256;  // levels with at most this many off-diagonal tiles run potrf + trsm in one launch
   double* lscr = nullptr;   // L_JJ of the fused levels' columns (nT tiles), copied back after the factorization
   // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
   int profFamily = -1;
@@ -1123,66 +1090,7 @@ int doFinalize(vb_handle h) {
           }
       }
     }
-    if (getenv("VIBA_SCHUR_STATS")) {  // analysis aid: MFMA counts of Schur tile-product schemes
-      auto blocks16 = [](uint64_t m) { int n = 0; for (int b = 0; b < 4; b++) n += ((m >> (16 * b)) & 0xffff) ? 1 : 0; return n; };
-      double cur = 0, grp = 0, dense = 0, useful = 0, grpTile = 0;
-      int64_t gsz[6] = {0, 0, 0, 0, 0, 0};
-      double shp[5][5] = {}, shpE[5][5] = {};
-      int64_t nGrp = 0;
-      for (int64_t t = 0; t < nTiles; t++) {
-        std::vector<std::pair<std::pair<uint64_t, uint64_t>, int>> sig;
-        for (int64_t e = tcnt[t]; e < tcnt[t + 1]; e++) {
-          const TileEnt& en = ents[e];
-          cur += (double)blocks16(en.maskI) * blocks16(en.maskJ);
-          useful += 3.0 * en.nI * en.nJ / 1024.0;
-          sig.push_back({{en.maskI, en.maskJ}, 1});
-        }
-        std::sort(sig.begin(), sig.end());
-        for (size_t i = 0; i < sig.size();) {
-          size_t j = i;
-          while (j < sig.size() && sig[j].first == sig[i].first) j++;
-          const int nI = __builtin_popcountll(sig[i].first.first), nJ = __builtin_popcountll(sig[i].first.second);
-          grp += std::ceil(3.0 * (j - i) / 4.0) * std::ceil(nI / 16.0) * std::ceil(nJ / 16.0);
-          grpTile += std::ceil(3.0 * (j - i) / 4.0) * blocks16(sig[i].first.first) * blocks16(sig[i].first.second);
-          gsz[std::min<size_t>(5, j - i <= 1 ? 0 : j - i <= 3 ? 1 : j - i <= 7 ? 2 : j - i <= 15 ? 3 : j - i <= 63 ? 4 : 5)] += j - i;
-          {  // MFMAs by compact shape (nbI, nbJ)
-            const int bi = (nI + 15) / 16, bj = (nJ + 15) / 16;
-            shp[bi][bj] += std::ceil(3.0 * (j - i) / 4.0) * bi * bj;
-            shpE[bi][bj] += (double)(j - i);
-          }
-          nGrp++;
-          i = j;
-        }
-        // dense K (3 rows per landmark, batches of 10 landmarks = 8 k-steps) in tile coordinates with
-        // the k-step's union mask, entries sorted by mask
-        {
-          std::vector<std::pair<uint64_t, uint64_t>> ms;
-          for (int64_t e = tcnt[t]; e < tcnt[t + 1]; e++) ms.push_back({ents[e].maskI, ents[e].maskJ});
-          std::sort(ms.begin(), ms.end());
-          for (size_t b0 = 0; b0 < ms.size(); b0 += 10)
-            for (int k = 0; k < 8; k++) {
-              uint64_t mi = 0, mj = 0;
-              for (int r = 4 * k; r < 4 * k + 4 && r < 30; r++) {
-                const size_t e = b0 + r / 3;
-                if (e < ms.size()) mi |= ms[e].first, mj |= ms[e].second;
-              }
-              dense += (double)blocks16(mi) * blocks16(mj);
-            }
-          std::vector<int> hist(8, 0);
-        }
-      }
-      fprintf(stderr, "[schur stats] entries %zu, MFMA-equivalents (16x16x4): current %.3g, dense-K union %.3g, "
-              "identical-mask groups %.3g in %lld groups (%.1f entries/group), useful %.3g\n",
-              ents.size(), cur, dense, grp, (long long)nGrp, (double)ents.size() / std::max<int64_t>(1, nGrp), useful);
-      fprintf(stderr, "[schur stats] identical-mask groups in tile coordinates (dense K) %.3g; entries in groups of "
-              "1 / 2-3 / 4-7 / 8-15 / 16-63 / 64+: %lld %lld %lld %lld %lld %lld\n", grpTile, (long long)gsz[0],
-              (long long)gsz[1], (long long)gsz[2], (long long)gsz[3], (long long)gsz[4], (long long)gsz[5]);
-      for (int bi = 1; bi <= 4; bi++)
-        for (int bj = 1; bj <= 4; bj++)
-          if (shpE[bi][bj] > 0)
-            fprintf(stderr, "[schur stats] compact blocks %d x %d: entries %.3g, MFMAs %.3g\n", bi, bj, shpE[bi][bj], shp[bi][bj]);
-    }
-    // entries of a tile in runs of identical (maskI, maskJ) (solver.hip schur_run2_kernel), by
+    // entries of a tile in runs of identical (maskI, maskJ) (solver.hip schur_run4_kernel), by
     // landmark within a run
     for (int64_t t = 0; t < nTiles; t++)
       std::sort(ents.begin() + tcnt[t], ents.begin() + tcnt[t + 1], [](const TileEnt& a, const TileEnt& b) {
@@ -1225,12 +1133,10 @@ int doFinalize(vb_handle h) {
     gstart.push_back((int64_t)gobs.size());
     d.nGroups = (int64_t)gred.size() / 4;
     if (upload(&d.grpStart, gstart) || upload(&d.grpObs, gobs) || upload(&d.grpRed, gred)) return VB_E_HIP;
-    std::vector<int32_t> tobs;
     // work items: a tile's landmark entries in near-equal chunks of at most kChunkLm; `kind` = 1 when
     // the tile is split over several items (fp64 atomics), else the item owns the tile (plain RMW).
     // Items run in tile-column order (xcd_block hands each XCD a contiguous range of them).
-    int64_t kChunkLm = 256;
-    if (const char* e = getenv("VIBA_SCHUR_CHUNK")) kChunkLm = std::max<int64_t>(8, std::min<int64_t>(256, atoll(e)));
+    const int64_t kChunkLm = 256;
     std::vector<int32_t> itemsPerTile(nTiles, 0);
     for (int32_t J = 0; J < nT; J++)
       for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
@@ -1260,9 +1166,6 @@ int doFinalize(vb_handle h) {
       for (int64_t t = 0; t < nTiles; t++)
         if (!stored[t]) clr.push_back((int32_t)t);
       h->nClear = (int64_t)clr.size();
-      if (getenv("VIBA_SCHUR_STATS"))
-        fprintf(stderr, "[schur stats] tiles %lld: %lld stored whole by one Schur item, %lld cleared\n", (long long)nTiles,
-                (long long)(nTiles - h->nClear), (long long)h->nClear);
       if (upload(&h->clearTilesD, clr)) return VB_E_HIP;
     }
     // per item: its runs of identical (maskI, maskJ) and its tasks (run, chunk of <= kSchurCh landmarks,
@@ -1270,7 +1173,7 @@ int doFinalize(vb_handle h) {
     // kept in (run, chunk) order per wave, so a wave rebuilds its row maps only when its run changes
     // (schur_run4_kernel: no run scan, no per-run global mask reads, balanced waves)
     std::vector<uint64_t> runsH;
-    std::vector<uint32_t> tasksH, chunksH;
+    std::vector<uint32_t> tasksH;
     for (TileWork& w : works) {
       const bool diag = w.I == w.J;
       std::vector<int> rs;
@@ -1285,11 +1188,6 @@ int doFinalize(vb_handle h) {
         double cost;
       };
       std::vector<Tk> tl;
-      w.chunkFirst = (int32_t)chunksH.size();
-      for (size_t r = 0; r + 1 < rs.size(); r++)
-        for (int c0 = rs[r]; c0 < rs[r + 1]; c0 += kSchurCh5)
-          chunksH.push_back((uint32_t)r | ((uint32_t)c0 << 8) | ((uint32_t)std::min(kSchurCh5, rs[r + 1] - c0) << 16));
-      w.nChunks = (uint16_t)(chunksH.size() - w.chunkFirst);
       for (size_t r = 0; r + 1 < rs.size(); r++) {
         const uint64_t mI = ents[w.start + rs[r]].maskI, mJ = diag ? mI : ents[w.start + rs[r]].maskJ;
         runsH.push_back(mI), runsH.push_back(mJ);
@@ -1322,11 +1220,11 @@ int doFinalize(vb_handle h) {
       }
       w.wOff[4] = (uint16_t)(tasksH.size() - w.taskFirst);
     }
-    if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH) || upload(&d.schurChunks, chunksH)) return VB_E_HIP;
+    if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH)) return VB_E_HIP;
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
     d.nTileWorks = (int64_t)works.size();
     h->nTileEnt = (int64_t)ents.size(), h->nObEnt = d.nGroups;
-    if (upload(&d.tileWorks, works) || upload(&d.tileEnts, ents) || upload(&d.tileObs, tobs)) return VB_E_HIP;
+    if (upload(&d.tileWorks, works) || upload(&d.tileEnts, ents)) return VB_E_HIP;
     // tiles this shard's partial system can touch: the enclosing range (vb_shard_tile_range) and the
     // exact set (vb_shard_tiles: landmark and observation-group targets; the root, which also holds
     // the small factors and the damping, receives rather than sends)
@@ -1360,11 +1258,7 @@ int doFinalize(vb_handle h) {
     }
     std::vector<std::vector<int32_t>> cols(nLev);
     for (int32_t J = 0; J < nT; J++) cols[level[J]].push_back(J);
-    int64_t fanWgs = 3072;  // re-tuned for the thin-separator order (2048: -0.5%, 4096-8192: -0.3%)
-    if (const char* e = getenv("VIBA_FANIN_WGS")) fanWgs = std::max<int64_t>(64, atoll(e));
-    // longest chunks first within each XCD's range of a fan-in launch (VIBA_FAN_SORT=0: list order):
-    // +0.9% on the thin-separator order
-    const bool fanSort = !(getenv("VIBA_FAN_SORT") && atoi(getenv("VIBA_FAN_SORT")) == 0);
+    const int64_t fanWgs = 3072;  // re-tuned for the thin-separator order (2048: -0.5%, 4096-8192: -0.3%)
     // Build one schedule.  colSel(J): columns factored here (potrf, trsm, solve diagonal tasks);
     // tgtSel(J): fan-in targets in column J; srcSel(K): contributions from column K; preSel(J): rows
     // whose x is known before the backward solve (their tile tasks run, they get no diagonal task).
@@ -1407,40 +1301,6 @@ int doFinalize(vb_handle h) {
       S.lvP.assign(nLev + 1, 0), S.lvT.assign(nLev + 1, 0), S.lvU.assign(nLev + 1, 0);
       S.lvPF.assign(nLev + 1, 0);
       std::vector<int32_t> ptf, ptfDiag;
-      S.lvF.assign(nLev + 1, 0), S.lvFd.assign(nLev, 0), S.lvPT.assign(nLev + 1, 0), S.lvPd.assign(nLev, 0);
-      std::vector<FacItem> facItems, ptItems;
-      if (getenv("VIBA_FAN_STATS")) {
-        // operand sharing among one column's fan-in targets: targets (I, J) whose lists hold the same
-        // source columns K (the same L_JK tiles) could stage L_JK once for all of them
-        int64_t C = 0, Cdiag = 0, st1 = 0, stAll = 0, st2 = 0, st4 = 0, nGrp = 0, inGrp = 0;
-        for (int32_t J = 0; J < nT; J++) {
-          if (!tgtSel(J)) continue;
-          std::map<std::vector<int32_t>, int64_t> groups;
-          for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
-            const int32_t t = h->colTilesH[c];
-            const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
-            if (m == 0) continue;
-            C += m;
-            if (h->colRowsH[c] == J) Cdiag += m;
-            std::vector<int32_t> key(m);
-            for (int64_t i = 0; i < m; i++) key[i] = pairs[2 * (b + i) + 1];
-            std::sort(key.begin(), key.end());
-            groups[key]++;
-          }
-          for (auto& [key, g] : groups) {
-            const int64_t m = (int64_t)key.size();
-            st1 += 2 * m * g, stAll += m * (g + 1);
-            st2 += m * (g + (g + 1) / 2), st4 += m * (g + (g + 3) / 4);
-            if (g > 1) nGrp++, inGrp += g * m;
-          }
-        }
-        fprintf(stderr, "[viba] fan-in sharing: %lld contributions (%lld into diagonal targets), %lld in %lld groups of "
-                "identical source lists; staged tiles single %lld, shared by pairs %.3f, by quads %.3f, by whole groups %.3f\n",
-                (long long)C, (long long)Cdiag, (long long)inGrp, (long long)nGrp, (long long)st1, (double)st2 / st1,
-                (double)st4 / st1, (double)stAll / st1);
-      }
-      std::vector<int32_t> binsH, fanP;
-      S.lvB.assign(nLev + 1, 0), S.lvNB.assign(nLev, 0), S.lvU2.assign(nLev + 1, 0);
       for (int32_t L = 0; L < nLev; L++) {
         int64_t total = 0;
         for (int32_t J : cols[L])
@@ -1466,7 +1326,7 @@ int doFinalize(vb_handle h) {
             }
           }
         }
-        if (fanSort) {  // longest chunks first: the dispatcher hands them out in order (LPT)
+        {  // longest chunks first within each XCD's range (the dispatcher hands them out in order, LPT): +0.9%
           const size_t u0 = (size_t)S.lvU[L];
           std::vector<std::array<int32_t, 4>> q((fan.size() / 4) - u0);
           for (size_t i = 0; i < q.size(); i++)
@@ -1481,84 +1341,6 @@ int doFinalize(vb_handle h) {
           for (size_t i = 0; i < q.size(); i++)
             for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
         }
-        if (h->fanPair) {
-          // the paired fan-in's items: per column, the targets grouped by their (ordered) source lists --
-          // the counting sort appends sources in one global order, so equal sets are equal sequences --
-          // paired within each group, chunked like the single items; longest first per XCD range
-          const size_t p0 = fanP.size() / 8;
-          for (int32_t J : cols[L]) {
-            if (!tgtSel(J)) continue;
-            const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
-            std::map<std::vector<int32_t>, std::vector<int32_t>> grp;
-            for (int64_t q = 0; q < n; q++) {
-              const int32_t t = h->colTilesH[c0 + q];
-              const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
-              if (m == 0) continue;
-              std::vector<int32_t> key(m);
-              for (int64_t i = 0; i < m; i++) key[i] = pairs[2 * (b + i) + 1];
-              grp[key].push_back(t);
-            }
-            for (auto& [key, mem] : grp) {
-              const int64_t m = (int64_t)key.size(), nch = (m + cs - 1) / cs;
-              for (size_t a = 0; a < mem.size(); a += 2) {
-                const int32_t t1 = mem[a], t2 = a + 1 < mem.size() ? mem[a + 1] : -1;
-                for (int64_t k = 0; k < nch; k++) {
-                  const int64_t s0 = m * k / nch, s1 = m * (k + 1) / nch;
-                  fanP.insert(fanP.end(), {t1, t2, (int32_t)(ccnt[t1] + s0), (int32_t)(t2 >= 0 ? ccnt[t2] + s0 : ccnt[t1] + s0),
-                                           (int32_t)(s1 - s0), nch > 1 ? 1 : 0, 0, 0});
-                }
-              }
-            }
-          }
-          const size_t nq = fanP.size() / 8 - p0, qq = nq / 8, rr = nq % 8;
-          std::vector<std::array<int32_t, 8>> q(nq);
-          for (size_t i = 0; i < nq; i++)
-            for (int k = 0; k < 8; k++) q[i][k] = fanP[8 * (p0 + i) + k];
-          auto wt = [](const std::array<int32_t, 8>& a) { return (int64_t)a[4] * (a[1] >= 0 ? 3 : 2); };
-          for (size_t x = 0, b0 = 0; x < 8; x++) {
-            const size_t len = qq + (x < rr ? 1 : 0);
-            std::stable_sort(q.begin() + b0, q.begin() + b0 + len, [&](const auto& a, const auto& b) { return wt(a) > wt(b); });
-            b0 += len;
-          }
-          for (size_t i = 0; i < nq; i++)
-            for (int k = 0; k < 8; k++) fanP[8 * (p0 + i) + k] = q[i][k];
-        }
-        S.lvU2[L + 1] = (int64_t)fanP.size() / 8;
-        if (h->fanStream > 0) {
-          // bins of the streamed fan-in: the level's items cut into 8 contiguous ranges (one per XCD, so a
-          // column's targets share that XCD's L2, as the per-item launch's xcd_block order does), each
-          // dealt longest-first to the least-loaded of its XCD's bins (b % 8 == x); weight = stages + 2
-          // (the item's start and atomics); the items are then laid out bin by bin
-          const size_t u0 = (size_t)S.lvU[L], nq = fan.size() / 4 - u0;
-          const int32_t nb = (int32_t)std::min<int64_t>((int64_t)nq, h->fanStream);
-          std::vector<std::vector<int32_t>> bin(nb);
-          std::vector<int64_t> load(nb, 0);
-          for (int32_t x = 0, q0 = 0; x < 8; x++) {
-            const int32_t len = (int32_t)(nq / 8 + ((size_t)x < nq % 8 ? 1 : 0));
-            std::vector<int32_t> ord(len);
-            for (int32_t i = 0; i < len; i++) ord[i] = q0 + i;
-            std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return fan[4 * (u0 + a) + 2] > fan[4 * (u0 + b) + 2]; });
-            for (int32_t i : ord) {
-              int32_t best = -1;
-              for (int32_t b = x % nb; b < nb; b += 8)
-                if (best < 0 || load[b] < load[best]) best = b;
-              if (best < 0) best = (int32_t)(i % nb);  // fewer bins than XCDs
-              bin[best].push_back(i), load[best] += 4 * (int64_t)fan[4 * (u0 + i) + 2] + 2;
-            }
-            q0 += len;
-          }
-          std::vector<int32_t> q(fan.begin() + 4 * u0, fan.end());
-          size_t w = 4 * u0;
-          binsH.push_back(0);
-          for (int32_t b = 0; b < nb; b++) {
-            for (int32_t i : bin[b])
-              for (int k = 0; k < 4; k++) fan[w++] = q[4 * (size_t)i + k];
-            binsH.push_back((int32_t)((w - 4 * u0) / 4));
-          }
-          S.lvNB[L] = nb, S.lvB[L + 1] = (int64_t)binsH.size();
-        } else {
-          S.lvB[L + 1] = S.lvB[L];
-        }
         S.lvP[L + 1] = (int64_t)pT.size(), S.lvT[L + 1] = (int64_t)tT.size(), S.lvU[L + 1] = (int64_t)fan.size() / 4;
         if (h->ptFuseMax > 0 && S.lvP[L + 1] > S.lvP[L] && S.lvT[L + 1] - S.lvT[L] <= h->ptFuseMax)
           for (int32_t J : cols[L]) {
@@ -1570,45 +1352,6 @@ int doFinalize(vb_handle h) {
             ptfDiag.insert(ptfDiag.end(), {dt, J});
           }
         S.lvPF[L + 1] = (int64_t)ptf.size() / 5;
-        // the same level as factor_level_kernel items: every diagonal tile of a factored column first
-        // (padded to a multiple of 8), then the off-diagonal tiles and the fan-in-only targets; a
-        // factored tile without contributions still gets one item (its potrf / trsm)
-        std::vector<FacItem> dg, od;
-        for (int32_t J : cols[L]) {
-          const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
-          const bool fac = colSel(J), tgt = tgtSel(J);
-          if (!fac && !tgt) continue;
-          for (int64_t q = 0; q < n; q++) {
-            const int32_t t = h->colTilesH[c0 + q];
-            const int64_t b = ccnt[t], m = tgt ? ccnt[t + 1] - b : 0;
-            if (m == 0 && !fac) continue;
-            const int64_t nch = std::max<int64_t>(1, (m + cs - 1) / cs);
-            const int32_t kind = fac ? (q == 0 ? 1 : 2) : 0;
-            for (int64_t k = 0; k < nch; k++) {
-              const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
-              const FacItem it{t, (int32_t)s0, (int32_t)(s1 - s0), (int32_t)nch, kind, J, h->colTilesH[c0], 0};
-              (kind == 1 ? dg : od).push_back(it);
-            }
-          }
-        }
-        while (dg.size() % 8) dg.push_back(FacItem{0, 0, -1, 1, 0, 0, 0, 0});
-        S.lvFd[L] = (int64_t)dg.size();
-        facItems.insert(facItems.end(), dg.begin(), dg.end());
-        facItems.insert(facItems.end(), od.begin(), od.end());
-        S.lvF[L + 1] = (int64_t)facItems.size();
-        // the potrf + trsm-only form (after a fanin_kernel launch): one item per factored tile, no fan-in
-        std::vector<FacItem> dg2, od2;
-        for (int32_t J : cols[L]) {
-          if (!colSel(J)) continue;
-          const int64_t c0 = h->colStart[J], n = h->colStart[J + 1] - c0;
-          for (int64_t q = 0; q < n; q++)
-            (q == 0 ? dg2 : od2).push_back(FacItem{h->colTilesH[c0 + q], 0, 0, 1, q == 0 ? 1 : 2, J, h->colTilesH[c0], 0});
-        }
-        while (dg2.size() % 8) dg2.push_back(FacItem{0, 0, -1, 1, 0, 0, 0, 0});
-        S.lvPd[L] = (int64_t)dg2.size();
-        ptItems.insert(ptItems.end(), dg2.begin(), dg2.end());
-        ptItems.insert(ptItems.end(), od2.begin(), od2.end());
-        S.lvPT[L + 1] = (int64_t)ptItems.size();
       }
       S.nLevels = nLev, S.nPairs = ccnt[nTiles];
       // fan-out solve task lists, by elimination level: every task of a level only waits on tasks of
@@ -1636,8 +1379,8 @@ int doFinalize(vb_handle h) {
       if (upload(&S.potrfTileD, pT) || upload(&S.potrfColD, pC) || upload(&S.trsmDiagD, tD) ||
           upload(&S.trsmTargetD, tT) || upload(&S.trsmColD, tC) || upload(&S.trsmRowD, tR) || upload(&S.updD, fan) ||
           upload(&S.fanPairsD, pairs) || upload(&S.tasksFD, tf) || upload(&S.tasksBD, tb) ||
-          upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.facD, facItems) || upload(&S.ptD, ptItems) ||
-          upload(&S.ptfD, ptf) || upload(&S.ptfDiagD, ptfDiag) || upload(&S.binD, binsH) || upload(&S.fanPD, fanP))
+          upload(&S.expFD, ef) || upload(&S.expBD, eb) || upload(&S.preReadyD, pre) || upload(&S.ptfD, ptf) ||
+          upload(&S.ptfDiagD, ptfDiag))
         return VB_E_HIP;
       S.nPtfDiag = (int64_t)ptfDiag.size() / 2;
       if (S.nPtfDiag && !h->lscr && alloc0(&h->lscr, (size_t)nT * TS * TS)) return VB_E_HIP;
@@ -1809,8 +1552,7 @@ int doFinalize(vb_handle h) {
   if (upload(&h->colTilesD, h->colTilesH) || upload(&h->colRowsD, h->colRowsH) ||
       upload(&h->rowTilesD, h->rowTilesH) || upload(&h->rowColD, h->rowColH))
     return VB_E_HIP;
-  if (alloc0(&h->dinv, (size_t)(nT + 1) * 1024) || alloc0(&h->linv, (size_t)nT * TS * TS) ||
-      alloc0(&h->facSync, (size_t)nTiles + nT + 1))
+  if (alloc0(&h->dinv, (size_t)(nT + 1) * 1024) || alloc0(&h->linv, (size_t)nT * TS * TS))
     return VB_E_HIP;
   d.nRS = h->nRS;
   if (h->rsDevice) {
@@ -1879,41 +1621,10 @@ void visualCostShard(vb_handle h, int comparable) {
 }
 
 // vb_damp_factor_solve's forward solve runs inside the factorization (potrf_forward / trsm_kernel)
-bool fwdFused(vb_handle h) {
-  return h->fwdInFactor && h->fusedFactor == 0 && h->partWorld <= 1 && !h->sharded && !h->legacySolve;
-}
+bool fwdFused(vb_handle h) { return h->partWorld <= 1 && !h->sharded; }
 
 void factorSeq(vb_handle h, const Sched& S) {
   Dev& d = h->d;
-  if (h->fusedFactor == 2) {  // per level: fanin_kernel, then one potrf + trsm launch (no fan-in items)
-    unsigned* epoch = h->facSync + d.nTiles + d.nT;
-    launch_bump_epoch(epoch, h->st);
-    for (int32_t L = 0; L < S.nLevels; L++) {
-      const int64_t u0 = S.lvU[L], f0 = S.lvPT[L];
-      profBegin(h, KF_GEMM);
-      launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
-      profEnd(h, KF_GEMM);
-      profBegin(h, KF_POTRF);
-      launch_factor_level(d, S.ptD + f0, (int)(S.lvPT[L + 1] - f0), (int)S.lvPd[L], S.fanPairsD, h->facSync,
-                          h->facSync + d.nTiles, epoch, h->dinv, h->st);
-      profEnd(h, KF_POTRF);
-    }
-    launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
-    return;
-  }
-  if (h->fusedFactor) {  // one factor_level_kernel launch per level (fan-in + potrf + trsm)
-    unsigned* epoch = h->facSync + d.nTiles + d.nT;
-    launch_bump_epoch(epoch, h->st);
-    for (int32_t L = 0; L < S.nLevels; L++) {
-      const int64_t f0 = S.lvF[L];
-      profBegin(h, KF_GEMM);
-      launch_factor_level(d, S.facD + f0, (int)(S.lvF[L + 1] - f0), (int)S.lvFd[L], S.fanPairsD, h->facSync,
-                          h->facSync + d.nTiles, epoch, h->dinv, h->st);
-      profEnd(h, KF_GEMM);
-    }
-    launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
-    return;
-  }
   // the forward solve of rhsWork into yvec, fused (schedule 0 of a single handle only)
   const bool fwd = fwdFused(h) && &S == &h->sch[0] && !h->factorOnly;
   double* fb = fwd ? h->rhsWork : nullptr;
@@ -1921,12 +1632,7 @@ void factorSeq(vb_handle h, const Sched& S) {
   for (int32_t L = 0; L < S.nLevels; L++) {
     const int64_t p0 = S.lvP[L], t0 = S.lvT[L], u0 = S.lvU[L];
     profBegin(h, KF_GEMM);
-    if (h->fanPair && S.lvU2.size())
-      launch_fanin_pair(d, S.fanPD + 8 * S.lvU2[L], S.fanPairsD, (int)(S.lvU2[L + 1] - S.lvU2[L]), h->st);
-    else if (S.lvNB.size() && S.lvNB[L] > 0)
-      launch_fanin_stream(d, S.updD + 4 * u0, S.binD + S.lvB[L], S.fanPairsD, S.lvNB[L], h->st);
-    else
-      launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
+    launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
     profEnd(h, KF_GEMM);
     if (S.lvPF[L + 1] > S.lvPF[L]) {  // potrf + trsm in one launch
       profBegin(h, KF_POTRF);
@@ -1946,32 +1652,12 @@ void factorSeq(vb_handle h, const Sched& S) {
   launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
 }
 
-// solve L L^T x = b (b is clobbered), result into x
-void solveSeq(vb_handle h, double* b, double* x) {
-  Dev& d = h->d;
-  for (int32_t J = 0; J < d.nT; J++) {
-    const int64_t c0 = h->colStart[J];
-    profBegin(h, KF_FWD);
-    launch_fwd(d, h->colTilesD + c0, h->colRowsD + c0, (int)(h->colStart[J + 1] - c0), h->linv + (int64_t)J * TS * TS,
-               b, h->yvec, h->st);
-    profEnd(h, KF_FWD);
-  }
-  for (int32_t J = d.nT - 1; J >= 0; J--) {
-    const int64_t r0 = h->rowStart[J];
-    profBegin(h, KF_BWD);
-    launch_bwd(d, J, h->rowTilesD + r0, h->rowColD + r0, (int)(h->rowStart[J + 1] - r0),
-               h->linv + (int64_t)J * TS * TS, h->yvec, x, h->st);
-    profEnd(h, KF_BWD);
-  }
-}
-
 // launch sequences are fixed by the symbolic structure: capture them once into HIP graphs
 // (unless one of their kernel families is being profiled, which needs per-launch events)
-int captureGraph(vb_handle h, const Sched* S, hipGraphExec_t* out) {
+int captureGraph(vb_handle h, const Sched& S, hipGraphExec_t* out) {
   hipGraph_t g;
   HIPCHK(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
-  if (S) factorSeq(h, *S);
-  else solveSeq(h, h->rhsWork, h->d.xRed);
+  factorSeq(h, S);
   HIPCHK(hipStreamEndCapture(h->st, &g));
   HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
   HIPCHK(hipGraphDestroy(g));
@@ -1990,16 +1676,9 @@ int factorReduced(vb_handle h, int which = 0) {
     return 0;
   }
   if (!S.graph)
-    if (int rc = captureGraph(h, &S, &S.graph)) return rc;
+    if (int rc = captureGraph(h, S, &S.graph)) return rc;
   HIPCHK(hipGraphLaunch(S.graph, h->st));
   return 0;
-}
-
-// resident workgroups per CU of the persistent fan-out solves (VIBA_SOLVE_WG_PER_CU; every launched
-// workgroup must be resident at once: the kernels' occupancy allows 3 per CU)
-int solveWgPerCU() {
-  static const int k = getenv("VIBA_SOLVE_WG_PER_CU") ? std::max(1, std::min(3, atoi(getenv("VIBA_SOLVE_WG_PER_CU")))) : 1;
-  return k;
 }
 
 // solves with rhsWork as right-hand side, result in xRed (schedule `which`, phases bit 0 forward,
@@ -2007,24 +1686,13 @@ int solveWgPerCU() {
 int solveReduced(vb_handle h, int which = 0, int phases = 3) {
   Sched& S = h->sch[which];
   if (!S.built) return fail(VB_E_STATE, "no solve schedule here (partition root on rank 0 only)");
-  if (!h->legacySolve || h->partWorld > 1) {
-    Dev& d = h->d;
-    profBegin(h, KF_FWD);
-    launch_solve_fanout(d, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD,
-                        h->rowTilesD, h->rowColD, h->linv, h->rhsWork, h->yvec, d.xRed, h->solveFlags,
-                        h->numCUs * solveWgPerCU(),
-                        h->st, phases, S.preReadyD, S.nPreReady);
-    profEnd(h, KF_FWD);
-    return 0;
-  }
-  const bool prof = h->profFamily == KF_FWD || h->profFamily == KF_BWD;
-  if (!h->useGraphs || prof) {
-    solveSeq(h, h->rhsWork, h->d.xRed);
-    return 0;
-  }
-  if (!h->solveGraph)
-    if (int rc = captureGraph(h, nullptr, &h->solveGraph)) return rc;
-  HIPCHK(hipGraphLaunch(h->solveGraph, h->st));
+  Dev& d = h->d;
+  // one persistent workgroup per CU (every launched workgroup must be resident at once)
+  profBegin(h, KF_FWD);
+  launch_solve_fanout(d, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD, h->rowTilesD,
+                      h->rowColD, h->linv, h->rhsWork, h->yvec, d.xRed, h->solveFlags, h->numCUs, h->st, phases,
+                      S.preReadyD, S.nPreReady);
+  profEnd(h, KF_FWD);
   return 0;
 }
 
@@ -2159,7 +1827,7 @@ int precondApply(vb_handle h, const double* r, double* z) {
     g.tiles = h->tilesGS;
     const Sched& S = h->sch[0];
     launch_solve_fanout(g, S.tasksFD, S.nF, S.tasksBD, S.nB, S.expFD, S.expBD, h->colTilesD, h->colRowsD, h->rowTilesD,
-                        h->rowColD, h->linv, h->pcgB, h->yvec, z, h->solveFlags, h->numCUs * solveWgPerCU(), h->st, 3,
+                        h->rowColD, h->linv, h->pcgB, h->yvec, z, h->solveFlags, h->numCUs, h->st, 3,
                         nullptr, 0);
     return 0;
   }
@@ -2264,12 +1932,6 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   vb_handle h = new vb_handle_s();
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
-  if (const char* e = getenv("VIBA_FUSED_FACTOR")) h->fusedFactor = atoi(e);
-  if (const char* e = getenv("VIBA_FWD_IN_FACTOR")) h->fwdInFactor = e[0] != '0';
-  if (const char* e = getenv("VIBA_SOLVE_LEGACY")) h->legacySolve = e[0] == '1';
-  if (const char* e = getenv("VIBA_PT_FUSE")) h->ptFuseMax = atoll(e);
-  if (const char* e = getenv("VIBA_FAN_STREAM")) h->fanStream = std::max<int64_t>(0, atoll(e));
-  if (const char* e = getenv("VIBA_FAN_PAIR")) h->fanPair = atoi(e) != 0;
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2296,12 +1958,12 @@ int vb_destroy(vb_handle h) {
   void* ptrs[] = {d.rvKind, d.rvHandle, d.rvDim, d.rvOff, d.rvRowEnd, d.obCostOrder, d.obPack, d.obCP, d.obPose, d.obExtr, d.obIntr, d.obVel,
                   d.obRS, d.obPt, d.obRed, d.obCol, d.obC, d.cache, d.Jt, d.lmObs, d.lmY, d.lmBlk, d.blkRed,
                   d.blkCol, d.pcRow, d.pcBlk, d.bxStart, d.bxEnt, d.Vchol, d.gp, d.z, d.xp, d.Y, d.yZero, d.gpNew, d.zNew, d.ptLm, d.oxStart, d.oxObs, d.oxSlot,
-                  d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.schurRuns, d.schurTasks, d.schurChunks, d.tileEnts, d.tileObs, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
+                  d.lxStart, d.lxLm, d.lxCol, d.lxChunk, d.tileWorks, d.schurRuns, d.schurTasks, d.tileEnts, d.grpStart, d.grpObs, d.grpRed, d.tileIdx, d.tiles, d.gRed, d.rhs, d.xRed, d.gRedNew, d.stepRed,
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.redS, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->lscr, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
-                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->lpTiles, h->lpLinv, h->lpT, h->clearTilesD, h->facSync,
+                  h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->lpTiles, h->lpLinv, h->lpT, h->clearTilesD,
                   (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise};
   for (void* p : ptrs)
     if (p) hipFree(p);
@@ -2330,12 +1992,11 @@ int vb_destroy(vb_handle h) {
   for (auto& e : h->profEv) hipEventDestroy(e);
   for (Sched& S : h->sch) {
     void* sp[] = {S.ptfD, S.ptfDiagD, S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
-                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD, S.facD, S.ptD, S.binD, S.fanPD};
+                  S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD};
     for (void* p : sp)
       if (p) hipFree(p);
     if (S.graph) hipGraphExecDestroy(S.graph);
   }
-  if (h->solveGraph) hipGraphExecDestroy(h->solveGraph);
   hipStreamDestroy(h->st);
   delete h;
   return 0;
@@ -2651,22 +2312,17 @@ int dampFactorSolveEnqueue(vb_handle h, double lambda, bool clearErr) {
   HIPCHK(hipEventRecord(h->ev[2], h->st));
   // the observation-group Gram blocks on the side stream beside the landmark elimination (both stream
   // records from HBM; neither reads what the other writes), joined before the tile products
-  // (VIBA_GROUPS_SIDE=0: in line)
-  static const bool groupsSide = !(getenv("VIBA_GROUPS_SIDE") && atoi(getenv("VIBA_GROUPS_SIDE")) == 0);
   const int addId = (h->isRoot || h->partWorld > 1) ? 1 : 0;
   launch_damp(d, lambda, addId, h->st);
-  if (groupsSide) {
-    HIPCHK(hipEventRecord(h->evFork, h->st));
-    HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
-    launch_groups(d, lambda, h->st2);
-    HIPCHK(hipEventRecord(h->evJoin, h->st2));
-  }
+  HIPCHK(hipEventRecord(h->evFork, h->st));
+  HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
+  launch_groups(d, lambda, h->st2);
+  HIPCHK(hipEventRecord(h->evJoin, h->st2));
   profBegin(h, KF_LANDMARK);
   launch_landmark(d, lambda, 0, d.lmB, d.lmE, h->st);
   profEnd(h, KF_LANDMARK);
   HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
-  if (groupsSide) HIPCHK(hipStreamWaitEvent(h->st, h->evJoin, 0));
-  else launch_groups(d, lambda, h->st);
+  HIPCHK(hipStreamWaitEvent(h->st, h->evJoin, 0));
   profBegin(h, KF_SCHUR);
   launch_schur_products(d, lambda, h->st);
   profEnd(h, KF_SCHUR);

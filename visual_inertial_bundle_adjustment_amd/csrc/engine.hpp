@@ -110,12 +110,6 @@ struct TileEnt {
   uint64_t maskI, maskJ;  // tile rows (r % 64) of those columns; ascending, so row r is column
                           // popcount(mask & ((1 << r) - 1)) of the run
 };
-// one work item of factor_level_kernel (solver.hip): fan-in of contributions [first, first + count) into
-// tile `target` (its list split over nch items), then kind 1 potrf (diagonal of column J) / 2 trsm with
-// the diagonal tile diagTile of column J / 0 nothing; count < 0: padding no-op
-struct FacItem {
-  int32_t target, first, count, nch, kind, J, diagTile, pad;
-};
 struct TileWork {
   int32_t tile, I, J, count;  // count <= 256 landmark entries
   int64_t start;              // into tileEnts
@@ -125,24 +119,10 @@ struct TileWork {
   // tasks at schurTasks[taskFirst ..), wave w's at [wOff[w], wOff[w + 1])
   int32_t runFirst, taskFirst;
   uint16_t nRuns, wOff[5];
-  // schur_run5_kernel: the item's landmark chunks (run | first entry << 8 | landmarks << 16, at most
-  // kSchurCh5 landmarks each) at schurChunks[chunkFirst ..)
-  int32_t chunkFirst;
-  uint16_t nChunks, pad2;
 };
 // one task of schur_run4_kernel (32 bits): run (8) | first entry of its landmark chunk (8) | landmarks
 // (6) | first compact block row (2); built at finalize with kSchurCh landmarks x kSchurTR block rows
-#ifndef VIBA_SCHUR_CH
-#define VIBA_SCHUR_CH 16
-#endif
-#ifndef VIBA_SCHUR_TR
-#define VIBA_SCHUR_TR 2
-#endif
-constexpr int kSchurCh = VIBA_SCHUR_CH, kSchurTR = VIBA_SCHUR_TR;
-#ifndef VIBA_SCHUR_CH5
-#define VIBA_SCHUR_CH5 12
-#endif
-constexpr int kSchurCh5 = VIBA_SCHUR_CH5;
+constexpr int kSchurCh = 16, kSchurTR = 2;
 
 struct Dev {
   // variables
@@ -206,9 +186,7 @@ struct Dev {
   TileWork* tileWorks = nullptr;
   uint64_t* schurRuns = nullptr;   // per run: maskI, maskJ
   uint32_t* schurTasks = nullptr;
-  uint32_t* schurChunks = nullptr;
   TileEnt* tileEnts = nullptr;
-  int32_t* tileObs = nullptr;  // (unused: direct terms go through the observation groups)
   // direct visual terms by observation group (observations sharing their 4 reduced blocks: one rig,
   // one camera): grpStart[g] .. grpStart[g + 1] into grpObs, grpRed[4 g + slot] the blocks
   int64_t nGroups = 0;

@@ -1,17 +1,15 @@
-// Sparse direct solve of the damped Gauss-Newton system (gfx950), replacing BaSpaCho's
-// sparse elimination of the point range + supernodal Cholesky (Optimizer.cpp:200-231).
+// Sparse direct solve of the damped Gauss-Newton system (gfx950), replacing BaSpaCho's sparse
+// elimination of the point range + supernodal Cholesky (Optimizer.cpp:200-231).
 //
-//   landmark_kernel      one thread per landmark: V = sum Jp^T Jp (damped, Optimizer.cpp:136-146),
-//                        3x3 Cholesky, z = L^-1 g_p, Y = L^-1 W for the landmark's distinct blocks
-//   schur_kernel         one workgroup per reduced variable X1 (column block of S): LDS-resident
-//                        accumulator of S(:, X1) = H_direct(:, X1) (+damping) - sum_l Y_l^T Y_l,
-//                        written once to the tile store (exclusive column ownership, no global
-//                        atomics); also the reduced RHS g' = g - sum_l Y^T z
-//   potrf_trsm_kernel /  right-looking tile Cholesky, one tile column per launch pair:
-//   gemm_update_kernel   in-wave left-looking potrf of the 64x64 diagonal tile in LDS, row-parallel
-//                        trsm, and the trailing update A_IK -= L_IJ L_KJ^T on fp64 MFMA
-//                        (v_mfma_f64_16x16x4_f64)
-//   fwd/bwd_kernel       tile triangular solves; backsub_kernel: points x_p = L^-T (z - Y x_c)
+//   landmark_obs_kernel   one wave per landmark: V = sum Jp^T Jp (damped, Optimizer.cpp:136-146), g_p, the
+//   (_wg, landmark_kernel) W panel in LDS, 3x3 Cholesky, z = L^-1 g_p, Y = L^-1 W
+//   obs_group_kernel      direct visual terms J~^T J~ per (rig, camera) group on fp64 MFMA
+//   schur_run4_kernel     S_IJ -= sum_l Y_lI^T Y_lJ by target tile, compact runs, register operands
+//   fanin_kernel          level-scheduled tile Cholesky: A_IJ -= sum_K L_IK L_JK^T (v_mfma_f64_16x16x4)
+//   potrf4_kernel,        64x64 diagonal factor (+ 16x16 block inverses), off-diagonal L_IJ = A_IJ L_JJ^-T;
+//   trsm_kernel,          the forward solve rides these launches
+//   potrf_trsm_kernel
+//   fwd/bwd_fanout_kernel persistent fan-out triangular solves; backsub_kernel x_p = L^-T (z - Y x_c)
 #include "device_math.hpp"
 #include "engine.hpp"
 #include <algorithm>
@@ -352,91 +350,22 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 // (its rows ascend with its columns), K is dense (3 rows per landmark), and the compact nJ x nI product
 // needs only ceil(nJ / 16) x ceil(nI / 16) blocks of v_mfma_f64_16x16x4_f64 per 4 K rows: 34M MFMAs
 // on config C against 70M for the tile-coordinate form (16-row masks, one padded k-step per landmark;
-// VIBA_SCHUR_STATS=1 prints the counts; the tile-coordinate and LDS-image forms are in the history,
-// DESIGN.md §8).  No images and no barriers: a task is (run, chunk of <= kCh landmarks, compact
+// that form and the LDS-image forms are in the history).  No images and no barriers: a task is (run, chunk of <= kCh landmarks, compact
 // block row a of the J side); a wave takes every fourth task of its item and accumulates the nI-wide
 // block row over the chunk's dense K (3 rows per landmark), its operands gathered straight from the Y
 // panel (lane l: compact column 16 a + (l & 15) / 16 b + (l & 15), K row 4 ks + (l >> 4)), the next
 // k-step's loads issued before the current MFMAs.  At the end of the task the block row is added into
 // the item's LDS tile accumulator with LDS atomics (tasks of different waves overlap), through
 // wave-private compact -> tile row maps.
-#ifndef VIBA_SCHUR_CH
-#define VIBA_SCHUR_CH 16
-#endif
-#ifndef VIBA_SCHUR_TR
-#define VIBA_SCHUR_TR 2
-#endif
-constexpr int kCh = VIBA_SCHUR_CH;  // landmarks per task
-constexpr int kTR = VIBA_SCHUR_TR;  // compact block rows per task (1 or 2)
-#ifndef VIBA_SCHUR_PF
-#define VIBA_SCHUR_PF 1
-#endif
-constexpr int kPF = VIBA_SCHUR_PF;  // k-steps of operand gathers in flight
-// schur_run2's gathers: 0 compiler-scheduled loads; 1 or 2 sets of hand-counted inline-asm loads in
-// flight ahead of the MFMAs
-#ifndef VIBA_SCHUR_PFD
-#define VIBA_SCHUR_PFD 0
-#endif
-#ifndef VIBA_SCHUR_EXPT
-#define VIBA_SCHUR_EXPT 0
-#endif
+constexpr int kCh = kSchurCh;  // landmarks per task
+constexpr int kTR = kSchurTR;  // compact block rows per task (1 or 2)
 
-// One task's K loop: acc[i][b] += A_i^T B_b over the dense K rows (3 per landmark) of landmarks
-// c0 .. c0 + rows / 3, A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block
-// b < NBI.  Lane (l4, l15) at k-step ks takes K row kr = 4 ks + l4, i.e. plane q = kr % 3 of landmark
-// c0 + kr / 3 (advanced incrementally), and gathers its NR + NBI operands at fixed offsets 16 i / 16 b
-// from the landmark's first panel column in tile J / I.  Columns past nJ / nI load neighbouring
-// panel data into accumulator rows / columns that are never stored; K rows past `rows` read the zero
-// pad.  The next step's gathers are issued before the current step's MFMAs.
-#ifndef VIBA_SCHUR_ASMLD
-#define VIBA_SCHUR_ASMLD 1
-#endif
-// one gather of an 8-B (fp64) / 4-B (fp32) operand at an immediate byte offset I * STRIDE, as inline asm
-// (invisible to hipcc's waitcnt pass: the caller waits with vm_wait and pins the destination)
-template <int STRIDE>
-__device__ __forceinline__ void gather_asm(double& dst, const double* p, int i) {
-  switch (i) {
-    case 0: asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
-    case 1: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
-    case 2: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
-    default: asm volatile("global_load_dwordx2 %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
-  }
-}
-template <int STRIDE>
-__device__ __forceinline__ void gather_asm(float& dst, const float* p, int i) {
-  switch (i) {
-    case 0: asm volatile("global_load_dword %0, %1, off" : "=v"(dst) : "v"(p) : "memory"); break;
-    case 1: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(STRIDE) : "memory"); break;
-    case 2: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(2 * STRIDE) : "memory"); break;
-    default: asm volatile("global_load_dword %0, %1, off offset:%2" : "=v"(dst) : "v"(p), "i"(3 * STRIDE) : "memory"); break;
-  }
-}
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// C -= acc of one task through the run's compact -> tile row maps.  VIBA_SCHUR_EPI=1 (default): every
-// map entry of the task read up front (one LDS wait), the adds predicated; 0: the map read per
-// accumulator row inside a branch (a wait per row)
-#ifndef VIBA_SCHUR_EPI
-#define VIBA_SCHUR_EPI 1
-#endif
+// C -= acc of one task through the run's compact -> tile row maps: every map entry of the task read up
+// front (one LDS wait), the adds predicated
 template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], int a0, int l4, int l15,
                                                const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
   int colT[NBI];
-#if VIBA_SCHUR_EXPT == 3
-  // diagnostic build: no scatter into C (the accumulators are still consumed), results garbage
-  double sink = 0.0;
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int b = 0; b < NBI; b++) sink += acc[i][b][0] + acc[i][b][3];
-  if (sink == 12345.678) C[l15] = sink;
-  return;
-#endif
-#if VIBA_SCHUR_EPI
   int rowT[NR][4];
 #pragma unroll
   for (int b = 0; b < NBI; b++) colT[b] = posI[min(16 * b + l15, TS - 1)];
@@ -453,39 +382,14 @@ __device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], in
       for (int b = 0; b < NBI; b++)
         if ((!DIAG || a0 + i <= b) && mv && 16 * b + l15 < nI) atomicAdd(C + rowT[i][q] * TS + colT[b], -(double)acc[i][b][q]);
     }
-#else
-#pragma unroll
-  for (int b = 0; b < NBI; b++) {
-    const int n = 16 * b + l15;
-    colT[b] = n < nI ? posI[n] : -1;
-  }
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int m = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q;
-      if (m >= nJ) continue;
-      double* Cr = C + posJ[m] * TS;
-#pragma unroll
-      for (int b = 0; b < NBI; b++)
-        if ((!DIAG || a0 + i <= b) && colT[b] >= 0) atomicAdd(Cr + colT[b], -(double)acc[i][b][q]);
-    }
-#endif
 }
 
-// rhs -= Y^T z over a chunk's landmarks (diagonal tiles), lanes over the run's compact I columns.
-// VIBA_SCHUR_RHS=1 (default): four landmarks' loads in flight per step; 0: one landmark at a time
-#ifndef VIBA_SCHUR_RHS
-#define VIBA_SCHUR_RHS 1
-#endif
+// rhs -= Y^T z over a chunk's landmarks (diagonal tiles), lanes over the run's compact I columns, four
+// landmarks' loads in flight per step
 __device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2], const TileEnt* ents, int c0, int nl,
                                           int lane, const uint8_t* posI, double* rq) {
-#if VIBA_SCHUR_EXPT == 4
-  return;  // diagnostic build: no rhs
-#endif
   const int64_t pq = d.nYcol;
   double racc = 0.0;
-#if VIBA_SCHUR_RHS
   int e = c0;
   for (; e + 4 <= c0 + nl; e += 4) {
     double y[4][3], z[4][3];
@@ -500,9 +404,6 @@ __device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2
     for (int u = 0; u < 4; u++) racc += y[u][0] * z[u][0] + y[u][1] * z[u][1] + y[u][2] * z[u][2];
   }
   for (; e < c0 + nl; e++) {
-#else
-  for (int e = c0; e < c0 + nl; e++) {
-#endif
     const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
     const double* zz = d.z + 3 * (int64_t)ents[e].lm;
     racc += (double)y[0] * zz[0] + (double)y[pq] * zz[1] + (double)y[2 * pq] * zz[2];
@@ -510,6 +411,13 @@ __device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2
   atomicAdd(&rq[posI[lane]], -racc);
 }
 
+// One task's K loop: acc[i][b] += A_i^T B_b over the dense K rows (3 per landmark) of landmarks
+// c0 .. c0 + rows / 3, A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block
+// b < NBI.  Lane (l4, l15) at k-step ks takes K row kr = 4 ks + l4, i.e. plane q = kr % 3 of landmark
+// c0 + kr / 3 (advanced incrementally), and gathers its NR + NBI operands at fixed offsets 16 i / 16 b
+// from the landmark's first panel column in tile J / I.  Columns past nJ / nI load neighbouring
+// panel data into accumulator rows / columns that are never stored; K rows past `rows` read the zero
+// pad.  The next step's gathers are issued before the current step's MFMAs.
 template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0, int rows, int a0, int l4, int l15,
                                            const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
@@ -525,12 +433,7 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
   int kr = l4, e = c0 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
   auto ld = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
     const bool kv = kr < rows;
-#if VIBA_SCHUR_EXPT == 1
-    // diagnostic build: every gather inside the first 4096 panel columns (L2-resident), results garbage
-    const uint2 c = make_uint2(ec[kv ? e : c0].x & 4095u, ec[kv ? e : c0].y & 4095u);
-#else
     const uint2 c = ec[kv ? e : c0];
-#endif
     const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
     const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
     const rec_t* pI = kv ? base + c.x : zp;
@@ -542,94 +445,12 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     if (q == 3) q = 0, e += 1;
   };
   auto mm = [&](const rec_t (&av)[NR], const rec_t (&bv)[NBI]) {
-#if VIBA_SCHUR_EXPT == 2
-    // diagnostic build: no MFMAs (the operands are still consumed), results garbage
-#pragma unroll
-    for (int i = 0; i < NR; i++)
-#pragma unroll
-      for (int b = 0; b < NBI; b++) acc[i][b][0] += av[i] + bv[b];
-#else
 #pragma unroll
     for (int i = 0; i < NR; i++)
 #pragma unroll
       for (int b = 0; b < NBI; b++)
         if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
-#endif
   };
-#if VIBA_SCHUR_PFD > 0
-  // the gathers as inline-asm loads counted by hand (hipcc's waitcnt pass put a vmcnt(0) in front of
-  // every step's MFMAs, so the loads issued a step ahead were waited for at once): VIBA_SCHUR_PFD sets
-  // of gathers in flight while a step's MFMAs run
-  constexpr int kN = NR + NBI;
-  auto lda = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
-    const bool kv = kr < rows;
-    const uint2 c = ec[kv ? e : c0];
-    const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
-    const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
-    const rec_t* pI = kv ? base + c.x : zp;
-#pragma unroll
-    for (int i = 0; i < NR; i++) gather_asm<16 * sizeof(rec_t)>(av[i], pJ, i);
-#pragma unroll
-    for (int b = 0; b < NBI; b++) gather_asm<16 * sizeof(rec_t)>(bv[b], pI, b);
-    kr += 4, e += 1, q += 1;
-    if (q == 3) q = 0, e += 1;
-  };
-  auto pin = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
-#pragma unroll
-    for (int i = 0; i < NR; i++) asm volatile("" : "+v"(av[i]));
-#pragma unroll
-    for (int b = 0; b < NBI; b++) asm volatile("" : "+v"(bv[b]));
-  };
-#if VIBA_SCHUR_PFD == 1
-  rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
-  lda(a0v, b0v);
-  for (int ks = 0; ks < nks; ks += 2) {
-    if (ks + 1 < nks) {
-      lda(a1v, b1v);
-      vm_wait<kN>();
-    } else {
-      vm_wait<0>();
-    }
-    pin(a0v, b0v);
-    mm(a0v, b0v);
-    if (ks + 1 < nks) {
-      if (ks + 2 < nks) {
-        lda(a0v, b0v);
-        vm_wait<kN>();
-      } else {
-        vm_wait<0>();
-      }
-      pin(a1v, b1v);
-      mm(a1v, b1v);
-    }
-  }
-#else
-  rec_t av[3][NR], bv[3][NBI];
-  lda(av[0], bv[0]);
-  if (1 < nks) lda(av[1], bv[1]);
-  // step k uses set k % 3; before its MFMAs step k + 2 is issued, then all but the two newest sets land
-  auto step = [&](int k, rec_t (&a)[NR], rec_t (&b)[NBI], rec_t (&an)[NR], rec_t (&bn)[NBI]) {
-    if (k + 2 < nks) {
-      lda(an, bn);
-      vm_wait<2 * kN>();
-    } else if (k + 1 < nks) {
-      vm_wait<kN>();
-    } else {
-      vm_wait<0>();
-    }
-    pin(a, b);
-    mm(a, b);
-  };
-  for (int ks = 0; ks < nks; ks += 3) {
-    step(ks, av[0], bv[0], av[2], bv[2]);
-    if (ks + 1 < nks) step(ks + 1, av[1], bv[1], av[0], bv[0]);
-    if (ks + 2 < nks) step(ks + 2, av[2], bv[2], av[1], bv[1]);
-  }
-#endif
-#elif VIBA_SCHUR_EXPT == 5
-  // diagnostic build: no k-loop (no gathers, no MFMAs), results garbage
-  if (nks < 0) acc[0][0][0] = 1.0;
-#else
   rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
   ld(a0v, b0v);
   for (int ks = 0; ks < nks; ks += 2) {
@@ -638,158 +459,20 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     if (ks + 2 < nks) ld(a0v, b0v);
     if (ks + 1 < nks) mm(a1v, b1v);
   }
-#endif
   // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
   schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
 }
 
-#ifndef VIBA_SCHUR_WPE
-#define VIBA_SCHUR_WPE 4
-#endif
-// diagnostic build (-DVIBA_SCHUR_TIMING): per-wave cycle sums of schur_run2's phases (s_memtime), read by
-// vb_debug_schur_times: 0 setup, 1 run scan, 2 tasks (3 of them k-loops + epilogues, 4 rhs), 5 wait at
-// the final barrier, 6 write-back, 7 waves
-#ifdef VIBA_SCHUR_TIMING
-__device__ unsigned long long g_schur_t[8];
-#define SCHUR_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
-#else
-#define SCHUR_T(x)
-#endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_SCHUR_WPE, VIBA_SCHUR_WPE))) schur_run2_kernel(Dev d, double lambda) {
-  __shared__ double C[TS * TS];
-  __shared__ uint32_t ecol[256][2];  // the entries' first panel columns (colI, colJ); the rest from global
-  __shared__ int16_t runStart[258];
-  __shared__ uint8_t posW[4][2][TS];
-  __shared__ double rq[TS];
-  __shared__ int nRunsS;
-  SCHUR_T(t0);
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
-  const TileWork wk = d.tileWorks[w];
-  const bool diag = wk.I == wk.J;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int cnt = wk.count;
-  const TileEnt* ents = d.tileEnts + wk.start;
-  if (tid < cnt) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
-  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
-  if (tid < TS) rq[tid] = 0.0;
-  __syncthreads();
-  SCHUR_T(t1);
-  if (wave == 0) {
-    int n = 0;
-    for (int e0 = 0; e0 < cnt; e0 += 64) {
-      const int e = e0 + lane;
-      const bool st = e < cnt && (e == 0 || ents[e].maskI != ents[e - 1].maskI || ents[e].maskJ != ents[e - 1].maskJ);
-      const uint64_t b = __ballot(st);
-      if (st) runStart[n + __popcll(b & ((1ull << lane) - 1))] = (int16_t)e;
-      n += __popcll(b);
-    }
-    if (lane == 0) runStart[n] = (int16_t)cnt, nRunsS = n;
-  }
-  __syncthreads();
-  SCHUR_T(t2);
-#ifdef VIBA_SCHUR_TIMING
-  unsigned long long tk = 0, tr = 0;
-#endif
-  const int nRuns = nRunsS;
-  uint8_t* posI = posW[wave][0];
-  uint8_t* posJ = posW[wave][1];
-  const uint2* ec2 = reinterpret_cast<const uint2*>(&ecol[0][0]);
-  int task = 0;
-  for (int r = 0; r < nRuns; r++) {
-    const int e0 = runStart[r], e1 = runStart[r + 1];
-    const uint64_t mI = uniform64(ents[e0].maskI), mJ = diag ? mI : uniform64(ents[e0].maskJ);
-    const int nI = __popcll(mI), nJ = __popcll(mJ);
-    const int nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4, nbR = (nbJ + kTR - 1) / kTR;
-    const int nch = (e1 - e0 + kCh - 1) / kCh;
-    const int nTask = nch * nbR;
-    bool mapped = false;
-    for (int t = 0; t < nTask; t++, task++) {
-      if ((task & 3) != wave) continue;
-      if (!mapped) {  // the run's compact -> tile row maps (wave-private)
-        if ((mI >> lane) & 1) posI[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
-        if ((mJ >> lane) & 1) posJ[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        mapped = true;
-      }
-      const int ch = t / nbR, a0 = kTR * (t - ch * nbR);
-      const int c0 = e0 + ch * kCh, nl = min(kCh, e1 - c0), rows = 3 * nl;
-      // one specialised task (k-loop + epilogue) per (I-side blocks, J-side rows of this task, diagonal
-      // tile): no per-MFMA predicates, gathers at immediate offsets from per-step base pointers
-      const int nr = min(kTR, nbJ - a0);
-      const int sel = ((nbI - 1) * 2 + (nr - 1)) * 2 + (diag ? 1 : 0);
-      SCHUR_T(ta);
-      switch (sel) {
-#define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
-  case ((NBI - 1) * 2 + (NR - 1)) * 2:                                                                \
-    schur_task<NBI, NR, false>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                 \
-    break;                                                                                            \
-  case ((NBI - 1) * 2 + (NR - 1)) * 2 + 1:                                                            \
-    schur_task<NBI, NR, true>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                  \
-    break;
-        VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(2, 2)
-        VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 1) VIBA_SCHUR_CASE(4, 2)
-#undef VIBA_SCHUR_CASE
-        default: break;
-      }
-      SCHUR_T(tb);
-      if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
-#ifdef VIBA_SCHUR_TIMING
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      SCHUR_T(tc);
-      tk += tb - ta, tr += tc - tb;
-#endif
-    }
-    if (mapped) __builtin_amdgcn_wave_barrier();  // the maps are rewritten by this wave's next run
-  }
-  SCHUR_T(t3);
-  __syncthreads();
-  SCHUR_T(t4);
-  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind == 1) {
-    for (int i = tid; i < TS * TS; i += 256)
-      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
-  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
-  } else {
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
-  }
-  if (diag && tid < TS) {
-    const int64_t row = (int64_t)wk.I * TS + tid;
-    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
-  }
-#ifdef VIBA_SCHUR_TIMING
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  SCHUR_T(t5);
-  if (lane == 0) {
-    atomicAdd(&g_schur_t[0], t1 - t0);
-    atomicAdd(&g_schur_t[1], t2 - t1);
-    atomicAdd(&g_schur_t[2], t3 - t2);
-    atomicAdd(&g_schur_t[3], tk);
-    atomicAdd(&g_schur_t[4], tr);
-    atomicAdd(&g_schur_t[5], t4 - t3);
-    atomicAdd(&g_schur_t[6], t5 - t4);
-    atomicAdd(&g_schur_t[7], 1ull);
-  }
-#endif
-}
-
-// schur_run2's assembly with its per-item bookkeeping moved to finalize (api.hip): the item's runs
-// (masks) and tasks come precomputed, the tasks dealt to the waves longest-first (TileWork::wOff), so
-// the kernel has no run scan (wave 0 reading every entry's masks from global), no per-run global mask
-// reads by every wave, no skipping over other waves' tasks, and balanced waves at the final barrier
-// (measured in a -DVIBA_SCHUR_TIMING build of schur_run2 on config C: 5 % run scan, ~29 % task
-// bookkeeping outside the k-loops, 7.6 % waiting at the final barrier).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_SCHUR_WPE, VIBA_SCHUR_WPE))) schur_run4_kernel(Dev d, double lambda) {
-  static_assert(kCh == kSchurCh && kTR == kSchurTR, "finalize's task shapes (engine.hpp) and the kernel's");
+// Schur tile products, one workgroup per work item (TileWork: a target tile and <= 256 of its landmark
+// entries).  The item's runs (masks) and its tasks come precomputed from finalize (api.hip), the
+// tasks dealt to the waves longest-first (TileWork::wOff), so the kernel has no run scan and the waves
+// are balanced at the final barrier.  Four waves per SIMD (the k-loops are bound by gather latency).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run4_kernel(Dev d, double lambda) {
   __shared__ double C[TS * TS];
   __shared__ uint32_t ecol[256][2];
   __shared__ uint64_t rmask[256][2];
   __shared__ uint8_t posW[4][2][TS];
   __shared__ double rq[TS];
-  SCHUR_T(t0);
   const int64_t w = xcd_block(blockIdx.x, gridDim.x);
   const TileWork* wp = d.tileWorks + w;  // fields read in place (a by-value copy went to scratch:
   const TileWork wk = *wp;                 // wOff is indexed by the wave)
@@ -806,11 +489,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
   for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
   if (tid < TS) rq[tid] = 0.0;
   __syncthreads();
-  SCHUR_T(t1);
-  SCHUR_T(t2);
-#ifdef VIBA_SCHUR_TIMING
-  unsigned long long tk = 0, tr = 0;
-#endif
   uint8_t* posI = posW[wave][0];
   uint8_t* posJ = posW[wave][1];
   const uint2* ec2 = reinterpret_cast<const uint2*>(&ecol[0][0]);
@@ -835,7 +513,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
     const int rows = 3 * nl;
     const int nr = min(kTR, nbJ - a0);
     const int sel = ((nbI - 1) * 2 + (nr - 1)) * 2 + (diag ? 1 : 0);
-    SCHUR_T(ta);
+    // one specialised task (k-loop + epilogue) per (I-side blocks, J-side rows of this task, diagonal
+    // tile): no per-MFMA predicates, gathers at immediate offsets from per-step base pointers
     switch (sel) {
 #define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
   case ((NBI - 1) * 2 + (NR - 1)) * 2:                                                                \
@@ -849,369 +528,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
 #undef VIBA_SCHUR_CASE
       default: break;
     }
-#ifdef VIBA_SCHUR_TIMING
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-#endif
-    SCHUR_T(tb);
     if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
-#ifdef VIBA_SCHUR_TIMING
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    SCHUR_T(tc);
-    tk += tb - ta, tr += tc - tb;
-#endif
-  }
-  SCHUR_T(t3);
-  __syncthreads();
-  SCHUR_T(t4);
-  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind == 1) {
-    for (int i = tid; i < TS * TS; i += 256)
-      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
-  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
-  } else {
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
-  }
-  if (diag && tid < TS) {
-    const int64_t row = (int64_t)wk.I * TS + tid;
-    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
-  }
-#ifdef VIBA_SCHUR_TIMING
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  SCHUR_T(t5);
-  if (lane == 0) {
-    atomicAdd(&g_schur_t[0], t1 - t0);
-    atomicAdd(&g_schur_t[1], t2 - t1);
-    atomicAdd(&g_schur_t[2], t3 - t2);
-    atomicAdd(&g_schur_t[3], tk);
-    atomicAdd(&g_schur_t[4], tr);
-    atomicAdd(&g_schur_t[5], t4 - t3);
-    atomicAdd(&g_schur_t[6], t5 - t4);
-    atomicAdd(&g_schur_t[7], 1ull);
-  }
-#endif
-}
-
-// Schur assembly with the operands staged in LDS (schur_run5_kernel): the workgroup walks its item's
-// landmark chunks (<= kSchurCh5 landmarks of one run, api.hip); per chunk all 256 threads gather the
-// chunk's compact panel rows -- K = 3 rows per landmark, 16 columns per block, the I-side blocks and (off
-// the diagonal) the J-side blocks -- into LDS with every load in flight at once, then the four waves
-// run the chunk's MFMAs from LDS.  A wave owns output blocks of the run (up to four; shapes with fewer
-// than four blocks split the k-steps two or four ways), and its accumulators persist over the run's
-// chunks: the compact -> tile scatter into the LDS tile (LDS atomics) happens once per run, not once per
-// task.  Two workgroups per CU (77 KB of LDS each): one stages while the other multiplies.  Diagonal
-// tiles also form rhs -= Y^T z from the staged I-side rows.
-constexpr int kCh5 = kSchurCh5;
-constexpr int kK5 = ((3 * kCh5 + 3) / 4) * 4;  // staged K rows per chunk (the MFMA's K = 4 steps)
-constexpr int kSB5 = kK5 * 16;                  // elements per staged 16-column block
-
-__global__ void __launch_bounds__(256, 2) schur_run5_kernel(Dev d, double lambda) {
-  __shared__ double C[TS * TS];
-  __shared__ rec_t stg[8 * kSB5];
-  __shared__ uint32_t ecol[256][2];
-  __shared__ uint64_t rmask[256][2];
-  __shared__ uint8_t posIs[TS], posJs[TS];
-  __shared__ double rq[TS];
-  __shared__ double zst[kK5];
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
-  const TileWork* wp = d.tileWorks + w;
-  const TileWork wk = *wp;
-  const bool diag = wk.I == wk.J;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const TileEnt* ents = d.tileEnts + wk.start;
-  if (tid < wk.count) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
-  if (tid < wk.nRuns) {
-    const uint64_t* rm = d.schurRuns + 2 * ((int64_t)wk.runFirst + tid);
-    rmask[tid][0] = rm[0], rmask[tid][1] = rm[1];
-  }
-  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
-  if (tid < TS) rq[tid] = 0.0;
-  const uint32_t* chunks = d.schurChunks + wk.chunkFirst;
-  const int64_t pq = d.nYcol;
-  // the wave's units of the current run: output block (ui, ub), k-steps [p nks / P, (p + 1) nks / P)
-  int nu = 0, ui[4] = {0, 0, 0, 0}, ub[4] = {0, 0, 0, 0}, up[4] = {0, 0, 0, 0}, P = 1;
-  hacc4_t acc[4];
-  int cur = -1, nI = 0, nJ = 0, nbI = 0, nbJ = 0;
-  auto flush = [&]() {  // C -= the wave's accumulated blocks of the current run (LDS atomics)
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      if (m >= nu) break;
-      const int n = 16 * ub[m] + l15;
-      const int colT = posIs[min(n, TS - 1)];
-      int rowT[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) rowT[q] = posJs[min(16 * ui[m] + kAccL4 * l4 + kAccR * q, TS - 1)];
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (n < nI && 16 * ui[m] + kAccL4 * l4 + kAccR * q < nJ) atomicAdd(&C[rowT[q] * TS + colT], -(double)acc[m][q]);
-    }
-  };
-  for (int ci = 0; ci < wk.nChunks; ci++) {
-    const uint32_t code = __builtin_amdgcn_readfirstlane(chunks[ci]);
-    const int r = code & 255, c0 = (code >> 8) & 255, nl = (code >> 16) & 63;
-    if (r != cur && cur >= 0) flush();
-    __syncthreads();  // flushes, the previous chunk's MFMAs and rhs are done with the maps and the stage
-    if (r != cur) {
-      const uint64_t mI = uniform64(rmask[r][0]), mJ = diag ? mI : uniform64(rmask[r][1]);
-      nI = __popcll(mI), nJ = __popcll(mJ), nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4;
-      if (wave == 0) {
-        if ((mI >> lane) & 1) posIs[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
-        if ((mJ >> lane) & 1) posJs[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
-      }
-      // the run's output blocks (row-major; diagonal tiles: b >= i), split over the waves
-      int nblk = 0;
-      for (int i = 0; i < nbJ; i++) nblk += diag ? nbI - i : nbI;
-      P = nblk >= 4 ? 1 : nblk == 1 ? 4 : 2;
-      nu = 0;
-      for (int u = wave; u < nblk * P && nu < 4; u += 4) {
-        int j = u % nblk, i = 0;
-        while (j >= (diag ? nbI - i : nbI)) j -= diag ? nbI - i : nbI, i++;
-        ui[nu] = i, ub[nu] = diag ? i + j : j, up[nu] = u / nblk, nu++;
-      }
-#pragma unroll
-      for (int m = 0; m < 4; m++) acc[m] = hacc4_t{0, 0, 0, 0};
-      cur = r;
-    }
-    // stage the chunk: row-block rb = (side-block sb, K row kr) holds 16 doubles of plane q of landmark
-    // c0 + kr / 3 from its first panel column in tile I (sb < nbI) or J; rows past the landmarks zero
-    const int nsb = diag ? nbI : nbI + nbJ, total = nsb * kK5, K = 3 * nl;
-    {
-      const int l16 = tid & 15, rb0 = tid >> 4;
-      constexpr int kU = (8 * kK5 + 15) / 16;
-      rec_t v[kU];
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const int rb = rb0 + 16 * u, sb = rb / kK5, kr = rb - sb * kK5;
-        v[u] = rec_t(0);
-        if (rb < total && kr < K) {
-          const int e = c0 + kr / 3, q = kr - 3 * (kr / 3);
-          const uint32_t col = sb < nbI ? ecol[e][0] + 16u * sb : ecol[e][1] + 16u * (sb - nbI);
-          v[u] = d.Y[q * pq + col + l16];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kU; u++) {
-        const int rb = rb0 + 16 * u;
-        if (rb < total) stg[rb * 16 + l16] = v[u];
-      }
-      if (diag && tid < kK5) zst[tid] = tid < K ? d.z[3 * (int64_t)ents[c0 + tid / 3].lm + tid % 3] : 0.0;
-    }
-    __syncthreads();
-    const int nks = (K + 3) >> 2;
-    const rec_t* sI = stg;
-    const rec_t* sJ = diag ? stg : stg + nbI * kSB5;
-    int klo[4], khi[4];
-#pragma unroll
-    for (int m = 0; m < 4; m++) klo[m] = up[m] * nks / P, khi[m] = (up[m] + 1) * nks / P;
-    for (int ks = 0; ks < nks; ks++) {
-      const int row = (4 * ks + l4) * 16 + l15;
-#pragma unroll
-      for (int m = 0; m < 4; m++)
-        if (m < nu && ks >= klo[m] && ks < khi[m])
-          acc[m] = mfma_h(sJ[ui[m] * kSB5 + row], sI[ub[m] * kSB5 + row], acc[m]);
-    }
-    if (diag && wave == 0 && lane < nI) {  // rhs -= Y^T z over the chunk's landmarks
-      const rec_t* y = sI + (lane >> 4) * kSB5 + (lane & 15);
-      double racc = 0.0;
-      for (int kr = 0; kr < K; kr++) racc += (double)y[kr * 16] * zst[kr];
-      atomicAdd(&rq[posIs[lane]], -racc);
-    }
-  }
-  if (cur >= 0) flush();
-  __syncthreads();
-  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind == 1) {
-    for (int i = tid; i < TS * TS; i += 256)
-      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
-  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
-  } else {
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
-  }
-  if (diag && tid < TS) {
-    const int64_t row = (int64_t)wk.I * TS + tid;
-    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
-  }
-}
-
-// The same assembly with the K-row bookkeeping taken out of the k-loop (schur_run3_kernel, default):
-// before a task, the wave writes one (I-side, J-side) element offset per K row into an LDS table --
-// row kr = 3 e + q of the task's landmarks -> q * nYcol + the entry's first panel column in tile I / J
-// (+ 16 a0 on the J side), rows past the task's landmarks -> the zero pad behind the panels.  A k-step
-// is then one broadcast ds_read_b64 of its row's offsets, two 64-bit address adds and the NR + NBI
-// gathers at immediate offsets, one step ahead of the MFMAs (schur_run2's per-step landmark / plane
-// advance, bounds select and plane-base select were ~20 VALU + 17 SALU per MFMA: DESIGN.md §8).
-template <int NBI, int NR, int DA0>
-__device__ __forceinline__ void schur_task3(const Dev& d, const uint2* rowOff, int nks, int a0r, int l4, int l15,
-                                            const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
-  // DA0 >= 0: diagonal tile, block row a0 = DA0 known at compile time, so the lower-triangle test of
-  // each block is static (a runtime a0 put a scalar branch in front of every MFMA)
-  constexpr bool DIAG = DA0 >= 0;
-  const int a0 = DIAG ? DA0 : a0r;
-  hacc4_t acc[NR][NBI];
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int b = 0; b < NBI; b++) acc[i][b] = hacc4_t{0, 0, 0, 0};
-  const rec_t* Y = d.Y + l15;
-#if VIBA_SCHUR_ASMLD
-  // the gathers as inline-asm loads, counted by hand: hipcc's own waitcnt pass cannot follow the two
-  // register sets around the loop's back edge and waited for the step just issued (vmcnt(0) before the
-  // current step's MFMAs), which left every gather's latency exposed.  Each set is pinned after its
-  // wait ("+v"), so nothing reads it early (cdna_hip_programming.md §5.7 item 1, form ii).
-  constexpr int kN = NR + NBI;
-  auto ld = [&](int ks, rec_t (&av)[NR], rec_t (&bv)[NBI]) {
-    const uint2 o = rowOff[4 * ks + l4];
-    const rec_t* pJ = Y + o.y;
-    const rec_t* pI = Y + o.x;
-#pragma unroll
-    for (int i = 0; i < NR; i++) gather_asm<16 * sizeof(rec_t)>(av[i], pJ, i);
-#pragma unroll
-    for (int b = 0; b < NBI; b++) gather_asm<16 * sizeof(rec_t)>(bv[b], pI, b);
-  };
-  auto pin = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
-#pragma unroll
-    for (int i = 0; i < NR; i++) asm volatile("" : "+v"(av[i]));
-#pragma unroll
-    for (int b = 0; b < NBI; b++) asm volatile("" : "+v"(bv[b]));
-  };
-#else
-  constexpr int kN = 0;
-  auto ld = [&](int ks, rec_t (&av)[NR], rec_t (&bv)[NBI]) {
-    const uint2 o = rowOff[4 * ks + l4];
-    const rec_t* pJ = Y + o.y;
-    const rec_t* pI = Y + o.x;
-#pragma unroll
-    for (int i = 0; i < NR; i++) av[i] = pJ[16 * i];
-#pragma unroll
-    for (int b = 0; b < NBI; b++) bv[b] = pI[16 * b];
-  };
-  auto pin = [&](rec_t (&)[NR], rec_t (&)[NBI]) {};
-#endif
-  auto mm = [&](const rec_t (&av)[NR], const rec_t (&bv)[NBI]) {
-#pragma unroll
-    for (int i = 0; i < NR; i++)
-#pragma unroll
-      for (int b = 0; b < NBI; b++)
-        if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
-  };
-  rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
-  ld(0, a0v, b0v);
-  for (int ks = 0; ks < nks; ks += 2) {
-    if (ks + 1 < nks) {
-      ld(ks + 1, a1v, b1v);
-      vm_wait<kN>();  // step ks's set landed (step ks + 1's stays in flight)
-    } else {
-      vm_wait<0>();
-    }
-    pin(a0v, b0v);
-    mm(a0v, b0v);
-    if (ks + 1 < nks) {
-      if (ks + 2 < nks) {
-        ld(ks + 2, a0v, b0v);
-        vm_wait<kN>();
-      } else {
-        vm_wait<0>();
-      }
-      pin(a1v, b1v);
-      mm(a1v, b1v);
-    }
-  }
-  schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
-}
-
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run3_kernel(Dev d, double lambda) {
-  __shared__ double C[TS * TS];
-  __shared__ uint32_t ecol[256][2];
-  __shared__ int16_t runStart[258];
-  __shared__ uint8_t posW[4][2][TS];
-  __shared__ uint2 rowTab[4][4 * ((3 * kCh + 3) / 4)];
-  __shared__ double rq[TS];
-  __shared__ int nRunsS;
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
-  const TileWork wk = d.tileWorks[w];
-  const bool diag = wk.I == wk.J;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int cnt = wk.count;
-  const TileEnt* ents = d.tileEnts + wk.start;
-  if (tid < cnt) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
-  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
-  if (tid < TS) rq[tid] = 0.0;
-  __syncthreads();
-  if (wave == 0) {
-    int n = 0;
-    for (int e0 = 0; e0 < cnt; e0 += 64) {
-      const int e = e0 + lane;
-      const bool st = e < cnt && (e == 0 || ents[e].maskI != ents[e - 1].maskI || ents[e].maskJ != ents[e - 1].maskJ);
-      const uint64_t b = __ballot(st);
-      if (st) runStart[n + __popcll(b & ((1ull << lane) - 1))] = (int16_t)e;
-      n += __popcll(b);
-    }
-    if (lane == 0) runStart[n] = (int16_t)cnt, nRunsS = n;
-  }
-  __syncthreads();
-  const int nRuns = nRunsS;
-  uint8_t* posI = posW[wave][0];
-  uint8_t* posJ = posW[wave][1];
-  uint2* rt = rowTab[wave];
-  const uint32_t pq = (uint32_t)d.nYcol, zeroOff = 3u * (uint32_t)d.nYcol;  // the 128 zeros behind the planes
-  int task = 0;
-  for (int r = 0; r < nRuns; r++) {
-    const int e0 = runStart[r], e1 = runStart[r + 1];
-    const uint64_t mI = uniform64(ents[e0].maskI), mJ = diag ? mI : uniform64(ents[e0].maskJ);
-    const int nI = __popcll(mI), nJ = __popcll(mJ);
-    const int nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4, nbR = (nbJ + kTR - 1) / kTR;
-    const int nch = (e1 - e0 + kCh - 1) / kCh;
-    const int nTask = nch * nbR;
-    bool mapped = false;
-    for (int t = 0; t < nTask; t++, task++) {
-      if ((task & 3) != wave) continue;
-      if (!mapped) {
-        if ((mI >> lane) & 1) posI[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
-        if ((mJ >> lane) & 1) posJ[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
-        mapped = true;
-      }
-      const int ch = t / nbR, a0 = kTR * (t - ch * nbR);
-      const int c0 = e0 + ch * kCh, nl = min(kCh, e1 - c0), rows = 3 * nl, nks = (rows + 3) >> 2;
-      __builtin_amdgcn_wave_barrier();  // the previous task's readers of rt are done
-      if (lane < 4 * nks) {
-        uint2 o = make_uint2(zeroOff, zeroOff);
-        if (lane < rows) {
-          const int e = c0 + lane / 3, q = lane - 3 * (lane / 3);
-          const uint32_t base = (uint32_t)q * pq;
-          o = make_uint2(base + ecol[e][0], base + ecol[e][1] + 16u * (uint32_t)a0);
-        }
-        rt[lane] = o;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const int nr = min(kTR, nbJ - a0);
-      static_assert(kTR == 2, "schur_run3_kernel's diagonal cases assume two block rows per task");
-      // off-diagonal: (NBI, NR); diagonal (nbI == nbJ): (NBI, a0), NR = min(2, NBI - a0)
-      const int sel = diag ? 16 + (nbI - 1) * 2 + (a0 >> 1) : ((nbI - 1) * 2 + (nr - 1));
-      switch (sel) {
-#define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
-  case (NBI - 1) * 2 + (NR - 1):                                                                      \
-    schur_task3<NBI, NR, -1>(d, rt, nks, a0, l4, l15, posI, posJ, nI, nJ, C);                         \
-    break;
-#define VIBA_SCHUR_DCASE(NBI, A0)                                                                     \
-  case 16 + (NBI - 1) * 2 + (A0 >> 1):                                                                \
-    schur_task3<NBI, (NBI - A0 < 2 ? NBI - A0 : 2), A0>(d, rt, nks, a0, l4, l15, posI, posJ, nI, nJ, C); \
-    break;
-        VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(2, 2)
-        VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 1) VIBA_SCHUR_CASE(4, 2)
-        VIBA_SCHUR_DCASE(1, 0) VIBA_SCHUR_DCASE(2, 0) VIBA_SCHUR_DCASE(3, 0) VIBA_SCHUR_DCASE(3, 2)
-        VIBA_SCHUR_DCASE(4, 0) VIBA_SCHUR_DCASE(4, 2)
-#undef VIBA_SCHUR_CASE
-#undef VIBA_SCHUR_DCASE
-        default: break;
-      }
-      if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
-    }
-    if (mapped) __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
@@ -1387,13 +704,6 @@ __global__ void __launch_bounds__(256) reduced_rhs_kernel(Dev d) {
 // r (B[4 r + (l >> 4)][l & 15]), so chained products need no data movement.  The only scalar work is
 // the factor + inverse of the four 16 x 16 diagonal blocks (dinv[J]: 4 x 256 doubles, column-major).
 
-__device__ __forceinline__ double readlane_d(double v, int l) {
-  const int64_t b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
-}
-
 // Broadcast lane J of each 16-lane row to the whole row: one v_mov_b64_dpp row_newbcast:J
 // (the 16 x 16 diagonal blocks live in lanes 0..15, one row / column per lane)
 template <int J>
@@ -1445,37 +755,6 @@ struct Chol16<16> {
   static __device__ __forceinline__ void run(double (&)[16], double (&)[16], int, bool&) {}
 };
 
-// Row block `w` (16 rows) of X = A L^-T, X overwriting A (both column-major TS x TS; A/L may be LDS or
-// global): for k = 0..3: X_k^T = Dinv_k (A_k^T - sum_{k2<k} L_{k,k2} X_k2^T).  Xt[k] keeps X_k^T.
-template <int NK>
-__device__ __forceinline__ void trsm_rowblock(double* A, const double* L, const double* dinv, int w, int lane,
-                                              double4_t (&Xt)[4]) {
-  const int lr = lane & 15, lq = lane >> 4;
-#pragma unroll
-  for (int k = 0; k < NK; k++) {
-    double4_t acc;
-#pragma unroll
-    for (int r = 0; r < 4; r++) acc[r] = A[(16 * k + lq + 4 * r) * TS + 16 * w + lr];
-#pragma unroll
-    for (int k2 = 0; k2 < k; k2++)
-#pragma unroll
-      for (int s = 0; s < 4; s++) acc = mfma64(-L[(16 * k2 + 4 * s + lq) * TS + 16 * k + lr], Xt[k2][s], acc);
-    double4_t res = double4_t{0, 0, 0, 0};
-#pragma unroll
-    for (int s = 0; s < 4; s++) res = mfma64(dinv[k * 256 + (4 * s + lq) * 16 + lr], acc[s], res);
-    Xt[k] = res;
-  }
-}
-
-#ifdef VIBA_POTRF_TIMING
-__device__ long long g_potrf_t[32];
-#define POTRF_T(k) do { if (threadIdx.x == 0 && blockIdx.x == 0) g_potrf_t[k] = (long long)__builtin_readcyclecounter(); } while (0)
-#define POTRF_TW(k) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 0) g_potrf_t[k] = (long long)__builtin_readcyclecounter(); } while (0)
-#else
-#define POTRF_T(k) do {} while (0)
-#define POTRF_TW(k) do {} while (0)
-#endif
-
 // Factor + invert the 16 x 16 diagonal block i of T (LDS) given S (its updated value, D layout; only
 // its lower triangle is valid): writes L_ii into T and Dinv_i into dinvS (LDS).  Cholesky first, lane
 // r holding row r (pivot chain only: DPP row broadcasts, v_rsq_f64 + Newton), then X = L^-1 with
@@ -1483,62 +762,6 @@ __device__ long long g_potrf_t[32];
 // term, so the serial chain is one FMA + one multiply per row (L from LDS by broadcast reads).
 // (A one-MFMA-per-pivot variant -- the rank-1 update as a v_mfma_f64_16x16x4_f64 on the D layout --
 // measured slower: each pivot then waits on a dependent MFMA + readlane, 7.9k vs 5.7k cycles.)
-// X = L^-1 from the registers of Chol16 (lane r: s[c] = L[r][c], c <= r): lane c computes column c,
-// taking L[r][k] from lane r by a DPP row broadcast instead of from LDS (no store / barrier / load
-// round trip; the 120 broadcasts do not depend on the substitution chain)
-template <int K, int R>
-struct Inv16Row {
-  static __device__ __forceinline__ void run(double (&acc)[16], const double (&s)[16]) {
-    acc[R] -= rowbcast<R>(s[K]) * acc[K];
-    Inv16Row<K, R + 1>::run(acc, s);
-  }
-};
-template <int K>
-struct Inv16Row<K, 16> {
-  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16]) {}
-};
-template <int K>
-struct Inv16 {
-  static __device__ __forceinline__ void run(double (&acc)[16], const double (&s)[16], const double (&invd)[16]) {
-    acc[K] *= invd[K];
-    Inv16Row<K, K + 1>::run(acc, s);
-    Inv16<K + 1>::run(acc, s, invd);
-  }
-};
-template <>
-struct Inv16<16> {
-  static __device__ __forceinline__ void run(double (&)[16], const double (&)[16], const double (&)[16]) {}
-};
-
-// diag16 with the inverse taken from registers (Inv16): potrf4_kernel<true> (VIBA_DIAG_INV=dpp)
-__device__ __forceinline__ void diag16_dpp(double* T, double* scratch, double* dinvS, int i, double4_t S, int lane,
-                                           bool& bad) {
-  const int lr = lane & 15, lq = lane >> 4;
-#pragma unroll
-  for (int r = 0; r < 4; r++) scratch[(lq + 4 * r) * 16 + lr] = S[r];  // row-major S[i'][j']
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double s[16], invd[16];
-#pragma unroll
-  for (int c = 0; c < 16; c++) s[c] = scratch[lr * 16 + c];
-  POTRF_TW(15 + 3 * i);
-  Chol16<0>::run(s, invd, lane, bad);
-  POTRF_TW(16 + 3 * i);
-  double acc[16];
-#pragma unroll
-  for (int r = 0; r < 16; r++) acc[r] = (r == lr) ? 1.0 : 0.0;
-  Inv16<0>::run(acc, s, invd);
-  POTRF_TW(17 + 3 * i);
-  if (lane < 16) {
-#pragma unroll
-    for (int c = 0; c < 16; c++) T[(16 * i + c) * TS + 16 * i + lane] = (c <= lane) ? s[c] : 0.0;
-#pragma unroll
-    for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = acc[r];  // rows above the lane stay +0.0
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
 __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS, int i, double4_t S, int lane,
                                        bool& bad) {
   const int lr = lane & 15, lq = lane >> 4;
@@ -1575,46 +798,6 @@ __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS
     for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = acc[r];  // rows above the lane stay +0.0
   }
   __builtin_amdgcn_wave_barrier();
-}
-
-// Blocked Cholesky of the TS x TS tile in LDS (one wave), left-looking by 16-row blocks i:
-// L_ik (k < i) by trsm_rowblock, then S = A_ii - sum_k L_ik L_ik^T and its 16 x 16 factor/inverse.
-template <int I>
-struct PotrfRow {
-  static __device__ __forceinline__ void run(double* T, double* scratch, double* dinvS, int lane, bool& bad) {
-    const int lr = lane & 15, lq = lane >> 4;
-    double4_t Lt[4];
-    POTRF_T(4 * I + 0);
-    trsm_rowblock<I>(T, T, dinvS, I, lane, Lt);
-    POTRF_T(4 * I + 1);
-    double4_t S;
-#pragma unroll
-    for (int r = 0; r < 4; r++) S[r] = T[(16 * I + lr) * TS + 16 * I + lq + 4 * r];  // lower part valid
-#pragma unroll
-    for (int k = 0; k < I; k++)
-#pragma unroll
-      for (int s = 0; s < 4; s++) S = mfma64(-Lt[k][s], Lt[k][s], S);
-#pragma unroll
-    for (int k = 0; k < I; k++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) T[(16 * k + lq + 4 * r) * TS + 16 * I + lr] = Lt[k][r];
-    __builtin_amdgcn_wave_barrier();
-    POTRF_T(4 * I + 2);
-    diag16(T, scratch, dinvS, I, S, lane, bad);
-    POTRF_T(4 * I + 3);
-    PotrfRow<I + 1>::run(T, scratch, dinvS, lane, bad);
-  }
-};
-template <>
-struct PotrfRow<4> {
-  static __device__ __forceinline__ void run(double*, double*, double*, int, bool&) {}
-};
-
-// one wave; on return T holds L (upper part zero) and dinvS the four 16 x 16 diagonal inverses
-__device__ __forceinline__ void potrf_blocked(double* T, double* scratch, double* dinvS, int lane, int32_t* err) {
-  bool bad = false;
-  PotrfRow<0>::run(T, scratch, dinvS, lane, bad);
-  if (bad && lane == 0) atomicOr(err, 8);
 }
 
 // copy n doubles LDS -> global with `nthreads` threads (pointer-stepped, bounded unroll: keeps the
@@ -1663,32 +846,6 @@ __device__ __forceinline__ void potrf_forward(const Dev& d, const double* T, con
   if (store) y[row] = row < d.nRed ? sh[lane] : 0.0;  // y_J also stays in sh[0, 64)
 }
 
-__global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileList, const int32_t* cols, double* dinvAll,
-                                                   const double* fwdB, double* fwdY) {
-  __shared__ double T[TS * TS];
-  __shared__ double scratch[256];
-  __shared__ double dinvS[1024];
-  const int lane = threadIdx.x;
-  POTRF_T(19);
-  double* A = d.tiles + (int64_t)tileList[blockIdx.x] * TS * TS;
-  double* dinvG = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
-  {
-    double v[TS];
-#pragma unroll
-    for (int c = 0; c < TS; c++) v[c] = A[c * TS + lane];
-#pragma unroll
-    for (int c = 0; c < TS; c++) T[c * TS + lane] = v[c];
-  }
-  __builtin_amdgcn_wave_barrier();
-  POTRF_T(16);
-  potrf_blocked(T, scratch, dinvS, lane, d.err);
-  POTRF_T(17);
-  if (fwdB) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB, fwdY, lane);
-  lds_to_global(A, T, TS * TS, lane, 64);
-  lds_to_global(dinvG, dinvS, 1024, lane, 64);
-  POTRF_T(18);
-}
-
 // The same factorization with four waves, right-looking over the 16-column blocks k: wave w keeps its
 // row block (A_wj^T for j <= w, D layout) in registers.  Wave k factors + inverts its diagonal block
 // (diag16); every wave below then forms L_wk = A_wk Dinv_k^T (4 MFMAs), publishes it in LDS and takes
@@ -1696,12 +853,10 @@ __global__ void __launch_bounds__(64) potrf_kernel(Dev d, const int32_t* tileLis
 // with L_jk -- while wave k + 1 is already in diag16.  Between two diag16 the chain is 8 dependent
 // MFMAs (the one-wave left-looking form chains up to 36 of them); the terms are subtracted in the same
 // order as there.  The upper blocks are written as zeros.
-template <bool kDppInv>
 __device__ __forceinline__ void potrf4_core(const Dev& d, const double* A, double* T, double* scratch, double* dinvS,
                                             int tid) {
   const int lane = tid & 63, w = tid >> 6;
   const int lr = lane & 15, lq = lane >> 4;
-  if (w == 0) POTRF_TW(0);
   double4_t R[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) {
@@ -1720,13 +875,9 @@ __device__ __forceinline__ void potrf4_core(const Dev& d, const double* A, doubl
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     if (w == k) {
-      POTRF_TW(1 + 2 * k);
-      if (kDppInv) diag16_dpp(T, scratch, dinvS, k, R[k], lane, bad);
-      else diag16(T, scratch, dinvS, k, R[k], lane, bad);
-      POTRF_TW(2 + 2 * k);
+      diag16(T, scratch, dinvS, k, R[k], lane, bad);
     }
     __syncthreads();
-    if (w == 3) POTRF_TW(9 + k);
     double4_t Lt = double4_t{0, 0, 0, 0};
     if (w > k) {
 #pragma unroll
@@ -1751,11 +902,9 @@ __device__ __forceinline__ void potrf4_core(const Dev& d, const double* A, doubl
     }
   }
   __syncthreads();
-  if (w == 0) POTRF_TW(13);
   if (bad && lane == 0) atomicOr(d.err, 8);
 }
 
-template <bool kDppInv>
 __global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileList, const int32_t* cols,
                                                      double* dinvAll, const double* fwdB, double* fwdY) {
   __shared__ double T[TS * TS];
@@ -1764,11 +913,10 @@ __global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileL
   const int tid = threadIdx.x, w = tid >> 6;
   double* A = d.tiles + (int64_t)tileList[blockIdx.x] * TS * TS;
   double* dinvG = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
-  potrf4_core<kDppInv>(d, A, T, scratch, dinvS, tid);
+  potrf4_core(d, A, T, scratch, dinvS, tid);
   if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB, fwdY, tid & 63);
   lds_to_global(A, T, TS * TS, tid, 256);
   lds_to_global(dinvG, dinvS, 1024, tid, 256);
-  if (w == 0) POTRF_TW(14);
 }
 
 // potrf + trsm of a level in ONE launch (the levels with few off-diagonal tiles, where the two launches
@@ -1779,7 +927,6 @@ __global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileL
 // diagonal tiles are copied back after the last level: copy_diag_kernel) and the inverses into dinv.
 // With the fused forward solve every block also derives y_J (only the writer stores it) for its
 // b_I -= L_IJ y_J.  items: (diagonal tile, column, target tile or -1, target row, writer) per block.
-template <bool kDppInv>
 __global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* items, double* Lscr, double* dinvAll,
                                                          double* fwdB, double* fwdY) {
   __shared__ double T[TS * TS];
@@ -1797,7 +944,7 @@ __global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* i
 #pragma unroll
       for (int r = 0; r < 4; r++) av[k][r] = At[(16 * k + lq + 4 * r) * TS + 16 * w + lr];
   }
-  potrf4_core<kDppInv>(d, d.tiles + (int64_t)diagT * TS * TS, T, scratch, dinvS, tid);
+  potrf4_core(d, d.tiles + (int64_t)diagT * TS * TS, T, scratch, dinvS, tid);
   if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, col, fwdB, fwdY, lane, writer != 0);
   if (writer) {
     lds_to_global(Lscr + (int64_t)col * TS * TS, T, TS * TS, tid, 256);
@@ -1921,25 +1068,14 @@ __global__ void __launch_bounds__(256) trsm_kernel(Dev d, const int32_t* diagLis
 // workgroups per CU matter more than the depth of one ring).  Writing stage s + R - 2 into buffer
 // (s + R - 2) % R is safe after one barrier per stage: its last reader was stage s - 2.  Odd columns
 // are stored rotated by 16 rows so each half-wave of a ds_read_b64 (two columns) hits all 64 banks.
-#ifndef VIBA_FAN_K
-#define VIBA_FAN_K 16
-#define VIBA_FAN_RING 3
-#endif
-#ifndef VIBA_FAN_LATE
-#define VIBA_FAN_LATE 1
-#endif
-constexpr int kFanK = VIBA_FAN_K;          // columns per stage
-constexpr int kFanRing = VIBA_FAN_RING;    // stages in the LDS ring (kFanRing - 2 in flight)
+constexpr int kFanK = 16;                  // columns per stage
+constexpr int kFanRing = 3;                // stages in the LDS ring (kFanRing - 1 in flight)
 constexpr int kStage = 2 * kFanK * TS;     // doubles per stage: [L_JK, L_IK][kFanK columns][64 rows]
-#ifndef VIBA_FAN_MFMA4
-#define VIBA_FAN_MFMA4 0
-#endif
-constexpr int kFanWaves = VIBA_FAN_MFMA4 == 3 ? 8 : 4;  // waves per fan-in workgroup
-constexpr int kGlds = kStage / 128 / kFanWaves;          // global_load_lds per wave per stage (1 KB = 128 doubles each)
+constexpr int kFanWaves = 4;               // waves per fan-in workgroup
+constexpr int kGlds = kStage / 128 / kFanWaves;  // global_load_lds per wave per stage (1 KB = 128 doubles each)
 // LDS row rotation of stage column t (rows stored at (row + rot) & 63): odd columns by 16, so a half-wave
-// reading two columns of one row range hits all 64 banks; the split-K 4x4x4 form (VIBA_FAN_MFMA4 == 2)
-// reads 4 row groups x 4 column quads x 2 columns per half-wave, so the quads are rotated by 4 more each
-__device__ __forceinline__ int fan_rot(int t) { return 16 * (t & 1) + (VIBA_FAN_MFMA4 >= 2 ? 4 * ((t >> 2) & 3) : 0); }
+// reading two columns of one row range hits all 64 banks
+__device__ __forceinline__ int fan_rot(int t) { return 16 * (t & 1); }
 
 __device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, int32_t start, int s, double* buf,
                                             int wave, int lane) {
@@ -1947,13 +1083,7 @@ __device__ __forceinline__ void fanin_issue(const Dev& d, const int32_t* pairs, 
   const int k0 = (s % (TS / kFanK)) * kFanK;
   // constant address space: scalar loads (lgkmcnt), so no vmcnt wait drains the LDS ring
   const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
-#ifdef VIBA_FAN_EXPT
-  // measurement build only (scripts/fan_expt.py): every contribution reads the same few L2-resident tiles,
-  // which separates the kernel's memory-system time from its issue / synchronisation time
-  const int64_t tk = (c & 7), ti = 8 + (c & 7);
-#else
   const int64_t tk = pc[2 * c + 1], ti = pc[2 * c];
-#endif
   const int hi = lane >> 5;
 #pragma unroll
   for (int j = 0; j < kGlds; j++) {
@@ -1970,134 +1100,31 @@ typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) unsigned int guint;
 
 // Fan-in accumulation of contributions [start, start + count) of one target: acc = sum L_IK L_JK^T over
-// the wave's 32 x 32 quadrant (ring in `stg`; every wave passes a barrier per stage, so all waves call it)
-#if VIBA_FAN_MFMA4 == 3
-typedef double fan_acc_t[8][4];
-#elif VIBA_FAN_MFMA4 == 2
-typedef double fan_acc_t[8][8];
-#elif VIBA_FAN_MFMA4
-typedef double fan_acc_t[2][8];
-#else
-typedef double4_t fan_acc_t[2][2];
-#endif
+// the wave's 32 x 32 quadrant (ring in `stg`; every wave passes a barrier per stage, so all waves call it).
+// Issue-after-barrier: kFanRing - 1 stages in flight; stage s + R - 1 goes into the buffer of stage
+// s - 1, whose readers all passed this iteration's barrier.
 __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, int32_t start, int32_t count,
-                                            double* stg, int wave, int lane, fan_acc_t& accOut) {
-  static_assert(kGlds * (kFanRing - 1) <= 63 && kFanRing <= 8 && kFanRing >= 3, "vmcnt range");
+                                            double* stg, int wave, int lane, double4_t (&acc)[2][2]) {
+  static_assert(kGlds * (kFanRing - 1) <= 63, "vmcnt range");
   const int l15 = lane & 15, l4 = lane >> 4;
-#if VIBA_FAN_MFMA4 == 3
-  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;  // eight 32 x 16 strips
-#else
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-#endif
   const int32_t nst = (TS / kFanK) * count;
-#if VIBA_FAN_MFMA4 >= 2
-  fan_acc_t& acc4 = accOut;
-#pragma unroll
-  for (int r = 0; r < 8; r++)
-#pragma unroll
-    for (int c = 0; c < (VIBA_FAN_MFMA4 == 3 ? 4 : 8); c++) acc4[r][c] = 0.0;
-  // operand lane map of the split-K form: lane 16 k' + 4 i + e reads stage column t = 4 i + k', row group
-  // member e (see below)
-  const int tq = 4 * ((lane >> 2) & 3) + (lane >> 4);
-  const int offA = tq * TS, rowA = pb + (lane & 3) + fan_rot(tq), rowB = qb + (lane & 3) + fan_rot(tq);
-#elif VIBA_FAN_MFMA4
-  fan_acc_t& acc4 = accOut;
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int c = 0; c < 8; c++) acc4[a][c] = 0.0;
-#else
-  fan_acc_t& acc = accOut;
 #pragma unroll
   for (int a = 0; a < 2; a++)
 #pragma unroll
     for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
-#endif
-#if VIBA_FAN_LATE
-  // issue-after-barrier: kFanRing - 1 stages in flight; stage s + R - 1 goes into the buffer of stage
-  // s - 1, whose readers all passed this iteration's barrier
   constexpr int kAhead = kFanRing - 1;
-#else
-  constexpr int kAhead = kFanRing - 2;
-#endif
   for (int s = 0; s < kAhead && s < nst; s++) fanin_issue(d, pairs, start, s, stg + s * kStage, wave, lane);
   for (int s = 0; s < nst; s++) {
-#if !VIBA_FAN_LATE
-    if (s + kAhead < nst) fanin_issue(d, pairs, start, s + kAhead, stg + ((s + kAhead) % kFanRing) * kStage, wave, lane);
-#endif
     // this wave's part of stage s landed (later stages may stay in flight)
-    switch (min(kAhead - (VIBA_FAN_LATE ? 1 : 0), nst - 1 - s)) {
-      case 6: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * kGlds) : "memory"); break;
-      case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * kGlds) : "memory"); break;
-      case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * kGlds) : "memory"); break;
-      case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * kGlds) : "memory"); break;
-      case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kGlds) : "memory"); break;
-      case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * kGlds) : "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
+    if (s + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGlds) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // ... and every other wave's
     __builtin_amdgcn_sched_barrier(0);
-#if VIBA_FAN_LATE
     if (s + kAhead < nst) fanin_issue(d, pairs, start, s + kAhead, stg + ((s + kAhead) % kFanRing) * kStage, wave, lane);
     __builtin_amdgcn_sched_barrier(0);
-#endif
     const double* bk = stg + (s % kFanRing) * kStage;
     const double* bi = bk + kFanK * TS;
-#if VIBA_FAN_MFMA4 == 3
-    // the split-K form on a 32 x 16 strip per wave (8 waves): 8 + 4 operand reads, 32 instructions
-    {
-      double av[8], bv[4];
-#pragma unroll
-      for (int r = 0; r < 8; r++) av[r] = bk[offA + ((rowA + 4 * r) & 63)];
-#pragma unroll
-      for (int c = 0; c < 4; c++) bv[c] = bi[offA + ((rowB + 4 * c) & 63)];
-#ifdef VIBA_FAN_NOMMA  // measurement build: the operand reads without the products
-#pragma unroll
-      for (int r = 0; r < 8; r++) acc4[r][r & 3] += av[r] * bv[r & 3];
-#else
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) acc4[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], bv[c], acc4[r][c], 0, 0, 0);
-#endif
-    }
-#elif VIBA_FAN_MFMA4 == 2
-    // split-K v_mfma_f64_4x4x4_4b: D_i[b][j] = sum_k' A(lane 16k' + 4i + b) B(lane 16k' + 4i + j) at lane
-    // 16b + 4i + j (profiles/r02_mfma4_layout.txt).  Block i takes the stage's columns 4i .. 4i + 3, so
-    // every block of one instruction adds into the same 4 x 4 piece of the quadrant and the blocks are
-    // summed once per target (fanin_store).  Row group r of the wave's 32 rows and column group c of its
-    // 32 columns: 8 + 8 operand reads feed 64 independent instructions (the 16x16x4 form's read count
-    // per flop), 64 accumulators.
-    {
-      double av[8], bv[8];
-#pragma unroll
-      for (int r = 0; r < 8; r++) av[r] = bk[offA + ((rowA + 4 * r) & 63)];
-#pragma unroll
-      for (int c = 0; c < 8; c++) bv[c] = bi[offA + ((rowB + 4 * c) & 63)];
-#pragma unroll
-      for (int r = 0; r < 8; r++)
-#pragma unroll
-        for (int c = 0; c < 8; c++) acc4[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], bv[c], acc4[r][c], 0, 0, 0);
-    }
-#elif VIBA_FAN_MFMA4
-    // v_mfma_f64_4x4x4_4b: D_i[b][j] = sum_k A(lane 16k + 4i + b) B(lane 16k + 4i + j), D_i[b][j] at lane
-    // 16b + 4i + j (profiles/r02_mfma4_layout.txt).  A of row group g is the 16x16x4 A operand (lane ->
-    // y row yb + 16g + (lane & 15), k = lane >> 4); B of column group c is x column xb + 4c + (lane & 3)
-    // for every i (a broadcast read).  16 instructions of 512 flops per k-step, 16 accumulators.
-#pragma unroll
-    for (int t0 = 0; t0 < kFanK; t0 += 4) {
-      const int t = t0 + l4, rot = (t & 1) * 16;
-      double av[2], bv[8];
-#pragma unroll
-      for (int a = 0; a < 2; a++) av[a] = bk[t * TS + ((pb + a * 16 + l15 + rot) & 63)];
-#pragma unroll
-      for (int c = 0; c < 8; c++) bv[c] = bi[t * TS + ((qb + 4 * c + (lane & 3) + rot) & 63)];
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int c = 0; c < 8; c++) acc4[a][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[a], bv[c], acc4[a][c], 0, 0, 0);
-    }
-#else
 #pragma unroll
     for (int t0 = 0; t0 < kFanK; t0 += 4) {
       const int t = t0 + l4, rot = (t & 1) * 16;
@@ -2106,97 +1133,17 @@ __device__ __forceinline__ void fanin_accum(const Dev& d, const int32_t* pairs, 
       for (int a = 0; a < 2; a++) av[a] = bk[t * TS + ((pb + a * 16 + l15 + rot) & 63)];
 #pragma unroll
       for (int b = 0; b < 2; b++) bv[b] = bi[t * TS + ((qb + b * 16 + l15 + rot) & 63)];
-#ifdef VIBA_FAN_NOMMA  // measurement build: the operand reads without the products
-#pragma unroll
-      for (int a = 0; a < 2; a++) acc[a][a][0] += av[a] * bv[a];
-#else
 #pragma unroll
       for (int a = 0; a < 2; a++)
 #pragma unroll
         for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
-#endif
     }
-#endif
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // C -= acc (the wave's quadrant): agent-scope fp64 atomics when the target's list is split over
 // several workgroups, else a read-modify-write with all 16 loads in flight before the stores
-#if VIBA_FAN_MFMA4 >= 2
-__device__ __forceinline__ double swz_xor8(double v) {
-  const int2 w = __builtin_bit_cast(int2, v);
-  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_ds_swizzle(w.x, 0x201f), __builtin_amdgcn_ds_swizzle(w.y, 0x201f)));
-}
-__device__ __forceinline__ double swz_xor4(double v) {
-  const int2 w = __builtin_bit_cast(int2, v);
-  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_ds_swizzle(w.x, 0x101f), __builtin_amdgcn_ds_swizzle(w.y, 0x101f)));
-}
-// C -= the split-K accumulators: acc[r][c] at lane 16b + 4i + j holds block i's part of C(q = qb + 4c + j,
-// p = pb + 4r + b).  The four blocks (lane bits 2-3) are summed by a reduce-scatter over the column
-// quads 4c1 .. 4c1 + 3: lane i keeps the sum of quad 4c1 + i, so each lane ends with 16 values at
-// q = qb + 16 c1 + (lane & 15), p = pb + 4r + (lane >> 4) -- the 16x16x4 form's store map
-__device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const fan_acc_t& acc4) {
-#if VIBA_FAN_MFMA4 == 3
-  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;
-  constexpr int kC1 = 1;
-#else
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  constexpr int kC1 = 2;
-#endif
-  const bool h2 = (lane & 8) != 0, h1 = (lane & 4) != 0;
-  double v[8][2];
-#pragma unroll
-  for (int r = 0; r < 8; r++)
-#pragma unroll
-    for (int c1 = 0; c1 < kC1; c1++) {
-      const double* g = acc4[r] + 4 * c1;
-      const double k0 = (h2 ? g[2] : g[0]) + swz_xor8(h2 ? g[0] : g[2]);
-      const double k1 = (h2 ? g[3] : g[1]) + swz_xor8(h2 ? g[1] : g[3]);
-      v[r][c1] = (h1 ? k1 : k0) + swz_xor4(h1 ? k0 : k1);
-    }
-  double* Cw = C + (pb + (lane >> 4)) * TS + qb + (lane & 15);
-  if (atomic) {
-#pragma unroll
-    for (int r = 0; r < 8; r++)
-#pragma unroll
-      for (int c1 = 0; c1 < kC1; c1++) atomicAdd(Cw + 4 * r * TS + 16 * c1, -v[r][c1]);
-  } else {
-    double o[8][2];
-#pragma unroll
-    for (int r = 0; r < 8; r++)
-#pragma unroll
-      for (int c1 = 0; c1 < kC1; c1++) o[r][c1] = Cw[4 * r * TS + 16 * c1];
-#pragma unroll
-    for (int r = 0; r < 8; r++)
-#pragma unroll
-      for (int c1 = 0; c1 < kC1; c1++) Cw[4 * r * TS + 16 * c1] = o[r][c1] - v[r][c1];
-  }
-}
-#elif VIBA_FAN_MFMA4
-// C -= acc4 (the wave's quadrant in the 4x4x4_4b output map: row x = qb + 4c + (lane & 3), column
-// y = pb + 16a + 4 ((lane >> 2) & 3) + (lane >> 4))
-__device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const fan_acc_t& acc4) {
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  double* Cw = C + (pb + 4 * ((lane >> 2) & 3) + (lane >> 4)) * TS + qb + (lane & 3);
-  if (atomic) {
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int c = 0; c < 8; c++) atomicAdd(Cw + 16 * a * TS + 4 * c, -acc4[a][c]);
-  } else {
-    double v[2][8];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int c = 0; c < 8; c++) v[a][c] = Cw[16 * a * TS + 4 * c];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int c = 0; c < 8; c++) Cw[16 * a * TS + 4 * c] = v[a][c] - acc4[a][c];
-  }
-}
-#else
 __device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, int lane, const double4_t (&acc)[2][2]) {
   const int l15 = lane & 15, l4 = lane >> 4;
   const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
@@ -2224,377 +1171,14 @@ __device__ __forceinline__ void fanin_store(double* C, bool atomic, int wave, in
         for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + b * 16] = v[a][b][r] - acc[a][b][r];
   }
 }
-#endif
 
 __global__ void __launch_bounds__(kFanWaves * 64) fanin_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
   __shared__ double stg[kFanRing * kStage];
   const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  fan_acc_t acc;
+  double4_t acc[2][2];
   fanin_accum(d, pairs, wk[1], wk[2], stg, wave, lane, acc);
   fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
-}
-
-// Streamed fan-in: one workgroup per bin of a level's work items (host-balanced, XCD-placed: bin b runs
-// on XCD b % 8), the LDS ring running on across the bin's items, so each item's first stages are in
-// flight while the previous item computes and stores (fanin_kernel refills the ring from empty for
-// every item).  Every item ends in agent-scope atomics (a single-writer target receives exactly one add
-// per element, so its result is that of the plain read-modify-write); their 16 vector-memory
-// operations per wave are younger than the stages issued before them, which the counted waits add in
-// (s_waitcnt vmcnt counts loads, stores, atomics and LDS-DMA together, in issue order).  Items hold at
-// least TS / kFanK stages, so at most one item end falls between a stage's issue and its use.
-__device__ __forceinline__ void fan_zero(fan_acc_t& acc) {
-#if VIBA_FAN_MFMA4
-  for (auto& row : acc)
-    for (auto& v : row) v = 0.0;
-#else
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
-#endif
-}
-
-__device__ __forceinline__ void fan_stage(const double* bk, int wave, int lane, fan_acc_t& acc) {
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  const double* bi = bk + kFanK * TS;
-#if VIBA_FAN_MFMA4 == 2
-  const int tq = 4 * ((lane >> 2) & 3) + (lane >> 4);
-  const int offA = tq * TS, rowA = pb + (lane & 3) + fan_rot(tq), rowB = qb + (lane & 3) + fan_rot(tq);
-  double av[8], bv[8];
-#pragma unroll
-  for (int r = 0; r < 8; r++) av[r] = bk[offA + ((rowA + 4 * r) & 63)];
-#pragma unroll
-  for (int c = 0; c < 8; c++) bv[c] = bi[offA + ((rowB + 4 * c) & 63)];
-#pragma unroll
-  for (int r = 0; r < 8; r++)
-#pragma unroll
-    for (int c = 0; c < 8; c++) acc[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], bv[c], acc[r][c], 0, 0, 0);
-#elif VIBA_FAN_MFMA4 == 0
-  const int l15 = lane & 15, l4 = lane >> 4;
-#pragma unroll
-  for (int t0 = 0; t0 < kFanK; t0 += 4) {
-    const int t = t0 + l4, rot = fan_rot(t);
-    double av[2], bv[2];
-#pragma unroll
-    for (int a = 0; a < 2; a++) av[a] = bk[t * TS + ((pb + a * 16 + l15 + rot) & 63)];
-#pragma unroll
-    for (int b = 0; b < 2; b++) bv[b] = bi[t * TS + ((qb + b * 16 + l15 + rot) & 63)];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int b = 0; b < 2; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
-  }
-#endif
-}
-
-#if (VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2) && VIBA_FAN_RING <= 5 && VIBA_FAN_LATE
-__global__ void __launch_bounds__(256) fanin_stream_kernel(Dev d, const int32_t* work, const int32_t* bins,
-                                                           const int32_t* pairs) {
-  static_assert(kGlds * (kFanRing - 2) + 16 <= 63 && kFanRing >= 3 && kFanRing <= 5, "vmcnt range");
-  static_assert(VIBA_FAN_LATE, "issue-after-barrier ring");
-  __shared__ double stg[kFanRing * kStage];
-  typedef const __attribute__((address_space(4))) int32_t cint;
-  cint* wk = (cint*)work;
-  cint* bn = (cint*)bins;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int32_t i0 = bn[blockIdx.x], i1 = bn[blockIdx.x + 1];
-  constexpr int kAhead = kFanRing - 1, kSt = TS / kFanK;
-  int32_t iI = i0, sI = 0, nI = i0 < i1 ? kSt * wk[4 * i0 + 2] : 0, issued = 0;
-  auto issueNext = [&]() {
-    fanin_issue(d, pairs, wk[4 * iI + 1], sI, stg + (issued % kFanRing) * kStage, wave, lane);
-    issued++;
-    if (++sI == nI) {
-      iI++, sI = 0;
-      nI = iI < i1 ? kSt * wk[4 * iI + 2] : 0;
-    }
-  };
-  for (int k = 0; k < kAhead && iI < i1; k++) issueNext();
-  int32_t g = 0, epiIssued = 0;  // stages below epiIssued were issued before the last item's atomics
-  for (int32_t it = i0; it < i1; it++) {
-    fan_acc_t acc;
-    fan_zero(acc);
-    const int32_t nst = kSt * wk[4 * it + 2];
-    for (int32_t s = 0; s < nst; s++, g++) {
-      // stage g landed: younger than it are the later stages issued so far and, if an item ended since
-      // its issue, that item's 16 atomics
-      switch (2 * min(kAhead - 1, issued - 1 - g) + (g < epiIssued ? 1 : 0)) {
-#define VIBA_FAN_WAIT(c) \
-  case c: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGlds * ((c) >> 1) + 16 * ((c) & 1)) : "memory"); break;
-        VIBA_FAN_WAIT(1) VIBA_FAN_WAIT(2) VIBA_FAN_WAIT(3) VIBA_FAN_WAIT(4) VIBA_FAN_WAIT(5) VIBA_FAN_WAIT(6)
-        VIBA_FAN_WAIT(7)
-#undef VIBA_FAN_WAIT
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-      }
-      __builtin_amdgcn_s_barrier();  // ... and every other wave's; the ring buffer of stage g - 1 is free
-      __builtin_amdgcn_sched_barrier(0);
-      if (iI < i1) issueNext();
-      __builtin_amdgcn_sched_barrier(0);
-      fan_stage(stg + (g % kFanRing) * kStage, wave, lane, acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    fanin_store(d.tiles + (int64_t)wk[4 * it] * TS * TS, true, wave, lane, acc);
-    __builtin_amdgcn_sched_barrier(0);
-    epiIssued = issued;
-  }
-}
-#endif
-
-// Paired fan-in (VIBA_FAN_PAIR): two targets (I1, J), (I2, J) of one column whose contribution lists
-// hold the same source columns K, in the same order (api.hip pairs them within the groups of identical
-// lists: 580k of config C's 701k contributions), stage L_JK once: 3 tiles per 2 products instead of 4,
-// and the product runs on v_mfma_f64_4x4x4_4b in a split-K-by-2 form that keeps the accumulators small
-// enough for two targets.  Eight waves; wave w owns the 32 x 16 strip p in [32 (w & 1), +32), q in
-// [16 (w >> 1), +16) of both targets.  A stage is 16 columns = two k-steps of 8; in a k-step, block i of
-// an instruction takes row group 2r + (i >> 1) and columns 4 (i & 1) .. 4 (i & 1) + 3 of the k-step, so
-// blocks i and i ^ 1 add two partials of one 4 x 4 piece (summed once per target by one swizzle) and
-// blocks 0 / 2 read the same B column group (one address, a broadcast).  Per k-step and wave: 4 A and
-// 4 + 4 B operand reads feed 32 instructions of 512 flops.  Items (8 int32): t1, t2 (< 0: one target),
-// first1, first2, count, atomic.
-constexpr int kPairWaves = 8;
-constexpr int kPK = 16;  // columns per stage (the single fan-in's kFanK may be rebuilt otherwise)
-constexpr int kPRing = 3;
-constexpr int kPStage = 3 * kPK * TS;  // [L_JK, L_I1K, L_I2K][kPK columns][64 rows]
-__device__ __forceinline__ int pair_rot(int t) { return 16 * ((t >> 2) & 1) + 8 * (t & 1); }
-
-template <int NT>  // tiles staged per stage: 3 (pair) or 2 (single target)
-__device__ __forceinline__ void pair_issue(const Dev& d, const int32_t* pairs, int32_t f1, int32_t f2, int s,
-                                           double* buf, int wave, int lane) {
-  constexpr int kG = NT * kPK / 2 / kPairWaves;  // 1 KB loads per wave per stage
-  const int64_t c = s / (TS / kPK);
-  const int k0 = (s % (TS / kPK)) * kPK;
-  const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
-  const int64_t tk = pc[2 * (f1 + c) + 1], t1 = pc[2 * (f1 + c)], t2 = NT == 3 ? pc[2 * (f2 + c)] : 0;
-  const int hi = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < kG; j++) {
-    const int i = wave * kG + j, tile = i / (kPK / 2), cp = i % (kPK / 2);
-    const int row = (2 * (lane & 31) - pair_rot(2 * cp + hi)) & 63;
-    const int64_t tt = tile == 0 ? tk : tile == 1 ? t1 : t2;
-    const double* src = d.tiles + tt * TS * TS + (int64_t)(k0 + 2 * cp + hi) * TS + row;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(buf + tile * kPK * TS + cp * 2 * TS),
-                                     16, 0, 0);
-  }
-}
-
-template <int NT>
-__device__ __forceinline__ void pair_accum(const Dev& d, const int32_t* pairs, int32_t f1, int32_t f2, int32_t count,
-                                           double* stg, int wave, int lane, double (&a1)[4][4], double (&a2)[4][4]) {
-  constexpr int kG = NT * kPK / 2 / kPairWaves;
-  constexpr int kAhead = kPRing - 1;
-  static_assert(kG * kAhead <= 63, "pair ring");
-  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;
-  const int kq = lane >> 4, i = (lane >> 2) & 3, e = lane & 3;
-  const int rowA = pb + 4 * (i >> 1) + e, colB = qb + e;
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) a1[r][c] = 0.0, a2[r][c] = 0.0;
-  const int32_t nst = (TS / kPK) * count;
-  for (int s = 0; s < kAhead && s < nst; s++) pair_issue<NT>(d, pairs, f1, f2, s, stg + s * kPStage, wave, lane);
-  for (int s = 0; s < nst; s++) {
-    switch (min(kAhead - 1, nst - 1 - s)) {
-      case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kG) : "memory"); break;
-      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + kAhead < nst) pair_issue<NT>(d, pairs, f1, f2, s + kAhead, stg + ((s + kAhead) % kPRing) * kPStage, wave, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    const double* bk = stg + (s % kPRing) * kPStage;
-#pragma unroll
-    for (int ks = 0; ks < 2; ks++) {
-      const int t = 8 * ks + 4 * (i & 1) + kq, rt = pair_rot(t);
-      const double* ak = bk + t * TS;
-      double av[4], b1[4], b2[4];
-#pragma unroll
-      for (int r = 0; r < 4; r++) av[r] = ak[(rowA + 8 * r + rt) & 63];
-#pragma unroll
-      for (int c = 0; c < 4; c++) b1[c] = ak[kPK * TS + ((colB + 4 * c + rt) & 63)];
-      if (NT == 3) {
-#pragma unroll
-        for (int c = 0; c < 4; c++) b2[c] = ak[2 * kPK * TS + ((colB + 4 * c + rt) & 63)];
-      }
-#ifdef VIBA_FAN_NOMMA  // measurement build: the operand reads without the products
-#pragma unroll
-      for (int r = 0; r < 4; r++) a1[r][r] += av[r] * b1[r] + (NT == 3 ? b2[r] : 0.0);
-#else
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) a1[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], b1[c], a1[r][c], 0, 0, 0);
-      if (NT == 3) {
-#pragma unroll
-        for (int r = 0; r < 4; r++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) a2[r][c] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[r], b2[c], a2[r][c], 0, 0, 0);
-      }
-#endif
-      __builtin_amdgcn_sched_barrier(0);  // one k-step's operands live at a time (4 waves per SIMD)
-    }
-  }
-}
-
-__device__ __forceinline__ double pair_swz_xor4(double v) {
-  const int2 w = __builtin_bit_cast(int2, v);
-  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_ds_swizzle(w.x, 0x101f), __builtin_amdgcn_ds_swizzle(w.y, 0x101f)));
-}
-
-// C -= acc: acc[r][c] at lane 16b + 4i + j is the partial (columns 4 (i & 1) ..) of C(q = qb + 4c + j,
-// p = pb + 4 (2r + (i >> 1)) + b); the two partials (lane bit 2) are summed by a reduce-scatter over
-// column-group pairs, so lane keeps q = qb + 8 c1 + (lane & 7), p = pb + 8r + 4 ((lane >> 3) & 1) + (lane >> 4)
-__device__ __forceinline__ void pair_store(double* C, bool atomic, int wave, int lane, const double (&acc)[4][4]) {
-  const int pb = (wave & 1) * 32, qb = (wave >> 1) * 16;
-  const bool kh = (lane & 4) != 0;
-  double v[4][2];
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-#pragma unroll
-    for (int c1 = 0; c1 < 2; c1++) {
-      const double g0 = acc[r][2 * c1], g1 = acc[r][2 * c1 + 1];
-      v[r][c1] = (kh ? g1 : g0) + pair_swz_xor4(kh ? g0 : g1);
-    }
-  double* Cw = C + (pb + 4 * ((lane >> 3) & 1) + (lane >> 4)) * TS + qb + (lane & 7);
-  if (atomic) {
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-      for (int c1 = 0; c1 < 2; c1++) atomicAdd(Cw + 8 * r * TS + 8 * c1, -v[r][c1]);
-  } else {
-    double o[4][2];
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-      for (int c1 = 0; c1 < 2; c1++) o[r][c1] = Cw[8 * r * TS + 8 * c1];
-#pragma unroll
-    for (int r = 0; r < 4; r++)
-#pragma unroll
-      for (int c1 = 0; c1 < 2; c1++) Cw[8 * r * TS + 8 * c1] = o[r][c1] - v[r][c1];
-  }
-}
-
-__global__ void __launch_bounds__(kPairWaves * 64) __attribute__((amdgpu_waves_per_eu(4, 4)))
-fanin_pair_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
-  __shared__ double stg[kPRing * kPStage];
-  const int32_t* wk = work + 8 * xcd_block(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double a1[4][4], a2[4][4];
-  if (wk[1] >= 0) {
-    pair_accum<3>(d, pairs, wk[2], wk[3], wk[4], stg, wave, lane, a1, a2);
-    pair_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[5] != 0, wave, lane, a1);
-    pair_store(d.tiles + (int64_t)wk[1] * TS * TS, wk[5] != 0, wave, lane, a2);
-  } else {
-    pair_accum<2>(d, pairs, wk[2], wk[2], wk[4], stg, wave, lane, a1, a2);
-    pair_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[5] != 0, wave, lane, a1);
-  }
-}
-
-// One elimination level of the tile Cholesky in ONE launch (fan-in + potrf + trsm; the 3-launch form is
-// fanin_kernel / potrf_kernel / trsm_kernel).  Item b (FacItem, 8 int32): fan-in of `count`
-// contributions into `target` -- its list may be split over `nch` items (atomics + an arrival ticket
-// cnt[target]: the last arriver finishes the tile) -- then by kind:
-//   1  diagonal tile of column J: wave 0 factors it (potrf_blocked in LDS, reusing the ring), writes L_JJ
-//      and the 16 x 16 block inverses dinv[J], and publishes colFlag[J];
-//   2  off-diagonal tile (I, J): waits for colFlag[J], then X = A L_JJ^-T on all four waves;
-//   0  fan-in only (a partial ROOT tile of a partitioned factorization).
-// Items [0, nDiag) are the diagonal ones (padded to a multiple of 8 with count < 0 no-ops); block b
-// < nDiag runs item b, the rest run the off-diagonal items in XCD-contiguous ranges (xcd_block), so on
-// every XCD all diagonal items are dispatched before any item that waits: no deadlock whatever the
-// occupancy, and the potrf latency overlaps the off-diagonal fan-in.  Hand-offs per the guide's G16
-// recipe (every wave s_waitcnt vmcnt(0) -> barrier -> lane 0 agent release -> s_waitcnt -> relaxed
-// agent ticket / flag; consumer: poll relaxed, agent acquire, s_waitcnt, barrier, plain loads).
-// No per-factorization reset: tickets are cumulative (every factorization adds exactly nch per split
-// target, so the last arriver is the one whose add makes the count a multiple of nch), and a column's
-// flag holds the epoch of the factorization that published it (epoch = *epochPtr, bumped by a one-thread
-// kernel ahead of every factorization).  (A memset node ahead of the launches in the captured graph
-// left stale flags visible on replays.)  Spins are bounded (error flag 16).
-__device__ __forceinline__ void release_agent() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-__device__ __forceinline__ void acquire_agent() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-__global__ void bump_epoch_kernel(unsigned* epoch) { __hip_atomic_fetch_add((guint*)epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-__global__ void __launch_bounds__(256, 3) factor_level_kernel(Dev d, const FacItem* items, int nDiag, const int32_t* pairs,
-                                                           unsigned* cnt, unsigned* colFlag, const unsigned* epochPtr,
-                                                           double* dinvAll) {
-  __shared__ double stg[kFanRing * kStage];
-  __shared__ int sLast;
-  const int b = (int)blockIdx.x;
-  const FacItem it = items[b < nDiag ? b : nDiag + (int)xcd_block(b - nDiag, (int64_t)gridDim.x - nDiag)];
-  if (it.count < 0) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  double* C = d.tiles + (int64_t)it.target * TS * TS;
-  if (it.count > 0) {
-#if VIBA_FAN_MFMA4 == 3  // the 8-wave fan-in has no fused-level form
-    if (tid == 0) atomicOr(d.err, 16);
-    return;
-#else
-    fan_acc_t acc;
-    fanin_accum(d, pairs, it.first, it.count, stg, wave, lane, acc);
-    fanin_store(C, it.nch > 1, wave, lane, acc);
-#endif
-  }
-  if (it.kind == 0) return;
-  // this workgroup's part of the target is out; is the tile complete?
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    if (it.nch > 1) {
-      release_agent();
-      sLast = (__hip_atomic_fetch_add((guint*)&cnt[it.target], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) %
-                  (unsigned)it.nch == 0u;
-    } else {
-      sLast = 1;
-    }
-    if (sLast) acquire_agent();
-  }
-  __syncthreads();
-  if (!sLast) return;
-  if (it.kind == 1) {
-    if (wave != 0) return;
-    double* T = stg;                     // 64 x 64 tile (32 KB)
-    double* scratch = stg + TS * TS;     // 256 doubles
-    double* dinvS = scratch + 256;       // 4 x 16 x 16 block inverses
-#pragma unroll 16
-    for (int c = 0; c < TS; c++) T[c * TS + lane] = C[c * TS + lane];
-    __builtin_amdgcn_wave_barrier();
-    potrf_blocked(T, scratch, dinvS, lane, d.err);
-    lds_to_global(C, T, TS * TS, lane, 64);
-    lds_to_global(dinvAll + (int64_t)it.J * 1024, dinvS, 1024, lane, 64);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      release_agent();
-      __hip_atomic_store((guint*)&colFlag[it.J], __hip_atomic_load((guint*)epochPtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return;
-  }
-  // kind 2: wait for L_JJ
-  if (tid == 0) {
-    const unsigned ep = __hip_atomic_load((guint*)epochPtr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned v = 0;
-    for (unsigned spins = 0;; spins++) {
-      v = __hip_atomic_load((guint*)&colFlag[it.J], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v == ep || spins > (1u << 24)) break;
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (v != ep) atomicOr(d.err, 16);
-    acquire_agent();
-  }
-  __syncthreads();
-  double4_t Xt[4];
-  trsm_rowblock<4>(C, d.tiles + (int64_t)it.diagTile * TS * TS, dinvAll + (int64_t)it.J * 1024, wave, lane, Xt);
-  const int lr = lane & 15, lq = lane >> 4;
-#pragma unroll
-  for (int k = 0; k < 4; k++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) C[(16 * k + lq + 4 * r) * TS + 16 * wave + lr] = Xt[k][r];
 }
 
 // Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
@@ -2623,65 +1207,6 @@ __global__ void __launch_bounds__(64) diag_inverse_kernel(Dev d, const int32_t* 
   double* out = linv + (int64_t)J * TS * TS + lane * TS;
 #pragma unroll
   for (int i = 0; i < TS; i++) out[i] = xi[i];
-}
-
-// ------------------------------------------------------------------ triangular solves
-// forward, column J: every block computes y_J = Linv_JJ b_J (GEMV); block 0 stores it into x;
-// block q >= 1 updates b_I -= L_IJ y_J for I = rows[q]
-__global__ void __launch_bounds__(64) fwd_kernel(Dev d, const int32_t* colTiles, const int32_t* tileRow, int n,
-                                                 const double* linvJ, double* b, double* x, int64_t nRed) {
-  __shared__ double bs[TS], y[TS];
-  const int lane = threadIdx.x;
-  const int J = tileRow[0];
-  const int64_t base = (int64_t)J * TS;
-  bs[lane] = (base + lane < nRed) ? b[base + lane] : 0.0;
-  __builtin_amdgcn_wave_barrier();
-  double yi = 0.0;
-#pragma unroll 16
-  for (int k = 0; k < TS; k++) yi += linvJ[k * TS + lane] * bs[k];
-  y[lane] = yi;
-  __builtin_amdgcn_wave_barrier();
-  if (blockIdx.x == 0) {
-    if (base + lane < nRed) x[base + lane] = yi;
-    return;
-  }
-  const int q = blockIdx.x;
-  if (q >= n) return;
-  const double* A = d.tiles + (int64_t)colTiles[q] * TS * TS;
-  const int64_t ib = (int64_t)tileRow[q] * TS;
-  double s = 0;
-#pragma unroll 16
-  for (int k = 0; k < TS; k++) s += A[k * TS + lane] * y[k];
-  if (ib + lane < nRed) b[ib + lane] -= s;
-}
-
-// backward, row J (descending): x_J = Linv_JJ^T t_J; block q >= 1 updates t_K -= L_JK^T x_J
-// for the tiles (J, K), K < J, listed in rowTiles (tile index) / rowCol (K)
-__global__ void __launch_bounds__(64) bwd_kernel(Dev d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n,
-                                                 const double* linvJ, double* t, double* x, int64_t nRed) {
-  __shared__ double ts[TS], xs[TS];
-  const int lane = threadIdx.x;
-  const int64_t base = (int64_t)J * TS;
-  ts[lane] = (base + lane < nRed) ? t[base + lane] : 0.0;
-  __builtin_amdgcn_wave_barrier();
-  double xk = 0.0;  // x_k = sum_i Linv(i, k) t_i
-#pragma unroll 16
-  for (int i = 0; i < TS; i++) xk += linvJ[lane * TS + i] * ts[i];
-  if (base + lane >= nRed) xk = 0.0;
-  xs[lane] = xk;
-  __builtin_amdgcn_wave_barrier();
-  if (blockIdx.x == 0) {
-    if (base + lane < nRed) x[base + lane] = xk;
-    return;
-  }
-  const int q = blockIdx.x - 1;
-  if (q >= n) return;
-  const double* A = d.tiles + (int64_t)rowTiles[q] * TS * TS;  // tile (J, K): rows of J, cols of K
-  const int64_t kb = (int64_t)rowCol[q] * TS;
-  double s = 0;
-#pragma unroll 16
-  for (int i = 0; i < TS; i++) s += A[lane * TS + i] * xs[i];
-  if (kb + lane < nRed) t[kb + lane] -= s;
 }
 
 // ------------------------------------------------------------------ persistent triangular solves
@@ -3034,10 +1559,9 @@ void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hip
 
 void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
-  static const int v1 = getenv("VIBA_LANDMARK_V1") ? atoi(getenv("VIBA_LANDMARK_V1")) : 0;
   if (mode == 2) {
     launchK(landmark_z_kernel, dim3(blocks(hi - lo, 256)), dim3(256), 0, st, d, lo, hi);
-  } else if (mode == 0 && !v1 && lo == d.lmB && hi == d.lmE) {
+  } else if (mode == 0 && lo == d.lmB && hi == d.lmE) {
     if (d.nLmSmall)
       launchK(landmark_obs_kernel, dim3(blocks(d.nLmSmall, 4)), dim3(256),
               (uint32_t)(4 * 3 * kLmSmallCols * sizeof(double)), st, d, lambda, (int64_t)0, d.nLmSmall, kLmSmallCols);
@@ -3068,16 +1592,7 @@ void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) 
   launch_schur_products(d, lambda, st);
 }
 void launch_schur_products(const Dev& d, double lambda, hipStream_t st) {
-  // VIBA_SCHUR_V: 4 (default) precomputed runs and balanced tasks (schur_run4_kernel); 2 the run scan in
-  // the kernel (schur_run2_kernel); 3 schur_run2 with the K-row offsets from an LDS table and hand-counted
-  // gathers (schur_run3_kernel; measured r03a on config C: Schur phase 6.50 ms against 6.15 for run2)
-  static const int v = getenv("VIBA_SCHUR_V") ? atoi(getenv("VIBA_SCHUR_V")) : 4;
-  if (d.nTileWorks) {
-    if (v == 2) launchK(schur_run2_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else if (v == 3) launchK(schur_run3_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else if (v == 5) launchK(schur_run5_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-    else launchK(schur_run4_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-  }
+  if (d.nTileWorks) launchK(schur_run4_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
   launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
 }
 void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
@@ -3092,27 +1607,11 @@ void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
 // trsm: b_I -= L_IJ y_J for its tile, rows[] = the tile's row I)
 void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st,
                   const double* fwdB, double* fwdY) {
-  // VIBA_POTRF_WAVES=1: the one-wave left-looking form; default the four-wave right-looking form, its
-  // diagonal inverses through LDS as in the one-wave form (VIBA_DIAG_INV=dpp: from registers)
-  static const int waves = [] {
-    const char* e = getenv("VIBA_POTRF_WAVES");
-    return e && atoi(e) == 1 ? 1 : 4;
-  }();
-  static const bool dppInv = [] {  // same speed measured; the LDS form needs 213 VGPRs instead of 468
-    const char* e = getenv("VIBA_DIAG_INV");
-    return e && std::string(e) == "dpp";
-  }();
-  if (n <= 0) return;
-  if (waves == 4 && dppInv) launchK(potrf4_kernel<true>, dim3(n), dim3(256), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
-  else if (waves == 4) launchK(potrf4_kernel<false>, dim3(n), dim3(256), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
-  else launchK(potrf_kernel, dim3(n), dim3(64), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
+  if (n > 0) launchK(potrf4_kernel, dim3(n), dim3(256), 0, st, d, tiles, cols, dinv, fwdB, fwdY);
 }
 void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, double* dinv, hipStream_t st,
                        double* fwdB, double* fwdY) {
-  static const bool dppInv = getenv("VIBA_DIAG_INV") && std::string(getenv("VIBA_DIAG_INV")) == "dpp";
-  if (n <= 0) return;
-  if (dppInv) launchK(potrf_trsm_kernel<true>, dim3(n), dim3(256), 0, st, d, items, Lscr, dinv, fwdB, fwdY);
-  else launchK(potrf_trsm_kernel<false>, dim3(n), dim3(256), 0, st, d, items, Lscr, dinv, fwdB, fwdY);
+  if (n > 0) launchK(potrf_trsm_kernel, dim3(n), dim3(256), 0, st, d, items, Lscr, dinv, fwdB, fwdY);
 }
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(copy_diag_kernel, dim3(n), dim3(256), 0, st, d, pairs, Lscr);
@@ -3147,22 +1646,6 @@ void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, cons
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
   if (n > 0) launchK(fanin_kernel, dim3(n), dim3(kFanWaves * 64), 0, st, d, work, pairs);
 }
-void launch_fanin_pair(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
-  if (n > 0) launchK(fanin_pair_kernel, dim3(n), dim3(kPairWaves * 64), 0, st, d, work, pairs);
-}
-void launch_fanin_stream(const Dev& d, const int32_t* work, const int32_t* bins, const int32_t* pairs, int nBins,
-                         hipStream_t st) {
-#if (VIBA_FAN_MFMA4 == 0 || VIBA_FAN_MFMA4 == 2) && VIBA_FAN_RING <= 5 && VIBA_FAN_LATE
-  if (nBins > 0) launchK(fanin_stream_kernel, dim3(nBins), dim3(256), 0, st, d, work, bins, pairs);
-#else
-  (void)d, (void)work, (void)bins, (void)pairs, (void)nBins, (void)st;
-#endif
-}
-void launch_factor_level(const Dev& d, const FacItem* items, int n, int nDiag, const int32_t* pairs, unsigned* cnt,
-                         unsigned* colFlag, const unsigned* epoch, double* dinv, hipStream_t st) {
-  if (n > 0) launchK(factor_level_kernel, dim3(n), dim3(256), 0, st, d, items, nDiag, pairs, cnt, colFlag, epoch, dinv);
-}
-void launch_bump_epoch(unsigned* epoch, hipStream_t st) { hipLaunchKernelGGL(bump_epoch_kernel, dim3(1), dim3(1), 0, st, epoch); }
 // inverses of the diagonal factor tiles of the listed columns (all columns if cols == nullptr)
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(diag_inverse_kernel, dim3((unsigned)n), dim3(64), 0, st, d, cols, linv);
@@ -3175,14 +1658,6 @@ __global__ void pad_diag_kernel(Dev d, const int64_t* rows, int64_t n) {
 }
 void launch_pad_diag(const Dev& d, const int64_t* rows, int64_t n, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(pad_diag_kernel, dim3(blocks(n, 256)), dim3(256), 0, st, d, rows, n);
-}
-void launch_fwd(const Dev& d, const int32_t* colTiles, const int32_t* tileRow, int n, const double* linvJ,
-                double* b, double* x, hipStream_t st) {
-  launchK(fwd_kernel, dim3(n), dim3(64), 0, st, d, colTiles, tileRow, n, linvJ, b, x, d.nRed);
-}
-void launch_bwd(const Dev& d, int J, const int32_t* rowTiles, const int32_t* rowCol, int n, const double* linvJ,
-                double* t, double* x, hipStream_t st) {
-  launchK(bwd_kernel, dim3(n + 1), dim3(64), 0, st, d, J, rowTiles, rowCol, n, linvJ, t, x, d.nRed);
 }
 void launch_backsub(const Dev& d, int mode, int64_t lo, int64_t hi, const double* xr, double* xp, hipStream_t st) {
   if (hi > lo)
@@ -3207,19 +1682,4 @@ void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, h
 
 }  // namespace viba
 
-#ifdef VIBA_POTRF_TIMING
-extern "C" int vb_debug_potrf_times(long long* out32) {
-  return hipMemcpyFromSymbol(out32, HIP_SYMBOL(viba::g_potrf_t), 32 * sizeof(long long)) == hipSuccess ? 0 : -3;
-}
-#endif
 
-#ifdef VIBA_SCHUR_TIMING
-extern "C" int vb_debug_schur_times(unsigned long long* out8, int reset) {
-  if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(viba::g_schur_t), 8 * sizeof(unsigned long long)) != hipSuccess) return -3;
-  if (reset) {
-    unsigned long long z[8] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(viba::g_schur_t), z, sizeof(z)) != hipSuccess) return -3;
-  }
-  return 0;
-}
-#endif
