@@ -70,15 +70,16 @@ def host_threads() -> tuple[int, int]:
     return max(1, min(nproc, share)), nproc
 
 
-def cpu_baseline(p, name: str = "C", steps: int = 1, recompute_preint: bool = False, warmup: int = 0):
+def cpu_baseline(p, name: str = "C", repeats: int = 3, recompute_preint: bool = False, warmup: int = 0):
     """The CPU baseline of BASELINE.md, measured on the FULL workload (no slice, no extrapolation):
     oracle/refcpu (this repository's restatement of the reference path: factor functors, the LM loop,
     point elimination + blocked Cholesky) runs `warmup` untimed iterations (as the GPU bench does, so the
-    timed iteration starts from the same kind of state as the GPU's), then times `steps` iterations of
-    Optimizer::optimize on the same generated problem, at 8 threads (the reference's numThreads default,
-    Optimizer.h:42 / Settings.h:87) and at the host's thread count.  Each timed run starts from the
-    variables after the warmup.  Reports iterations/s per thread count and the last iteration's phase
-    split."""
+    timed iterations start from the same kind of state as the GPU's), then `repeats` individually timed
+    full iterations of Optimizer::optimize at the job's thread count (value = 1 / median, with the
+    spread), and one more at 8 threads (the reference's numThreads default, Optimizer.h:42 /
+    Settings.h:87) for comparison.  Reports the median iteration's phase split."""
+    import statistics
+
     from oracle.refcpu import RefEngine
     from visual_inertial_bundle_adjustment_amd import synth
     from visual_inertial_bundle_adjustment_amd.engine import Settings
@@ -87,32 +88,39 @@ def cpu_baseline(p, name: str = "C", steps: int = 1, recompute_preint: bool = Fa
     synth.load_into(e, p, rs_device=True, recompute_preint=recompute_preint)
     log(f"[bench] cpu baseline: oracle loaded in {time.perf_counter() - t:.1f}s")
     nthr, nproc = host_threads()
-    runs = {}
+
+    def one_iteration():
+        s = Settings.default(max_num_iterations=1, stop_if_no_improvement_for=10**6, distance_from_troubled_iteration=0)
+        t0 = time.perf_counter()
+        out = e.optimize(s)
+        return (time.perf_counter() - t0) * 1e3 / max(1, out.num_iterations), e.phase_times()
+
+    e.set_threads(nthr)
     if warmup:
-        e.set_threads(nthr)
         t = time.perf_counter()
         e.optimize(Settings.default(max_num_iterations=warmup, stop_if_no_improvement_for=10**6,
                                     distance_from_troubled_iteration=0))
         log(f"[bench] cpu baseline: {warmup} warmup iteration(s) in {time.perf_counter() - t:.1f}s")
     e.backup()
-    for th in sorted({8, nthr}):
+    runs = [one_iteration() for _ in range(repeats)]
+    ms = [r[0] for r in runs]
+    med = statistics.median(ms)
+    ph = runs[ms.index(sorted(ms)[len(ms) // 2])][1]
+    log(f"[bench] cpu baseline {nthr} threads: iterations {', '.join(f'{x:.0f}' for x in ms)} ms (median {med:.0f})")
+    out8 = None
+    if nthr != 8:  # the reference's default thread count, one iteration from the same state as the first
         e.restore()
-        e.set_threads(th)
-        s = Settings.default(max_num_iterations=steps, stop_if_no_improvement_for=10**6,
-                             distance_from_troubled_iteration=0)
-        t0 = time.perf_counter()
-        out = e.optimize(s)
-        dt = time.perf_counter() - t0
-        ph = e.phase_times()
-        runs[th] = {"value": out.num_iterations / dt, "ms_per_step": dt * 1e3 / max(1, out.num_iterations),
-                    "phases_ms": {k: round(v, 1) for k, v in ph.items()}}
-        log(f"[bench] cpu baseline {th} threads: {runs[th]['ms_per_step']:.0f} ms/iteration, phases {ph}")
-    best = max(runs, key=lambda k: runs[k]["value"])
-    return {"value": runs[best]["value"], "unit": "LM iterations/s", "cores": best, "kind": "port",
-            "nproc": nproc, "threads": {str(k): v for k, v in runs.items()},
-            "sample": f"{steps} full LM iteration(s) of oracle/refcpu on the whole config-{name} problem "
-                      f"({p.num_obs} obs) after {warmup} untimed warmup iteration(s), measured at 8 threads and at "
-                      f"{nthr} (nproc {nproc}); value = the faster"}
+        e.set_threads(8)
+        m8, ph8 = one_iteration()
+        out8 = {"ms_per_step": m8, "phases_ms": {k: round(v, 1) for k, v in ph8.items()}}
+        log(f"[bench] cpu baseline 8 threads: {m8:.0f} ms/iteration")
+    return {"value": 1e3 / med, "unit": "LM iterations/s", "cores": nthr, "kind": "port", "nproc": nproc,
+            "iterations_ms": [round(x, 1) for x in ms], "median_ms": med, "min_ms": min(ms), "max_ms": max(ms),
+            "spread": (max(ms) - min(ms)) / med, "phases_ms": {k: round(v, 1) for k, v in ph.items()},
+            "threads_8": out8,
+            "sample": f"{repeats} individually timed full LM iterations of oracle/refcpu on the whole config-{name} "
+                      f"problem ({p.num_obs} obs) at {nthr} threads (nproc {nproc}) after {warmup} untimed warmup "
+                      f"iteration(s); value = 1 / median; one more iteration at 8 threads for comparison"}
 
 
 def mixed_vs_fp64(p, device, rs_device):

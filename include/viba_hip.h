@@ -178,7 +178,7 @@ typedef struct vb_summary { /* Optimizer::Summary (Optimizer.h:93-99) */
   int32_t num_troubled_seqs;
   int32_t largest_troubled_seq;
   int32_t num_iterations;
-  int32_t reserved;
+  int32_t num_rescaled; /* iterations whose full step failed the reduction / failure-rate test (step rescaling) */
 } vb_summary;
 
 typedef struct vb_cost_stats { /* CostStats (Factor.h:20-30) */
@@ -341,6 +341,10 @@ int vb_compute_covariances(vb_handle h, double damping, int64_t n_blocks, const 
  * model cost reduction is negated, which takes the reference's "quadratic model failing numerically"
  * branch (Optimizer.cpp:835-854: damping *= dampingAdjustOnFail, the step is kept) */
 int vb_debug_negate_model_reduction(vb_handle h, int iteration);
+/* test fault injection: iteration `iteration` (0-based, -1 = off) of the next vb_optimize calls fails as
+ * a reduced-system breakdown would (VB_E_NUMERIC after the step and cost pass were queued): the
+ * variables must come back to that iteration's linearization point */
+int vb_debug_fail_iteration(vb_handle h, int iteration);
 /* test support: slot of reduced tile (I, J) in the vb_reduced_buffers tile store (-1: not stored) */
 int vb_debug_tile_slot(vb_handle h, int32_t I, int32_t J, int64_t* slot);
 /* iterations and relative residual of the last PCG solve (PCG::Result) */

@@ -35,7 +35,8 @@ inline SE3 bodyImuWorldAtImageRow(const SE3& T_bw, const V3& velWorld, const Cam
                                   double imageRow) {
   if (!(cam.isRollingShutter() || cam.hasTimeOffset())) return T_bw;
   if (!rs) throw std::runtime_error("findOrDie: rig without rolling-shutter data");
-  const double timeParamFactor = imageRow / cam.h - 0.5;
+  // VisualFactor.cpp:306-311: `float imageRow` over `int imageHeight()` is a float division
+  const double timeParamFactor = (double)((float)imageRow / (float)(int)cam.h) - 0.5;
   const double dtSec = cam.readoutTimeSec() * timeParamFactor - cam.off;
   const RSEstimate est = rs_getEstimate(*rs, dtSec, velWorld, T_bw.inverse());
   return est.T_mid_atT.inverse() * T_bw;

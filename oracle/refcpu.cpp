@@ -1043,7 +1043,7 @@ bool lpInit(Problem& P) {
       eps = 1e-8f;
     }
     if (beFactor(P, P.lpL)) {
-      double sum = 0.0;
+      float sum = 0.0f;  // Eigen::Vector<float>::sum() (Preconditioner.h:216-218): an fp32 sum, which overflows
       for (float v : P.lpL) sum += v;
       if (std::isfinite(sum)) return true;
     }
@@ -1647,7 +1647,7 @@ struct RefSettings {
 };
 struct RefSummary {
   double initialCost, finalCost;
-  int32_t numTroubledSeqs, largestTroubledSeq, numIterations, reserved;
+  int32_t numTroubledSeqs, largestTroubledSeq, numIterations, numRescaled;
 };
 
 int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb pre, void* user,
@@ -1656,7 +1656,7 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
   double damping = s->damping;
   int it = 0, lastImpr = 0, lastTroubled = -10;
   double initialCost = 0, finalCost = 0, troubledStartDamping = damping;
-  int troubledStart = 0, nTroubled = 0, largestTroubled = 0;
+  int troubledStart = 0, nTroubled = 0, largestTroubled = 0, nRescaled = 0;
   bool dontRetry = false;
   char buf[512];
   auto acceptable = [](const int64_t* st) {
@@ -1692,6 +1692,7 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
     double applied = 1.0;
     bool okRate = acceptable(st);
     if (s->maxStepAttempts > 0 && (ratioRedToExp < s->minRelRed || !okRate)) {
+      nRescaled++;
       double backRed;
       if ((rc = ref_gradient_dot_step(h, dontRetry, &backRed))) return rc;
       double sf = backRed > 0 ? modelRed / (modelRed + backRed) : s->stepDec;
@@ -1777,6 +1778,7 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
   out->numTroubledSeqs = nTroubled;
   out->largestTroubledSeq = largestTroubled;
   out->numIterations = it;
+  out->numRescaled = nRescaled;
   return 0;
 }
 

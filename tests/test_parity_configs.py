@@ -81,6 +81,22 @@ def test_config_B_full_size_one_step_matches_oracle():
 
 
 @pytest.mark.gpu
+def test_config_C_full_size_one_step_matches_oracle():
+    """The benchmarked workload itself (config C: 10k rigs, 300k landmarks, 5.94M observations, the bench's
+    device-rebuilt rolling-shutter tables): one full LM step of the HIP engine against the oracle at the
+    box's thread count, at the tolerances of every other step-parity test (Optimizer.cpp:807-897)."""
+    p = synth.generate(synth.config("C"))
+    assert len(p.const[1]) == 10000 and len(p.const[0]) == 300000 and p.num_obs > 5_900_000
+    g, r = _pair(p, threads=oracle_threads())
+    assert g.reduced_order() == r.reduced_order() and g.total_order() == r.total_order()
+    og = one_step(g)
+    g.close()
+    orf = one_step(r)
+    print(f"config C: cost0 {orf['cost0']:.9g} cost1 {orf['cost1']:.9g} stats1 {orf['stats1']}")
+    _assert_step(og, orf)
+
+
+@pytest.mark.gpu
 def test_config_C_slice_one_step_matches_oracle():
     p = synth.generate(synth.config("C", n_kf=1000, n_lm=30000))
     g, r = _pair(p, threads=oracle_threads())

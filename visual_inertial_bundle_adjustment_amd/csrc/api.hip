@@ -25,6 +25,7 @@ namespace viba {
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st);
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_fold_red(const Dev& d, hipStream_t st);
+void launch_spec_commit(const Dev& d, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_assemble(const Dev& d, int mode, double* gOut, hipStream_t st, int part = 3);
@@ -85,7 +86,7 @@ void launch_lp_damp(float* t32, const int32_t* tileIdx, int32_t nT, const int64_
 void launch_lp_factor_level(float* t32, const int32_t* work, int nWork, const int32_t* pairs, const int32_t* diag,
                             const int32_t* cols, int nDiag, const int32_t* targets, const int32_t* tcols, int nTrsm,
                             float* linv, hipStream_t st);
-void launch_lp_nonfinite(const float* x, int64_t n, int32_t* flag, hipStream_t st);
+void launch_lp_nonfinite(const float* x, int64_t n, int32_t* flag, float* sum, hipStream_t st);
 void launch_lp_fwd_level(const float* t32, const int32_t* cols, int nCols, const int32_t* targets, const int32_t* tcols,
                          const int32_t* trows, int nTrsm, const float* linv, float* t, hipStream_t st);
 void launch_lp_bwd_level(const float* t32, const int64_t* colStart, const int32_t* colTiles, const int32_t* colRows,
@@ -260,7 +261,7 @@ struct Sched {
           *trsmColD = nullptr, *updD = nullptr, *fanPairsD = nullptr, *trsmRowD = nullptr;
   int32_t *tasksFD = nullptr, *tasksBD = nullptr, *expFD = nullptr, *expBD = nullptr, *preReadyD = nullptr;
   int64_t nF = 0, nB = 0, nPreReady = 0;  // preReady: rows whose x is known before the backward solve
-  hipGraphExec_t graph = nullptr;
+  hipGraphExec_t graph[2] = {nullptr, nullptr};  // per tile store (vb_handle_s::tileSet)
   bool built = false;
 };
 
@@ -343,6 +344,7 @@ struct vb_handle_s {
   // iterative reduced solve (vb_set_solver; pcg.hip): S x = rhsWork by PCG over the unfactored tiles
   int solverType = VB_SOLVER_DIRECT, pcgMaxIt = 40;  // Optimizer.h:43-45 defaults
   int faultNegModelRedIt = -1;  // vb_debug_negate_model_reduction (test fault injection)
+  int faultFailIt = -1;         // vb_debug_fail_iteration (test fault injection)
   double pcgTol = 1e-10;
   int32_t pcgIters = 0;
   double pcgRelRes = 0.0;
@@ -352,8 +354,23 @@ struct vb_handle_s {
   double *jacL = nullptr, *tilesGS = nullptr;  // Jacobi block factors / Gauss-Seidel pseudo-factor
   // LowerPrecSolvePrecond (lowprec.hip): fp32 factor tiles, fp32 diagonal-tile inverses, fp32 vector
   float *lpTiles = nullptr, *lpLinv = nullptr, *lpT = nullptr;
-  // the tile factorization's launches, captured into a HIP graph per schedule (VIBA_NO_GRAPHS=1: eager)
+  // the tile factorization's launches, captured into a HIP graph per schedule and tile store
+  // (VIBA_NO_GRAPHS=1: eager)
   bool useGraphs = true;
+  // vb_optimize's speculative linearization (specEnqueue): the next iteration's rolling-shutter rebuild
+  // and linearization are queued behind this iteration's cost pass, before the host reads its scalars,
+  // into a second tile store, ResultCache, gradient and rolling-shutter table set (and reduction /
+  // error slots red[48, 64), err[4, 6)); they are swapped in when the step is accepted at full size
+  // (specCommit), and left unused otherwise (the host then takes the step-rescaling path, which needs
+  // this iteration's factor, cache and tables as they are)
+  double *tilesAlt = nullptr, *cacheAlt = nullptr, *gRedAlt = nullptr;
+  double *rsSAlt = nullptr, *rsIAlt = nullptr, *rsGAlt = nullptr;
+  int32_t* rsNAlt = nullptr;
+  int tileSet = 0;            // which of the two tile stores d.tiles is (selects the factorization graph)
+  hipStream_t stR = nullptr;  // the scalar readback, beside the speculative work
+  hipEvent_t evCost = nullptr, evS[2][4] = {};
+  double* hostRed = nullptr;  // pinned readback buffer: red[0, 17), then err[0, 2) as int32
+  size_t profAtCost = 0;      // profiled event pairs recorded before evCost
   // state
   bool linearized = false, factored = false;
   vb_phase_times times{};
@@ -1583,7 +1600,8 @@ int doFinalize(vb_handle h) {
         upload(&d.rsN, cnt))
       return VB_E_HIP;
   }
-  if (alloc0(&d.red, 64) || alloc0(&d.redS, 64 * 8) || alloc0(&d.err, 4)) return VB_E_HIP;
+  if (alloc0(&d.red, 64) || alloc0(&d.redS, 64 * 8) || alloc0(&d.err, 8)) return VB_E_HIP;
+  d.cacheW = d.cache;
   h->finalized = true;
   return 0;
 }
@@ -1603,8 +1621,7 @@ void joinSmall(vb_handle h) {
 }
 
 // visual kernels over this shard's observations (+ the root's constant-point observations)
-void visualLinShard(vb_handle h, int updateCache, int dontRetry) {
-  const Dev& d = h->d;
+void visualLinShard(vb_handle h, const Dev& d, int updateCache, int dontRetry) {
   profBegin(h, KF_VISUAL_LIN);
   launch_visual_lin(d, updateCache, dontRetry, d.obB, d.obE, h->st);
   launch_visual_lin(d, updateCache, dontRetry, d.fB, d.fE, h->st);
@@ -1675,9 +1692,10 @@ int factorReduced(vb_handle h, int which = 0) {
     factorSeq(h, S);
     return 0;
   }
-  if (!S.graph)
-    if (int rc = captureGraph(h, S, &S.graph)) return rc;
-  HIPCHK(hipGraphLaunch(S.graph, h->st));
+  hipGraphExec_t& g = S.graph[h->tileSet];
+  if (!g)
+    if (int rc = captureGraph(h, S, &g)) return rc;
+  HIPCHK(hipGraphLaunch(g, h->st));
   return 0;
 }
 
@@ -1743,9 +1761,10 @@ int pcgPrepare(vb_handle h) {
   return 0;
 }
 
-// LowerPrecSolvePrecond::init (Preconditioner.h:180-213): S cast to fp32 and factored by the direct
-// solver's tile schedule in fp32 (lowprec.hip); while the factor holds a non-finite value (the
-// reference sums it), redo it from S with the diagonal raised: epsilon 0, then 1e-8, then x3 per attempt
+// LowerPrecSolvePrecond::init (Preconditioner.h:180-218): S cast to fp32 and factored by the direct
+// solver's tile schedule in fp32 (lowprec.hip); while the fp32 sum of the factor is not finite (a
+// non-finite entry, or finite entries whose sum overflows), redo it from S with the diagonal raised:
+// epsilon 0, then 1e-8, then x3 per attempt
 int lpInit(vb_handle h) {
   Dev& d = h->d;
   const Sched& S = h->sch[0];
@@ -1765,12 +1784,15 @@ int lpInit(vb_handle h) {
                              S.potrfColD + p0, (int)(S.lvP[L + 1] - p0), S.trsmTargetD + t0, S.trsmColD + t0,
                              (int)(S.lvT[L + 1] - t0), h->lpLinv, h->st);
     }
-    HIPCHK(hipMemsetAsync(d.err + 3, 0, sizeof(int32_t), h->st));  // err[3]: a non-finite factor entry
-    launch_lp_nonfinite(h->lpTiles, nEl, d.err + 3, h->st);
-    int32_t bad = 0;
-    HIPCHK(hipMemcpyAsync(&bad, d.err + 3, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+    // err[3]: a non-finite factor entry; err[2] (as fp32): the factor's sum (Preconditioner.h:216-218)
+    HIPCHK(hipMemsetAsync(d.err + 2, 0, 2 * sizeof(int32_t), h->st));
+    launch_lp_nonfinite(h->lpTiles, nEl, d.err + 3, reinterpret_cast<float*>(d.err + 2), h->st);
+    int32_t w[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(w, d.err + 2, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
     HIPCHK(hipStreamSynchronize(h->st));
-    if (!bad) return 0;
+    float sum;
+    std::memcpy(&sum, &w[0], sizeof(float));
+    if (!w[1] && std::isfinite(sum)) return 0;
   }
   return fail(VB_E_NUMERIC, "LowerPrecSolvePrecond: the fp32 factor keeps breaking down");
 }
@@ -1964,7 +1986,8 @@ int vb_destroy(vb_handle h) {
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
                   h->rhsWork, h->linv, h->lscr, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
                   h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->lpTiles, h->lpLinv, h->lpT, h->clearTilesD,
-                  (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise};
+                  (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise,
+                  h->tilesAlt, h->cacheAlt, h->gRedAlt, h->rsSAlt, h->rsIAlt, h->rsGAlt, h->rsNAlt};
   for (void* p : ptrs)
     if (p) hipFree(p);
   for (int k = 0; k < 9; k++) {
@@ -1990,12 +2013,19 @@ int vb_destroy(vb_handle h) {
   if (h->evZJoin) hipEventDestroy(h->evZJoin);
   if (h->stZ) hipStreamSynchronize(h->stZ), hipStreamDestroy(h->stZ);
   for (auto& e : h->profEv) hipEventDestroy(e);
+  if (h->evCost) hipEventDestroy(h->evCost);
+  for (auto& row : h->evS)
+    for (hipEvent_t e : row)
+      if (e) hipEventDestroy(e);
+  if (h->stR) hipStreamSynchronize(h->stR), hipStreamDestroy(h->stR);
+  if (h->hostRed) hipHostFree(h->hostRed);
   for (Sched& S : h->sch) {
     void* sp[] = {S.ptfD, S.ptfDiagD, S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
                   S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD};
     for (void* p : sp)
       if (p) hipFree(p);
-    if (S.graph) hipGraphExecDestroy(S.graph);
+    for (hipGraphExec_t g : S.graph)
+      if (g) hipGraphExecDestroy(g);
   }
   hipStreamDestroy(h->st);
   delete h;
@@ -2246,12 +2276,11 @@ int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_
   return 0;
 }
 
-// vb_linearize's device work, no host read (cost in red[0], errors in err)
-int linearizeEnqueue(vb_handle h, int update_cache, int dont_retry_failed) {
-  Dev& d = h->d;
-  HIPCHK(hipEventRecord(h->ev[0], h->st));
-  HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
-  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+// vb_linearize's device work over the buffers of `d` (h->d, or the speculative copy of vb_optimize:
+// another tile store, cache write buffer, reduction and error slots), no host read, no reset of the
+// reduction / error slots (the caller's); events evA / evB bracket it
+int linearizeBody(vb_handle h, const Dev& d, int update_cache, int dont_retry_failed, hipEvent_t evA, hipEvent_t evB) {
+  HIPCHK(hipEventRecord(evA, h->st));
   // the reduced system is cleared and the small factors assembled on the side stream while the visual
   // factors linearize on the main stream (they write only their records and the cost)
   const bool side = smallHere(h, 0);
@@ -2284,11 +2313,18 @@ int linearizeEnqueue(vb_handle h, int update_cache, int dont_retry_failed) {
     HIPCHK(hipEventRecord(h->evJoin, h->st2));
     HIPCHK(hipEventRecord(h->evZJoin, h->stZ));
   }
-  visualLinShard(h, update_cache, dont_retry_failed);
+  visualLinShard(h, d, update_cache, dont_retry_failed);
   joinSmall(h);
   if (side) HIPCHK(hipStreamWaitEvent(h->st, h->evZJoin, 0));
-  HIPCHK(hipEventRecord(h->ev[1], h->st));
+  HIPCHK(hipEventRecord(evB, h->st));
   return 0;
+}
+// cost in red[0], errors in err
+int linearizeEnqueue(vb_handle h, int update_cache, int dont_retry_failed) {
+  Dev& d = h->d;
+  HIPCHK(hipMemsetAsync(d.red, 0, 64 * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  return linearizeBody(h, d, update_cache, dont_retry_failed, h->ev[0], h->ev[1]);
 }
 
 int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* cost) {
@@ -2369,7 +2405,7 @@ int vb_gradient_dot_step(vb_handle h, int dont_retry_failed, double* back_red) {
   HIPCHK(hipMemsetAsync(d.gRedNew, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   HIPCHK(hipMemsetAsync(d.red, 0, 1 * sizeof(double), h->st));
   forkSmall(h, 1, d.gRedNew);
-  visualLinShard(h, 0, dont_retry_failed);
+  visualLinShard(h, h->d, 0, dont_retry_failed);
   joinSmall(h);
   launch_landmark(d, 0.0, 1, d.lmB, d.lmE, h->st);
   launch_reduced_grad(d, 0, h->st);
@@ -2605,6 +2641,11 @@ int vb_debug_negate_model_reduction(vb_handle h, int iteration) {
   h->faultNegModelRedIt = iteration;
   return 0;
 }
+int vb_debug_fail_iteration(vb_handle h, int iteration) {
+  if (!h) return fail(VB_E_ARG, "null handle");
+  h->faultFailIt = iteration;
+  return 0;
+}
 // slot of tile (I, J) of the reduced tile store (vb_reduced_buffers), -1 when it is not stored
 int vb_debug_tile_slot(vb_handle h, int32_t I, int32_t J, int64_t* slot) {
   if (!h || !h->finalized || !slot) return fail(VB_E_STATE, "vb_debug_tile_slot before vb_finalize");
@@ -2804,7 +2845,80 @@ int vb_reduced_buffers(vb_handle h, double** matrix, int64_t* matrix_len, double
   return 0;
 }
 
-// Optimizer::optimize (Optimizer.cpp:768-1106), direct solver
+// ---- vb_optimize's speculative linearization of the next iteration (vb_handle_s::tilesAlt ..)
+int specPrepare(vb_handle h) {
+  if (h->tilesAlt) return 0;
+  Dev& d = h->d;
+  if (alloc0(&h->tilesAlt, (size_t)d.nTiles * TS * TS) || alloc0(&h->cacheAlt, d.nObs) ||
+      alloc0(&h->gRedAlt, (size_t)d.nT * TS))
+    return VB_E_HIP;
+  if (h->rsDevice) {
+    const int64_t ns = h->rsOff[h->nRS];
+    if (alloc0(&h->rsSAlt, ns * 11) || alloc0(&h->rsIAlt, (ns - h->nRS) * 9) || alloc0(&h->rsGAlt, (size_t)h->nRS * 3) ||
+        alloc0(&h->rsNAlt, h->nRS))
+      return VB_E_HIP;
+  }
+  for (auto& row : h->evS)
+    for (hipEvent_t& e : row) HIPCHK(hipEventCreate(&e));
+  HIPCHK(hipEventCreateWithFlags(&h->evCost, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&h->stR, hipStreamNonBlocking));
+  HIPCHK(hipHostMalloc((void**)&h->hostRed, 32 * sizeof(double), hipHostMallocDefault));
+  return 0;
+}
+// the buffers the speculative work writes instead of h->d's
+Dev specDev(vb_handle h) {
+  Dev ds = h->d;
+  ds.tiles = h->tilesAlt, ds.cacheW = h->cacheAlt, ds.gRed = h->gRedAlt;
+  ds.red = h->d.red + 48, ds.err = h->d.err + 4;
+  if (h->rsDevice) ds.rsS = h->rsSAlt, ds.rsI = h->rsIAlt, ds.rsG = h->rsGAlt, ds.rsN = h->rsNAlt;
+  return ds;
+}
+// ark_vi_ba's preStepCallback (the rolling-shutter rebuild at the accepted variables) and the
+// linearization of the next iteration, queued behind this iteration's cost pass; event set p
+int specEnqueue(vb_handle h, int dontRetry, int p) {
+  const Dev ds = specDev(h);
+  HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
+  HIPCHK(hipEventRecord(h->evS[p][0], h->st));
+  if (h->rsDevice) launch_rs_build(ds, h->st);
+  HIPCHK(hipEventRecord(h->evS[p][1], h->st));
+  return linearizeBody(h, ds, 1, dontRetry, h->evS[p][2], h->evS[p][3]);
+}
+// the step was accepted at full size: the speculative buffers become the handle's
+void specCommit(vb_handle h) {
+  Dev& d = h->d;
+  std::swap(d.tiles, h->tilesAlt);
+  std::swap(d.cache, h->cacheAlt);
+  d.cacheW = d.cache;
+  std::swap(d.gRed, h->gRedAlt);
+  if (h->rsDevice) {
+    std::swap(d.rsS, h->rsSAlt), std::swap(d.rsI, h->rsIAlt);
+    std::swap(d.rsG, h->rsGAlt), std::swap(d.rsN, h->rsNAlt);
+  }
+  h->tileSet ^= 1;
+  launch_spec_commit(d, h->st);
+}
+// the iteration's scalars red[0, n) and error words, read on the readback stream once the cost pass
+// (evCost) is done, while whatever was queued behind it runs
+int readIterScalars(vb_handle h, double* out, int n) {
+  HIPCHK(hipStreamWaitEvent(h->stR, h->evCost, 0));
+  HIPCHK(hipMemcpyAsync(h->hostRed, h->d.red, n * sizeof(double), hipMemcpyDeviceToHost, h->stR));
+  HIPCHK(hipMemcpyAsync(h->hostRed + 24, h->d.err, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, h->stR));
+  HIPCHK(hipStreamSynchronize(h->stR));
+  std::copy(h->hostRed, h->hostRed + n, out);
+  h->profDone = h->profAtCost;
+  int32_t ee[2];
+  std::memcpy(ee, h->hostRed + 24, sizeof(ee));
+  return errFromWords(h, ee);
+}
+
+// Optimizer::optimize (Optimizer.cpp:768-1106).  Per iteration the linearization, damp + eliminate +
+// factor + solve, backup, box-plus and cost pass are queued back to back and the host reads their
+// scalars once.  Unless a prestep callback or --recompute-preint needs the host between iterations, the
+// next iteration's rolling-shutter rebuild and linearization are queued speculatively behind the cost
+// pass (into second buffers, specEnqueue), so the device works while the host decides; they are used
+// when the step is accepted at full size, the common case.  An error after the backup restores the
+// variables of the iteration's linearization point before returning.
 int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb pre, void* user, vb_summary* out) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "vb_optimize before vb_finalize");
   vb_settings s;
@@ -2813,39 +2927,78 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
   double damping = s.damping;
   int it = 0, lastImpr = 0, lastTroubled = -10;
   double initialCost = 0, finalCost = 0, troubledStartDamping = damping;
-  int troubledStart = 0, nTroubled = 0, largestTroubled = 0;
+  int troubledStart = 0, nTroubled = 0, largestTroubled = 0, nRescaled = 0;
   int dontRetry = 0;
   auto acceptable = [](const vb_cost_stats& st) {
     const double rate = st.num_invalid / (st.num_total + 1.0);
     return rate < 0.03 && (st.num_invalid < st.num_prev_invalid * 2.0 + 50);
   };
+  const bool preint = h->recomputePreint && h->pi.n > 0;
+  const bool speculate = !pre && !preint && !h->sharded && h->partWorld <= 1;
+  if (speculate)
+    if (int rc = specPrepare(h)) return rc;
+  bool specQueued = false;  // the current iteration's rebuild + linearization were queued speculatively
+  int specSet = 0;
   int rc;
   char buf[512];
+  // an error after this iteration's backup: the variables go back to the linearization point
+  bool backedUp = false;
+  auto bail = [&](int code) {
+    if (backedUp && vb_restore(h) == 0) (void)hipStreamSynchronize(h->st);
+    (void)hipStreamSynchronize(h->st);
+    return code;
+  };
   while (true) {
     auto t0 = std::chrono::steady_clock::now();
-    // ark_vi_ba's preStepCallback (main_AriaKit_ViBa.cpp:95-101): updateRollingShutterData
-    // and, under --recompute-preint, the preintegrations from the IMU streams (InertialFactors.cpp:19-70)
-    const bool preint = h->recomputePreint && h->pi.n > 0;
-    if ((h->rsDevice || preint) && (rc = rsUpdateAsync(h, h->rsDevice, preint))) return rc;
-    if (pre) pre(it, user);
-    // linearize, damp + eliminate + factor + solve, backup, box-plus and the cost pass queued back to back;
-    // the host reads their scalars (costs, CostStats, model reduction, step ratios) and errors once,
-    // after the cost pass: none of them changes what the queued work does
+    backedUp = false;
+    if (specQueued) {
+      specCommit(h);
+    } else {
+      // ark_vi_ba's preStepCallback (main_AriaKit_ViBa.cpp:95-101): updateRollingShutterData
+      // and, under --recompute-preint, the preintegrations from the IMU streams (InertialFactors.cpp:19-70)
+      if ((h->rsDevice || preint) && (rc = rsUpdateAsync(h, h->rsDevice, preint))) return bail(rc);
+      if (pre) pre(it, user);
+      if ((rc = linearizeEnqueue(h, 1, dontRetry))) return bail(rc);
+    }
+    // damp + eliminate + factor + solve, backup, box-plus and the cost pass queued back to back; the host
+    // reads their scalars (costs, CostStats, model reduction, step ratios) and errors once, after the cost
+    // pass: none of them changes what the queued work does
     double prevCost, modelRed, ratios[3], newCost;
     vb_cost_stats st;
-    if ((rc = linearizeEnqueue(h, 1, dontRetry)) || (rc = dampFactorSolveEnqueue(h, damping, false)) ||
-        (rc = vb_backup(h)) || (rc = applyStepEnqueue(h, 0, 10, 11)) || (rc = costEnqueue(h, 1, false)))
-      return rc;
+    if ((rc = dampFactorSolveEnqueue(h, damping, false))) return bail(rc);
+    if ((rc = vb_backup(h))) return bail(rc);
+    backedUp = true;
+    if ((rc = applyStepEnqueue(h, 0, 10, 11)) || (rc = costEnqueue(h, 1, false))) return bail(rc);
+    const bool wasSpec = specQueued;
+    const int wasSet = specSet;
+    specQueued = false;
+    if (speculate) {
+      HIPCHK(hipEventRecord(h->evCost, h->st));
+      h->profAtCost = h->profUsed;
+      // the next iteration's rebuild + linearization, assuming this step is accepted at full size (not
+      // after the last iteration: its work would only be discarded)
+      if (it + 1 < s.max_num_iterations) {
+        specSet ^= 1;
+        if ((rc = specEnqueue(h, dontRetry, specSet))) return bail(rc);
+        specQueued = true;
+      }
+    }
     profHarvestPrefix(h, h->profDone);  // the previous iteration's event times, read while this one runs
     {
       double r[17];
-      if ((rc = readRedErr(h, r, 17))) return rc;
+      if ((rc = speculate ? readIterScalars(h, r, 17) : readRedErr(h, r, 17))) return bail(rc);
+      if (it == h->faultFailIt) return bail(fail(VB_E_NUMERIC, "reduced system Cholesky breakdown (injected)"));
       prevCost = r[0], modelRed = 0.5 * r[16];
       const double n = (double)std::max<int64_t>(1, h->nParams);
       ratios[0] = r[8], ratios[1] = std::sqrt(r[9] / n), ratios[2] = r[10] / n;
       costStats(h, r + 1, &newCost, &st);
-      h->times.linearize_ms = elapsed(h->ev[0], h->ev[1]);
-      if (h->rsTimed) h->times.rs_update_ms = elapsed(h->ev[8], h->ev[9]), h->rsTimed = false;
+      if (wasSpec) {
+        h->times.linearize_ms = elapsed(h->evS[wasSet][2], h->evS[wasSet][3]);
+        if (h->rsDevice) h->times.rs_update_ms = elapsed(h->evS[wasSet][0], h->evS[wasSet][1]);
+      } else {
+        h->times.linearize_ms = elapsed(h->ev[0], h->ev[1]);
+        if (h->rsTimed) h->times.rs_update_ms = elapsed(h->ev[8], h->ev[9]), h->rsTimed = false;
+      }
       h->times.schur_ms = elapsed(h->ev[2], h->ev[3]);
       h->times.factor_ms = elapsed(h->ev[3], h->ev[4]);
       h->times.solve_ms = elapsed(h->ev[4], h->ev[5]);
@@ -2870,18 +3023,20 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     double ratioRedToExp = costRed / modelRed;
     double applied = 1.0;
     bool okRate = acceptable(st);
+    bool rescaled = false;
     if (s.max_step_factor_attempts > 0 && (ratioRedToExp < s.min_relative_cost_reduction || !okRate)) {
+      rescaled = true, nRescaled++;
       double backRed;
-      if ((rc = vb_gradient_dot_step(h, dontRetry, &backRed))) return rc;
+      if ((rc = vb_gradient_dot_step(h, dontRetry, &backRed))) return bail(rc);
       double sf = backRed > 0 ? modelRed / (modelRed + backRed) : s.step_factor_decrease;
       for (int i = 0; i < s.max_step_factor_attempts; i++) {
         applied *= sf;
-        if ((rc = vb_scale_step(h, sf)) || (rc = vb_restore(h))) return rc;
+        if ((rc = vb_scale_step(h, sf)) || (rc = vb_restore(h))) return bail(rc);
         double rr[3];
-        if ((rc = vb_apply_step(h, 0, rr))) return rc;
+        if ((rc = vb_apply_step(h, 0, rr))) return bail(rc);
         vb_cost_stats stF;
         double costF;
-        if ((rc = vb_cost(h, 1, &costF, &stF))) return rc;
+        if ((rc = vb_cost(h, 1, &costF, &stF))) return bail(rc);
         const double redF = prevCost - newCost;  // Optimizer.cpp:935 (reference uses the full-step cost)
         const double rF = redF / (modelRed * applied);
         if (rF >= s.min_relative_cost_reduction && acceptable(stF)) {
@@ -2890,13 +3045,13 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
         }
         if (s.try_sub_step) {
           double br;
-          if ((rc = vb_gradient_dot_step(h, dontRetry, &br))) return rc;
-          if ((rc = vb_solve_with_new_gradient(h))) return rc;
+          if ((rc = vb_gradient_dot_step(h, dontRetry, &br))) return bail(rc);
+          if ((rc = vb_solve_with_new_gradient(h))) return bail(rc);
           double r2[3];
-          if ((rc = vb_apply_step(h, 1, r2))) return rc;
+          if ((rc = vb_apply_step(h, 1, r2))) return bail(rc);
           vb_cost_stats stS;
           double costS;
-          if ((rc = vb_cost(h, 1, &costS, &stS))) return rc;
+          if ((rc = vb_cost(h, 1, &costS, &stS))) return bail(rc);
           const double redS = prevCost - costS;
           const double rS = redS / (modelRed * applied);
           if (rS >= s.min_relative_cost_reduction && acceptable(stS)) {
@@ -2912,10 +3067,13 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
                       : costRed < s.absolute_cost_tolerance          ? "absolute cost"
                       : ratios[1] < s.variables_tolerance            ? "variable"
                                                                      : nullptr;
-    if (newCost > prevCost || !okRate) {
+    const bool rejected = newCost > prevCost || !okRate;
+    // the speculative linearization assumed the full step stays applied
+    if (rejected || rescaled) specQueued = false;
+    if (rejected) {
       if (lastTroubled != it - 1) troubledStartDamping = damping, troubledStart = it;
       damping *= s.damping_adjust_on_fail;
-      if ((rc = vb_restore(h))) return rc;
+      if ((rc = vb_restore(h))) return bail(rc);
       if (damping > s.damping_max) break;
       lastTroubled = it;
     } else {
@@ -2930,7 +3088,6 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
         damping *= s.damping_adjust_on_average_step;
       finalCost = newCost;
     }
-    HIPCHK(hipStreamSynchronize(h->st));
     h->times.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     it++;
     if (log && s.verbose) {
@@ -2944,10 +3101,13 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     if (it >= lastImpr + s.stop_if_no_improvement_for && it >= lastTroubled + s.distance_from_troubled_iteration) break;
     if (it >= s.max_num_iterations) break;
   }
+  // (a speculative linearization left queued by a convergence stop is never committed; its buffers are
+  // the spare ones)
+  HIPCHK(hipStreamSynchronize(h->st));
   if (out) {
     out->initial_cost = initialCost, out->final_cost = finalCost;
     out->num_troubled_seqs = nTroubled, out->largest_troubled_seq = largestTroubled, out->num_iterations = it;
-    out->reserved = 0;
+    out->num_rescaled = nRescaled;
   }
   return 0;
 }

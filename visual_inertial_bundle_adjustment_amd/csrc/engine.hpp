@@ -152,6 +152,8 @@ struct Dev {
   int32_t* obCol = nullptr;  // 4 per obs (column offset in the landmark's Y panel, -1)
   double* obC = nullptr;     // 6 per obs
   double* cache = nullptr;   // ResultCache per obs
+  double* cacheW = nullptr;  // where an updating linearization writes it: cache, or (vb_optimize's speculative
+                             // linearization of the next iteration) a second buffer swapped in on commit
   rec_t* Jt = nullptr;  // whitened visual Jacobian records (fp32 in the VIBA_MIXED build)
   // landmarks
   int64_t nPts = 0;

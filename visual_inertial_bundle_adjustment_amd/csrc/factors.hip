@@ -233,6 +233,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
     const double c0 = d.cache[o];
     if (dontRetry && c0 < 0.0) {
       ok = false;
+      if (updateCache) d.cacheW[o] = c0;  // (carried into the write buffer of a speculative linearization)
     } else {
       const double* obsC = d.obCP + (ob + lane) * 6;
       const double* Xp = d.var[0] + (int64_t)pa.y * 3;
@@ -251,7 +252,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
                            (pb.w & 2) != 0, v, &oor);
         if (oor) atomicOr(d.err, 1);
       }
-      if (!ok && (updateCache || dontRetry)) d.cache[o] = -1.0;
+      if (!ok && (updateCache || dontRetry)) (updateCache ? d.cacheW : d.cache)[o] = -1.0;
     }
     if (ok) {
       const double s = v.e[0] * v.e[0] + v.e[1] * v.e[1];
@@ -259,7 +260,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
       huber_jet2(d.reproj.a, d.reproj.b, d.reproj.k2, d.reproj.h, s, rho, drho);
       w = sqrt(drho);
       acc[0] = 0.5 * rho;
-      if (updateCache) d.cache[o] = 0.5 * rho;
+      if (updateCache) d.cacheW[o] = 0.5 * rho;
     }
   }
   // region B (intrinsics already in place from the evaluation): scale by w, velocity, copy out
@@ -1143,6 +1144,14 @@ __global__ void fold_red_kernel(Dev d) {
   if (s != 0.0) atomicAdd(d.red + k, s);
 }
 void launch_fold_red(const Dev& d, hipStream_t st) { hipLaunchKernelGGL(fold_red_kernel, dim3(1), dim3(64), 0, st, d); }
+// vb_optimize's speculative linearization accepted: its cost (red[48]) and error words (err[4, 6)) become
+// the iteration's (red[0], err[0, 2))
+__global__ void spec_commit_kernel(Dev d) {
+  const int k = threadIdx.x;
+  if (k == 0) d.red[0] = d.red[48];
+  if (k < 2) d.err[k] = d.err[4 + k];
+}
+void launch_spec_commit(const Dev& d, hipStream_t st) { hipLaunchKernelGGL(spec_commit_kernel, dim3(1), dim3(64), 0, st, d); }
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
   const int64_t n = hi - lo;

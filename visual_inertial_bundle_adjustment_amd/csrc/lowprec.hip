@@ -117,11 +117,21 @@ __global__ void __launch_bounds__(256) lp_trsm_kernel(float* t32, const int32_t*
   tile_store<float>(T, 1.0f, wave, lane, acc);
 }
 
-__global__ void lp_nonfinite_kernel(const float* x, int64_t n, int32_t* flag) {
+// the retry test of LowerPrecSolvePrecond::init (Preconditioner.h:216-218): !isfinite(sum of the fp32
+// factor).  The sum is formed in fp32 as the reference's Eigen sum is (per-thread, then wave, then one
+// fp32 atomic per wave: a different order than a sequential sum, so only totals within rounding of
+// FLT_MAX can decide differently); a non-finite entry makes it non-finite as well, flagged directly
+__global__ void lp_nonfinite_kernel(const float* x, int64_t n, int32_t* flag, float* sum) {
   bool bad = false;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+  float s = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     bad |= !isfinite(x[i]);
+    s += x[i];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
   if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+  if ((threadIdx.x & 63) == 0 && s != 0.0f) atomicAdd(sum, s);
 }
 
 // forward solve, one level: t_J = L_JJ^-1 t_J for the level's columns (one wave each)
@@ -192,8 +202,8 @@ void launch_lp_factor_level(float* t32, const int32_t* work, int nWork, const in
   if (nDiag) hipLaunchKernelGGL(lp_potrf_kernel, dim3(nDiag), dim3(256), 0, st, t32, diag, cols, linv);
   if (nTrsm) hipLaunchKernelGGL(lp_trsm_kernel, dim3(nTrsm), dim3(256), 0, st, t32, targets, tcols, linv);
 }
-void launch_lp_nonfinite(const float* x, int64_t n, int32_t* flag, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(lp_nonfinite_kernel, dim3(2048), dim3(256), 0, st, x, n, flag);
+void launch_lp_nonfinite(const float* x, int64_t n, int32_t* flag, float* sum, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(lp_nonfinite_kernel, dim3(2048), dim3(256), 0, st, x, n, flag, sum);
 }
 void launch_lp_fwd_level(const float* t32, const int32_t* cols, int nCols, const int32_t* targets, const int32_t* tcols,
                          const int32_t* trows, int nTrsm, const float* linv, float* t, hipStream_t st) {

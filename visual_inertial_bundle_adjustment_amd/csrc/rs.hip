@@ -174,7 +174,9 @@ __global__ void __launch_bounds__(256) rs_row_pose_kernel(Dev d, int64_t n, cons
     if (t < 0) {
       atomicOr(d.err, 2);
     } else {
-      const double tpf = obsRow[i] / cam[3] - 0.5;
+      // T_bodyImu_world_atImageRow(..., float imageRow) (VisualFactor.cpp:306-311): imageRow / imageHeight()
+      // is float / int, a float division
+      const double tpf = (double)((float)obsRow[i] / (float)(int)cam[3]) - 0.5;
       const double ro = cam[4] != 0.0 ? cam[5] : 0.0;
       const double dt = ro * tpf - cam[6];
       const int64_t s0 = d.rsOff[t];

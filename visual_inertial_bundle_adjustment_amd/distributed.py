@@ -179,6 +179,7 @@ class ShardedOptimizer:
             lists = comm.all_gather_obj(engine.shard_tiles().tolist())
             self.tile_lists = [comm.torch.tensor(t, dtype=comm.torch.int32, device=comm.device) for t in lists]
         self.sync = getattr(engine, "synchronize", lambda: None)
+        self.phases = _PhaseClock(self.ext)
 
     @staticmethod
     def _engine_stream(engine, comm):
@@ -205,7 +206,9 @@ class ShardedOptimizer:
     def damp_factor_solve(self, lam):
         e, c = self.e, self.c
         self.n_factor += 1
+        self.phases.mark("schur_ms")
         e.assemble_reduced(lam)
+        self.phases.mark("factor_ms")
         S, b = self._buffers()
         if self.tile_lists is not None:
             self.sync_torch()
@@ -216,6 +219,7 @@ class ShardedOptimizer:
         self.sync_torch()
         if c.rank == 0:
             e.factor_solve_reduced()
+        self.phases.mark("solve_ms")
         S, b = self._buffers()
         c.broadcast_from_root(b)
         self.sync_torch()
@@ -266,6 +270,7 @@ class ShardedOptimizer:
         it, last_impr, last_troubled = 0, 0, -10
         initial_cost = final_cost = 0.0
         troubled_start_damping, troubled_start, n_troubled, largest_troubled = damping, 0, 0, 0
+        n_rescaled = 0
         dont_retry = False
 
         def acceptable(st):
@@ -273,8 +278,10 @@ class ShardedOptimizer:
             return rate < 0.03 and st[1] < st[2] * 2.0 + 50
 
         while True:
+            self.phases.mark("rs_update_ms")
             if getattr(e, "rs_device", False):  # ark_vi_ba's preStepCallback (vb_optimize does the same)
                 e.update_rs_tables()
+            self.phases.mark("linearize_ms")
             prev_cost = self.linearize(dont_retry)
             final_cost = prev_cost
             if it == 0:
@@ -283,14 +290,18 @@ class ShardedOptimizer:
             if model_red < 0:  # Optimizer.cpp:835-854 (see vb_optimize)
                 damping *= s.damping_adjust_on_fail
             e.backup()
+            self.phases.mark("step_ms")
             ratios = self.apply_step(0)
+            self.phases.mark("cost_ms")
             new_cost, st = self.cost(True)
+            self.phases.close_iteration()
             cost_red = prev_cost - new_cost
             ratio_red_to_cost = cost_red / new_cost
             ratio_red_to_exp = cost_red / model_red
             applied = 1.0
             ok_rate = acceptable(st)
             if s.max_step_factor_attempts > 0 and (ratio_red_to_exp < s.min_relative_cost_reduction or not ok_rate):
+                n_rescaled += 1
                 back_red = self.gradient_dot_step(dont_retry)
                 sf = model_red / (model_red + back_red) if back_red > 0 else s.step_factor_decrease
                 for _ in range(s.max_step_factor_attempts):
@@ -345,7 +356,43 @@ class ShardedOptimizer:
         out = Summary()
         out.initial_cost, out.final_cost = initial_cost, final_cost
         out.num_troubled_seqs, out.largest_troubled_seq, out.num_iterations = n_troubled, largest_troubled, it
+        out.num_rescaled = n_rescaled
         return out
+
+
+class _PhaseClock:
+    """Per-phase device time of the last LM iteration (vb_phase_times semantics), from torch.cuda events
+    recorded on the engine's stream at the phase boundaries: no extra synchronisation; the times are read
+    once the iteration's cost has been read back.  A phase's time includes its collectives and any
+    stream idle while the host stages them (gloo).  Host engines: nothing is recorded."""
+
+    NAMES = ("rs_update_ms", "linearize_ms", "schur_ms", "factor_ms", "solve_ms", "step_ms", "cost_ms")
+
+    def __init__(self, ext):
+        self.ext = ext
+        self.ms = {k: 0.0 for k in self.NAMES}
+        self.marks = []
+
+    def mark(self, name):
+        """The phase `name` starts here (None: the iteration ends)."""
+        if self.ext is None:
+            return
+        import torch
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(self.ext)
+        self.marks.append((name, ev))
+
+    def close_iteration(self):
+        if self.ext is None or not self.marks:
+            return
+        self.mark(None)
+        self.marks[-1][1].synchronize()
+        ms = {k: 0.0 for k in self.NAMES}
+        for (name, a), (_, b) in zip(self.marks, self.marks[1:]):
+            if name is not None:
+                ms[name] += a.elapsed_time(b)
+        ms["total_ms"] = self.marks[0][1].elapsed_time(self.marks[-1][1])
+        self.ms, self.marks = ms, []
 
 
 class PartitionedOptimizer(ShardedOptimizer):
@@ -367,6 +414,7 @@ class PartitionedOptimizer(ShardedOptimizer):
         self.ext = self._engine_stream(engine, comm)
         self.n_factor = 0
         self.tile_lists = None
+        self.phases = _PhaseClock(self.ext)
 
     def _exchange(self, what, reduce):
         e, c = self.e, self.c
@@ -403,11 +451,14 @@ class PartitionedOptimizer(ShardedOptimizer):
     def damp_factor_solve(self, lam):
         e, c = self.e, self.c
         self.n_factor += 1
+        self.phases.mark("schur_ms")
         e.assemble_reduced(lam)
+        self.phases.mark("factor_ms")
         e.factor_part(0)
         self._exchange(0, True)
         if c.rank == 0:
             e.factor_part(1)
+        self.phases.mark("solve_ms")
         return c.sum(self._solve(0))[0]
 
     def solve_with_new_gradient(self):
@@ -481,6 +532,10 @@ def run_sharded(args, rank: int, world: int, local: int):
     synth.load_into(e, p, rs_device=getattr(args, "rs_tables", "device") == "device")
     st = e.problem_stats()
     comm = ShardComm(rank, world, dev)
+    # the collectives' transport as it actually ran: RCCL (nccl backend) over xGMI, or gloo through host
+    # memory (the one-GPU test box, VIBA_DIST_BACKEND=gloo)
+    wire = "RCCL" if comm.nccl else "gloo (host-staged)"
+    same_device = os.environ.get("VIBA_DIST_SAME_DEVICE") == "1"
     if mode == "partition":
         info = comm.all_gather_obj(e.part_info())
         log(f"[bench] {world} ranks, config {args.config}: {p.summary()}; partitioned factorization: subtree "
@@ -488,12 +543,12 @@ def run_sharded(args, rank: int, world: int, local: int):
             f"local {[i[2] for i in info]} root {info[0][3]}")
         opt = PartitionedOptimizer(e, comm)
         parallelism = (f"nested-dissection subtree x{world} (landmarks, factor, solves per rank), ROOT separators "
-                       f"on rank 0, RCCL reduce/broadcast of ROOT tiles and rows")
+                       f"on rank 0, {wire} reduce/broadcast of ROOT tiles and rows")
     else:
         log(f"[bench] {world} ranks, config {args.config}: {p.summary()}; landmark shards, Schur entries lm "
             f"{st[8]} obs {st[9]}")
         opt = ShardedOptimizer(e, comm)
-        parallelism = f"landmark shards x{world}, RCCL tile exchange to rank 0"
+        parallelism = f"landmark shards x{world}, {wire} tile exchange to rank 0"
 
     def settings(n):
         return Settings.default(max_num_iterations=n, stop_if_no_improvement_for=10**6,
@@ -525,7 +580,9 @@ def run_sharded(args, rank: int, world: int, local: int):
         contrib = st[6] if rank == 0 else 0
     flops = float(opt.n_factor) * contrib * 2.0 * 64 ** 3
     per_rank = comm.all_gather_obj((launches, kms, flops))
-    ph = e.phase_times()
+    phases = comm.all_gather_obj({k: round(v, 3) for k, v in opt.phases.ms.items()})
+    ph = phases[0]
+    dist_backend = dist.get_backend()
     dist.destroy_process_group()
     if rank != 0:
         return
@@ -535,17 +592,16 @@ def run_sharded(args, rank: int, world: int, local: int):
         achieved = None
     else:
         achieved = f0 / (k0 * 1e-3) / 1e12
-    from bench import pmc_traffic
     roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
             "frac": None if achieved is None else achieved / FP64_MFMA_PEAK_TF,
-            # HBM bytes per fan-in launch from the committed 1-GPU PMC passes (profiles/pmc_summary.json);
-            # a rank's subtree launches are the same kernel over a subset of the same levels
-            "traffic": pmc_traffic("fanin_kernel"), "traffic_source": "profiles/pmc_summary.json (1 GPU)",
+            # no PMC pass of a rank's own launches: the 1-GPU per-launch bytes cover the whole schedule's
+            # levels, not a rank's subtree + ROOT levels, so they are not this line's traffic
+            "traffic": None,
             "kernel": "fanin_kernel on rank 0 (its subtree + the ROOT separators), HIP events on the engine stream",
             "flops_per_launch": f0 / max(1, l0), "avg_launch_ms": k0 / max(1, l0), "launches": l0,
             "per_rank_tflops": [f / (k * 1e-3) / 1e12 if k > 0 else None for _, k, f in per_rank]}
-    log(f"[bench] timed {iters} its in {elapsed:.3f}s; rank 0 last it: lin {ph.linearize_ms:.2f} schur "
-        f"{ph.schur_ms:.2f} factor {ph.factor_ms:.2f} solve {ph.solve_ms:.2f} ms; fan-in {achieved} TF/s")
+    log(f"[bench] timed {iters} its in {elapsed:.3f}s; rank 0 last it: " +
+        " ".join(f"{k[:-3]} {v:.2f}" for k, v in ph.items()) + f" ms; fan-in {achieved} TF/s")
     cpu = None
     if not args.no_cpu_baseline:
         e.close()
@@ -561,8 +617,9 @@ def run_sharded(args, rank: int, world: int, local: int):
            "data": "synthetic (seeded Aria-like generator, csrc/synth.cpp)",
            "config": {"workload": f"config {args.config}: {st[0]} obs, {p.num_points} landmarks, "
                                   f"{p.vars[1].shape[0]} rigs, reduced order {st[3]}",
-                      "parallelism": parallelism},
+                      "parallelism": parallelism, "backend": dist_backend,
+                      "ranks_share_one_gpu": same_device},
            "roofline": roof, "cpu_baseline": cpu,
-           "phases_ms_rank0": {k: round(getattr(ph, k), 3) for k, _ in ph._fields_},
+           "phases_ms_rank0": ph, "phases_ms_per_rank": phases,
            "cost": [s.initial_cost, s.final_cost]}
     print(json.dumps(out), flush=True)

@@ -61,7 +61,9 @@ class Summary(C.Structure):
     """Optimizer::Summary (lib/small_thing/Optimizer.h:93-99)."""
     _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
                 ("num_troubled_seqs", C.c_int32), ("largest_troubled_seq", C.c_int32),
-                ("num_iterations", C.c_int32), ("reserved", C.c_int32)]
+                ("num_iterations", C.c_int32),
+                # iterations whose full step failed the reduction / failure-rate test (step rescaling)
+                ("num_rescaled", C.c_int32)]
 
 
 class PhaseTimes(C.Structure):
@@ -328,6 +330,11 @@ class CEngineBase:
         """Test fault injection: negate the model cost reduction in LM iteration `iteration` of the next
         optimize (Optimizer.cpp:835-854 branch); -1 disables."""
         self._check(self._fn("debug_negate_model_reduction", [C.c_int])(self.h, int(iteration)))
+
+    def debug_fail_iteration(self, iteration: int):
+        """Test fault: iteration `iteration` of the next optimize calls fails as a reduced-system breakdown
+        would (VB_E_NUMERIC after the step was applied); the variables must be restored."""
+        self._check(self._fn("debug_fail_iteration", [C.c_int])(self.h, int(iteration)))
 
     def pcg_stats(self):
         """(iterations, relative residual) of the last PCG solve (PCG::Result)."""
