@@ -17,7 +17,8 @@ from visual_inertial_bundle_adjustment_amd.engine import CEngineBase, Settings, 
 from visual_inertial_bundle_adjustment_amd.kinds import VAR_DATA
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_ref", "librefcpu.so")
+# VIBA_ORACLE_LIB: another build of the same source (scripts/sanitize.sh: ASan + UBSan)
+LIB = os.environ.get("VIBA_ORACLE_LIB", os.path.join(HERE, "_ref", "librefcpu.so"))
 P = C.c_void_p
 
 
