@@ -4,7 +4,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${1:-pmc_lin}
-KS=${2:-10,11,12,13}
+KS=${2:-10,12,13,14,15}
 export TMPDIR=/tmp
 mkdir -p $R/gpurun_out/$TAG
 cd /tmp

@@ -85,9 +85,12 @@ def test_session_folder_step_matches_oracle():
     assert abs(og["model_red"] - orf["model_red"]) <= 1e-9 * abs(orf["model_red"])
     assert abs(og["cost1"] - orf["cost1"]) <= 1e-9 * abs(orf["cost1"])
     assert og["stats1"] == orf["stats1"]
+    # (1e-9: the triangulated points start near their optimum, so their gradients are cancellation residues
+    # of terms many orders larger; the fp64 summation order -- atomics on the device -- shows at ~1e-10 of
+    # the largest entry)
     for a, b in zip(og["grad"], orf["grad"]):
         if b.size:
-            assert rel(a, b) < 1e-10
+            assert rel(a, b) < 1e-9
     for a, b in zip(og["step"], orf["step"]):
         if b.size:
             assert rel(a, b) < 1e-8
