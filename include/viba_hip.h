@@ -457,8 +457,10 @@ int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
  *  nSmallFactors, Schur landmark-pair entries, Schur observation-pair entries,
  *  fan-in launches per factorization, tiles of S without the symbolic fill] */
 int vb_problem_stats(vb_handle h, int64_t* out12);
-/* tuning aid: average kernel time [us] of one factorization kernel on scratch tiles
- * (which: 0 potrf, 1 trsm, 2 update + fused next-diagonal potrf, 3 update) */
+/* tuning aid: average time [us] of one kernel launch: on scratch tiles (which: 0 potrf, 1 trsm, 2 fan-in)
+ * or, alone on the handle's own data (its results are not meant to be used afterwards), 10 visual
+ * linearization, 12 landmark elimination, 13 observation-group Gram blocks, 14 Schur tile products,
+ * 15 visual cost pass */
 int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us);
 
 #ifdef __cplusplus

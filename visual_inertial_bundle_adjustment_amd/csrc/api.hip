@@ -454,11 +454,14 @@ int checkErr(vb_handle h) {
 int errFromWords(vb_handle h, const int32_t* ee) {
   const int32_t e = ee[0];
   if (int rc = checkRsErr(h, ee[1])) return rc;
+  // in causal order within an iteration: the linearization, the elimination and factorization, then the
+  // cost pass at the stepped variables (whose lookups a broken step can push out of range)
   if (e & 1) return fail(VB_E_RANGE, "RollingShutterData::getEstimate: out of range");
   if (e & 2) return fail(VB_E_NUMERIC, "landmark 3x3 Cholesky breakdown");
   if (e & 8) return fail(VB_E_NUMERIC, "reduced system Cholesky breakdown (not positive definite)");
   if (e & 4) return fail(VB_E_STATE, "internal: Schur contribution outside the symbolic structure");
   if (e & 16) return fail(VB_E_HIP, "internal: triangular-solve hand-off timed out");
+  if (e & 32) return fail(VB_E_RANGE, "RollingShutterData::getEstimate: out of range (cost pass)");
   return 0;
 }
 
@@ -3370,6 +3373,36 @@ extern "C" int vb_rs_row_poses(int64_t n_imu, const int64_t* imu_t_ns, const dou
 // which: 0 potrf, 1 trsm (one tile), 2/3 update (one pair)
 extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us) {
   if (!h || !h->finalized || iters <= 0) return fail(VB_E_STATE, "vb_bench_kernel needs a finalized handle");
+  if (which >= 10) {  // kernels of the linearize / Schur phases alone, on the handle's own data
+    Dev& d = h->d;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipStreamSynchronize(h->st));
+    double total = 0;
+    for (int it = 0; it < iters + 1; it++) {
+      HIPCHK(hipEventRecord(e0, h->st));
+      switch (which) {
+        case 10:  // visual linearization (records)
+          launch_visual_lin(d, 0, 0, d.obB, d.obE, h->st);
+          launch_visual_lin(d, 0, 0, d.fB, d.fE, h->st);
+          break;
+        case 12: launch_landmark(d, 1e-5, 0, d.lmB, d.lmE, h->st); break;  // landmark elimination
+        case 13: launch_groups(d, 1e-5, h->st); break;                     // observation-group Gram blocks
+        case 14: launch_schur_products(d, 1e-5, h->st); break;             // Schur tile products
+        case 15: launch_visual_cost(d, 1, d.obB, d.obE, h->st); break;     // cost pass (visual)
+        default: return fail(VB_E_ARG, "vb_bench_kernel: unknown kernel");
+      }
+      HIPCHK(hipEventRecord(e1, h->st));
+      HIPCHK(hipStreamSynchronize(h->st));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+      if (it > 0) total += ms;
+    }
+    hipEventDestroy(e0), hipEventDestroy(e1);
+    if (avg_us) *avg_us = total * 1e3 / iters;
+    return checkErr(h) == VB_E_HIP ? VB_E_HIP : 0;
+  }
   Dev d = h->d;  // copy: tiles / err redirected to scratch
   std::vector<double> A(TS * TS), B(TS * TS);
   uint64_t sd = 12345;

@@ -340,7 +340,7 @@ __global__ void __launch_bounds__(256) visual_cost_kernel(Dev d, int comparable,
     } else {
       const double* vp = d.var[2] + (int64_t)pb.z * 3;
       ok = rs_eval<false>(d, obsC, rs, X, Tbw, Tcb, cam, mk(vp[0], vp[1], vp[2]), false, false, v, &oor);
-      if (oor) atomicOr(d.err, 1);
+      if (oor) atomicOr(d.err, 32);  // (bit 32: in the cost pass, after the iteration's solve)
     }
     const double prev = d.cache[o];
     const bool prevInvalid = prev < 0.0;
