@@ -891,7 +891,7 @@ int doFinalize(vb_handle h) {
         const int32_t r = obRed[o * 4 + s];
         if (r < 0) continue;
         const int64_t q = std::lower_bound(blkRed.begin() + lmBlk[l], blkRed.begin() + lmBlk[l + 1], r) - blkRed.begin();
-        obCol[o * 4 + s] = blkCol[q];
+        obCol[o * 4 + s] = (blkCol[q] << 5) | h->rvDim[r];  // panel column and width (<= 17) in one word
       }
   }
   // reduced row of every landmark panel column

@@ -149,7 +149,7 @@ struct Dev {
   // observation's 6 doubles, so a lane's first loads are two coalesced 16 B reads, not an index chain
   int32_t* obPack = nullptr;  // 8 per position
   double* obCP = nullptr;     // 6 per position
-  int32_t* obCol = nullptr;  // 4 per obs (column offset in the landmark's Y panel, -1)
+  int32_t* obCol = nullptr;  // 4 per obs: (column offset in the landmark's Y panel << 5) | block width, -1
   double* obC = nullptr;     // 6 per obs
   double* cache = nullptr;   // ResultCache per obs
   double* cacheW = nullptr;  // where an updating linearization writes it: cache, or (vb_optimize's speculative

@@ -153,6 +153,36 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
 // landmark_obs_wg_kernel, whose panel is per workgroup.  Measured on config C: 1.04 + 0.72 ms against
 // 2.63 for the per-column landmark_kernel; one 48 KB per-wave class for all ran at 2.9 ms and the
 // per-workgroup kernel for all at 2.1 (occupancy vs. barriers).
+// one observation's share of a half-wave (lane jj = slot column j of slot s): the point Jacobian
+// (broadcast), the lane's two slot-column planes, the packed panel column / block width of the slot, and
+// (lane jj == 0) the residual; observations past o1 load observation o0 and add nothing
+struct ObsCols {
+  double a[6], x0, x1, e0, e1;
+  int32_t pc;
+};
+__device__ __forceinline__ void obs_cols_load(const Dev& d, const rec_t* Jt, int64_t o, int64_t o1, int64_t o0, int pl,
+                                              int st, int s, int jj, ObsCols& q) {
+  const bool valid = o < o1;
+  if (!valid) o = o0;
+  const rec_t* r = Jt + o * kJA;
+#pragma unroll
+  for (int k = 0; k < 6; k++) q.a[k] = r[kJpt + k];
+  const rec_t* x = jt_plane(Jt, d.nObsPad, o, pl);
+  q.x0 = x[0], q.x1 = x[st];
+  q.pc = valid ? d.obCol[o * 4 + s] : -1;
+  q.e0 = jj == 0 ? (double)r[kJe] : 0.0, q.e1 = jj == 0 ? (double)r[kJe + 1] : 0.0;
+}
+// W(:, column) += Jp^T J_x(:, j) for the lane's slot column (LDS atomics: both half-waves may hit a shared
+// calibration block)
+__device__ __forceinline__ void obs_cols_add(const ObsCols& q, int j, double* W) {
+  if (q.pc >= 0 && j < (q.pc & 31)) {
+    const int c = (q.pc >> 5) + j;
+    atomicAdd(&W[3 * c + 0], q.a[0] * q.x0 + q.a[3] * q.x1);
+    atomicAdd(&W[3 * c + 1], q.a[1] * q.x0 + q.a[4] * q.x1);
+    atomicAdd(&W[3 * c + 2], q.a[2] * q.x0 + q.a[5] * q.x1);
+  }
+}
+
 constexpr int kLmBigCols = 2048;  // 3 x 2048 doubles = 48 KB of dynamic LDS per workgroup; wider: per-column path
 
 __global__ void __launch_bounds__(256) landmark_obs_kernel(Dev d, double lambda, int64_t first, int64_t n, int cap) {
@@ -174,25 +204,20 @@ __global__ void __launch_bounds__(256) landmark_obs_kernel(Dev d, double lambda,
   const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
   const int pl = slotPlane(s) + j, st = slotStride(s);
   double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  // software-pipelined by one observation: the next observation's record reads are in flight while
+  // this one's products go into the panel
+  ObsCols q, qn;
+  obs_cols_load(d, Jt, o0 + h, o1, o0, pl, st, s, jj, q);
   for (int64_t o = o0 + h; o < o1; o += 2) {
-    const rec_t* r = Jt + o * kJA;
-    const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
-    const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
-    const rec_t* x = jt_plane(Jt, d.nObsPad, o, pl);
-    const double x0 = x[0], x1 = x[st];
-    const int32_t X = d.obRed[o * 4 + s];
+    obs_cols_load(d, Jt, o + 2, o1, o0, pl, st, s, jj, qn);
     if (jj == 0) {
-      const double e0 = r[kJe], e1 = r[kJe + 1];
-      g0 += a0 * e0 + b0 * e1, g1 += a1 * e0 + b1 * e1, g2 += a2 * e0 + b2 * e1;
-      v00 += a0 * a0 + b0 * b0, v10 += a1 * a0 + b1 * b0, v20 += a2 * a0 + b2 * b0;
-      v11 += a1 * a1 + b1 * b1, v21 += a2 * a1 + b2 * b1, v22 += a2 * a2 + b2 * b2;
+      g0 += q.a[0] * q.e0 + q.a[3] * q.e1, g1 += q.a[1] * q.e0 + q.a[4] * q.e1, g2 += q.a[2] * q.e0 + q.a[5] * q.e1;
+      v00 += q.a[0] * q.a[0] + q.a[3] * q.a[3], v10 += q.a[1] * q.a[0] + q.a[4] * q.a[3];
+      v20 += q.a[2] * q.a[0] + q.a[5] * q.a[3], v11 += q.a[1] * q.a[1] + q.a[4] * q.a[4];
+      v21 += q.a[2] * q.a[1] + q.a[5] * q.a[4], v22 += q.a[2] * q.a[2] + q.a[5] * q.a[5];
     }
-    if (X >= 0 && j < d.rvDim[X]) {
-      const int c = d.obCol[o * 4 + s] + j;
-      atomicAdd(&W[3 * c + 0], a0 * x0 + b0 * x1);
-      atomicAdd(&W[3 * c + 1], a1 * x0 + b1 * x1);
-      atomicAdd(&W[3 * c + 2], a2 * x0 + b2 * x1);
-    }
+    obs_cols_add(q, j, W);
+    q = qn;
   }
   g0 = wave_sum(g0), g1 = wave_sum(g1), g2 = wave_sum(g2);
   v00 = wave_sum(v00), v10 = wave_sum(v10), v20 = wave_sum(v20);
@@ -246,25 +271,18 @@ __global__ void __launch_bounds__(256) landmark_obs_wg_kernel(Dev d, double lamb
   const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
   const int pl = slotPlane(s) + j, st = slotStride(s);
   double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // v00 v10 v20 v11 v21 v22 g0 g1 g2
+  ObsCols q, qn;
+  obs_cols_load(d, Jt, o0 + h, o1, o0, pl, st, s, jj, q);
   for (int64_t o = o0 + h; o < o1; o += 8) {
-    const rec_t* r = Jt + o * kJA;
-    const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
-    const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
-    const rec_t* x = jt_plane(Jt, d.nObsPad, o, pl);
-    const double x0 = x[0], x1 = x[st];
-    const int32_t X = d.obRed[o * 4 + s];
+    obs_cols_load(d, Jt, o + 8, o1, o0, pl, st, s, jj, qn);
     if (jj == 0) {
-      const double e0 = r[kJe], e1 = r[kJe + 1];
-      v[6] += a0 * e0 + b0 * e1, v[7] += a1 * e0 + b1 * e1, v[8] += a2 * e0 + b2 * e1;
-      v[0] += a0 * a0 + b0 * b0, v[1] += a1 * a0 + b1 * b0, v[2] += a2 * a0 + b2 * b0;
-      v[3] += a1 * a1 + b1 * b1, v[4] += a2 * a1 + b2 * b1, v[5] += a2 * a2 + b2 * b2;
+      v[6] += q.a[0] * q.e0 + q.a[3] * q.e1, v[7] += q.a[1] * q.e0 + q.a[4] * q.e1, v[8] += q.a[2] * q.e0 + q.a[5] * q.e1;
+      v[0] += q.a[0] * q.a[0] + q.a[3] * q.a[3], v[1] += q.a[1] * q.a[0] + q.a[4] * q.a[3];
+      v[2] += q.a[2] * q.a[0] + q.a[5] * q.a[3], v[3] += q.a[1] * q.a[1] + q.a[4] * q.a[4];
+      v[4] += q.a[2] * q.a[1] + q.a[5] * q.a[4], v[5] += q.a[2] * q.a[2] + q.a[5] * q.a[5];
     }
-    if (X >= 0 && j < d.rvDim[X]) {
-      const int c = d.obCol[o * 4 + s] + j;
-      atomicAdd(&W[3 * c + 0], a0 * x0 + b0 * x1);
-      atomicAdd(&W[3 * c + 1], a1 * x0 + b1 * x1);
-      atomicAdd(&W[3 * c + 2], a2 * x0 + b2 * x1);
-    }
+    obs_cols_add(q, j, W);
+    q = qn;
   }
 #pragma unroll
   for (int k = 0; k < 9; k++) v[k] = wave_sum(v[k]);
