@@ -31,10 +31,11 @@ KF_VISUAL_LIN, KF_LANDMARK, KF_SCHUR, KF_POTRF, KF_GEMM, KF_FWD, KF_BWD, KF_BACK
 SOLVERS = {"direct": 0, "pcg-trivial": 1, "pcg-jacobi": 2, "pcg-gauss-seidel": 3, "pcg-lower-prec": 4}
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 FP64_MFMA_PEAK_TF = 78.6   # MI355X fp64 matrix peak (spec)
-# what v_mfma_f64_16x16x4_f64 sustains on this chip with independent accumulators and no memory traffic
-# (scripts/micro/mfma_peak.hip, profiles/r02_mfma_peak.txt: 47.7 TF/s at 2385 MHz; the 4x4x4_4b form
-# reaches 74 TF/s there but lost 20-25 % inside the fan-in)
-FP64_MFMA_16X16X4_MEASURED_TF = 47.7
+# what the fp64 MFMA sustains on this chip with independent accumulators and no memory traffic
+# (scripts/micro/mfma_peak.hip, profiles/r03_mfma_peak.txt): v_mfma_f64_4x4x4_4b 74.9 TF/s (NACC 8, 4
+# workgroups per CU), the hardware's practical fp64 matrix ceiling; the 16x16x4 form the fan-in issues
+# sustains 47.7 TF/s, a limit of that instruction, not of the chip
+FP64_MFMA_4X4X4_MEASURED_TF = 74.9
 
 
 def log(*a):
@@ -279,8 +280,8 @@ def main():
                 "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
                           "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
                 "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches,
-                "instruction_peak": FP64_MFMA_16X16X4_MEASURED_TF,
-                "frac_of_instruction_peak": achieved / FP64_MFMA_16X16X4_MEASURED_TF}
+                "ceiling_4x4x4_measured": FP64_MFMA_4X4X4_MEASURED_TF,
+                "frac_of_4x4x4_ceiling": achieved / FP64_MFMA_4X4X4_MEASURED_TF}
     elif args.profile_family == KF_SYMV:
         # every tile of S (stored tiles less the symbolic fill) once (32 KB) + x and y rows (1 KB) per launch
         b = st[11] * (64 * 64 * 8 + 2 * 64 * 8)
