@@ -711,12 +711,10 @@ __global__ void __launch_bounds__(256) reduced_rhs_kernel(Dev d) {
 }
 
 // ------------------------------------------------------------------ tile Cholesky
-// Right-looking tile Cholesky, two launches per tile column J (factorSeq in api.hip):
-//   trsm_kernel    L_IJ = A_IJ L_JJ^-T for the off-diagonal tiles of column J
-//   update_kernel  A_IK -= L_IJ L_KJ^T for every pair I >= K of column J (fp64 MFMA); the block whose
-//                  target is the next diagonal tile (J+1, J+1) factors it right after its update, so
-//                  the next column's trsm finds L_{J+1,J+1} ready (potrf_kernel covers the columns
-//                  whose diagonal receives no update from the previous column, and column 0).
+// Level-scheduled tile Cholesky (factorSeq in api.hip), per elimination level of the nested-dissection
+// order: fanin_kernel (A_IJ -= sum_K L_IK L_JK^T for the level's target tiles), then potrf4_kernel on
+// the level's diagonal tiles and trsm_kernel (L_IJ = A_IJ L_JJ^-T) on its off-diagonal ones, or both in
+// one potrf_trsm_kernel launch on the levels with few off-diagonal tiles.
 // Inside a tile everything is blocked by 16 and runs on v_mfma_f64_16x16x4_f64, computed TRANSPOSED:
 // an accumulator D (lane l, register r) = D[(l >> 4) + 4 r][l & 15] is exactly the B operand of k-step
 // r (B[4 r + (l >> 4)][l & 15]), so chained products need no data movement.  The only scalar work is
@@ -1422,9 +1420,15 @@ __global__ void __launch_bounds__(256) backsub_kernel(Dev d, int mode, int64_t l
   const rec_t* Y = d.Y + cb;
   const int64_t yq = d.nYcol;
   double t0 = 0, t1 = 0, t2 = 0;
-  for (int64_t c = lane; c < ncol; c += 64) {
-    const double v = xr[d.pcRow[cb + c]];
-    t0 += Y[c] * v, t1 += Y[yq + c] * v, t2 += Y[2 * yq + c] * v;
+  // two columns per lane and step: both row-index loads, then both gathers of x, in flight together
+  for (int64_t c = lane; c < ncol; c += 128) {
+    const bool two = c + 64 < ncol;
+    const int32_t ra = d.pcRow[cb + c], rb = two ? d.pcRow[cb + c + 64] : ra;
+    const double ya0 = Y[c], ya1 = Y[yq + c], ya2 = Y[2 * yq + c];
+    const double yb0 = two ? (double)Y[c + 64] : 0.0, yb1 = two ? (double)Y[yq + c + 64] : 0.0;
+    const double yb2 = two ? (double)Y[2 * yq + c + 64] : 0.0;
+    const double va = xr[ra], vb = xr[rb];
+    t0 += ya0 * va + yb0 * vb, t1 += ya1 * va + yb1 * vb, t2 += ya2 * va + yb2 * vb;
   }
   t0 = wave_sum(t0), t1 = wave_sum(t1), t2 = wave_sum(t2);
   if (lane != 0) return;
