@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from visual_inertial_bundle_adjustment_amd import synth  # noqa: E402
 from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings  # noqa: E402
 
-NAMES = {10: "visual_lin (eval + record stores)", 12: "landmark elimination",
+NAMES = {0: "potrf4 (one tile, scratch)", 1: "trsm (one tile, scratch)", 2: "fan-in (one pair, scratch)",
+         10: "visual_lin (eval + record stores)", 12: "landmark elimination",
          13: "observation-group Gram blocks", 14: "Schur tile products", 15: "visual cost pass"}
 
 
