@@ -460,7 +460,8 @@ int vb_problem_stats(vb_handle h, int64_t* out12);
 /* tuning aid: average time [us] of one kernel launch: on scratch tiles (which: 0 potrf, 1 trsm, 2 fan-in)
  * or, alone on the handle's own data (its results are not meant to be used afterwards), 10 visual
  * linearization, 12 landmark elimination, 13 observation-group Gram blocks, 14 Schur tile products,
- * 15 visual cost pass */
+ * 15 visual cost pass, 16 small factors' evaluation, 17 / 18 their assembly (IMU kinds / the rest, from
+ * the staging of an earlier 16), 19 the reduced system's clear */
 int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us);
 
 #ifdef __cplusplus

@@ -14,7 +14,9 @@ from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings  # 
 
 NAMES = {0: "potrf4 (one tile, scratch)", 1: "trsm (one tile, scratch)", 2: "fan-in (one pair, scratch)",
          10: "visual_lin (eval + record stores)", 12: "landmark elimination",
-         13: "observation-group Gram blocks", 14: "Schur tile products", 15: "visual cost pass"}
+         13: "observation-group Gram blocks", 14: "Schur tile products", 15: "visual cost pass",
+         16: "small factors' evaluation", 17: "small assembly, IMU kinds", 18: "small assembly, other kinds",
+         19: "reduced-system clear"}
 
 
 def main():
@@ -27,8 +29,11 @@ def main():
     for prec in precs:
         e = HipEngine(imu_calib_options=p.imu_calib_options, precision=prec)
         synth.load_into(e, p, rs_device=True)
-        e.optimize(Settings.default(max_num_iterations=2, stop_if_no_improvement_for=10**6,
-                                    distance_from_troubled_iteration=0))
+        try:  # records and staging in place (a diagnostic build may not converge)
+            e.optimize(Settings.default(max_num_iterations=2, stop_if_no_improvement_for=10**6,
+                                        distance_from_troubled_iteration=0))
+        except Exception as ex:
+            print(f"[probe] optimize: {ex}", file=sys.stderr)
         f = e._fn("bench_kernel", [C.c_int, C.c_int, C.POINTER(C.c_double)])
         res = {}
         for w in which:

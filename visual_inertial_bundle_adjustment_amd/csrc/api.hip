@@ -357,6 +357,7 @@ struct vb_handle_s {
   // the tile factorization's launches, captured into a HIP graph per schedule and tile store
   // (VIBA_NO_GRAPHS=1: eager)
   bool useGraphs = true;
+  bool specEarly = true;  // specEarly beside the cost pass (VIBA_SPEC_EARLY=0: inside the speculative linearization)
   // vb_optimize's speculative linearization (specEnqueue): the next iteration's rolling-shutter rebuild
   // and linearization are queued behind this iteration's cost pass, before the host reads its scalars,
   // into a second tile store, ResultCache, gradient and rolling-shutter table set (and reduction /
@@ -1963,6 +1964,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   vb_handle h = new vb_handle_s();
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
+  if (const char* e = getenv("VIBA_SPEC_EARLY")) h->specEarly = e[0] != '0';
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2285,22 +2287,10 @@ int vb_set_landmark_shard(vb_handle h, int64_t lm_begin, int64_t lm_end, int is_
   return 0;
 }
 
-// vb_linearize's device work over the buffers of `d` (h->d, or the speculative copy of vb_optimize:
-// another tile store, cache write buffer, reduction and error slots), no host read, no reset of the
-// reduction / error slots (the caller's); events evA / evB bracket it
-int linearizeBody(vb_handle h, const Dev& d, int update_cache, int dont_retry_failed, hipEvent_t evA, hipEvent_t evB) {
-  HIPCHK(hipEventRecord(evA, h->st));
-  // the reduced system is cleared and the small factors assembled on the side stream while the visual
-  // factors linearize on the main stream (they write only their records and the cost)
-  const bool side = smallHere(h, 0);
-  hipStream_t zs = side ? h->stZ : h->st;
-  if (side) {
-    HIPCHK(hipEventRecord(h->evFork, h->st));
-    HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
-    HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
-    launch_small_eval(d, 0, d.gRed, h->st2);
-  }
-  if (h->clearTilesD) {  // the tiles no Schur item stores whole
+// the reduced system's clear on stream zs: the tiles no Schur item stores whole, the gradient, the
+// padded diagonal
+int clearReduced(vb_handle h, const Dev& d, hipStream_t zs) {
+  if (h->clearTilesD) {
     launch_zero_tiles(d.tiles, h->clearTilesD, h->nClear, zs);
   } else if (h->zeroRuns.empty()) {
     HIPCHK(hipMemsetAsync(d.tiles, 0, (size_t)d.nTiles * TS * TS * sizeof(double), zs));
@@ -2310,7 +2300,37 @@ int linearizeBody(vb_handle h, const Dev& d, int update_cache, int dont_retry_fa
   }
   HIPCHK(hipMemsetAsync(d.gRed, 0, (size_t)d.nT * TS * sizeof(double), zs));
   if (h->isRoot || h->partWorld > 1) launch_pad_diag(d, h->padRowsD, h->nPadRows, zs);
-  if (side) {
+  return 0;
+}
+
+// vb_linearize's device work over the buffers of `d` (h->d, or the speculative copy of vb_optimize:
+// another tile store, cache write buffer, reduction and error slots), no host read, no reset of the
+// reduction / error slots (the caller's); events evA / evB bracket it.  early: the small factors'
+// evaluation and the clear were queued on stZ already (specEarly)
+int linearizeBody(vb_handle h, const Dev& d, int update_cache, int dont_retry_failed, hipEvent_t evA, hipEvent_t evB,
+                  bool early = false) {
+  HIPCHK(hipEventRecord(evA, h->st));
+  // the reduced system is cleared and the small factors assembled on the side stream while the visual
+  // factors linearize on the main stream (they write only their records and the cost)
+  const bool side = smallHere(h, 0);
+  hipStream_t zs = side ? h->stZ : h->st;
+  if (side && !early) {
+    HIPCHK(hipEventRecord(h->evFork, h->st));
+    HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
+    HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
+    launch_small_eval(d, 0, d.gRed, h->st2);
+  }
+  if (!early)
+    if (int rc = clearReduced(h, d, zs)) return rc;
+  if (side && early) {
+    // evaluation and clear done in order on stZ: the IMU kinds' assembly on st2 waits for both
+    HIPCHK(hipEventRecord(h->evZero, h->stZ));
+    HIPCHK(hipStreamWaitEvent(h->st2, h->evZero, 0));
+    launch_small_assemble(d, 0, d.gRed, h->st2, 1);
+    launch_small_assemble(d, 0, d.gRed, h->stZ, 2);
+    HIPCHK(hipEventRecord(h->evJoin, h->st2));
+    HIPCHK(hipEventRecord(h->evZJoin, h->stZ));
+  } else if (side) {
     // the IMU kinds' assembly on st2, the other kinds' on stZ after the clear: both wait for the clear
     // and the evaluation
     HIPCHK(hipEventRecord(h->evZero, h->stZ));
@@ -2884,14 +2904,32 @@ Dev specDev(vb_handle h) {
 }
 // ark_vi_ba's preStepCallback (the rolling-shutter rebuild at the accepted variables) and the
 // linearization of the next iteration, queued behind this iteration's cost pass; event set p
-int specEnqueue(vb_handle h, int dontRetry, int p) {
+// With early set, specEarly queued the small factors' evaluation and the clear beside the cost pass.
+int specEnqueue(vb_handle h, int dontRetry, int p, bool early) {
   const Dev ds = specDev(h);
-  HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
-  HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
+  if (!early) {
+    HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
+    HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
+  }
   HIPCHK(hipEventRecord(h->evS[p][0], h->st));
   if (h->rsDevice) launch_rs_build(ds, h->st);
   HIPCHK(hipEventRecord(h->evS[p][1], h->st));
-  return linearizeBody(h, ds, 1, dontRetry, h->evS[p][2], h->evS[p][3]);
+  return linearizeBody(h, ds, 1, dontRetry, h->evS[p][2], h->evS[p][3], early);
+}
+// The part of the speculative linearization that needs only the stepped variables, queued on stZ after
+// the box-plus so it runs beside the cost pass (which leaves the HBM and most CUs idle): the small
+// factors' evaluation into the staging slots and the clear of the spare tile store and gradient.  The
+// staging slots are free there (the iteration's assembly is joined, and vb_gradient_dot_step's
+// evaluation forks from the main stream after the speculative linearization's join).
+int specEarly(vb_handle h) {
+  if (!smallHere(h, 0)) return 0;
+  const Dev ds = specDev(h);
+  HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
+  HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
+  HIPCHK(hipEventRecord(h->evFork, h->st));
+  HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
+  launch_small_eval(ds, 0, ds.gRed, h->stZ);
+  return clearReduced(h, ds, h->stZ);
 }
 // the step was accepted at full size: the speculative buffers become the handle's
 void specCommit(vb_handle h) {
@@ -2977,7 +3015,10 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     if ((rc = dampFactorSolveEnqueue(h, damping, false))) return bail(rc);
     if ((rc = vb_backup(h))) return bail(rc);
     backedUp = true;
-    if ((rc = applyStepEnqueue(h, 0, 10, 11)) || (rc = costEnqueue(h, 1, false))) return bail(rc);
+    if ((rc = applyStepEnqueue(h, 0, 10, 11))) return bail(rc);
+    const bool early = speculate && it + 1 < s.max_num_iterations && smallHere(h, 0) && h->specEarly;
+    if (early && (rc = specEarly(h))) return bail(rc);
+    if ((rc = costEnqueue(h, 1, false))) return bail(rc);
     const bool wasSpec = specQueued;
     const int wasSet = specSet;
     specQueued = false;
@@ -2988,7 +3029,7 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
       // after the last iteration: its work would only be discarded)
       if (it + 1 < s.max_num_iterations) {
         specSet ^= 1;
-        if ((rc = specEnqueue(h, dontRetry, specSet))) return bail(rc);
+        if ((rc = specEnqueue(h, dontRetry, specSet, early))) return bail(rc);
         specQueued = true;
       }
     }
@@ -3397,6 +3438,13 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
         case 13: launch_groups(d, 1e-5, h->st); break;                     // observation-group Gram blocks
         case 14: launch_schur_products(d, 1e-5, h->st); break;             // Schur tile products
         case 15: launch_visual_cost(d, 1, d.obB, d.obE, h->st); break;     // cost pass (visual)
+        // the small factors (staging for 17 / 18 from an earlier 16) and the clear; they change the tiles
+        case 16: launch_small_eval(d, 0, d.gRed, h->st); break;
+        case 17: launch_small_assemble(d, 0, d.gRed, h->st, 1); break;
+        case 18: launch_small_assemble(d, 0, d.gRed, h->st, 2); break;
+        case 19:
+          if (int rc = clearReduced(h, d, h->st)) return rc;
+          break;
         default: return fail(VB_E_ARG, "vb_bench_kernel: unknown kernel");
       }
       HIPCHK(hipEventRecord(e1, h->st));

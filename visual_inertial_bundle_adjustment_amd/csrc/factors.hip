@@ -879,10 +879,19 @@ __global__ void __launch_bounds__(64) small_kernel(Dev d, SmallLaunch L) {
 // jacobian accumulation, InertialFactor / PriorFactor / RandomWalkFactor).
 // MM: row capacity of the launch (its kinds' residual sizes), so that the per-wave LDS copy of the
 // whitened Jacobian is only as large as needed (IMU factors: 9 rows -> 6 workgroups per CU)
+// The active columns are ordered by reduced row and the lower-triangle entries enumerated column by
+// column, so the lanes of one atomic instruction add into consecutive rows of a tile column (a few
+// cache lines per instruction instead of one line per lane: the L2's atomic rate bounds this kernel).
+// The entries' tiles come from a per-wave table over the factor's distinct tile rows, filled
+// lane-parallel before the entry loop (rows beyond the table look theirs up); sized so the IMU launch
+// keeps 6 workgroups per CU.
+constexpr int kAsmTiles = 7;
 template <int MM>
 __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, double* gOut, int64_t s0, int64_t s1) {
   __shared__ double Jl[4][MM * kMaxCols];
-  __shared__ int32_t act[4][kMaxCols][2];  // active column: (staged column, reduced row)
+  __shared__ int32_t act[4][kMaxCols][2];  // active column: (staged column, reduced row << 5 | tile-row slot + 1)
+  __shared__ int32_t trow[4][kAsmTiles];   // the factor's distinct tile rows
+  __shared__ int32_t tpair[4][kAsmTiles * kAsmTiles];  // tileIdx of (tile row u, tile row v), u >= v
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t slot = s0 + (int64_t)blockIdx.x * 4 + wave;
   if (slot >= s1) return;
@@ -913,15 +922,31 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
         if (i < m) J[i * kMaxCols + j] = col[i];
     }
   }
+  const int T = d.T;
   if (lane == 0) {
-    int n = 0;
+    // the factor's variables by first reduced row (insertion sort, <= 10), then their columns
+    int32_t vro[10], vs[10], nvar = 0;
     for (int s = 0; s < nv; s++) {
       const int red = mt[5 + s];
       if (red < 0) continue;
-      const int64_t ro = d.rvOff[red];
-      for (int i = 0; i < mt[25 + s]; i++) act[wave][n][0] = mt[15 + s] + i, act[wave][n][1] = (int32_t)(ro + i), n++;
+      const int32_t ro = (int32_t)d.rvOff[red];
+      int k = nvar++;
+      for (; k > 0 && vro[k - 1] > ro; k--) vro[k] = vro[k - 1], vs[k] = vs[k - 1];
+      vro[k] = ro, vs[k] = s;
     }
-    act[wave][kMaxCols - 1][1] = n;  // count (slot kMaxCols - 1 is never a column: colc <= 80 incl. scratch)
+    int n = 0, nu = 0;
+    for (int k = 0; k < nvar; k++) {
+      const int s = vs[k];
+      for (int i = 0; i < mt[25 + s]; i++) {
+        const int32_t R = vro[k] + i, t = R / T;
+        int u = 0;
+        while (u < nu && trow[wave][u] != t) u++;
+        if (u == nu && nu < kAsmTiles) trow[wave][nu++] = t;
+        act[wave][n][0] = mt[15 + s] + i, act[wave][n][1] = R << 5 | (u < kAsmTiles ? u + 1 : 0), n++;
+      }
+    }
+    // counts (slot kMaxCols - 1 is never a column: colc <= 80 incl. scratch)
+    act[wave][kMaxCols - 1][0] = nu, act[wave][kMaxCols - 1][1] = n;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -930,21 +955,35 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
     const int c = act[wave][a][0];
     double g = 0;
     for (int r = 0; r < m; r++) g += J[r * kMaxCols + c] * se[1 + r];
-    if (owns_col(d, act[wave][a][1] / d.T)) atomicAdd(gOut + act[wave][a][1], drho * g);
+    const int32_t R = act[wave][a][1] >> 5;
+    if (owns_col(d, R / T)) atomicAdd(gOut + R, drho * g);
   }
   if (mode != 0) return;
+  const int nu = act[wave][kMaxCols - 1][0];
+  for (int q = lane; q < nu * nu; q += 64) {
+    const int tu = trow[wave][q / nu], tv = trow[wave][q % nu];
+    tpair[wave][q] = tu >= tv ? d.tileIdx[(int64_t)tu * d.nT + tv] : -1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  // entry p of the column-major lower triangle: column b, row a >= b (R_a >= R_b by the ordering);
+  // q = P - 1 - p decoded row-major gives (A - 1 - b, A - 1 - a)
   const int P = A * (A + 1) / 2;
   for (int p = lane; p < P; p += 64) {
-    int a = (int)((sqrtf(8.0f * p + 1.0f) - 1.0f) * 0.5f);  // f32 estimate, corrected below
-    while (a * (a + 1) / 2 > p) a--;
-    while ((a + 1) * (a + 2) / 2 <= p) a++;
-    const int b = p - a * (a + 1) / 2;
+    const int q = P - 1 - p;
+    int i = (int)((sqrtf(8.0f * q + 1.0f) - 1.0f) * 0.5f);  // f32 estimate, corrected below
+    while (i * (i + 1) / 2 > q) i--;
+    while ((i + 1) * (i + 2) / 2 <= q) i++;
+    const int b = A - 1 - i, a = A - 1 - (q - i * (i + 1) / 2);
     const int ca = act[wave][a][0], cb = act[wave][b][0];
     double hs = 0;
     for (int r = 0; r < m; r++) hs += J[r * kMaxCols + ca] * J[r * kMaxCols + cb];
-    int64_t R = act[wave][a][1], C = act[wave][b][1];
-    if (R < C) { const int64_t t = R; R = C; C = t; }
-    if (owns_col(d, C / d.T)) atomicAdd(tile_addr(d, R, C), drho * hs);
+    const int32_t wa = act[wave][a][1], wb = act[wave][b][1];
+    const int32_t R = wa >> 5, C = wb >> 5, uR = (wa & 31) - 1, uC = (wb & 31) - 1;
+    if (!owns_col(d, C / T)) continue;
+    double* dst = uR >= 0 && uC >= 0 ? d.tiles + (int64_t)tpair[wave][uR * nu + uC] * T * T + (C % T) * T + (R % T)
+                                     : tile_addr(d, R, C);
+    atomicAdd(dst, drho * hs);
   }
 }
 
