@@ -923,7 +923,44 @@ __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, do
     }
   }
   const int T = d.T;
-  if (lane == 0) {
+  // the factor's variables, lane s < nv: first reduced row, dimension, staged column (dimension 0: none)
+  int32_t vro = 0x7fffffff, vdim = 0, vcol = 0;
+  if (lane < nv) {
+    const int red = mt[5 + lane];
+    if (red >= 0) vro = (int32_t)d.rvOff[red], vdim = mt[25 + lane], vcol = mt[15 + lane];
+  }
+  int32_t vstart = 0, nAct = 0;  // first active column of the lane's variable in row order; column count
+  for (int s = 0; s < nv; s++) {
+    const int32_t ro = __builtin_amdgcn_readlane(vro, s), dim = __builtin_amdgcn_readlane(vdim, s);
+    if (ro < vro) vstart += dim;
+    nAct += dim;
+  }
+  if (nAct <= 64) {  // lane j: active column j; the distinct tile rows by ballot rounds
+    const bool on = lane < nAct;
+    int32_t R = 0, c = 0;
+    for (int s = 0; s < nv; s++) {
+      const int32_t st = __builtin_amdgcn_readlane(vstart, s), dim = __builtin_amdgcn_readlane(vdim, s);
+      if (lane >= st && lane < st + dim) {
+        R = __builtin_amdgcn_readlane(vro, s) + (lane - st);
+        c = __builtin_amdgcn_readlane(vcol, s) + (lane - st);
+      }
+    }
+    const int32_t t = R / T;
+    uint64_t left = __ballot(on);
+    int nu = 0, u = -1;
+    while (left) {
+      const int32_t tl = __builtin_amdgcn_readlane(t, __builtin_ctzll(left));
+      const bool hit = on && t == tl;
+      left &= ~__ballot(hit);
+      if (nu < kAsmTiles) {
+        if (hit) u = nu;
+        if (lane == 0) trow[wave][nu] = tl;
+        nu++;
+      }
+    }
+    if (on) act[wave][lane][0] = c, act[wave][lane][1] = R << 5 | (u + 1);
+    if (lane == 0) act[wave][kMaxCols - 1][0] = nu, act[wave][kMaxCols - 1][1] = nAct;
+  } else if (lane == 0) {
     // the factor's variables by first reduced row (insertion sort, <= 10), then their columns
     int32_t vro[10], vs[10], nvar = 0;
     for (int s = 0; s < nv; s++) {
