@@ -22,7 +22,8 @@ def per_kernel(d, counter):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            k = r["Kernel_Name"].split("(")[0].replace("viba::", "").replace("void ", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+            k = k.replace("viba::", "").replace("void ", "")
             k = k.split("<")[0].strip()
             tot[k] += float(r["Counter_Value"])
             n[k] += 1
