@@ -651,24 +651,68 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
     if (row1 >= 0 && gc1 != 0.0) atomicAdd(gOut + row1, gc1);
   }
   if (mode != 0) return;
-  // H: D[m][n], m = l4 + 4 k (+16), n = l15 (+16); rows of m / n via the lanes that own those columns
+  // H (32 x 32, symmetric) into LDS over the reduction buffer (this wave has read it): D[m][n],
+  // m = kAccL4 l4 + kAccR k (+16), n = l15 (+16); the cross block also mirrored
+  double* H = &red_[0][0][0];
 #pragma unroll
-  for (int blk = 0; blk < 3; blk++) {
-    const int mb = blk == 0 ? 0 : 16, nb = blk == 2 ? 16 : 0;
-    const int rn = nb ? row1 : row0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int m = kAccL4 * l4 + kAccR * k;
-      const int rm = __shfl(mb ? row1 : row0, m, 64);
-      double v = t[4 * blk + k];
-      if (rm < 0 || rn < 0 || v == 0.0) continue;
-      if (rm == rn) v *= 1.0 + lambda;
-      else if (blk != 1 && rm < rn) continue;  // symmetric blocks: each pair once
-      const int64_t R = max(rm, rn), Cc = min(rm, rn);
-      double* pt = tile_ptr(d, R, Cc);
-      if (pt) atomicAdd(pt, v);
-      else atomicOr(d.err, 4);
-    }
+  for (int k = 0; k < 4; k++) {
+    const int m = kAccL4 * l4 + kAccR * k;
+    H[m * 32 + l15] = t[k];
+    H[(16 + m) * 32 + 16 + l15] = t[8 + k];
+    H[(16 + m) * 32 + l15] = t[4 + k], H[l15 * 32 + 16 + m] = t[4 + k];
+  }
+  // the valid columns ordered by reduced row (lane c < 32: column c), their distinct tile rows
+  int32_t* ord = reinterpret_cast<int32_t*>(H + 32 * 32);  // [32] column at sorted position
+  int32_t* crow = ord + 32;                                // [32] column's reduced row
+  int32_t* cu = crow + 32;                                 // [32] column's tile-row slot
+  int32_t* trow = cu + 32;                                 // [8] distinct tile rows
+  int32_t* tpair = trow + 8;                               // [64] tileIdx of (tile row u, v)
+  const int rowc = lane < 32 ? (lane < 16 ? row0 : row1) : -1;  // lane c < 32: column c
+  const bool val = rowc >= 0;
+  int rank = 0;
+  for (int c = 0; c < 32; c++) {
+    const int rc = __builtin_amdgcn_readlane(rowc, c);
+    if (rc >= 0 && rc < rowc) rank++;
+  }
+  const int nc = __popcll(__ballot(val));
+  if (val) ord[rank] = lane;
+  const int tr = rowc / TS;
+  uint64_t left = __ballot(val);
+  int nu = 0, u = -1;
+  while (left) {
+    const int tl = __builtin_amdgcn_readlane(tr, __builtin_ctzll(left));
+    const bool hit = val && tr == tl;
+    left &= ~__ballot(hit);
+    if (hit) u = nu;
+    if (lane == 0) trow[nu] = tl;
+    nu++;  // <= 8: four variables, a tile row boundary inside each at most
+  }
+  if (lane < 32) crow[lane] = rowc, cu[lane] = u;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  for (int q = lane; q < nu * nu; q += 64) {
+    const int tu = trow[q / nu], tv = trow[q % nu];
+    tpair[q] = tu >= tv ? d.tileIdx[(int64_t)tu * d.nT + tv] : -1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  // lower-triangle entries column by column over the ordered columns (consecutive lanes on consecutive
+  // rows of one tile column); diagonal damped by (1 + lambda)
+  const int P = nc * (nc + 1) / 2;
+  for (int p = lane; p < P; p += 64) {
+    const int q = P - 1 - p;
+    int i = (int)((sqrtf(8.0f * q + 1.0f) - 1.0f) * 0.5f);
+    while (i * (i + 1) / 2 > q) i--;
+    while ((i + 1) * (i + 2) / 2 <= q) i++;
+    const int b = nc - 1 - i, a = nc - 1 - (q - i * (i + 1) / 2);
+    const int ca = ord[a], cb = ord[b];
+    double v = H[ca * 32 + cb];
+    if (v == 0.0) continue;
+    const int R = crow[ca], C = crow[cb];
+    if (a == b) v *= 1.0 + lambda;
+    const int32_t ti = tpair[cu[ca] * nu + cu[cb]];
+    if (ti >= 0) atomicAdd(d.tiles + (int64_t)ti * TS * TS + (C % TS) * TS + (R % TS), v);
+    else atomicOr(d.err, 4);
   }
 }
 
