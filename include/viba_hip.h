@@ -187,7 +187,9 @@ typedef struct vb_cost_stats { /* CostStats (Factor.h:20-30) */
   int64_t num_prev_invalid;
 } vb_cost_stats;
 
-typedef struct vb_phase_times { /* per-phase device time of the last LM iteration [ms] */
+typedef struct vb_phase_times { /* per-phase device time of the last LM iteration [ms]; linearize_ms of an
+                                   iteration vb_optimize linearized speculatively excludes the small
+                                   factors and the clear, which ran beside the previous cost pass */
   double linearize_ms, schur_ms, factor_ms, solve_ms, step_ms, cost_ms, total_ms;
   double rs_update_ms; /* device rolling-shutter table rebuild (0 with host tables) */
 } vb_phase_times;
