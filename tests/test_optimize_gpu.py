@@ -3,8 +3,10 @@ path, and the rescaling count, against the oracle's Optimizer::optimize (Optimiz
 
 vb_optimize queues the next iteration's rolling-shutter rebuild and linearization behind the cost pass,
 into second buffers, before the host has read the iteration's scalars; they are used only when the step
-is accepted at full size.  A prestep callback turns that off (the callback must run before the
-linearization), so the same problem with and without a callback runs both controller paths.
+is accepted at full size.  Its small factors and the clear start right after the box-plus, beside the
+cost pass (VIBA_SPEC_EARLY=0 at handle creation keeps them inside the speculative linearization).  A
+prestep callback turns speculation off (the callback must run before the linearization), so the same
+problem with and without a callback runs both controller paths.
 """
 from __future__ import annotations
 
@@ -38,12 +40,15 @@ def _assert_vars_close(g, r, tol=1e-7):
 
 @pytest.mark.parametrize("which", ["A", "miniB"])
 def test_speculative_and_plain_controller_match_oracle(which):
-    """The same optimize with speculation (no callback) and without (a prestep callback): both follow the
-    oracle's trajectory -- iterations, troubled sequences, rescaled steps, final cost, variables."""
+    """The same optimize with speculation (no callback; its side work beside the cost pass or inside the
+    speculative linearization) and without (a prestep callback): all follow the oracle's trajectory --
+    iterations, troubled sequences, rescaled steps, final cost, variables."""
     p = synth.generate(synth.config(which))
     runs = []
-    for cb in (None, lambda it: None):
-        e = hip()(imu_calib_options=p.imu_calib_options)
+    for cb, early in ((None, "1"), (None, "0"), (lambda it: None, "1")):
+        with pytest.MonkeyPatch.context() as mp:
+            mp.setenv("VIBA_SPEC_EARLY", early)  # read when the handle is created
+            e = hip()(imu_calib_options=p.imu_calib_options)
         synth.load_into(e, p, rs_device=True)
         runs.append((e, e.optimize(_settings(max_num_iterations=12), prestep=cb)))
     r = RefEngine(imu_calib_options=p.imu_calib_options)
