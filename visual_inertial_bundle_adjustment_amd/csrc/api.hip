@@ -788,6 +788,8 @@ int doFinalize(vb_handle h) {
   }
   h->rvOff[nRV] = off;
   const int64_t nRed = off;
+  // the small-factor assembly packs a reduced row with 5 more bits into an int32 (factors.hip)
+  if (nRed >= ((int64_t)1 << 26)) return fail(VB_E_ARG, "reduced system order must stay below 2^26");
   // owner of every tile column (parts start on tile boundaries; trailing padding joins the last part)
   {
     const int64_t nTc = (nRed + TS - 1) / TS;

@@ -889,7 +889,8 @@ constexpr int kAsmTiles = 7;
 template <int MM>
 __global__ void __launch_bounds__(256) small_assemble_kernel(Dev d, int mode, double* gOut, int64_t s0, int64_t s1) {
   __shared__ double Jl[4][MM * kMaxCols];
-  __shared__ int32_t act[4][kMaxCols][2];  // active column: (staged column, reduced row << 5 | tile-row slot + 1)
+  // active column: (staged column, reduced row << 5 | tile-row slot + 1; reduced rows < 2^26)
+  __shared__ int32_t act[4][kMaxCols][2];
   __shared__ int32_t trow[4][kAsmTiles];   // the factor's distinct tile rows
   __shared__ int32_t tpair[4][kAsmTiles * kAsmTiles];  // tileIdx of (tile row u, tile row v), u >= v
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
