@@ -167,9 +167,26 @@ def banded_contributions(p, device, rs_device, precision):
         del os.environ["VIBA_ND_OFF"]
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: run this script under torch.distributed.run with N ranks
+    (one per GPU, RCCL) as a child process, before anything here touches a GPU, and return its exit code
+    (the driver's own N > 1 form sets WORLD_SIZE and never comes here)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Under torch.distributed.run it must equal WORLD_SIZE; without it, "
+                         "N > 1 launches torch.distributed.run with N ranks as a child process")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C")
@@ -200,7 +217,12 @@ def main():
     if args.solver != "direct" and args.profile_family == KF_GEMM:
         args.profile_family = KF_SYMV  # no fan-in without the factorization: the PCG product instead
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:
+        log(f"[bench] --gpus {args.gpus} but WORLD_SIZE {world}: one rank per GPU is expected")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -263,15 +285,18 @@ def main():
         # nothing event-timed (the factorization ran from its HIP graph, or the family never launched)
         roof = None
     elif args.profile_family == KF_GEMM:
-        # st[6] tile-pair contributions per factorization (2 * 64^3 flops each), st[10] fan-in launches
-        # per factorization
-        per_launch = st[6] * 2.0 * 64 ** 3 / max(1, st[10])
+        # st[6] tile-pair contributions per factorization (2 * 64^3 flops each); one factorization per
+        # LM iteration (the rescaled / sub-step attempts reuse it), and the launches are the fan-in
+        # launches actually timed (levels without contributions launch none: 88 of the 89 levels at
+        # config C), so flops per launch = contributions x iterations / launches
+        fan_per_factor = launches / max(1, iters)
+        per_launch = st[6] * 2.0 * 64 ** 3 / max(1e-9, fan_per_factor)
         achieved = per_launch / (avg_ms * 1e-3) / 1e12
         # compulsory HBM bytes of one launch: within a level every contribution's L_IK is a distinct
         # tile (a column K has at most one ancestor column per level) and every L_JK is also the
         # I-side tile of the diagonal contribution (J, J, K), so the operands are pairs x 32 KB; each
         # target tile is read and written once (st[5] tiles over the launches bounds the targets)
-        compulsory = (st[6] * 64 * 64 * 8 + st[5] * 2 * 64 * 64 * 8) / max(1, st[10])
+        compulsory = (st[6] * 64 * 64 * 8 + st[5] * 2 * 64 * 64 * 8) / max(1e-9, fan_per_factor)
         traffic = pmc_traffic("fanin_kernel")
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": traffic,
@@ -280,6 +305,7 @@ def main():
                 "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
                           "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
                 "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches,
+                "fanin_launches_per_factorization": fan_per_factor, "levels": int(st[10]),
                 "ceiling_4x4x4_measured": FP64_MFMA_4X4X4_MEASURED_TF,
                 "frac_of_4x4x4_ceiling": achieved / FP64_MFMA_4X4X4_MEASURED_TF}
     elif args.profile_family == KF_SYMV:
@@ -347,4 +373,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -155,6 +155,7 @@ struct Problem {
   std::vector<int64_t> jacOff;
   std::vector<double> Vchol;      // per point lower Cholesky (9 doubles)
   std::vector<double> step, substep, gradNew;
+  bool absTerms = false;  // ref_abs_gradient: accumulate |A|^T |e| (the magnitude a gradient entry sums)
   // landmark shard (multi-device controller test): points [lmB, lmE) of the elimination range;
   // the root also owns the constant-point observations and every non-visual factor
   int64_t lmB = 0, lmE = -1;
@@ -608,6 +609,13 @@ double singleGradHess(Problem& P, int fk, int64_t k, double* g, bool hess, bool 
     A[s] = o.P.r ? mul(o.P, o.fe.J[s]) : o.fe.J[s];
     A[s] = scale(A[s], drho);
     Mat gs = tmul(A[s], e);  // iAdjJac^T e
+    if (P.absTerms) {  // test aid: sum of |A_ij e_i| (every product term's magnitude)
+      for (int j = 0; j < gs.r; j++) {
+        double a = 0;
+        for (int i = 0; i < m; i++) a += std::fabs(A[s](i, j) * e(i, 0));
+        gs(j, 0) = a;
+      }
+    }
     for (int i = 0; i < gs.r; i++) addTo(P, g[P.pstart[pi[s]] + i], gs(i, 0));
     if (hess) {
       for (int t = 0; t < s; t++) {
@@ -1638,6 +1646,18 @@ int ref_get_gradient(void* h, int kind, double* out) {
   Problem& P = *(Problem*)h;
   return getPerKind(P, P.grad, kind, out);
 }
+// Test aid (no reference counterpart): per entry of the gradient at the current variables, the sum of
+// the magnitudes of the terms computeGradHess adds into it (sum over factors and residual rows of
+// |rho' (P J)_ij e_i|).  A parity tolerance scaled by it bounds summation-order round-off per entry,
+// also for entries that are cancellation residues of much larger terms.
+int ref_abs_gradient(void* h, int kind, double* out) {
+  Problem& P = *(Problem*)h;
+  std::vector<double> g(P.order, 0.0);
+  P.absTerms = true;
+  computeGradHess(P, g.data(), false, false, false);
+  P.absTerms = false;
+  return getPerKind(P, g, kind, out);
+}
 
 // Optimizer::optimize (Optimizer.cpp:768-1106), direct solver; settings as vb_settings layout
 struct RefSettings {
@@ -1700,7 +1720,10 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
         applied *= sf;
         ref_scale_step(h, sf);
         ref_restore(h);
-        ref_apply_step(h, 0, ratios + 0);  // ratios of scaled steps are not used later
+        // :927 discards the scaled step's ratios: the variable tolerance (:1017) reads the full step's
+        // ratioS2Vn2 from :886, so these go to a scratch array
+        double rr[3];
+        ref_apply_step(h, 0, rr);
         int64_t stF[3];
         double costF;
         if ((rc = ref_cost(h, 1, &costF, stF))) return rc;
@@ -1718,7 +1741,6 @@ int ref_optimize(void* h, const RefSettings* s, ref_log_cb log, ref_prestep_cb p
           double br;
           if ((rc = ref_gradient_dot_step(h, dontRetry, &br))) return rc;
           ref_solve_with_new_gradient(h);
-          double rr[3];
           ref_apply_step(h, 1, rr);
           int64_t stS[3];
           double costS;

@@ -32,6 +32,19 @@ def one_step(engine, lam=1e-5):
     return out
 
 
+def gradient_entry_errors(grad, grad_ref, oracle):
+    """Per kind, max over entries of |grad - grad_ref| / (sum of the magnitudes of the terms the entry
+    sums, from the oracle at the same variables).  Summation-order round-off keeps this at a few ulp x
+    sqrt(terms); a wrong or lost term shows at O(1)."""
+    out = {}
+    for k, (a, b) in enumerate(zip(grad, grad_ref)):
+        if b.size:
+            s = oracle.abs_gradient(k)
+            d = np.abs(np.asarray(a) - b)
+            out[k] = float(np.max(d / np.maximum(s, 1e-300), initial=0.0))
+    return out
+
+
 def make(engine_cls, which="A", **kw):
     p = synth.generate(synth.config(which, **kw))
     e = engine_cls(imu_calib_options=p.imu_calib_options)

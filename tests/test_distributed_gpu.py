@@ -166,3 +166,58 @@ def test_config_C_multi_process(mode, precision, tmp_path):
     if mode == "partition":
         part = [np.load(tmp_path / f"rank{k}.npz")["part"] for k in range(world)]
         assert all(q[0] > 0 for q in part), part
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["partition", "shard"])
+def test_eight_ranks_config_B(mode, tmp_path):
+    """The 8-rank protocols themselves (config D's rank count), on this one-GPU box: eight processes share
+    cuda:0 over gloo at config-B size (2k rigs, 60k landmarks, 1.19M observations).  Partitioned: each rank
+    factors its subtree three levels below the top separators, rank 0 the ROOT separators above them;
+    shards: eight landmark bands, rank 0 factors.  Against the single GPU and the oracle over 3 iterations."""
+    world, which, its = 8, "B", 3
+    mp.spawn(_worker, args=(world, _free_port(), which, its, str(tmp_path), mode), nprocs=world, join=True)
+    _check_against_single(tmp_path, world, which, its)
+    if mode == "partition":
+        part = [np.load(tmp_path / f"rank{k}.npz")["part"] for k in range(world)]
+        assert all(q[0] > 0 for q in part), part  # every rank factors a subtree
+        assert part[0][1] > 0 and part[0][3] > 0, part[0]
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_line(tmp_path):
+    """`bench.py --gpus 2` (no launcher: it starts torch.distributed.run itself) with two gloo ranks sharing
+    cuda:0 on config B: one JSON line with n_gpus 2, the phase split of rank 0 filled in, and the single-GPU
+    engine's costs over the same warmup + timed iterations."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, VIBA_DIST_BACKEND="gloo", VIBA_DIST_SAME_DEVICE="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--config", "B", "--steps", "3",
+           "--warmup", "1", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=550)
+    (tmp_path / "bench.log").write_text(out.stderr)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["config"]["ranks_share_one_gpu"]
+    ph = line["phases_ms_rank0"]
+    assert ph["schur_ms"] > 0 and ph["factor_ms"] > 0 and ph["solve_ms"] > 0, ph
+    assert line["roofline"]["frac"] is not None and 0 < line["roofline"]["frac"] < 1
+    from visual_inertial_bundle_adjustment_amd import synth
+    from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
+    p = synth.generate(synth.config("B"))
+    e = HipEngine(imu_calib_options=p.imu_calib_options)
+    synth.load_into(e, p)
+
+    def settings(n):
+        return Settings.default(max_num_iterations=n, stop_if_no_improvement_for=10**6,
+                                distance_from_troubled_iteration=0)
+    e.optimize(settings(1))
+    s = e.optimize(settings(3))
+    e.close()
+    c0, c1 = line["cost"]
+    assert abs(c0 - s.initial_cost) <= 1e-10 * s.initial_cost
+    assert abs(c1 - s.final_cost) <= 1e-9 * s.final_cost
+

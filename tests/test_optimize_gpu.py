@@ -122,3 +122,21 @@ def test_nan_point_is_an_error_and_keeps_the_variables():
     assert ex.value.code == -4
     for k in range(NUM_VAR_KINDS - 1):
         assert np.array_equal(e.get_vars(k), v0[k], equal_nan=True), VAR_NAMES[k]
+
+
+def test_speculation_buffers_unavailable_falls_back_to_plain_controller():
+    """When the speculative linearization's spare buffers cannot be had (VIBA_DEBUG_SPEC_FAIL=1: specPrepare
+    fails after its first allocations and frees them), vb_optimize runs the plain controller instead of
+    failing, twice in a row on the same handle, and follows the oracle."""
+    p = synth.generate(synth.config("miniB"))
+    with pytest.MonkeyPatch.context() as mp:
+        mp.setenv("VIBA_DEBUG_SPEC_FAIL", "1")  # read when the handle is created
+        e = hip()(imu_calib_options=p.imu_calib_options)
+    synth.load_into(e, p, rs_device=True)
+    r = RefEngine(imu_calib_options=p.imu_calib_options)
+    synth.load_into(r, p, rs_device=True)
+    for its in (4, 5):
+        sg, sr = e.optimize(_settings(max_num_iterations=its)), r.optimize(_settings(max_num_iterations=its))
+        assert sg.num_iterations == sr.num_iterations and sg.num_rescaled == sr.num_rescaled
+        assert abs(sg.final_cost - sr.final_cost) <= 1e-9 * sr.final_cost
+    _assert_vars_close(e, r)

@@ -73,7 +73,7 @@ def test_rs_row_poses_errors():
 
 
 def test_session_folder_step_matches_oracle():
-    from parity_util import one_step, rel
+    from parity_util import gradient_entry_errors, one_step, rel
     q = adapter.build_problem(session.SessionData.load(GOLDEN))
     g, r = _engines(q)
     # the device's preintegrations of every inertial row against the oracle's
@@ -85,12 +85,14 @@ def test_session_folder_step_matches_oracle():
     assert abs(og["model_red"] - orf["model_red"]) <= 1e-9 * abs(orf["model_red"])
     assert abs(og["cost1"] - orf["cost1"]) <= 1e-9 * abs(orf["cost1"])
     assert og["stats1"] == orf["stats1"]
-    # (1e-9: the triangulated points start near their optimum, so their gradients are cancellation residues
-    # of terms many orders larger; the fp64 summation order -- atomics on the device -- shows at ~1e-10 of
-    # the largest entry)
-    for a, b in zip(og["grad"], orf["grad"]):
-        if b.size:
-            assert rel(a, b) < 1e-9
+    # per entry, against the sum of the magnitudes of the terms the entry adds up (the oracle's
+    # ref_abs_gradient at x0): the triangulated points start near their optimum, so their gradients are
+    # cancellation residues of terms many orders larger, and a tolerance relative to the largest entry
+    # (1e-9 here until round 4) cannot tell summation order from an assembly error.  Measured:
+    # gradient_entry_errors() below.
+    worst = gradient_entry_errors(og["grad"], orf["grad"], r)
+    print('gradient entry errors / term magnitudes:', worst)
+    assert max(worst.values()) < 1e-12, worst
     for a, b in zip(og["step"], orf["step"]):
         if b.size:
             assert rel(a, b) < 1e-8

@@ -372,6 +372,9 @@ struct vb_handle_s {
   hipEvent_t evCost = nullptr, evS[2][4] = {};
   double* hostRed = nullptr;  // pinned readback buffer: red[0, 17), then err[0, 2) as int32
   size_t profAtCost = 0;      // profiled event pairs recorded before evCost
+  bool specReady = false;     // every speculative buffer, event and stream above exists (specPrepare)
+  bool specFailDebug = false; // VIBA_DEBUG_SPEC_FAIL=1 at creation: specPrepare fails after its first
+                              // allocations (test of the release + plain-controller fallback)
   // state
   bool linearized = false, factored = false;
   vb_phase_times times{};
@@ -1967,6 +1970,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
   if (const char* e = getenv("VIBA_SPEC_EARLY")) h->specEarly = e[0] != '0';
+  if (const char* e = getenv("VIBA_DEBUG_SPEC_FAIL")) h->specFailDebug = e[0] == '1';
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2877,24 +2881,43 @@ int vb_reduced_buffers(vb_handle h, double** matrix, int64_t* matrix_len, double
 }
 
 // ---- vb_optimize's speculative linearization of the next iteration (vb_handle_s::tilesAlt ..)
-int specPrepare(vb_handle h) {
-  if (h->tilesAlt) return 0;
+// Frees whatever specPrepare got before a failure (nothing has been swapped into h->d then).
+void specRelease(vb_handle h) {
+  for (void* p : {(void*)h->tilesAlt, (void*)h->cacheAlt, (void*)h->gRedAlt, (void*)h->rsSAlt, (void*)h->rsIAlt,
+                  (void*)h->rsGAlt, (void*)h->rsNAlt})
+    if (p) (void)hipFree(p);
+  h->tilesAlt = h->cacheAlt = h->gRedAlt = h->rsSAlt = h->rsIAlt = h->rsGAlt = nullptr;
+  h->rsNAlt = nullptr;
+  for (auto& row : h->evS)
+    for (hipEvent_t& e : row)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+  if (h->evCost) (void)hipEventDestroy(h->evCost), h->evCost = nullptr;
+  if (h->stR) (void)hipStreamDestroy(h->stR), h->stR = nullptr;
+  if (h->hostRed) (void)hipHostFree(h->hostRed), h->hostRed = nullptr;
+  (void)hipGetLastError();
+}
+// The spare tile store (nTiles x 32 KB: 2.2 GB at config C), ResultCache, gradient and rolling-shutter
+// tables of the speculative linearization, allocated at the first vb_optimize that speculates.  Returns
+// false when any of it cannot be had: the caller then runs the plain controller (no speculation), as
+// before the speculative path existed, instead of failing a problem that fits without it.
+bool specPrepare(vb_handle h) {
+  if (h->specReady) return true;
   Dev& d = h->d;
-  if (alloc0(&h->tilesAlt, (size_t)d.nTiles * TS * TS) || alloc0(&h->cacheAlt, d.nObs) ||
-      alloc0(&h->gRedAlt, (size_t)d.nT * TS))
-    return VB_E_HIP;
-  if (h->rsDevice) {
+  bool ok = !alloc0(&h->tilesAlt, (size_t)d.nTiles * TS * TS) && !alloc0(&h->cacheAlt, d.nObs) &&
+            !alloc0(&h->gRedAlt, (size_t)d.nT * TS) && !h->specFailDebug;
+  if (ok && h->rsDevice) {
     const int64_t ns = h->rsOff[h->nRS];
-    if (alloc0(&h->rsSAlt, ns * 11) || alloc0(&h->rsIAlt, (ns - h->nRS) * 9) || alloc0(&h->rsGAlt, (size_t)h->nRS * 3) ||
-        alloc0(&h->rsNAlt, h->nRS))
-      return VB_E_HIP;
+    ok = !alloc0(&h->rsSAlt, ns * 11) && !alloc0(&h->rsIAlt, (ns - h->nRS) * 9) &&
+         !alloc0(&h->rsGAlt, (size_t)h->nRS * 3) && !alloc0(&h->rsNAlt, h->nRS);
   }
   for (auto& row : h->evS)
-    for (hipEvent_t& e : row) HIPCHK(hipEventCreate(&e));
-  HIPCHK(hipEventCreateWithFlags(&h->evCost, hipEventDisableTiming));
-  HIPCHK(hipStreamCreateWithFlags(&h->stR, hipStreamNonBlocking));
-  HIPCHK(hipHostMalloc((void**)&h->hostRed, 32 * sizeof(double), hipHostMallocDefault));
-  return 0;
+    for (hipEvent_t& e : row) ok = ok && hipEventCreate(&e) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&h->evCost, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipStreamCreateWithFlags(&h->stR, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&h->hostRed, 32 * sizeof(double), hipHostMallocDefault) == hipSuccess;
+  if (!ok) specRelease(h);
+  h->specReady = ok;
+  return ok;
 }
 // the buffers the speculative work writes instead of h->d's
 Dev specDev(vb_handle h) {
@@ -2983,9 +3006,8 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     return rate < 0.03 && (st.num_invalid < st.num_prev_invalid * 2.0 + 50);
   };
   const bool preint = h->recomputePreint && h->pi.n > 0;
-  const bool speculate = !pre && !preint && !h->sharded && h->partWorld <= 1;
-  if (speculate)
-    if (int rc = specPrepare(h)) return rc;
+  // (no memory for the spare buffers: the plain controller, which needs none)
+  const bool speculate = !pre && !preint && !h->sharded && h->partWorld <= 1 && specPrepare(h);
   bool specQueued = false;  // the current iteration's rebuild + linearization were queued speculatively
   int specSet = 0;
   int rc;
@@ -3025,7 +3047,7 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     const int wasSet = specSet;
     specQueued = false;
     if (speculate) {
-      HIPCHK(hipEventRecord(h->evCost, h->st));
+      if (hipEventRecord(h->evCost, h->st) != hipSuccess) return bail(fail(VB_E_HIP, "hipEventRecord"));
       h->profAtCost = h->profUsed;
       // the next iteration's rebuild + linearization, assuming this step is accepted at full size (not
       // after the last iteration: its work would only be discarded)
@@ -3457,6 +3479,12 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
     }
     hipEventDestroy(e0), hipEventDestroy(e1);
     if (avg_us) *avg_us = total * 1e3 / iters;
+    // the timed launches left partial sums in the striped reduction slots (no fold_red after them) and
+    // overwrote tiles, gradient and staging: clear the slots, and make the handle re-linearize before
+    // any solve or cost comparison uses that state
+    HIPCHK(hipMemsetAsync(d.redS, 0, 64 * 8 * sizeof(double), h->st));
+    HIPCHK(hipStreamSynchronize(h->st));
+    h->linearized = h->factored = false;
     return checkErr(h) == VB_E_HIP ? VB_E_HIP : 0;
   }
   Dev d = h->d;  // copy: tiles / err redirected to scratch
