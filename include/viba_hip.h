@@ -445,6 +445,39 @@ int vb_share_x(vb_handle h, double** xred, int64_t* len);
  *  of the ROOT schedule (rank 0 only), ROOT tiles exchanged per factorization] */
 int vb_part_info(vb_handle h, int64_t* out5);
 
+/* ---------------------------------------------------------------- deferred mode (multi-process LM)
+ * The multi-process controllers (distributed.py) read the LM scalars once per iteration, as
+ * vb_optimize does (Optimizer.cpp:800-1097 reads them phase by phase).  With vb_set_deferred(h, 1) the
+ * phase functions above (vb_update_rs_tables, vb_linearize, vb_assemble_reduced, vb_factor_solve_reduced,
+ * vb_solve_reduced, vb_factor_part, vb_solve_part, vb_part_exchange, vb_share_x, vb_pack_shard_tiles,
+ * vb_add_tiles, vb_back_substitute_which, vb_apply_step_raw, vb_cost) queue their device work and
+ * return without waiting; their scalar outputs are NaN, and the values stay in device slots
+ * (vb_scalar_slots) that the caller all-reduces in place on the handle's stream (vb_stream, RCCL) and
+ * reads once (vb_read_scalars).  Errors stay in the error words and are reported by vb_read_scalars. */
+int vb_set_deferred(vb_handle h, int on);
+/* device pointers: red[0] linearization cost, [1] cost-pass cost, [2..4] CostStats (numTotal of the
+ * visual factors, numInvalid, numPrevInvalid), [8] max step ratio, [9] sum of squared step ratios,
+ * [10] sum of step ratios, [16] twice the model cost reduction -- this handle's partials; err[0..2)
+ * error bit words (max / bitwise-or reducible) */
+int vb_scalar_slots(vb_handle h, double** red, int32_t** err);
+/* what numTotal adds for this handle's non-visual factors in the cost pass (the root's, else 0) */
+int vb_small_factor_count(vb_handle h, int64_t* n);
+/* record the point after which the slots hold the iteration's scalars (work queued later, e.g. a
+ * speculative linearization, does not delay vb_read_scalars); needs vb_spec_prepare */
+int vb_mark_scalars(vb_handle h);
+/* copy red[0, n) (n <= 24) to the host after the mark (or after all queued work) and return the error
+ * the error words encode (0 if none) */
+int vb_read_scalars(vb_handle h, double* out, int n);
+/* vb_optimize's speculative next-iteration linearization for an external controller: *ok = 1 when its
+ * spare buffers (a second tile store, ResultCache, gradient, rolling-shutter tables) are allocated */
+int vb_spec_prepare(vb_handle h, int* ok);
+/* queue the rolling-shutter rebuild (if device-built) and the linearization at the current variables
+ * into the spare buffers (ark_vi_ba's preStepCallback + Optimizer.cpp:807-812 of the next iteration) */
+int vb_spec_linearize(vb_handle h, int dont_retry_failed);
+/* use = 1 (the step stayed applied at full size): the spare buffers become the handle's and the handle
+ * is linearized (cost partial in red[0]); use = 0: dropped */
+int vb_spec_commit(vb_handle h, int use);
+
 /* the HIP stream of the handle (hipStream_t), for interop with torch / RCCL */
 void* vb_stream(vb_handle h);
 
@@ -457,7 +490,8 @@ int vb_profile_kernel(vb_handle h, int family);
 int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
 /* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs (per factorization),
  *  nSmallFactors, Schur landmark-pair entries, Schur observation-pair entries,
- *  fan-in launches per factorization, tiles of S without the symbolic fill] */
+ *  elimination levels (one fan-in launch each, except a level without contributions), tiles of S
+ *  without the symbolic fill] */
 int vb_problem_stats(vb_handle h, int64_t* out12);
 /* tuning aid: average time [us] of one kernel launch: on scratch tiles (which: 0 potrf, 1 trsm, 2 fan-in)
  * or, alone on the handle's own data (its results are not meant to be used afterwards), 10 visual

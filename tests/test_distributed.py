@@ -40,12 +40,14 @@ def _worker(rank, world, port, which, its, out_dir):
     n_pts = (e.total_order() - e.reduced_order()) // 3
     cuts = [n_pts * r // world for r in range(world + 1)]
     e.set_landmark_shard(cuts[rank], cuts[rank + 1], rank == 0)
-    s = ShardedOptimizer(e, ShardComm(rank, world, None)).optimize(_settings(its))
+    opt = ShardedOptimizer(e, ShardComm(rank, world, None))
+    s = opt.optimize(_settings(its))
     f = e.lib.ref_var_param
     f.restype, f.argtypes = C.c_int64, [C.c_void_p, C.c_int, C.c_int64]
     pts = e.get_vars(0)
     own = np.array([cuts[rank] <= f(e.h, 0, k) < cuts[rank + 1] for k in range(len(pts))])
-    res = {"iters": s.num_iterations, "initial": s.initial_cost, "final": s.final_cost, "own": own, "pts": pts}
+    res = {"iters": s.num_iterations, "initial": s.initial_cost, "final": s.final_cost, "own": own, "pts": pts,
+           "reads": np.array(opt.reads_per_iteration)}
     for k in range(1, 8):
         res[f"v{k}"] = e.get_vars(k)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
@@ -74,6 +76,12 @@ def test_two_shards_match_single_process(which, its, tmp_path):
         if len(ref):
             for k in range(world):
                 assert rel(r[k][f"v{kind}"], ref) < tol, kind
+    # one host read of the LM scalars per iteration that keeps its full step (the reduced scalars of
+    # linearize, model reduction, step ratios and cost pass read together); the step-rescaling path
+    # reads phase by phase, as Optimizer.cpp:907-1011 does
+    reads = r[0]["reads"]
+    assert len(reads) == s.num_iterations
+    assert all(n == 1 for n, resc in reads if not resc), reads
     pts = np.where(r[0]["own"][:, None], r[0]["pts"], r[1]["pts"])
     assert np.all(r[0]["own"] ^ r[1]["own"] | ~(r[0]["own"] | r[1]["own"]))
     assert rel(pts, e.get_vars(0)) < tol

@@ -48,8 +48,10 @@ def _worker(rank, world, port, which, its, out_dir, mode="shard", precision="fp6
         e.set_landmark_shard(lb, le, rank == 0)
         cls = ShardedOptimizer
     synth.load_into(e, p)
-    s = cls(e, ShardComm(rank, world, torch.device("cuda", 0))).optimize(Settings.default(max_num_iterations=its))
-    res = {"iters": s.num_iterations, "initial": s.initial_cost, "final": s.final_cost}
+    opt = cls(e, ShardComm(rank, world, torch.device("cuda", 0)))
+    s = opt.optimize(Settings.default(max_num_iterations=its))
+    res = {"iters": s.num_iterations, "initial": s.initial_cost, "final": s.final_cost,
+           "reads": np.array(opt.reads_per_iteration), "spec": opt.spec_used}
     if mode == "partition":
         res["part"] = np.array(e.part_info())
     for k in range(1, 8):
@@ -98,6 +100,13 @@ def _check_against_single(tmp_path, world, which, its, precision="fp64"):
     fp64) on the same inputs"""
     from parity_util import rel
     r = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
+    for k in range(world):
+        # the controller's pipelining: one host read of the LM scalars per iteration that keeps its full
+        # step (everything else -- exchanges, RCCL collectives -- is queued on the engine stream), and the
+        # next iteration's linearization queued speculatively behind the cost pass
+        reads = r[k]["reads"]
+        assert all(n == 1 for n, resc in reads if not resc), reads
+        assert bool(r[k]["spec"])
     for engine, ref_prec in ((precision, precision), ("oracle", "fp64")):
         ref = _reference_run(which, its, engine)
         cost_tol, var_tol = _TOL[(precision, ref_prec)]

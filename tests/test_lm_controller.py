@@ -68,15 +68,16 @@ def _py_worker(rank, world, port, which, settings_bytes, out_dir):
     n_pts = (e.total_order() - e.reduced_order()) // 3
     e.set_landmark_shard(0, n_pts, True)
     opt = ShardedOptimizer(e, ShardComm(rank, world, None))
-    # record every box-plus's ratios (full step first, then the rescaled attempts)
+    # record every box-plus's RMS ratio (full step first, then the rescaled attempts)
     applied = []
-    inner = opt.apply_step
+    inner = e.apply_step_raw
+    n = max(1, e.num_params())
 
-    def apply_step(which):
+    def apply_step_raw(which=0):
         r = inner(which)
-        applied.append((which, *r))
+        applied.append((which, r[0], (r[1] / n) ** 0.5, r[2] / n))
         return r
-    opt.apply_step = apply_step
+    e.apply_step_raw = apply_step_raw
     s = opt.optimize(Settings.from_buffer_copy(settings_bytes))
     np.savez(os.path.join(out_dir, "py.npz"), iters=s.num_iterations, rescaled=s.num_rescaled,
              final=s.final_cost, applied=np.array(applied),

@@ -373,6 +373,12 @@ struct vb_handle_s {
   double* hostRed = nullptr;  // pinned readback buffer: red[0, 17), then err[0, 2) as int32
   size_t profAtCost = 0;      // profiled event pairs recorded before evCost
   bool specReady = false;     // every speculative buffer, event and stream above exists (specPrepare)
+  // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
+  // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
+  bool deferred = false;
+  bool scalarsMarked = false;  // vb_mark_scalars recorded evCost since the last read
+  int specSet = 0;             // vb_spec_linearize's event set
+  bool specPending = false;    // a vb_spec_linearize awaits vb_spec_commit
   bool specFailDebug = false; // VIBA_DEBUG_SPEC_FAIL=1 at creation: specPrepare fails after its first
                               // allocations (test of the release + plain-controller fallback)
   // state
@@ -2134,6 +2140,7 @@ int vb_update_rs_tables(vb_handle h) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "vb_update_rs_tables before vb_finalize");
   if (!h->rsDevice) return fail(VB_E_STATE, "vb_update_rs_tables without vb_set_rs_rigs");
   if (int rc = rsUpdateAsync(h)) return rc;
+  if (h->deferred) return 0;
   int32_t e = 0;
   HIPCHK(hipMemcpyAsync(&e, h->d.err + 1, sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
   HIPCHK(hipStreamSynchronize(h->st));
@@ -2365,6 +2372,12 @@ int linearizeEnqueue(vb_handle h, int update_cache, int dont_retry_failed) {
 int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* cost) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "vb_linearize before vb_finalize");
   if (int rc = linearizeEnqueue(h, update_cache, dont_retry_failed)) return rc;
+  h->scalarsMarked = false;
+  if (h->deferred) {  // cost in red[0]
+    if (cost) *cost = std::nan("");
+    h->linearized = true, h->factored = false;
+    return 0;
+  }
   double c = 0;
   if (int rc = readRed(h, &c, 0, 1)) return rc;
   if (int rc = checkErr(h)) return rc;
@@ -2375,14 +2388,11 @@ int vb_linearize(vb_handle h, int update_cache, int dont_retry_failed, double* c
   return 0;
 }
 
-// vb_damp_factor_solve's device work (model dot in red[16]); clearErr = false keeps the linearization's
-// error bits for one check at the end of the iteration (vb_optimize)
-int dampFactorSolveEnqueue(vb_handle h, double lambda, bool clearErr) {
+// damp + eliminate the landmarks (of this shard) into the reduced system and its RHS: the observation-
+// group Gram blocks on the side stream beside the landmark elimination (both stream records from HBM;
+// neither reads what the other writes), joined before the tile products
+int assembleEnqueue(vb_handle h, double lambda) {
   Dev& d = h->d;
-  if (clearErr) HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  HIPCHK(hipEventRecord(h->ev[2], h->st));
-  // the observation-group Gram blocks on the side stream beside the landmark elimination (both stream
-  // records from HBM; neither reads what the other writes), joined before the tile products
   const int addId = (h->isRoot || h->partWorld > 1) ? 1 : 0;
   launch_damp(d, lambda, addId, h->st);
   HIPCHK(hipEventRecord(h->evFork, h->st));
@@ -2397,6 +2407,16 @@ int dampFactorSolveEnqueue(vb_handle h, double lambda, bool clearErr) {
   profBegin(h, KF_SCHUR);
   launch_schur_products(d, lambda, h->st);
   profEnd(h, KF_SCHUR);
+  return 0;
+}
+
+// vb_damp_factor_solve's device work (model dot in red[16]); clearErr = false keeps the linearization's
+// error bits for one check at the end of the iteration (vb_optimize)
+int dampFactorSolveEnqueue(vb_handle h, double lambda, bool clearErr) {
+  Dev& d = h->d;
+  if (clearErr) HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
+  HIPCHK(hipEventRecord(h->ev[2], h->st));
+  if (int rc = assembleEnqueue(h, lambda)) return rc;
   HIPCHK(hipEventRecord(h->ev[3], h->st));
   const bool fused = !pcgMode(h) && fwdFused(h);
   if (fused)  // the factorization runs the forward solve of rhsWork (into yvec)
@@ -2715,10 +2735,14 @@ int applyStepEnqueue(vb_handle h, int which, int e0, int e1) {
 }
 int vb_apply_step_raw(vb_handle h, int which, double raw[3]) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
-  if (int rc = applyStepEnqueue(h, which, 6, 7)) return rc;
+  if (int rc = applyStepEnqueue(h, which, 10, 11)) return rc;
+  if (h->deferred) {  // raw ratios in red[8..10]
+    if (raw) raw[0] = raw[1] = raw[2] = std::nan("");
+    return 0;
+  }
   double r[3];
   if (int rc = readRed(h, r, 8, 3)) return rc;
-  h->times.step_ms = elapsed(h->ev[6], h->ev[7]);
+  h->times.step_ms = elapsed(h->ev[10], h->ev[11]);
   if (raw) raw[0] = r[0], raw[1] = r[1], raw[2] = r[2];
   return 0;
 }
@@ -2753,7 +2777,11 @@ void costStats(vb_handle h, const double* r, double* cost, vb_cost_stats* stats)
 }
 int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
-  if (int rc = costEnqueue(h, comparable, true)) return rc;
+  if (int rc = costEnqueue(h, comparable, !h->deferred)) return rc;
+  if (h->deferred) {  // cost and CostStats in red[1..4] (vb_small_factor_count: the root's addition)
+    if (cost) *cost = std::nan("");
+    return 0;
+  }
   double r[4];
   if (int rc = readRed(h, r, 1, 4)) return rc;
   if (int rc = checkErr(h)) return rc;
@@ -3199,14 +3227,14 @@ int vb_pack_shard_tiles(vb_handle h, double** buf, int64_t* len) {
   if (!h || !h->finalized || !buf || !len) return fail(VB_E_STATE, "not finalized");
   const int64_t n = (int64_t)h->shardTiles.size();
   if (n) launch_tile_gather(h->d, h->shardTilesD, n, h->shardPack, h->st);
-  HIPCHK(hipStreamSynchronize(h->st));
+  if (!h->deferred) HIPCHK(hipStreamSynchronize(h->st));
   *buf = h->shardPack, *len = n * TS * TS;
   return 0;
 }
 int vb_add_tiles(vb_handle h, const int32_t* tiles_dev, int64_t n, const double* buf_dev) {
   if (!h || !h->finalized || n < 0 || (n && (!tiles_dev || !buf_dev))) return fail(VB_E_ARG, "bad vb_add_tiles arguments");
   if (n) launch_tile_scatter_add(h->d, tiles_dev, n, buf_dev, h->st);
-  HIPCHK(hipStreamSynchronize(h->st));
+  if (!h->deferred) HIPCHK(hipStreamSynchronize(h->st));
   return 0;
 }
 int vb_shard_tile_range(vb_handle h, int64_t* first_double, int64_t* num_doubles) {
@@ -3218,28 +3246,27 @@ int vb_shard_tile_range(vb_handle h, int64_t* first_double, int64_t* num_doubles
 // partial S (damped, Schur-reduced over this shard) in the tile store and partial RHS in rhs
 int vb_assemble_reduced(vb_handle h, double lambda) {
   if (!h || !h->linearized) return fail(VB_E_STATE, "vb_assemble_reduced needs vb_linearize");
-  Dev& d = h->d;
-  HIPCHK(hipMemsetAsync(d.err, 0, sizeof(int32_t), h->st));
-  launch_landmark(d, lambda, 0, d.lmB, d.lmE, h->st);
-  HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
-  launch_schur(d, lambda, (h->isRoot || h->partWorld > 1) ? 1 : 0, h->st);
-  HIPCHK(hipStreamSynchronize(h->st));
-  if (int rc = checkErr(h)) return rc;
+  if (!h->deferred) HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
+  HIPCHK(hipEventRecord(h->ev[2], h->st));
+  if (int rc = assembleEnqueue(h, lambda)) return rc;
+  HIPCHK(hipEventRecord(h->ev[3], h->st));
   h->linearized = false;
-  return 0;
+  if (h->deferred) return 0;
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkErr(h);
 }
 // root: factor the (summed) tile store and solve with the (summed) rhs; x_red is left in rhs
 int vb_factor_solve_reduced(vb_handle h) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
-  HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
+  if (!h->deferred) HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
   if (int rc = factorReduced(h)) return rc;
   HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (int rc = solveReduced(h)) return rc;
   HIPCHK(hipMemcpyAsync(h->d.rhs, h->d.xRed, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  HIPCHK(hipStreamSynchronize(h->st));
-  if (int rc = checkErr(h)) return rc;
   h->factored = true;
-  return 0;
+  if (h->deferred) return 0;
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkErr(h);
 }
 // root: solve with the existing factor, rhs -> x_red (left in rhs)
 int vb_solve_reduced(vb_handle h) {
@@ -3247,7 +3274,7 @@ int vb_solve_reduced(vb_handle h) {
   HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (int rc = solveReduced(h)) return rc;
   HIPCHK(hipMemcpyAsync(h->d.rhs, h->d.xRed, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
-  HIPCHK(hipStreamSynchronize(h->st));
+  if (!h->deferred) HIPCHK(hipStreamSynchronize(h->st));
   return 0;
 }
 // x_red (broadcast into rhs) -> step (which 0) / sub-step (which 1) of this shard; which 0 also
@@ -3258,7 +3285,9 @@ int vb_back_substitute_which(vb_handle h, int which, double* mcr) {
   HIPCHK(hipMemcpyAsync(d.xRed, d.rhs, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   backSubstitute(h, which);
   double v = 0;
-  if (which == 0) {
+  if (h->deferred) {  // partial model dot in red[16]
+    v = std::nan("");
+  } else if (which == 0) {
     if (int rc = readRed(h, &v, 16, 1)) return rc;
   } else {
     HIPCHK(hipStreamSynchronize(h->st));
@@ -3291,22 +3320,23 @@ int vb_set_partition(vb_handle h, int rank, int world) {
 // which 0: this rank's subtree columns (+ their fan-in into the ROOT tiles); 1 (rank 0): ROOT columns
 int vb_factor_part(vb_handle h, int which) {
   if (!h || !h->finalized || which < 0 || which > 1) return fail(VB_E_STATE, "vb_factor_part: bad state / schedule");
-  HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
+  if (!h->deferred) HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
   if (int rc = factorReduced(h, which)) return rc;
-  HIPCHK(hipStreamSynchronize(h->st));
-  if (int rc = checkErr(h)) return rc;
   h->factored = true;
-  return 0;
+  if (h->deferred) return 0;
+  HIPCHK(hipStreamSynchronize(h->st));
+  return checkErr(h);
 }
 // phase 0: rhsWork = rhs, forward solve over this rank's subtree (partial ROOT rows of rhsWork);
 // 1 (rank 0): forward + backward over the ROOT columns (ROOT rows of rhsWork summed);
 // 2: backward over this rank's subtree (ROOT rows of xRed given)
 int vb_solve_part(vb_handle h, int phase) {
   if (!h || !h->factored || phase < 0 || phase > 2) return fail(VB_E_STATE, "vb_solve_part: bad state / phase");
-  HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
+  if (!h->deferred) HIPCHK(hipMemsetAsync(h->d.err, 0, sizeof(int32_t), h->st));
   if (phase == 0)
     HIPCHK(hipMemcpyAsync(h->rhsWork, h->d.rhs, (size_t)h->d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, h->st));
   if (int rc = solveReduced(h, phase == 1 ? 1 : 0, phase == 0 ? 1 : phase == 1 ? 3 : 2)) return rc;
+  if (h->deferred) return 0;
   HIPCHK(hipStreamSynchronize(h->st));
   return checkErr(h);
 }
@@ -3322,10 +3352,81 @@ int vb_part_exchange(vb_handle h, int what, int dir, double** buf, int64_t* len)
   double* base = tiles ? h->d.tiles : what == 1 ? h->rhsWork : h->d.xRed;
   double* pk = tiles ? h->rootPack : h->rowPack;
   launch_chunk_copy(base, idx, n, tiles ? TS * TS : TS, pk, dir == 0 ? 0 : 1, h->st);
-  HIPCHK(hipStreamSynchronize(h->st));
+  if (!h->deferred) HIPCHK(hipStreamSynchronize(h->st));
   *buf = pk, *len = n * (tiles ? TS * TS : TS);
   return 0;
 }
+// ---------------- deferred mode: one host read per LM iteration in the multi-process controllers
+// (distributed.py).  With it on, the phase functions (vb_update_rs_tables, vb_linearize,
+// vb_assemble_reduced, vb_factor_solve_reduced, vb_solve_reduced, vb_factor_part, vb_solve_part,
+// vb_part_exchange, vb_share_x, vb_pack_shard_tiles, vb_add_tiles, vb_back_substitute_which,
+// vb_apply_step_raw, vb_cost) only queue their work; the scalars they would return stay in the
+// reduction slots, which the caller all-reduces in place on the handle's stream (RCCL) and reads once.
+int vb_set_deferred(vb_handle h, int on) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_set_deferred before vb_finalize");
+  h->deferred = on != 0;
+  return 0;
+}
+// red: [0] linearization cost, [1] cost pass cost, [2] observations evaluated, [3] invalid, [4] invalid
+// at the linearization point, [8] max |step| / |x| ratio, [9] sum of squared ratios, [10] sum of ratios,
+// [16] 2 x model cost reduction (partials of this handle); err: two error words (bitwise, max-reducible)
+int vb_scalar_slots(vb_handle h, double** red, int32_t** err) {
+  if (!h || !h->finalized) return fail(VB_E_STATE, "vb_scalar_slots before vb_finalize");
+  if (red) *red = h->d.red;
+  if (err) *err = h->d.err;
+  return 0;
+}
+// what the cost pass's CostStats.numTotal adds for the non-visual factors this handle evaluates
+int vb_small_factor_count(vb_handle h, int64_t* n) {
+  if (!h || !h->finalized || !n) return fail(VB_E_STATE, "vb_small_factor_count before vb_finalize");
+  *n = 0;
+  if (h->isRoot)
+    for (int k = 1; k < 14; k++) *n += h->d.sf[k].n;
+  return 0;
+}
+// the point on the stream after which the slots hold the iteration's (reduced) scalars: work queued
+// later (a speculative linearization) does not delay vb_read_scalars.  Needs vb_spec_prepare.
+int vb_mark_scalars(vb_handle h) {
+  if (!h || !h->specReady) return fail(VB_E_STATE, "vb_mark_scalars needs vb_spec_prepare");
+  if (hipEventRecord(h->evCost, h->st) != hipSuccess) return fail(VB_E_HIP, "hipEventRecord");
+  h->profAtCost = h->profUsed;
+  h->scalarsMarked = true;
+  return 0;
+}
+// red[0, n) (n <= 24) and the error words, after the mark (or the whole queue without one); the
+// return code is the error the words encode
+int vb_read_scalars(vb_handle h, double* out, int n) {
+  if (!h || !h->finalized || !out || n < 0 || n > 24) return fail(VB_E_ARG, "bad vb_read_scalars arguments");
+  const bool marked = h->scalarsMarked;
+  h->scalarsMarked = false;
+  return marked ? readIterScalars(h, out, n) : readRedErr(h, out, n);
+}
+// the speculative linearization of vb_optimize for an external controller: *ok = 0 when its spare
+// buffers cannot be had (then the controller linearizes every iteration itself)
+int vb_spec_prepare(vb_handle h, int* ok) {
+  if (!h || !h->finalized || !ok) return fail(VB_E_STATE, "vb_spec_prepare before vb_finalize");
+  *ok = specPrepare(h) ? 1 : 0;
+  return 0;
+}
+// queue the rolling-shutter rebuild and the linearization at the current (stepped) variables into the
+// spare buffers, behind everything queued so far
+int vb_spec_linearize(vb_handle h, int dont_retry_failed) {
+  if (!h || !h->specReady) return fail(VB_E_STATE, "vb_spec_linearize needs vb_spec_prepare");
+  h->specSet ^= 1;
+  h->specPending = true;
+  return specEnqueue(h, dont_retry_failed, h->specSet, false);
+}
+// use = 1: the step stayed applied at full size, the spare buffers become the handle's (the
+// linearization cost moves to red[0]); use = 0: drop them (the next vb_linearize overwrites)
+int vb_spec_commit(vb_handle h, int use) {
+  if (!h || !h->specReady || !h->specPending) return fail(VB_E_STATE, "vb_spec_commit without vb_spec_linearize");
+  h->specPending = false;
+  if (!use) return 0;
+  specCommit(h);
+  h->linearized = true, h->factored = false;
+  return 0;
+}
+
 // [subtree tile columns of this rank, ROOT tile columns, fan-in contributions of the local schedule,
 //  of the ROOT schedule (rank 0), ROOT tiles exchanged]
 int vb_part_info(vb_handle h, int64_t* out5) {
@@ -3345,7 +3446,7 @@ int vb_share_x(vb_handle h, double** xred, int64_t* len) {
   HIPCHK(hipMemsetAsync(d.rhs, 0, (size_t)d.nT * TS * sizeof(double), h->st));
   launch_chunk_copy(d.xRed, h->ownRowsD, h->nOwnRows, TS, h->ownPack, 0, h->st);
   launch_chunk_copy(d.rhs, h->ownRowsD, h->nOwnRows, TS, h->ownPack, 1, h->st);
-  HIPCHK(hipStreamSynchronize(h->st));
+  if (!h->deferred) HIPCHK(hipStreamSynchronize(h->st));
   *xred = d.rhs, *len = (int64_t)d.nT * TS;
   return 0;
 }

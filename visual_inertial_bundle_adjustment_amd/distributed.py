@@ -4,21 +4,26 @@ Every rank holds the whole problem but owns one time band of landmarks (landmark
 earliest observing rig, cut into contiguous ranges balanced by observation count): it linearizes the
 visual factors of its landmarks, eliminates them and forms its partial damped Schur-reduced system.
 The root (rank 0) also owns every small factor (IMU, omega, random walks, priors), the constant-point
-observations and the identity damping term.  Per LM iteration:
+observations and the identity damping term.  Per LM iteration, everything is queued on the engine's
+stream (deferred mode, vb_set_deferred) and the host reads the LM scalars ONCE:
 
-  1. each rank: linearize (partial cost)                           -> all-reduce 1 scalar
+  1. each rank: linearize (partial cost) -- or commit the linearization queued speculatively behind the
+     previous iteration's cost pass
   2. each rank: partial reduced system S_r, RHS b_r                 (vb_assemble_reduced)
-  3. S = sum S_r on the root: each rank sends only the contiguous tile band its landmarks touch
-     (point-to-point over RCCL/xGMI), b = sum b_r by reduce
+  3. S = sum S_r on the root: each rank sends the tiles its landmarks touch (point-to-point over
+     RCCL/xGMI), b = sum b_r by reduce
   4. root: factor S, solve x_red                                    (vb_factor_solve_reduced)
   5. broadcast x_red (reduced order x 8 B)
-  6. each rank: back-substitute its points, partial model reduction -> all-reduce 1 scalar
-  7. box-plus (every rank applies the reduced step; points per shard), step ratios -> all-reduce
-  8. cost pass (partial cost + CostStats)                           -> all-reduce 4 scalars
-The LM decisions (Optimizer.cpp:768-1106, restated by vb_optimize) run identically on every rank
-from the all-reduced scalars.  The bad-step path (step rescale, sub-step with the existing factor)
-uses the same pattern (vb_gradient_dot_step partial scalar; vb_assemble_new_rhs -> reduce ->
-root vb_solve_reduced -> broadcast -> vb_back_substitute_which(1)).
+  6. each rank: back-substitute its points (partial model reduction)
+  7. box-plus (every rank applies the reduced step; points per shard) (partial step ratios)
+  8. cost pass (partial cost + CostStats)
+  9. the partial scalars of 1, 6, 7, 8 all-reduced in place on the engine stream, then the next
+     iteration's linearization queued speculatively (vb_spec_linearize), then one host read
+The LM decisions (Optimizer.cpp:834-1097, restated by vb_optimize) run identically on every rank from
+the reduced scalars.  The bad-step path (step rescale, sub-step with the existing factor) reads its
+scalars phase by phase, as the reference does (vb_gradient_dot_step partial scalar; vb_assemble_new_rhs
+-> reduce -> root vb_solve_reduced -> broadcast -> vb_back_substitute_which(1)), and drops the
+speculative linearization.
 
 The controller is engine-agnostic: the HIP engine (device buffers, RCCL) in production, the CPU
 oracle (host buffers, gloo) in the CPU tests.
@@ -27,8 +32,8 @@ Stream ordering, not host round trips: with the HIP engine, the loop runs with t
 set to the engine's own HIP stream (torch.cuda.ExternalStream over vb_stream).  RCCL then queues
 each collective behind the engine kernels that produced its input, and the engine kernels that
 consume its output queue behind the collective, so no exchange needs a stream or device
-synchronisation; the host waits only where the LM logic reads a scalar (cost, model reduction,
-step ratios), as Optimizer::optimize does.
+synchronisation; the host waits once per iteration, for the reduced LM scalars (with gloo, the
+one-GPU test transport, every exchange is additionally staged through host memory).
 """
 from __future__ import annotations
 
@@ -47,18 +52,19 @@ from .engine import Settings, Summary
 class _CudaArray:
     """Minimal __cuda_array_interface__ exporter for a device pointer (no copy)."""
 
-    def __init__(self, ptr: int, n: int):
-        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False),
+    def __init__(self, ptr: int, n: int, typestr: str = "<f8"):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
                                          "version": 3, "strides": None}
 
 
-def _tensor(ptr: int, n: int, device):
+def _tensor(ptr: int, n: int, device, int32: bool = False):
     import torch
     if n == 0:
-        return torch.zeros(0, dtype=torch.float64, device=device)
+        return torch.zeros(0, dtype=torch.int32 if int32 else torch.float64, device=device)
     if device is None or device.type == "cpu":
-        return torch.from_numpy(np.ctypeslib.as_array((C.c_double * n).from_address(ptr)))
-    return torch.as_tensor(_CudaArray(ptr, n), device=device)
+        ct = C.c_int32 if int32 else C.c_double
+        return torch.from_numpy(np.ctypeslib.as_array((ct * n).from_address(ptr)))
+    return torch.as_tensor(_CudaArray(ptr, n, "<i4" if int32 else "<f8"), device=device)
 
 
 class ShardComm:
@@ -73,16 +79,21 @@ class ShardComm:
         self.rank, self.world, self.device = rank, world, device
         self.nccl = dist.get_backend() == "nccl"
         self.sdev = device if self.nccl else None  # where scalar tensors live
+        # host waits for an LM scalar (a collective whose result the host reads): the measure of the
+        # controller's pipelining (tests/test_distributed*.py count it per iteration)
+        self.host_reads = 0
 
     # scalars
     def sum(self, *vals):
         t = self.torch.tensor(vals, dtype=self.torch.float64, device=self.sdev)
         self.dist.all_reduce(t)
+        self.host_reads += 1
         return t.tolist()
 
     def max(self, v):
         t = self.torch.tensor([v], dtype=self.torch.float64, device=self.sdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self.host_reads += 1
         return t.item()
 
     def all_gather_obj(self, obj):
@@ -161,6 +172,91 @@ class ShardComm:
                     w.wait()
 
 
+# ------------------------------------------------------------------ one scalar read per iteration
+class _IterScalars:
+    """The LM scalars of one iteration (vb_scalar_slots layout: [0] linearization cost, [1] cost pass
+    cost, [2..4] CostStats, [8] max step ratio, [9] sum of squared ratios, [10] sum of ratios, [16] twice
+    the model cost reduction), reduced over the ranks and read by the host ONCE per iteration.
+
+    HIP engine (deferred mode, vb_set_deferred): the phase functions leave their partials in the
+    engine's device slots.  With RCCL they are all-reduced in place on the engine stream (sum; the max
+    ratio and the error words by max), the scalar point is marked (vb_mark_scalars) so work queued after
+    it -- the next iteration's speculative linearization -- does not delay the read, and the host reads
+    them once (vb_read_scalars).  With gloo (host-staged) the host reads the partials once and the
+    reduction runs on host tensors.  Host engines (the oracle): the phase functions return their
+    partials, collected here, reduced over gloo."""
+
+    SUM = [0, 1, 2, 3, 4, 9, 10, 16]
+
+    def __init__(self, engine, comm: ShardComm):
+        self.e, self.c = engine, comm
+        torch = comm.torch
+        self.device = (hasattr(engine, "scalar_slots") and comm.device is not None
+                       and comm.device.type != "cpu")
+        if self.device:
+            rp, ep = engine.scalar_slots()
+            self.red = _tensor(rp, 24, comm.device)
+            self.err = _tensor(ep, 2, comm.device, int32=True)
+            small = engine.small_factor_count()
+            self.spec = engine.spec_prepare()
+        else:
+            self.host = np.zeros(17)
+            small = 0  # the host engine's CostStats count every factor it evaluates
+            self.spec = False
+        # numTotal of the non-visual factors (the deferred cost pass leaves them out of red[2])
+        self.n_small = int(sum(comm.all_gather_obj(small)))
+        self.torch = torch
+
+    def set(self, i, v):
+        """a host engine's partial (device slots are written by the engine itself)"""
+        if not self.device:
+            self.host[i] = v
+
+    def read(self, queue_after=None):
+        """reduce + one host read; queue_after() is called once the scalars' point is queued (so the
+        work it queues overlaps the read).  Returns the 17 reduced scalars (numTotal completed)."""
+        c, torch = self.c, self.torch
+        dist = c.dist
+        if self.device and c.nccl:
+            red, err = self.red, self.err
+            mx = torch.cat([red[8:9], err.to(torch.float64)])
+            dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+            red[5:9].zero_()
+            red[11:16].zero_()
+            dist.all_reduce(red[0:17])
+            red[8:9].copy_(mx[0:1])
+            err.copy_(mx[1:3].to(torch.int32))
+            if self.spec:
+                self.e.mark_scalars()
+            if queue_after:
+                queue_after()
+            rc, v = self.e.read_scalars(17, check=False)
+        else:
+            if self.device:
+                if self.spec:
+                    self.e.mark_scalars()
+                if queue_after:
+                    queue_after()
+                rc, v = self.e.read_scalars(17, check=False)
+            else:
+                rc, v = 0, self.host.copy()
+            t = torch.tensor([v[i] for i in self.SUM], dtype=torch.float64)
+            m = torch.tensor([v[8], -float(rc)], dtype=torch.float64)
+            dist.all_reduce(t)
+            dist.all_reduce(m, op=dist.ReduceOp.MAX)
+            v = np.zeros(17)
+            v[self.SUM] = t.numpy()
+            v[8], rc = float(m[0]), -int(round(float(m[1])))
+        c.host_reads += 1
+        if rc:  # every rank raises the same code (the error words are reduced over the ranks)
+            from .engine import VbError
+            raise VbError(rc, f"LM iteration failed (error words over {c.world} ranks; this rank's last error: "
+                              f"{self.e.last_error()})")
+        v = np.array(v, dtype=np.float64)
+        v[2] += self.n_small
+        return v
+
+
 # ------------------------------------------------------------------ the sharded LM controller
 class ShardedOptimizer:
     """Optimizer::optimize (Optimizer.cpp:768-1106) over landmark shards; mirrors vb_optimize."""
@@ -203,7 +299,9 @@ class ShardedOptimizer:
     def linearize(self, dont_retry):
         return self.c.sum(self.e.linearize(True, dont_retry))[0]
 
-    def damp_factor_solve(self, lam):
+    def factor_solve_partial(self, lam):
+        """damp + eliminate + exchange + factor + solve + back-substitute; returns this rank's partial
+        model cost reduction (NaN in deferred mode: it stays in the engine's slot 16 as twice that)"""
         e, c = self.e, self.c
         self.n_factor += 1
         self.phases.mark("schur_ms")
@@ -223,7 +321,10 @@ class ShardedOptimizer:
         S, b = self._buffers()
         c.broadcast_from_root(b)
         self.sync_torch()
-        return c.sum(e.back_substitute(0))[0]
+        return e.back_substitute(0)
+
+    def damp_factor_solve(self, lam):
+        return self.c.sum(self.factor_solve_partial(lam))[0]
 
     def gradient_dot_step(self, dont_retry):
         return self.c.sum(self.e.gradient_dot_step(dont_retry))[0]
@@ -272,87 +373,136 @@ class ShardedOptimizer:
         troubled_start_damping, troubled_start, n_troubled, largest_troubled = damping, 0, 0, 0
         n_rescaled = 0
         dont_retry = False
+        deferred = hasattr(e, "set_deferred")
+        sc = _IterScalars(e, self.c)
+        self.spec_used = sc.spec
+        spec_pending = False  # the next iteration's linearization was queued speculatively
+        # per iteration: (host reads of LM scalars, whether it took the step-rescaling path)
+        self.reads_per_iteration = []
+        reads0 = self.c.host_reads
 
         def acceptable(st):
             rate = st[1] / (st[0] + 1.0)
             return rate < 0.03 and st[1] < st[2] * 2.0 + 50
 
-        while True:
-            self.phases.mark("rs_update_ms")
-            if getattr(e, "rs_device", False):  # ark_vi_ba's preStepCallback (vb_optimize does the same)
-                e.update_rs_tables()
-            self.phases.mark("linearize_ms")
-            prev_cost = self.linearize(dont_retry)
-            final_cost = prev_cost
-            if it == 0:
-                initial_cost = prev_cost
-            model_red = self.damp_factor_solve(damping)
-            if model_red < 0:  # Optimizer.cpp:835-854 (see vb_optimize)
-                damping *= s.damping_adjust_on_fail
-            e.backup()
-            self.phases.mark("step_ms")
-            ratios = self.apply_step(0)
-            self.phases.mark("cost_ms")
-            new_cost, st = self.cost(True)
-            self.phases.close_iteration()
-            cost_red = prev_cost - new_cost
-            ratio_red_to_cost = cost_red / new_cost
-            ratio_red_to_exp = cost_red / model_red
-            applied = 1.0
-            ok_rate = acceptable(st)
-            if s.max_step_factor_attempts > 0 and (ratio_red_to_exp < s.min_relative_cost_reduction or not ok_rate):
-                n_rescaled += 1
-                back_red = self.gradient_dot_step(dont_retry)
-                sf = model_red / (model_red + back_red) if back_red > 0 else s.step_factor_decrease
-                for _ in range(s.max_step_factor_attempts):
-                    applied *= sf
-                    e.scale_step(sf)
-                    e.restore()
-                    self.apply_step(0)
-                    cost_f, st_f = self.cost(True)
-                    red_f = prev_cost - new_cost  # Optimizer.cpp:935
-                    r_f = red_f / (model_red * applied)
-                    if r_f >= s.min_relative_cost_reduction and acceptable(st_f):
-                        new_cost, st, cost_red, ratio_red_to_exp, ok_rate = cost_f, st_f, red_f, r_f, True
-                        break
-                    if s.try_sub_step:
-                        self.gradient_dot_step(dont_retry)
-                        self.solve_with_new_gradient()
-                        self.apply_step(1)
-                        cost_s, st_s = self.cost(True)
-                        red_s = prev_cost - cost_s
-                        r_s = red_s / (model_red * applied)
-                        if r_s >= s.min_relative_cost_reduction and acceptable(st_s):
-                            new_cost, st, cost_red, ratio_red_to_exp, ok_rate = cost_s, st_s, red_s, r_s, True
-                            break
-                    dont_retry = True
-                    sf = s.step_factor_decrease
-            tol = (ratio_red_to_cost < s.relative_cost_tolerance or cost_red < s.absolute_cost_tolerance
-                   or ratios[1] < s.variables_tolerance)
-            if new_cost > prev_cost or not ok_rate:
-                if last_troubled != it - 1:
-                    troubled_start_damping, troubled_start = damping, it
-                damping *= s.damping_adjust_on_fail
-                e.restore()
-                if damping > s.damping_max:
-                    break
-                last_troubled = it
-            else:
-                if last_troubled == it - 1 and troubled_start_damping < 1e1 and damping > 1e-3:
-                    n_troubled += 1
-                    largest_troubled = max(largest_troubled, it - troubled_start)
-                if ratio_red_to_exp >= s.min_relative_cost_reduction and applied > s.min_step_factor_for_good:
-                    damping = max(damping * s.damping_adjust_on_good_step, s.damping_min)
+        try:
+            while True:
+                # ---- queued: linearize, damp + eliminate + exchange + factor + solve, backup, box-plus,
+                # cost pass; their scalars reduced over the ranks and read once (vb_optimize's pattern)
+                if deferred:
+                    e.set_deferred(True)
+                if spec_pending:
+                    e.spec_commit(True)  # the step stayed applied at full size: its linearization is ready
+                    spec_pending = False
                 else:
-                    damping *= s.damping_adjust_on_average_step
-                final_cost = new_cost
-            it += 1
-            if not tol:
-                last_impr = it
-            if it >= last_impr + s.stop_if_no_improvement_for and it >= last_troubled + s.distance_from_troubled_iteration:
-                break
-            if it >= s.max_num_iterations:
-                break
+                    self.phases.mark("rs_update_ms")
+                    if getattr(e, "rs_device", False):  # ark_vi_ba's preStepCallback (as vb_optimize)
+                        e.update_rs_tables()
+                    self.phases.mark("linearize_ms")
+                    sc.set(0, e.linearize(True, dont_retry))
+                sc.set(16, 2.0 * self.factor_solve_partial(damping))
+                e.backup()
+                self.phases.mark("step_ms")
+                for i, x in zip((8, 9, 10), e.apply_step_raw(0)):
+                    sc.set(i, x)
+                self.phases.mark("cost_ms")
+                cost, st = e.cost(True)
+                sc.set(1, cost)
+                for i, x in zip((2, 3, 4), st):
+                    sc.set(i, x)
+                self.phases.mark(None)
+                speculate = sc.spec and it + 1 < s.max_num_iterations
+
+                def queue_spec():
+                    self.phases.mark("spec_linearize_ms")
+                    e.spec_linearize(dont_retry)
+                    self.phases.mark(None)
+                v = sc.read(queue_spec if speculate else None)
+                spec_pending = speculate
+                if deferred:
+                    e.set_deferred(False)
+                self.phases.close_iteration()
+                n = max(1, self.n_params)
+                prev_cost, new_cost, model_red = v[0], v[1], 0.5 * v[16]
+                st = (int(round(v[2])), int(round(v[3])), int(round(v[4])))
+                ratios = (v[8], math.sqrt(v[9] / n), v[10] / n)
+                # ---- the LM decisions (Optimizer.cpp:834-1097), identical on every rank
+                final_cost = prev_cost
+                if it == 0:
+                    initial_cost = prev_cost
+                if model_red < 0:  # Optimizer.cpp:835-854 (see vb_optimize)
+                    damping *= s.damping_adjust_on_fail
+                cost_red = prev_cost - new_cost
+                ratio_red_to_cost = cost_red / new_cost
+                ratio_red_to_exp = cost_red / model_red
+                applied = 1.0
+                ok_rate = acceptable(st)
+                rescaled = False
+                if s.max_step_factor_attempts > 0 and (ratio_red_to_exp < s.min_relative_cost_reduction or not ok_rate):
+                    rescaled, n_rescaled = True, n_rescaled + 1
+                    back_red = self.gradient_dot_step(dont_retry)
+                    sf = model_red / (model_red + back_red) if back_red > 0 else s.step_factor_decrease
+                    for _ in range(s.max_step_factor_attempts):
+                        applied *= sf
+                        e.scale_step(sf)
+                        e.restore()
+                        self.apply_step(0)  # (its ratios are discarded, Optimizer.cpp:927)
+                        cost_f, st_f = self.cost(True)
+                        red_f = prev_cost - new_cost  # Optimizer.cpp:935
+                        r_f = red_f / (model_red * applied)
+                        if r_f >= s.min_relative_cost_reduction and acceptable(st_f):
+                            new_cost, st, cost_red, ratio_red_to_exp, ok_rate = cost_f, st_f, red_f, r_f, True
+                            break
+                        if s.try_sub_step:
+                            self.gradient_dot_step(dont_retry)
+                            self.solve_with_new_gradient()
+                            self.apply_step(1)
+                            cost_s, st_s = self.cost(True)
+                            red_s = prev_cost - cost_s
+                            r_s = red_s / (model_red * applied)
+                            if r_s >= s.min_relative_cost_reduction and acceptable(st_s):
+                                new_cost, st, cost_red, ratio_red_to_exp, ok_rate = cost_s, st_s, red_s, r_s, True
+                                break
+                        dont_retry = True
+                        sf = s.step_factor_decrease
+                tol = (ratio_red_to_cost < s.relative_cost_tolerance or cost_red < s.absolute_cost_tolerance
+                       or ratios[1] < s.variables_tolerance)
+                rejected = new_cost > prev_cost or not ok_rate
+                if spec_pending and (rejected or rescaled):  # it assumed the full step stays applied
+                    e.spec_commit(False)
+                    spec_pending = False
+                if rejected:
+                    if last_troubled != it - 1:
+                        troubled_start_damping, troubled_start = damping, it
+                    damping *= s.damping_adjust_on_fail
+                    e.restore()
+                    if damping > s.damping_max:
+                        break
+                    last_troubled = it
+                else:
+                    if last_troubled == it - 1 and troubled_start_damping < 1e1 and damping > 1e-3:
+                        n_troubled += 1
+                        largest_troubled = max(largest_troubled, it - troubled_start)
+                    if ratio_red_to_exp >= s.min_relative_cost_reduction and applied > s.min_step_factor_for_good:
+                        damping = max(damping * s.damping_adjust_on_good_step, s.damping_min)
+                    else:
+                        damping *= s.damping_adjust_on_average_step
+                    final_cost = new_cost
+                self.reads_per_iteration.append((self.c.host_reads - reads0, rescaled))
+                reads0 = self.c.host_reads
+                it += 1
+                if not tol:
+                    last_impr = it
+                if it >= last_impr + s.stop_if_no_improvement_for and it >= last_troubled + s.distance_from_troubled_iteration:
+                    break
+                if it >= s.max_num_iterations:
+                    break
+        finally:
+            if spec_pending:  # a convergence stop left it queued: never used
+                e.spec_commit(False)
+            if deferred:
+                e.set_deferred(False)
+            self.phases.close_iteration(final=True)
         out = Summary()
         out.initial_cost, out.final_cost = initial_cost, final_cost
         out.num_troubled_seqs, out.largest_troubled_seq, out.num_iterations = n_troubled, largest_troubled, it
@@ -361,20 +511,24 @@ class ShardedOptimizer:
 
 
 class _PhaseClock:
-    """Per-phase device time of the last LM iteration (vb_phase_times semantics), from torch.cuda events
-    recorded on the engine's stream at the phase boundaries: no extra synchronisation; the times are read
-    once the iteration's cost has been read back.  A phase's time includes its collectives and any
-    stream idle while the host stages them (gloo).  Host engines: nothing is recorded."""
+    """Per-phase device time of an LM iteration (vb_phase_times semantics), from torch.cuda events recorded
+    on the engine's stream at the phase boundaries, without extra synchronisation: an iteration's marks are
+    evaluated at the next iteration's close (or the final one), when the device has passed them.  A phase's
+    time includes its collectives and any stream idle while the host stages them (gloo).  An iteration whose
+    linearization was queued speculatively by the previous one has no rs_update / linearize marks; the
+    previous iteration's spec_linearize_ms is that work.  Host engines: nothing is recorded."""
 
-    NAMES = ("rs_update_ms", "linearize_ms", "schur_ms", "factor_ms", "solve_ms", "step_ms", "cost_ms")
+    NAMES = ("rs_update_ms", "linearize_ms", "schur_ms", "factor_ms", "solve_ms", "step_ms", "cost_ms",
+             "spec_linearize_ms")
 
     def __init__(self, ext):
         self.ext = ext
         self.ms = {k: 0.0 for k in self.NAMES}
-        self.marks = []
+        self.marks = []    # the iteration being queued
+        self.pending = []  # the last closed iteration, evaluated at the next close
 
     def mark(self, name):
-        """The phase `name` starts here (None: the iteration ends)."""
+        """The phase `name` starts here (None: nothing is timed from here)."""
         if self.ext is None:
             return
         import torch
@@ -382,17 +536,24 @@ class _PhaseClock:
         ev.record(self.ext)
         self.marks.append((name, ev))
 
-    def close_iteration(self):
-        if self.ext is None or not self.marks:
-            return
-        self.mark(None)
-        self.marks[-1][1].synchronize()
+    def _evaluate(self, marks):
+        marks[-1][1].synchronize()
         ms = {k: 0.0 for k in self.NAMES}
-        for (name, a), (_, b) in zip(self.marks, self.marks[1:]):
+        for (name, a), (_, b) in zip(marks, marks[1:]):
             if name is not None:
                 ms[name] += a.elapsed_time(b)
-        ms["total_ms"] = self.marks[0][1].elapsed_time(self.marks[-1][1])
-        self.ms, self.marks = ms, []
+        ms["total_ms"] = marks[0][1].elapsed_time(marks[-1][1])
+        self.ms = ms
+
+    def close_iteration(self, final=False):
+        if self.ext is None:
+            return
+        if self.pending:
+            self._evaluate(self.pending)
+        self.pending, self.marks = self.marks, []
+        if final and self.pending:
+            self._evaluate(self.pending)
+            self.pending = []
 
 
 class PartitionedOptimizer(ShardedOptimizer):
@@ -448,7 +609,7 @@ class PartitionedOptimizer(ShardedOptimizer):
         self.sync_torch()
         return e.back_substitute(which)
 
-    def damp_factor_solve(self, lam):
+    def factor_solve_partial(self, lam):
         e, c = self.e, self.c
         self.n_factor += 1
         self.phases.mark("schur_ms")
@@ -459,7 +620,7 @@ class PartitionedOptimizer(ShardedOptimizer):
         if c.rank == 0:
             e.factor_part(1)
         self.phases.mark("solve_ms")
-        return c.sum(self._solve(0))[0]
+        return self._solve(0)
 
     def solve_with_new_gradient(self):
         self.e.assemble_new_rhs()
@@ -581,6 +742,7 @@ def run_sharded(args, rank: int, world: int, local: int):
     flops = float(opt.n_factor) * contrib * 2.0 * 64 ** 3
     per_rank = comm.all_gather_obj((launches, kms, flops))
     phases = comm.all_gather_obj({k: round(v, 3) for k, v in opt.phases.ms.items()})
+    reads = opt.reads_per_iteration
     ph = phases[0]
     dist_backend = dist.get_backend()
     dist.destroy_process_group()
@@ -621,5 +783,8 @@ def run_sharded(args, rank: int, world: int, local: int):
                       "ranks_share_one_gpu": same_device},
            "roofline": roof, "cpu_baseline": cpu,
            "phases_ms_rank0": ph, "phases_ms_per_rank": phases,
+           # the controller's pipelining: host reads of LM scalars per timed iteration (1 unless the
+           # iteration rescaled its step), and whether the next linearization was queued speculatively
+           "host_reads_per_iteration": [int(n) for n, _ in reads], "speculative_linearization": bool(opt.spec_used),
            "cost": [s.initial_cost, s.final_cost]}
     print(json.dumps(out), flush=True)

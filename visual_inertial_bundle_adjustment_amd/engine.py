@@ -128,9 +128,12 @@ class CEngineBase:
 
     def _check(self, rc: int):
         if rc != 0:
-            err = getattr(self.lib, self.prefix + "last_error")
-            err.restype = C.c_char_p
-            raise VbError(rc, err().decode())
+            raise VbError(rc, self.last_error())
+
+    def last_error(self) -> str:
+        err = getattr(self.lib, self.prefix + "last_error")
+        err.restype = C.c_char_p
+        return err().decode()
 
     # ---------------------------------------------------------------- problem
     def set_vars(self, kind: int, data, const=None):
@@ -545,6 +548,47 @@ class HipEngine(CEngineBase):
 
     def add_tiles(self, tiles_dev: int, n: int, buf_dev: int):
         self._check(self._fn("add_tiles", [C.c_void_p, C.c_int64, C.c_void_p])(self.h, tiles_dev, n, buf_dev))
+
+    # deferred mode: one scalar read per LM iteration in the multi-process controllers (viba_hip.h)
+    def set_deferred(self, on: bool):
+        self._check(self._fn("set_deferred", [C.c_int])(self.h, int(on)))
+
+    def scalar_slots(self):
+        """(device pointer of red[0..24), device pointer of err[0..2)): the phase functions' partial
+        scalars in deferred mode (vb_scalar_slots)."""
+        r, e = P(), P()
+        self._check(self._fn("scalar_slots", [C.POINTER(P), C.POINTER(P)])(self.h, C.byref(r), C.byref(e)))
+        return r.value, e.value
+
+    def small_factor_count(self) -> int:
+        n = C.c_int64()
+        self._check(self._fn("small_factor_count", [C.POINTER(C.c_int64)])(self.h, C.byref(n)))
+        return n.value
+
+    def mark_scalars(self):
+        self._check(self._fn("mark_scalars", [])(self.h))
+
+    def read_scalars(self, n: int = 17, check: bool = True):
+        """red[0, n) on the host, after vb_mark_scalars' point.  check: raise the error the error words
+        hold; else return (code, values) so a multi-process caller can agree on it first."""
+        out = np.zeros(n)
+        rc = self._fn("read_scalars", [_dp, C.c_int])(self.h, out.ctypes.data_as(_dp), n)
+        if check:
+            self._check(rc)
+            return out
+        return rc, out
+
+
+    def spec_prepare(self) -> bool:
+        ok = C.c_int()
+        self._check(self._fn("spec_prepare", [C.POINTER(C.c_int)])(self.h, C.byref(ok)))
+        return bool(ok.value)
+
+    def spec_linearize(self, dont_retry=False):
+        self._check(self._fn("spec_linearize", [C.c_int])(self.h, int(dont_retry)))
+
+    def spec_commit(self, use: bool):
+        self._check(self._fn("spec_commit", [C.c_int])(self.h, int(use)))
 
     # partitioned factorization (HIP engine only; include/viba_hip.h vb_set_partition)
     def bench_kernel(self, which: int, iters: int = 200) -> float:
