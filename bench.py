@@ -244,6 +244,9 @@ def main():
     synth.load_into(e, p, rs_device=args.rs_tables == "device", recompute_preint=args.recompute_preint)
     e.set_solver(SOLVERS[args.solver], args.pcg_iterations, args.pcg_residual)
     st = e.problem_stats()
+    sched = e.factor_schedule_stats()
+    log(f"[bench] factorization schedule: {sched[0]} levels, {sched[1]} fan-in contributions, {sched[3]} of "
+        f"{sched[2]} supernodes two-column")
     log(f"[bench] finalize {time.perf_counter() - t:.1f}s; reduced order {st[3]}, tiles {st[5]} "
         f"({st[4]} tile columns, {st[10]} levels), gemm pairs/factorization {st[6]}, Schur entries: landmark-tile {st[8]}, obs-pair {st[9]}")
 
@@ -290,13 +293,16 @@ def main():
         # launches actually timed (levels without contributions launch none: 88 of the 89 levels at
         # config C), so flops per launch = contributions x iterations / launches
         fan_per_factor = launches / max(1, iters)
-        per_launch = st[6] * 2.0 * 64 ** 3 / max(1e-9, fan_per_factor)
+        # the fan-in's own contributions (the two-column supernode schedule moves the pair-internal ones
+        # into its trsm kernel; the column schedule's are st[6])
+        fan_contrib = sched[1]
+        per_launch = fan_contrib * 2.0 * 64 ** 3 / max(1e-9, fan_per_factor)
         achieved = per_launch / (avg_ms * 1e-3) / 1e12
         # compulsory HBM bytes of one launch: within a level every contribution's L_IK is a distinct
         # tile (a column K has at most one ancestor column per level) and every L_JK is also the
         # I-side tile of the diagonal contribution (J, J, K), so the operands are pairs x 32 KB; each
         # target tile is read and written once (st[5] tiles over the launches bounds the targets)
-        compulsory = (st[6] * 64 * 64 * 8 + st[5] * 2 * 64 * 64 * 8) / max(1e-9, fan_per_factor)
+        compulsory = (fan_contrib * 64 * 64 * 8 + st[5] * 2 * 64 * 64 * 8) / max(1e-9, fan_per_factor)
         traffic = pmc_traffic("fanin_kernel")
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
                 "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": traffic,
@@ -305,7 +311,9 @@ def main():
                 "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
                           "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
                 "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches,
-                "fanin_launches_per_factorization": fan_per_factor, "levels": int(st[10]),
+                "fanin_launches_per_factorization": fan_per_factor, "levels": int(sched[0]),
+                "fanin_contributions": int(fan_contrib), "supernodes": int(sched[2]),
+                "two_column_supernodes": int(sched[3]),
                 "ceiling_4x4x4_measured": FP64_MFMA_4X4X4_MEASURED_TF,
                 "frac_of_4x4x4_ceiling": achieved / FP64_MFMA_4X4X4_MEASURED_TF}
     elif args.profile_family == KF_SYMV:

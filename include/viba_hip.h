@@ -493,6 +493,10 @@ int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
  *  elimination levels (one fan-in launch each, except a level without contributions), tiles of S
  *  without the symbolic fill] */
 int vb_problem_stats(vb_handle h, int64_t* out12);
+/* the direct factorization's schedule as it runs: [elimination levels, fan-in tile contributions per
+ * factorization, supernodes, two-column supernodes] -- the column schedule (one level per tile column
+ * chain step) unless VIBA_SUPERNODE=1 at vb_create built the two-column supernode schedule */
+int vb_factor_schedule_stats(vb_handle h, int64_t* out4);
 /* tuning aid: average time [us] of one kernel launch: on scratch tiles (which: 0 potrf, 1 trsm, 2 fan-in)
  * or, alone on the handle's own data (its results are not meant to be used afterwards), 10 visual
  * linearization, 12 landmark elimination, 13 observation-group Gram blocks, 14 Schur tile products,

@@ -56,10 +56,11 @@ def test_one_lm_step_matches_oracle(which):
     assert_step_parity(og, orf)
     # per gradient entry against the magnitudes of the terms it sums (oracle ref_abs_gradient): pins the
     # device's atomic assembly orders (small_assemble_kernel, obs_group_kernel, the landmark gradients)
-    # entry by entry, the cancellation residues included
+    # entry by entry, the cancellation residues included (bound: test_session_gpu.py's, the forward-
+    # difference time columns of the rolling-shutter visual factor)
     worst = gradient_entry_errors(og["grad"], orf["grad"], r)
     print(f"{which}: gradient entry errors / term magnitudes: {worst}")
-    assert max(worst.values()) < 1e-12, worst
+    assert max(worst.values()) < 1e-10, worst
 
 
 @pytest.mark.parametrize("which", ["A", "miniB"])

@@ -88,11 +88,12 @@ def test_session_folder_step_matches_oracle():
     # per entry, against the sum of the magnitudes of the terms the entry adds up (the oracle's
     # ref_abs_gradient at x0): the triangulated points start near their optimum, so their gradients are
     # cancellation residues of terms many orders larger, and a tolerance relative to the largest entry
-    # (1e-9 here until round 4) cannot tell summation order from an assembly error.  Measured:
-    # gradient_entry_errors() below.
+    # (1e-9 here until round 4) cannot tell summation order from an assembly error.  The bound: the
+    # rolling-shutter time columns are forward differences with eps = 1e-6 (VisualFactor.cpp), so a term's
+    # own round-off reaches ~2^-52 / 1e-6 = 2e-10 of it; measured 7.5e-12 (r05)
     worst = gradient_entry_errors(og["grad"], orf["grad"], r)
     print('gradient entry errors / term magnitudes:', worst)
-    assert max(worst.values()) < 1e-12, worst
+    assert max(worst.values()) < 1e-10, worst
     for a, b in zip(og["step"], orf["step"]):
         if b.size:
             assert rel(a, b) < 1e-8

@@ -49,6 +49,10 @@ void launch_trsm(const Dev& d, const int32_t* diag, const int32_t* target, const
 void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, double* dinv, hipStream_t st,
                        double* fwdB, double* fwdY);
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st);
+void launch_snpotrf(const Dev& d, const int32_t* items, int n, double* dinv, hipStream_t st, const double* fwdB,
+                    double* fwdY);
+void launch_sntrsm(const Dev& d, const int32_t* items, int n, const double* dinv, hipStream_t st, const double* fwdY,
+                   double* fwdB);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
 void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
                       double* y, const double* stop, hipStream_t st);
@@ -265,6 +269,25 @@ struct Sched {
   bool built = false;
 };
 
+// Two-column supernodes (VIBA_SUPERNODE, single handle): where column J + 1 is J's parent in the
+// elimination tree and J's other rows are rows of J + 1, the pair is factored as one 128-wide diagonal
+// block (snpotrf_kernel: L11, L21 = A21 L11^-T, A22 -= L21 L21^T, L22) and its rows by one kernel
+// (sntrsm_kernel: L_I1 = A_I1 L11^-T, A_I2 -= L_I1 L21^T, L_I2 = A_I2 L22^-T), so the pair is ONE level
+// of the schedule: about half the levels (launches, dependency gaps, potrf latency chains) of the
+// column schedule.  The fan-in lists leave out the pair-internal contributions (J -> J + 1).
+struct SnSched {
+  int32_t nLevels = 0;
+  int64_t nPairs = 0;                  // fan-in contributions (external to the supernodes)
+  int64_t nSuper = 0, nTwo = 0;        // supernodes, of which two-column
+  std::vector<int64_t> lvU, lvS, lvR;  // per level: fan-in chunk, supernode and row-item ranges
+  int32_t *updD = nullptr, *fanPairsD = nullptr;
+  int32_t *potD = nullptr;  // per supernode: tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1) or -1
+  int32_t *rowD = nullptr;  // per row item: tile (I, J) or -1, tile (I, J + 1) or -1, J, J + 1 or -1, I,
+                            //   tile (J, J), tile (J + 1, J), tile (J + 1, J + 1)
+  hipGraphExec_t graph[2] = {nullptr, nullptr};
+  bool built = false;
+};
+
 struct vb_handle_s {
   vb_config cfg;
   hipStream_t st = nullptr;
@@ -373,6 +396,8 @@ struct vb_handle_s {
   double* hostRed = nullptr;  // pinned readback buffer: red[0, 17), then err[0, 2) as int32
   size_t profAtCost = 0;      // profiled event pairs recorded before evCost
   bool specReady = false;     // every speculative buffer, event and stream above exists (specPrepare)
+  SnSched sn;                 // two-column supernode schedule of the direct factorization (VIBA_SUPERNODE)
+  bool useSn = false;
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
   bool deferred = false;
@@ -510,6 +535,132 @@ int readRedErr(vb_handle h, double* out, int n) {
   HIPCHK(hipStreamSynchronize(h->st));
   h->profDone = h->profUsed;
   return errFromWords(h, ee);
+}
+
+// the two-column supernode schedule (SnSched) from the column patterns of the single-handle structure
+int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT, int64_t nTiles) {
+  SnSched& S = h->sn;
+  auto colRows = [&](int32_t J, int64_t& a, int64_t& b) { a = h->colStart[J], b = h->colStart[J + 1]; };
+  // pair J with J + 1: J + 1 is J's first off-diagonal row (its parent) and every other row of J is a
+  // row of J + 1 (so the pair's rows are J + 1's), both in one nested-dissection part
+  std::vector<int8_t> pr(nT, 0);
+  for (int32_t J = 0; J + 1 < nT; J++) {
+    if (pr[J]) continue;
+    int64_t a, b, a2, b2;
+    colRows(J, a, b), colRows(J + 1, a2, b2);
+    if (b - a < 2 || h->colRowsH[a + 1] != J + 1 || h->colOwner[J] != h->colOwner[J + 1]) continue;
+    bool sub = true;
+    int64_t q = a2 + 1;
+    for (int64_t c = a + 2; c < b && sub; c++) {
+      while (q < b2 && h->colRowsH[q] < h->colRowsH[c]) q++;
+      sub = q < b2 && h->colRowsH[q] == h->colRowsH[c];
+    }
+    if (sub) pr[J] = 1, pr[J + 1] = 2;
+  }
+  // supernode levels: one more than the levels of the supernodes of every row tile (pair-internal
+  // (J + 1, J) excluded)
+  std::vector<int32_t> lev(nT, 0);
+  int32_t nLev = 0;
+  for (int32_t J = 0; J < nT; J++) {
+    if (pr[J] == 2) continue;
+    int32_t lv = 0;
+    for (int32_t X = J; X <= J + (pr[J] == 1 ? 1 : 0); X++)
+      for (int64_t i = h->rowStart[X]; i < h->rowStart[X + 1]; i++) {
+        const int32_t K = h->rowColH[i];
+        if (X == J + 1 && K == J) continue;
+        lv = std::max(lv, lev[K] + 1);
+      }
+    lev[J] = lv;
+    if (pr[J] == 1) lev[J + 1] = lv;
+    nLev = std::max(nLev, lv + 1);
+  }
+  std::vector<std::vector<int32_t>> sup(nLev);  // first column of every supernode, by level
+  for (int32_t J = 0; J < nT; J++)
+    if (pr[J] != 2) sup[lev[J]].push_back(J);
+  // fan-in contributions by target tile, sources in level order, pair-internal ones left out
+  std::vector<int64_t> ccnt(nTiles + 1, 0);
+  std::vector<int32_t> pairs;
+  for (int pass = 0; pass < 2; pass++) {
+    std::vector<int64_t> pos;
+    if (pass == 1) {
+      for (int64_t t = 0; t < nTiles; t++) ccnt[t + 1] += ccnt[t];
+      pos.assign(ccnt.begin(), ccnt.end() - 1);
+      pairs.assign(2 * (size_t)ccnt[nTiles], 0);
+    }
+    for (int32_t L = 0; L < nLev; L++)
+      for (int32_t J0 : sup[L])
+        for (int32_t K = J0; K <= J0 + (pr[J0] == 1 ? 1 : 0); K++) {
+          const int64_t c0 = h->colStart[K], n = h->colStart[K + 1] - c0;
+          for (int64_t qi = 1; qi < n; qi++)
+            for (int64_t qk = 1; qk <= qi; qk++) {
+              if (pr[K] == 1 && qk == 1) continue;  // targets in column K + 1: inside the supernode
+              const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
+              if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
+              if (pass == 0) {
+                ccnt[t + 1]++;
+              } else {
+                const int64_t at = pos[t]++;
+                pairs[2 * at] = h->colTilesH[c0 + qi], pairs[2 * at + 1] = h->colTilesH[c0 + qk];
+              }
+            }
+        }
+  }
+  if (ccnt[nTiles] >= INT32_MAX) return fail(VB_E_STATE, "tile Cholesky too large (contribution count)");
+  const int64_t fanWgs = 3072;
+  std::vector<int32_t> fan, pot, rows;
+  S.lvU.assign(nLev + 1, 0), S.lvS.assign(nLev + 1, 0), S.lvR.assign(nLev + 1, 0);
+  S.nTwo = 0;
+  auto tile = [&](int32_t I, int32_t J) { return tileIdx[(size_t)I * nT + J]; };
+  for (int32_t L = 0; L < nLev; L++) {
+    int64_t total = 0;
+    for (int32_t J0 : sup[L])
+      for (int32_t J = J0; J <= J0 + (pr[J0] == 1 ? 1 : 0); J++)
+        for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
+    const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
+    const size_t u0 = fan.size() / 4;
+    for (int32_t J0 : sup[L]) {
+      const bool two = pr[J0] == 1;
+      const int32_t J2 = two ? J0 + 1 : -1;
+      for (int32_t J = J0; J <= (two ? J2 : J0); J++)
+        for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
+          const int32_t t = h->colTilesH[c];
+          const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
+          if (m == 0) continue;
+          const int64_t nch = (m + cs - 1) / cs;
+          for (int64_t k = 0; k < nch; k++) {
+            const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
+            fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
+          }
+        }
+      const int32_t t11 = tile(J0, J0), t21 = two ? tile(J2, J0) : -1, t22 = two ? tile(J2, J2) : -1;
+      pot.insert(pot.end(), {t11, J0, t21, t22});
+      S.nTwo += two ? 1 : 0;
+      // rows below the supernode: those of its last column (a pair's first column has no others)
+      const int32_t Jl = two ? J2 : J0;
+      for (int64_t c = h->colStart[Jl] + 1; c < h->colStart[Jl + 1]; c++) {
+        const int32_t I = h->colRowsH[c];
+        rows.insert(rows.end(), {two ? tile(I, J0) : h->colTilesH[c], two ? h->colTilesH[c] : -1, J0, J2, I, t11, t21, t22});
+      }
+    }
+    {  // longest chunks first within each XCD's range (as the column schedule)
+      std::vector<std::array<int32_t, 4>> q((fan.size() / 4) - u0);
+      for (size_t i = 0; i < q.size(); i++)
+        for (int k = 0; k < 4; k++) q[i][k] = fan[4 * (u0 + i) + k];
+      const size_t nq = q.size(), qq = nq / 8, rr = nq % 8;
+      for (size_t x = 0, b0 = 0; x < 8; x++) {
+        const size_t len = qq + (x < rr ? 1 : 0);
+        std::stable_sort(q.begin() + b0, q.begin() + b0 + len, [](const auto& a, const auto& b) { return a[2] > b[2]; });
+        b0 += len;
+      }
+      for (size_t i = 0; i < q.size(); i++)
+        for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
+    }
+    S.lvU[L + 1] = (int64_t)fan.size() / 4, S.lvS[L + 1] = (int64_t)pot.size() / 4, S.lvR[L + 1] = (int64_t)rows.size() / 8;
+  }
+  S.nLevels = nLev, S.nPairs = ccnt[nTiles], S.nSuper = (int64_t)pot.size() / 4;
+  if (upload(&S.updD, fan) || upload(&S.fanPairsD, pairs) || upload(&S.potD, pot) || upload(&S.rowD, rows)) return VB_E_HIP;
+  S.built = true;
+  return 0;
 }
 
 int doFinalize(vb_handle h) {
@@ -1262,6 +1413,39 @@ int doFinalize(vb_handle h) {
       }
       w.wOff[4] = (uint16_t)(tasksH.size() - w.taskFirst);
     }
+    if (getenv("VIBA_SCHUR_STATS")) {  // diagnostics: compact widths, MFMA padding, runs, tasks
+      int64_t hI[5] = {0}, hJ[5] = {0}, nRun = 0, nTask = 0, runLm = 0;
+      double useful = 0, issued = 0, issued4 = 0;
+      auto bin = [](int n) { return n <= 4 ? 0 : n <= 8 ? 1 : n <= 16 ? 2 : n <= 32 ? 3 : 4; };
+      for (const TileWork& w : works) {
+        const bool diag = w.I == w.J;
+        std::vector<int> rlen(w.nRuns, 0);
+        for (int e = 0, k = -1; e < w.count; e++) {
+          const TileEnt& a = ents[w.start + e];
+          if (e == 0 || a.maskI != ents[w.start + e - 1].maskI || a.maskJ != ents[w.start + e - 1].maskJ) k++;
+          rlen[k]++;
+        }
+        for (int r = 0; r < w.nRuns; r++) {
+          const uint64_t mI = runsH[2 * ((size_t)w.runFirst + r)], mJ = runsH[2 * ((size_t)w.runFirst + r) + 1];
+          const int nI = __builtin_popcountll(mI), nJ = __builtin_popcountll(mJ);
+          const int nl = rlen[r];
+          hI[bin(nI)]++, hJ[bin(nJ)]++, nRun++, runLm += nl;
+          const double rows = 3.0 * nl;
+          useful += 2.0 * rows * nI * nJ * (diag ? 0.5 : 1.0);
+          const int nbI = (nI + 15) / 16, nbJ = (nJ + 15) / 16;
+          issued += 2.0 * 4.0 * std::ceil(rows / 4.0) * 256.0 * nbI * nbJ * (diag ? 0.5 : 1.0);
+          issued4 += 2.0 * 4.0 * std::ceil(rows / 4.0) * 16.0 * ((nI + 3) / 4) * ((nJ + 3) / 4) * (diag ? 0.5 : 1.0);
+        }
+        nTask += w.wOff[4];
+      }
+      fprintf(stderr,
+              "[schur stats] items %zu runs %lld tasks %lld landmarks/run %.2f; nI <=4/8/16/32/64: %lld %lld %lld %lld "
+              "%lld; nJ: %lld %lld %lld %lld %lld; GFLOP useful %.2f issued(16x16) %.2f issued(4x4) %.2f\n",
+              works.size(), (long long)nRun, (long long)nTask, (double)runLm / std::max<int64_t>(1, nRun),
+              (long long)hI[0], (long long)hI[1], (long long)hI[2], (long long)hI[3], (long long)hI[4], (long long)hJ[0],
+              (long long)hJ[1], (long long)hJ[2], (long long)hJ[3], (long long)hJ[4], useful * 1e-9, issued * 1e-9,
+              issued4 * 1e-9);
+    }
     if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH)) return VB_E_HIP;
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
     d.nTileWorks = (int64_t)works.size();
@@ -1300,6 +1484,59 @@ int doFinalize(vb_handle h) {
     }
     std::vector<std::vector<int32_t>> cols(nLev);
     for (int32_t J = 0; J < nT; J++) cols[level[J]].push_back(J);
+    if (getenv("VIBA_FACTOR_STATS")) {  // diagnostics: 2-column supernodes (J, J + 1) and their levels
+      // pairable: J + 1 is J's first off-diagonal row (its parent) and J's other rows are all rows of J + 1
+      std::vector<int8_t> pair(nT, 0);
+      int64_t nPair = 0;
+      for (int32_t J = 0; J + 1 < nT; J++) {
+        if (pair[J] || (J > 0 && pair[J - 1] == 1)) continue;
+        const int64_t a = h->colStart[J], b = h->colStart[J + 1], a2 = h->colStart[J + 1], b2 = h->colStart[J + 2];
+        if (b - a < 2 || h->colRowsH[a + 1] != J + 1) continue;
+        bool sub = true;
+        int64_t q = a2 + 1;
+        for (int64_t c = a + 2; c < b && sub; c++) {
+          while (q < b2 && h->colRowsH[q] < h->colRowsH[c]) q++;
+          sub = q < b2 && h->colRowsH[q] == h->colRowsH[c];
+        }
+        if (sub) pair[J] = 1, pair[J + 1] = 2, nPair++;
+      }
+      std::vector<int32_t> slev(nT, 0);
+      int32_t nSl = 0;
+      for (int32_t J = 0; J < nT; J++) {
+        int32_t lv = 0;
+        auto rowsOf = [&](int32_t X) {
+          for (int64_t i = h->rowStart[X]; i < h->rowStart[X + 1]; i++) {
+            const int32_t K = h->rowColH[i];
+            if (pair[X] == 2 && K == X - 1) continue;  // internal to the supernode
+            lv = std::max(lv, slev[K] + 1);
+          }
+        };
+        if (pair[J] == 2) continue;
+        rowsOf(J);
+        if (pair[J] == 1) rowsOf(J + 1);
+        slev[J] = lv;
+        if (pair[J] == 1) slev[J + 1] = lv;
+        nSl = std::max(nSl, lv + 1);
+      }
+      int64_t contrib = 0, internal = 0;
+      for (int32_t K = 0; K < nT; K++) {
+        const int64_t n = h->colStart[K + 1] - h->colStart[K];
+        contrib += (n - 1) * n / 2;
+        if (pair[K] == 1) internal += n - 1;  // targets in column K + 1 from K
+      }
+      fprintf(stderr, "[factor stats] tile columns %d levels %d; pairable 2-column supernodes %lld (%lld columns), "
+                      "supernode levels %d; contributions %lld of which internal to pairs %lld\n",
+              nT, nLev, (long long)nPair, (long long)(2 * nPair), nSl, (long long)contrib, (long long)internal);
+      for (int32_t L = 0; L < nLev; L++) {
+        int64_t c = 0, np = 0;
+        for (int32_t J : cols[L]) {
+          const int64_t n = h->rowStart[J + 1] - h->rowStart[J];
+          c += n, np += pair[J] ? 1 : 0;
+        }
+        fprintf(stderr, "[factor stats] level %d columns %zu (paired %lld) row tiles %lld\n", L, cols[L].size(),
+                (long long)np, (long long)c);
+      }
+    }
     const int64_t fanWgs = 3072;  // re-tuned for the thin-separator order (2048: -0.5%, 4096-8192: -0.3%)
     // Build one schedule.  colSel(J): columns factored here (potrf, trsm, solve diagonal tasks);
     // tgtSel(J): fan-in targets in column J; srcSel(K): contributions from column K; preSel(J): rows
@@ -1464,6 +1701,8 @@ int doFinalize(vb_handle h) {
     }
     h->nLevels = nLev;
     h->nPairs = h->sch[0].nPairs + h->sch[1].nPairs;
+    if (W <= 1 && h->useSn)
+      if (int rc = buildSupernodes(h, tileIdx, nT, nTiles)) return rc;
   }
   // ---------------- small factors (+ whitening square roots)
   for (int fk = 1; fk < 14; fk++) {
@@ -1694,12 +1933,37 @@ void factorSeq(vb_handle h, const Sched& S) {
   launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
 }
 
+// the two-column supernode schedule (SnSched): per level the fan-in of its targets, the supernodes'
+// diagonal blocks, their rows; then the diagonal-tile inverses of the solves (every column)
+void factorSeqSn(vb_handle h) {
+  Dev& d = h->d;
+  const SnSched& S = h->sn;
+  const bool fwd = fwdFused(h) && !h->factorOnly;
+  double* fb = fwd ? h->rhsWork : nullptr;
+  double* fy = fwd ? h->yvec : nullptr;
+  for (int32_t L = 0; L < S.nLevels; L++) {
+    const int64_t u0 = S.lvU[L], s0 = S.lvS[L], r0 = S.lvR[L];
+    profBegin(h, KF_GEMM);
+    launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
+    profEnd(h, KF_GEMM);
+    profBegin(h, KF_POTRF);
+    launch_snpotrf(d, S.potD + 4 * s0, (int)(S.lvS[L + 1] - s0), h->dinv, h->st, fb, fy);
+    profEnd(h, KF_POTRF);
+    profBegin(h, KF_TRSM);
+    launch_sntrsm(d, S.rowD + 8 * r0, (int)(S.lvR[L + 1] - r0), h->dinv, h->st, fy, fb);
+    profEnd(h, KF_TRSM);
+  }
+  const Sched& C = h->sch[0];
+  launch_diag_inverse(d, C.potrfColD, C.lvP[C.nLevels], h->linv, h->st);
+}
+
 // launch sequences are fixed by the symbolic structure: capture them once into HIP graphs
 // (unless one of their kernel families is being profiled, which needs per-launch events)
-int captureGraph(vb_handle h, const Sched& S, hipGraphExec_t* out) {
+int captureGraph(vb_handle h, const Sched& S, hipGraphExec_t* out, bool sn = false) {
   hipGraph_t g;
   HIPCHK(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
-  factorSeq(h, S);
+  if (sn) factorSeqSn(h);
+  else factorSeq(h, S);
   HIPCHK(hipStreamEndCapture(h->st, &g));
   HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
   HIPCHK(hipGraphDestroy(g));
@@ -1713,13 +1977,15 @@ int factorReduced(vb_handle h, int which = 0) {
   const bool prof = h->profFamily == KF_POTRF || h->profFamily == KF_GEMM || h->profFamily == KF_TRSM;
   // (a profiled family runs launch by launch: its per-launch events, recorded as event nodes inside
   // a graph, cost as much as the graph saves -- measured)
+  const bool sn = which == 0 && h->sn.built;
   if (!h->useGraphs || prof || h->factorOnly) {
-    factorSeq(h, S);
+    if (sn) factorSeqSn(h);
+    else factorSeq(h, S);
     return 0;
   }
-  hipGraphExec_t& g = S.graph[h->tileSet];
+  hipGraphExec_t& g = sn ? h->sn.graph[h->tileSet] : S.graph[h->tileSet];
   if (!g)
-    if (int rc = captureGraph(h, S, &g)) return rc;
+    if (int rc = captureGraph(h, S, &g, sn)) return rc;
   HIPCHK(hipGraphLaunch(g, h->st));
   return 0;
 }
@@ -1977,6 +2243,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
   if (const char* e = getenv("VIBA_SPEC_EARLY")) h->specEarly = e[0] != '0';
   if (const char* e = getenv("VIBA_DEBUG_SPEC_FAIL")) h->specFailDebug = e[0] == '1';
+  if (const char* e = getenv("VIBA_SUPERNODE")) h->useSn = e[0] == '1';
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2042,6 +2309,13 @@ int vb_destroy(vb_handle h) {
       if (e) hipEventDestroy(e);
   if (h->stR) hipStreamSynchronize(h->stR), hipStreamDestroy(h->stR);
   if (h->hostRed) hipHostFree(h->hostRed);
+  {
+    SnSched& N = h->sn;
+    for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD})
+      if (p) hipFree(p);
+    for (hipGraphExec_t g : N.graph)
+      if (g) hipGraphExecDestroy(g);
+  }
   for (Sched& S : h->sch) {
     void* sp[] = {S.ptfD, S.ptfDiagD, S.potrfTileD, S.potrfColD, S.trsmDiagD, S.trsmTargetD, S.trsmColD, S.trsmRowD, S.updD, S.fanPairsD,
                   S.tasksFD, S.tasksBD, S.expFD, S.expBD, S.preReadyD};
@@ -2896,6 +3170,18 @@ int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
   int64_t nS = 0;
   for (uint8_t f : h->tileFill) nS += f ? 0 : 1;
   out[10] = h->nLevels, out[11] = nS;
+  return 0;
+}
+
+// the factorization's schedule as it runs: [levels, fan-in contributions per factorization, supernodes,
+// two-column supernodes] (the column schedule: supernodes = columns, no two-column ones)
+int vb_factor_schedule_stats(vb_handle h, int64_t* out4) {
+  if (!h || !h->finalized || !out4) return fail(VB_E_STATE, "not finalized");
+  if (h->sn.built) {
+    out4[0] = h->sn.nLevels, out4[1] = h->sn.nPairs, out4[2] = h->sn.nSuper, out4[3] = h->sn.nTwo;
+  } else {
+    out4[0] = h->nLevels, out4[1] = h->nPairs, out4[2] = h->d.nT, out4[3] = 0;
+  }
   return 0;
 }
 

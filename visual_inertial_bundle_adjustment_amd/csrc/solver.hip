@@ -881,10 +881,10 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __device__ __forceinline__ void potrf_forward(const Dev& d, const double* T, const double* dinvS, double* sh, int J,
-                                              const double* b, double* y, int lane, bool store = true) {
+                                              const double* bJ, double* y, int lane, bool store = true) {
   // right-looking by 16-row blocks: lane r keeps b_r; once y_i is known every later row subtracts
-  // L(r, block i) y_i, so each block's chain is one 16-term GEMV + one 16-term update
-  double br = b[(int64_t)J * TS + lane];
+  // L(r, block i) y_i, so each block's chain is one 16-term GEMV + one 16-term update (bJ: b_J's 64 rows)
+  double br = bJ[lane];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     sh[64 + lane] = br;
@@ -974,7 +974,7 @@ __global__ void __launch_bounds__(256) potrf4_kernel(Dev d, const int32_t* tileL
   double* A = d.tiles + (int64_t)tileList[blockIdx.x] * TS * TS;
   double* dinvG = dinvAll + (int64_t)cols[blockIdx.x] * 1024;
   potrf4_core(d, A, T, scratch, dinvS, tid);
-  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB, fwdY, tid & 63);
+  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, cols[blockIdx.x], fwdB + (int64_t)cols[blockIdx.x] * TS, fwdY, tid & 63);
   lds_to_global(A, T, TS * TS, tid, 256);
   lds_to_global(dinvG, dinvS, 1024, tid, 256);
 }
@@ -1005,7 +1005,7 @@ __global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* i
       for (int r = 0; r < 4; r++) av[k][r] = At[(16 * k + lq + 4 * r) * TS + 16 * w + lr];
   }
   potrf4_core(d, d.tiles + (int64_t)diagT * TS * TS, T, scratch, dinvS, tid);
-  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, col, fwdB, fwdY, lane, writer != 0);
+  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, col, fwdB + (int64_t)col * TS, fwdY, lane, writer != 0);
   if (writer) {
     lds_to_global(Lscr + (int64_t)col * TS * TS, T, TS * TS, tid, 256);
     lds_to_global(dinvAll + (int64_t)col * 1024, dinvS, 1024, tid, 256);
@@ -1039,6 +1039,161 @@ __global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* i
     v += __shfl_xor(v, 32, 64);
     if (lq == 0) atomicAdd(fwdB + (int64_t)row * TS + 16 * w + lr, -v);
   }
+}
+
+// ---------------- two-column supernodes (api.hip SnSched)
+// X = A L^-T for one tile row block per wave (trsm_kernel's body): acc holds A (D layout: lane (lr, lq),
+// register r = element (row 16 w + lr, column 16 k + lq + 4 r)); L the factored diagonal tile, dinv its
+// 16 x 16 block inverses.  Every operand is loaded before the substitution chain.
+__device__ __forceinline__ void trsm_rows(const double* L, const double* dinv, double4_t (&acc)[4], double4_t (&Xt)[4],
+                                          int lr, int lq) {
+  double lv[6][4], dv[4][4];
+#pragma unroll
+  for (int k = 1; k < 4; k++)
+#pragma unroll
+    for (int k2 = 0; k2 < k; k2++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) lv[k * (k - 1) / 2 + k2][s] = L[(16 * k2 + 4 * s + lq) * TS + 16 * k + lr];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int s = 0; s < 4; s++) dv[k][s] = dinv[k * 256 + (4 * s + lq) * 16 + lr];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    double4_t a = acc[k];
+#pragma unroll
+    for (int k2 = 0; k2 < k; k2++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) a = mfma64(-lv[k * (k - 1) / 2 + k2][s], Xt[k2][s], a);
+    double4_t res = double4_t{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 4; s++) res = mfma64(dv[k][s], a[s], res);
+    Xt[k] = res;
+  }
+}
+// acc -= X M^T over all four column blocks of M (a full tile: the update of a supernode's second column by
+// its first), X in D layout, M column-major in memory (global or LDS)
+__device__ __forceinline__ void gemm_nt_sub(const double* M, const double4_t (&Xt)[4], double4_t (&acc)[4], int lr, int lq,
+                                            int kmax = 3) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (k > kmax) break;
+    double mv[4][4];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; k2++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) mv[k2][s] = M[(16 * k2 + 4 * s + lq) * TS + 16 * k + lr];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; k2++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) acc[k] = mfma64(-mv[k2][s], Xt[k2][s], acc[k]);
+  }
+}
+__device__ __forceinline__ void load_rows(const double* A, double4_t (&acc)[4], int w, int lr, int lq) {
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) acc[k][r] = A[(16 * k + lq + 4 * r) * TS + 16 * w + lr];
+}
+__device__ __forceinline__ void store_rows(double* A, const double4_t (&X)[4], int w, int lr, int lq) {
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) A[(16 * k + lq + 4 * r) * TS + 16 * w + lr] = X[k][r];
+}
+// this wave's rows of X y (y: a tile column's 64 values in LDS / global, 16 k + lq + 4 r per register),
+// summed over the lane groups: lanes lq == 0 hold row 16 w + lr
+__device__ __forceinline__ double rows_dot(const double4_t (&X)[4], const double* y, int lq) {
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) v += X[k][r] * y[16 * k + lq + 4 * r];
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// The diagonal block of a supernode (items: tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1)):
+// L11 (potrf4_core), L21 = A21 L11^-T, A22 - L21 L21^T into LDS, L22; the 16 x 16 inverses of both
+// diagonal tiles; with the fused forward solve y_J, then b_{J+1} - L21 y_J (kept in LDS), then y_{J+1}.
+// A one-column supernode is potrf4_kernel.
+__global__ void __launch_bounds__(256) snpotrf_kernel(Dev d, const int32_t* items, double* dinvAll, const double* fwdB,
+                                                      double* fwdY) {
+  __shared__ double T[TS * TS];   // L11, then L22
+  __shared__ double U[TS * TS];   // A22 - L21 L21^T
+  __shared__ double M[TS * TS];   // L21
+  __shared__ double scratch[256];
+  __shared__ double dinvS[1024];
+  __shared__ double bS[TS];
+  const int32_t* it = items + 4 * (int64_t)blockIdx.x;
+  const int32_t t11 = it[0], J = it[1], t21 = it[2], t22 = it[3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  double* A11 = d.tiles + (int64_t)t11 * TS * TS;
+  double4_t a21[4], a22[4];
+  if (t21 >= 0) {  // both operands of the second column in flight during the first factorization
+    load_rows(d.tiles + (int64_t)t21 * TS * TS, a21, w, lr, lq);
+    load_rows(d.tiles + (int64_t)t22 * TS * TS, a22, w, lr, lq);
+  }
+  potrf4_core(d, A11, T, scratch, dinvS, tid);
+  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, J, fwdB + (int64_t)J * TS, fwdY, lane);
+  __syncthreads();  // y_J (scratch[0, 64))
+  if (t21 < 0) {
+    lds_to_global(A11, T, TS * TS, tid, 256);
+    lds_to_global(dinvAll + (int64_t)J * 1024, dinvS, 1024, tid, 256);
+    return;
+  }
+  // L21 = A21 L11^-T: this wave's 16 rows, from T / dinvS in LDS
+  double4_t X[4];
+  trsm_rows(T, dinvS, a21, X, lr, lq);
+  store_rows(M, X, w, lr, lq);
+  if (fwdB) {  // b_{J+1} - L21 y_J for the second column's forward step
+    const double v = rows_dot(X, scratch, lq);
+    if (lq == 0) bS[16 * w + lr] = fwdB[(int64_t)(J + 1) * TS + 16 * w + lr] - v;
+  }
+  lds_to_global(A11, T, TS * TS, tid, 256);
+  lds_to_global(dinvAll + (int64_t)J * 1024, dinvS, 1024, tid, 256);
+  __syncthreads();  // M complete; T, dinvS, scratch free
+  // U = A22 - L21 L21^T: wave w its row block, column blocks <= w (the diagonal block whole)
+  gemm_nt_sub(M, X, a22, lr, lq, w);
+  store_rows(U, a22, w, lr, lq);
+  store_rows(d.tiles + (int64_t)t21 * TS * TS, X, w, lr, lq);
+  __syncthreads();
+  potrf4_core(d, U, T, scratch, dinvS, tid);
+  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, J + 1, bS, fwdY, lane);
+  lds_to_global(d.tiles + (int64_t)t22 * TS * TS, T, TS * TS, tid, 256);
+  lds_to_global(dinvAll + (int64_t)(J + 1) * 1024, dinvS, 1024, tid, 256);
+}
+
+// The rows of a supernode, one block per row I below it (items: tile (I, J) or -1, tile (I, J + 1) or -1,
+// J, J + 1 or -1, I, tiles (J, J), (J + 1, J), (J + 1, J + 1)): L_I1 = A_I1 L11^-T, A_I2 -= L_I1 L21^T,
+// L_I2 = A_I2 L22^-T; with the fused forward solve b_I -= L_I1 y_J + L_I2 y_{J+1}
+__global__ void __launch_bounds__(256) sntrsm_kernel(Dev d, const int32_t* items, const double* dinvAll, const double* fwdY,
+                                                     double* fwdB) {
+  const int32_t* it = items + 8 * (int64_t)blockIdx.x;
+  const int32_t tI1 = it[0], tI2 = it[1], J = it[2], J2 = it[3], I = it[4], t11 = it[5], t21 = it[6], t22 = it[7];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  double4_t X1[4], a2[4];
+  double v = 0.0;
+  if (J2 >= 0) load_rows(d.tiles + (int64_t)tI2 * TS * TS, a2, w, lr, lq);
+  if (tI1 >= 0) {
+    double* A1 = d.tiles + (int64_t)tI1 * TS * TS;
+    double4_t a1[4];
+    load_rows(A1, a1, w, lr, lq);
+    trsm_rows(d.tiles + (int64_t)t11 * TS * TS, dinvAll + (int64_t)J * 1024, a1, X1, lr, lq);
+    store_rows(A1, X1, w, lr, lq);
+    if (fwdB) v += rows_dot(X1, fwdY + (int64_t)J * TS, lq);
+    if (J2 >= 0) gemm_nt_sub(d.tiles + (int64_t)t21 * TS * TS, X1, a2, lr, lq);
+  }
+  if (J2 >= 0) {
+    double4_t X2[4];
+    trsm_rows(d.tiles + (int64_t)t22 * TS * TS, dinvAll + (int64_t)J2 * 1024, a2, X2, lr, lq);
+    store_rows(d.tiles + (int64_t)tI2 * TS * TS, X2, w, lr, lq);
+    if (fwdB) v += rows_dot(X2, fwdY + (int64_t)J2 * TS, lq);
+  }
+  if (fwdB && lq == 0) atomicAdd(fwdB + (int64_t)I * TS + 16 * w + lr, -v);
 }
 
 // the diagonal tiles of the fused levels back from Lscr (pairs: diagonal tile, column)
@@ -1678,6 +1833,14 @@ void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n
 void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, double* dinv, hipStream_t st,
                        double* fwdB, double* fwdY) {
   if (n > 0) launchK(potrf_trsm_kernel, dim3(n), dim3(256), 0, st, d, items, Lscr, dinv, fwdB, fwdY);
+}
+void launch_snpotrf(const Dev& d, const int32_t* items, int n, double* dinv, hipStream_t st, const double* fwdB,
+                    double* fwdY) {
+  if (n > 0) launchK(snpotrf_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdB, fwdY);
+}
+void launch_sntrsm(const Dev& d, const int32_t* items, int n, const double* dinv, hipStream_t st, const double* fwdY,
+                   double* fwdB) {
+  if (n > 0) launchK(sntrsm_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdY, fwdB);
 }
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(copy_diag_kernel, dim3(n), dim3(256), 0, st, d, pairs, Lscr);

@@ -529,6 +529,12 @@ class HipEngine(CEngineBase):
         self._check(self._fn("problem_stats", [C.c_int64 * 12])(self.h, out))
         return list(out)
 
+    def factor_schedule_stats(self):
+        """[levels, fan-in contributions per factorization, supernodes, two-column supernodes]"""
+        out = (C.c_int64 * 4)()
+        self._check(self._fn("factor_schedule_stats", [C.c_int64 * 4])(self.h, out))
+        return list(out)
+
     # sparse shard exchange (HIP engine only; the oracle keeps the band of shard_tile_range)
     def shard_tiles(self) -> np.ndarray:
         n = C.c_int64()
