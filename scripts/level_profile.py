@@ -17,7 +17,10 @@ def wgs(r):
 
 def kname(r):
     n = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("viba::", "").split("<")[0]
-    return "potrf_kernel" if n in ("potrf4_kernel", "potrf_trsm_kernel") else n
+    if n == "sntrsm_kernel":  # the two-column supernode schedule (VIBA_SUPERNODE=1)
+        return "trsm_kernel"
+    return "potrf_kernel" if n in ("potrf4_kernel", "potrf_trsm_kernel", "snpotrf_kernel", "snpotrf8_kernel",
+                                   "snpotrf_trsm8_kernel") else n
 
 
 ks = [(kname(r), int(r["Start_Timestamp"]), int(r["End_Timestamp"]), wgs(r)) for r in rows]

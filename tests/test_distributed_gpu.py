@@ -218,7 +218,7 @@ def test_bench_two_ranks_line(tmp_path):
     from visual_inertial_bundle_adjustment_amd.engine import HipEngine, Settings
     p = synth.generate(synth.config("B"))
     e = HipEngine(imu_calib_options=p.imu_calib_options)
-    synth.load_into(e, p)
+    synth.load_into(e, p, rs_device=True)  # as bench.py (--rs-tables device)
 
     def settings(n):
         return Settings.default(max_num_iterations=n, stop_if_no_improvement_for=10**6,

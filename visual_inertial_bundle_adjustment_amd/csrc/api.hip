@@ -51,6 +51,8 @@ void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, 
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st);
 void launch_snpotrf(const Dev& d, const int32_t* items, int n, double* dinv, hipStream_t st, const double* fwdB,
                     double* fwdY);
+void launch_snpotrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, double* dinv, hipStream_t st,
+                         double* fwdB, double* fwdY);
 void launch_sntrsm(const Dev& d, const int32_t* items, int n, const double* dinv, hipStream_t st, const double* fwdY,
                    double* fwdB);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
@@ -284,6 +286,12 @@ struct SnSched {
   int32_t *potD = nullptr;  // per supernode: tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1) or -1
   int32_t *rowD = nullptr;  // per row item: tile (I, J) or -1, tile (I, J + 1) or -1, J, J + 1 or -1, I,
                             //   tile (J, J), tile (J + 1, J), tile (J + 1, J + 1)
+  // levels with few rows: diagonal block + one row per block in one launch (snpotrf_trsm8_kernel); items
+  // (tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1) or -1, tile (I, J) or -1, tile (I, J + 1) or
+  // -1, I or -1, writer); their factored diagonal-block tiles come back from the scratch at the end
+  std::vector<int64_t> lvF;
+  int32_t *fusD = nullptr, *copyD = nullptr;
+  int64_t nCopy = 0;
   hipGraphExec_t graph[2] = {nullptr, nullptr};
   bool built = false;
 };
@@ -396,8 +404,8 @@ struct vb_handle_s {
   double* hostRed = nullptr;  // pinned readback buffer: red[0, 17), then err[0, 2) as int32
   size_t profAtCost = 0;      // profiled event pairs recorded before evCost
   bool specReady = false;     // every speculative buffer, event and stream above exists (specPrepare)
-  SnSched sn;                 // two-column supernode schedule of the direct factorization (VIBA_SUPERNODE)
-  bool useSn = false;
+  SnSched sn;                 // two-column supernode schedule of the direct factorization
+  bool useSn = true;          // VIBA_SUPERNODE=0 at creation: the column schedule
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
   bool deferred = false;
@@ -420,6 +428,7 @@ struct vb_handle_s {
   hipEvent_t evZero = nullptr, evSmallE = nullptr, evZJoin = nullptr;
   int64_t ptFuseMax = 256;  // levels with at most this many off-diagonal tiles run potrf + trsm in one launch
   double* lscr = nullptr;   // L_JJ of the fused levels' columns (nT tiles), copied back after the factorization
+  double* lscrSn = nullptr; // the supernode schedule's: L11 / L22 at [J] / [J + 1], L21 at [nT + J]
   // per-kernel-family device timing (vb_profile_kernel): event pairs around every launch
   int profFamily = -1;
   std::vector<hipEvent_t> profEv;
@@ -607,8 +616,10 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
   }
   if (ccnt[nTiles] >= INT32_MAX) return fail(VB_E_STATE, "tile Cholesky too large (contribution count)");
   const int64_t fanWgs = 3072;
-  std::vector<int32_t> fan, pot, rows;
-  S.lvU.assign(nLev + 1, 0), S.lvS.assign(nLev + 1, 0), S.lvR.assign(nLev + 1, 0);
+  int64_t fuseMax = 256;  // levels with at most this many row items run snpotrf_trsm8_kernel
+  if (const char* e = getenv("VIBA_SN_FUSE")) fuseMax = atoll(e);
+  std::vector<int32_t> fan, pot, rows, fus, copy;
+  S.lvU.assign(nLev + 1, 0), S.lvS.assign(nLev + 1, 0), S.lvR.assign(nLev + 1, 0), S.lvF.assign(nLev + 1, 0);
   S.nTwo = 0;
   auto tile = [&](int32_t I, int32_t J) { return tileIdx[(size_t)I * nT + J]; };
   for (int32_t L = 0; L < nLev; L++) {
@@ -618,6 +629,12 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
         for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
     const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
     const size_t u0 = fan.size() / 4;
+    int64_t nRowsL = 0;
+    for (int32_t J0 : sup[L]) {
+      const int32_t Jl = pr[J0] == 1 ? J0 + 1 : J0;
+      nRowsL += h->colStart[Jl + 1] - h->colStart[Jl] - 1;
+    }
+    const bool fused = nRowsL <= fuseMax;
     for (int32_t J0 : sup[L]) {
       const bool two = pr[J0] == 1;
       const int32_t J2 = two ? J0 + 1 : -1;
@@ -633,10 +650,21 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
           }
         }
       const int32_t t11 = tile(J0, J0), t21 = two ? tile(J2, J0) : -1, t22 = two ? tile(J2, J2) : -1;
-      pot.insert(pot.end(), {t11, J0, t21, t22});
       S.nTwo += two ? 1 : 0;
       // rows below the supernode: those of its last column (a pair's first column has no others)
       const int32_t Jl = two ? J2 : J0;
+      if (fused) {
+        copy.insert(copy.end(), {t11, J0});
+        if (two) copy.insert(copy.end(), {t22, J2, t21, nT + J0});
+        if (h->colStart[Jl + 1] - h->colStart[Jl] == 1) fus.insert(fus.end(), {t11, J0, t21, t22, -1, -1, -1, 1});
+        for (int64_t c = h->colStart[Jl] + 1; c < h->colStart[Jl + 1]; c++) {
+          const int32_t I = h->colRowsH[c];
+          fus.insert(fus.end(), {t11, J0, t21, t22, two ? tile(I, J0) : h->colTilesH[c], two ? h->colTilesH[c] : -1, I,
+                                 c == h->colStart[Jl] + 1 ? 1 : 0});
+        }
+        continue;
+      }
+      pot.insert(pot.end(), {t11, J0, t21, t22});
       for (int64_t c = h->colStart[Jl] + 1; c < h->colStart[Jl + 1]; c++) {
         const int32_t I = h->colRowsH[c];
         rows.insert(rows.end(), {two ? tile(I, J0) : h->colTilesH[c], two ? h->colTilesH[c] : -1, J0, J2, I, t11, t21, t22});
@@ -656,9 +684,16 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
         for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
     }
     S.lvU[L + 1] = (int64_t)fan.size() / 4, S.lvS[L + 1] = (int64_t)pot.size() / 4, S.lvR[L + 1] = (int64_t)rows.size() / 8;
+    S.lvF[L + 1] = (int64_t)fus.size() / 8;
   }
-  S.nLevels = nLev, S.nPairs = ccnt[nTiles], S.nSuper = (int64_t)pot.size() / 4;
-  if (upload(&S.updD, fan) || upload(&S.fanPairsD, pairs) || upload(&S.potD, pot) || upload(&S.rowD, rows)) return VB_E_HIP;
+  S.nLevels = nLev, S.nPairs = ccnt[nTiles];
+  S.nSuper = 0;
+  for (int32_t J = 0; J < nT; J++) S.nSuper += pr[J] != 2 ? 1 : 0;
+  S.nCopy = (int64_t)copy.size() / 2;
+  if (upload(&S.updD, fan) || upload(&S.fanPairsD, pairs) || upload(&S.potD, pot) || upload(&S.rowD, rows) ||
+      upload(&S.fusD, fus) || upload(&S.copyD, copy))
+    return VB_E_HIP;
+  if (S.nCopy && !h->lscrSn && alloc0(&h->lscrSn, 2 * (size_t)nT * TS * TS)) return VB_E_HIP;
   S.built = true;
   return 0;
 }
@@ -1947,12 +1982,15 @@ void factorSeqSn(vb_handle h) {
     launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
     profEnd(h, KF_GEMM);
     profBegin(h, KF_POTRF);
+    if (S.lvF[L + 1] > S.lvF[L])
+      launch_snpotrf_trsm(d, S.fusD + 8 * S.lvF[L], (int)(S.lvF[L + 1] - S.lvF[L]), h->lscrSn, h->dinv, h->st, fb, fy);
     launch_snpotrf(d, S.potD + 4 * s0, (int)(S.lvS[L + 1] - s0), h->dinv, h->st, fb, fy);
     profEnd(h, KF_POTRF);
     profBegin(h, KF_TRSM);
     launch_sntrsm(d, S.rowD + 8 * r0, (int)(S.lvR[L + 1] - r0), h->dinv, h->st, fy, fb);
     profEnd(h, KF_TRSM);
   }
+  if (S.nCopy) launch_copy_diag(d, S.copyD, (int)S.nCopy, h->lscrSn, h->st);
   const Sched& C = h->sch[0];
   launch_diag_inverse(d, C.potrfColD, C.lvP[C.nLevels], h->linv, h->st);
 }
@@ -2274,7 +2312,7 @@ int vb_destroy(vb_handle h) {
                   d.stepPt, d.subRed, d.subPt, d.lmList, d.rsOff, d.rsS, d.rsI, d.rsG, d.rsN, d.imuT, d.imuV, d.rsMid, d.rsHalf,
                   d.rsCalib, d.red, d.redS, d.err, h->colTilesD,
                   h->colRowsD, h->rowTilesD, h->rowColD, h->padRowsD, h->colStartD, h->rowStartD, h->solveFlags, h->rootTilesD, h->rootRowsD, h->rootPack, h->rowPack, h->ownRowsD, h->ownPack, h->shardTilesD, h->shardPack, (void*)h->d.colOwner, h->dinv, h->yvec,
-                  h->rhsWork, h->linv, h->lscr, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
+                  h->rhsWork, h->linv, h->lscr, h->lscrSn, h->refStartD, h->refObsD, h->refPtD, h->refBackD, h->refAccD,
                   h->symvTilesD, h->symvRCD, h->pcgR, h->pcgZ, h->pcgP, h->pcgAp, h->pcgB, h->jacL, h->tilesGS, h->lpTiles, h->lpLinv, h->lpT, h->clearTilesD,
                   (void*)h->pi.src, (void*)h->pi.t, (void*)h->pi.v, (void*)h->pi.off, (void*)h->pi.noise,
                   h->tilesAlt, h->cacheAlt, h->gRedAlt, h->rsSAlt, h->rsIAlt, h->rsGAlt, h->rsNAlt};
@@ -2311,7 +2349,7 @@ int vb_destroy(vb_handle h) {
   if (h->hostRed) hipHostFree(h->hostRed);
   {
     SnSched& N = h->sn;
-    for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD})
+    for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD, (void*)N.fusD, (void*)N.copyD})
       if (p) hipFree(p);
     for (hipGraphExec_t g : N.graph)
       if (g) hipGraphExecDestroy(g);

@@ -822,6 +822,7 @@ struct Chol16<16> {
 // term, so the serial chain is one FMA + one multiply per row (L from LDS by broadcast reads).
 // (A one-MFMA-per-pivot variant -- the rank-1 update as a v_mfma_f64_16x16x4_f64 on the D layout --
 // measured slower: each pivot then waits on a dependent MFMA + readlane, 7.9k vs 5.7k cycles.)
+template <int LDT = TS>
 __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS, int i, double4_t S, int lane,
                                        bool& bad) {
   const int lr = lane & 15, lq = lane >> 4;
@@ -838,7 +839,7 @@ __device__ __forceinline__ void diag16(double* T, double* scratch, double* dinvS
     for (int c = 0; c < 16; c++) {
       const double v = (c <= lane) ? s[c] : 0.0;
       scratch[lane * 16 + c] = v;
-      T[(16 * i + c) * TS + 16 * i + lane] = v;
+      T[(16 * i + c) * LDT + 16 * i + lane] = v;
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1114,6 +1115,246 @@ __device__ __forceinline__ double rows_dot(const double4_t (&X)[4], const double
   return v;
 }
 
+// potrf4_core generalised to a (16 NB)-wide diagonal block held as up to three tiles (A11; for NB = 8 also
+// A21 = tile (J + 1, J), A22 = tile (J + 1, J + 1)): NB waves, wave w keeps its 16-row block of the
+// lower triangle in registers; L goes to LDS T (stride LDT), the 16 x 16 block inverses to dinvS
+// (NB x 256).  Waves >= NB only pass the barriers.  Between two diag16 the chain is 8 dependent MFMAs.
+// With b0 (the fused forward solve; b1: the second column's 64 rows) the forward substitution runs inside
+// the block loop: wave k forms y_k = Dinv_k b_k right after its diag16, and every wave below subtracts
+// L_wk y_k from its rows with the L_wk it just formed -- no serial pass after the factorization.  y goes to
+// yb[128, 128 + 16 NB) (yb[0, 16 NB): staging of b).
+template <int NB, int LDT>
+__device__ __forceinline__ void potrf_core(const Dev& d, const double* A11, const double* A21, const double* A22,
+                                           double* T, double* scratch, double* dinvS, int tid,
+                                           const double* b0 = nullptr, const double* b1 = nullptr,
+                                           double* yb = nullptr) {
+  const int lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  double bw = 0.0;  // b of this wave's 16 rows (lane: row 16 w + lr)
+  if (b0 && w < NB) bw = (w < 4 ? b0 : b1)[16 * (w & 3) + lr];
+  double4_t R[NB];
+  if (w < NB) {
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+      const double* P = w < 4 ? A11 : (j < 4 ? A21 : A22);
+      const int rr = 16 * (w & 3), cc = 16 * (j & 3);
+      if (j < w) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) R[j][r] = P[(cc + lq + 4 * r) * TS + rr + lr];
+      } else if (j == w) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) R[j][r] = P[(cc + lr) * TS + rr + lq + 4 * r];  // lower part valid
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) T[(16 * j + lq + 4 * r) * LDT + 16 * w + lr] = 0.0;
+      }
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    if (w == k) {
+      diag16<LDT>(T, scratch, dinvS, k, R[k], lane, bad);
+      if (b0) {  // y_k = Dinv_k b_k (this wave's rows are final)
+        if (lq == 0) yb[16 * k + lr] = bw;
+        wave_sync_lds();
+        if (lq == 0) {
+          double v = 0.0;
+#pragma unroll
+          for (int m = 0; m < 16; m++) v += dinvS[k * 256 + m * 16 + lr] * yb[16 * k + m];
+          yb[128 + 16 * k + lr] = v;
+        }
+      }
+    }
+    __syncthreads();
+    double4_t Lt = double4_t{0, 0, 0, 0};
+    if (w > k && w < NB) {
+#pragma unroll
+      for (int s = 0; s < 4; s++) Lt = mfma64(dinvS[k * 256 + (4 * s + lq) * 16 + lr], R[k][s], Lt);
+#pragma unroll
+      for (int r = 0; r < 4; r++) T[(16 * k + lq + 4 * r) * LDT + 16 * w + lr] = Lt[r];
+      if (b0) {  // b_w -= L_wk y_k (lane (lr, lq) holds L(16 w + lr, 16 k + lq + 4 r))
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) v += Lt[r] * yb[128 + 16 * k + lq + 4 * r];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        bw -= v;
+      }
+#pragma unroll
+      for (int j = k + 1; j < NB; j++)
+        if (j == w) {
+#pragma unroll
+          for (int s = 0; s < 4; s++) R[j] = mfma64(-Lt[s], Lt[s], R[j]);
+        }
+    }
+    if (k < NB - 2) {
+      __syncthreads();
+#pragma unroll
+      for (int j = k + 1; j < NB - 1; j++)
+        if (j < w && w < NB) {
+#pragma unroll
+          for (int s = 0; s < 4; s++) R[j] = mfma64(-T[(16 * k + 4 * s + lq) * LDT + 16 * j + lr], Lt[s], R[j]);
+        }
+    }
+  }
+  __syncthreads();
+  if (bad && lane == 0) atomicOr(d.err, 8);
+}
+
+// this wave's 16 rows of [A_I1 A_I2] L^-T over the (16 NB)-wide factored block in LDS (T, dinvS):
+// a[k] = column block k of A (D layout) in, X[k] out
+template <int NB, int LDT>
+__device__ __forceinline__ void trsm_lds(const double* T, const double* dinvS, const double4_t (&a)[NB], double4_t (&X)[NB],
+                                         int lr, int lq) {
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    double4_t acc = a[k];
+#pragma unroll
+    for (int k2 = 0; k2 < k; k2++)
+#pragma unroll
+      for (int s = 0; s < 4; s++) acc = mfma64(-T[(16 * k2 + 4 * s + lq) * LDT + 16 * k + lr], X[k2][s], acc);
+    double4_t res = double4_t{0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 4; s++) res = mfma64(dinvS[k * 256 + (4 * s + lq) * 16 + lr], acc[s], res);
+    X[k] = res;
+  }
+}
+
+// block (bi, bj) (16 x 16) of the factored diagonal block in LDS -> its global tile (the 64 x 64 tiles
+// of a pair: (J, J) blocks < 4, (J + 1, J) rows >= 4, (J + 1, J + 1) both >= 4)
+template <int NB, int LDT>
+__device__ __forceinline__ void store_block_tiles(double* L11, double* L21, double* L22, const double* T, int tid,
+                                                  int nthreads) {
+  for (int i = tid; i < (16 * NB) * (16 * NB); i += nthreads) {
+    const int col = i / (16 * NB), row = i % (16 * NB);
+    if (row < 64 && col >= 64) continue;  // upper block (none stored)
+    double* P = row < 64 ? L11 : (col < 64 ? L21 : L22);
+    P[(col & 63) * TS + (row & 63)] = T[col * LDT + row];
+  }
+}
+
+// Two-column supernode diagonal block on eight waves (items as snpotrf_kernel): the 128 x 128 Cholesky
+// right-looking by 16-column blocks (8 diag16 steps: the two potrf4 chains with the L21 solve and the
+// A22 update folded into the same block loop), the 16 x 16 inverses, the fused forward solve.  A
+// one-column supernode runs the 64-wide form on waves 0-3.
+__global__ void __launch_bounds__(512) snpotrf8_kernel(Dev d, const int32_t* items, double* dinvAll, const double* fwdB,
+                                                       double* fwdY) {
+  __shared__ double T[128 * 128];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[8 * 256];
+  __shared__ double yb[256];
+  const int32_t* it = items + 4 * (int64_t)blockIdx.x;
+  const int32_t t11 = it[0], J = it[1], t21 = it[2], t22 = it[3];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double* A11 = d.tiles + (int64_t)t11 * TS * TS;
+  if (t21 < 0) {
+    potrf_core<4, 128>(d, A11, nullptr, nullptr, T, scratch, dinvS, tid, fwdB ? fwdB + (int64_t)J * TS : nullptr,
+                       nullptr, yb);
+    if (fwdB && w == 0) {
+      const int64_t row = (int64_t)J * TS + lane;
+      fwdY[row] = row < d.nRed ? yb[128 + lane] : 0.0;
+    }
+    store_block_tiles<4, 128>(A11, nullptr, nullptr, T, tid, 512);
+    for (int i = tid; i < 1024; i += 512) dinvAll[(int64_t)J * 1024 + i] = dinvS[i];
+    return;
+  }
+  double* A21 = d.tiles + (int64_t)t21 * TS * TS;
+  double* A22 = d.tiles + (int64_t)t22 * TS * TS;
+  potrf_core<8, 128>(d, A11, A21, A22, T, scratch, dinvS, tid, fwdB ? fwdB + (int64_t)J * TS : nullptr,
+                     fwdB ? fwdB + (int64_t)(J + 1) * TS : nullptr, yb);
+  if (fwdB && w < 2) {
+    const int64_t row = (int64_t)(J + w) * TS + lane;
+    fwdY[row] = row < d.nRed ? yb[128 + 64 * w + lane] : 0.0;
+  }
+  store_block_tiles<8, 128>(A11, A21, A22, T, tid, 512);
+  for (int i = tid; i < 2048; i += 512) dinvAll[(int64_t)J * 1024 + i] = dinvS[i];  // J and J + 1, consecutive
+}
+
+// Levels with few rows: the supernode's diagonal block and ONE of its rows per block (potrf_trsm_kernel
+// for supernodes).  Every block of a supernode factors the diagonal block itself from the untouched tiles
+// (identical result), then forms its row [L_I1 L_I2] = [A_I1 A_I2] L^-T from LDS; the writer block
+// stores L11 / L22 into Lscr[J] / Lscr[J + 1] and L21 into Lscr[nT + J] (the tiles are still being read
+// by the others; copy_diag_kernel puts them back after the last level), the inverses and y.
+// items: tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1), tile (I, J) or -1, tile (I, J + 1) or
+// -1, I (or -1: no row), writer
+__global__ void __launch_bounds__(512) snpotrf_trsm8_kernel(Dev d, const int32_t* items, double* Lscr, double* dinvAll,
+                                                            double* fwdB, double* fwdY) {
+  __shared__ double T[128 * 128];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[8 * 256];
+  __shared__ double yb[256];
+  const int32_t* it = items + 8 * xcd_block(blockIdx.x, gridDim.x);  // one supernode's rows on one XCD
+  const int32_t t11 = it[0], J = it[1], t21 = it[2], t22 = it[3], tI1 = it[4], tI2 = it[5], I = it[6], writer = it[7];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lr = lane & 15, lq = lane >> 4;
+  const bool two = t21 >= 0;
+  const int64_t nT = d.nT;
+  const double* A11 = d.tiles + (int64_t)t11 * TS * TS;
+  const double* b0 = fwdB ? fwdB + (int64_t)J * TS : nullptr;
+  if (two)
+    potrf_core<8, 128>(d, A11, d.tiles + (int64_t)t21 * TS * TS, d.tiles + (int64_t)t22 * TS * TS, T, scratch, dinvS, tid,
+                       b0, fwdB ? fwdB + (int64_t)(J + 1) * TS : nullptr, yb);
+  else
+    potrf_core<4, 128>(d, A11, nullptr, nullptr, T, scratch, dinvS, tid, b0, nullptr, yb);
+  // the row's operands (waves 0-3: 16 rows each), in flight during the forward step (loaded before the
+  // factorization they spill: the factorization's registers are live)
+  double4_t a[8];
+  if (I >= 0 && w < 4) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int32_t t = k < 4 ? tI1 : tI2;
+      if (t >= 0 && (k < 4 || two)) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) a[k][r] = d.tiles[(int64_t)t * TS * TS + (16 * (k & 3) + lq + 4 * r) * TS + 16 * w + lr];
+      } else {
+        a[k] = double4_t{0, 0, 0, 0};
+      }
+    }
+  }
+  if (fwdB && writer && w < (two ? 2 : 1)) {
+    const int64_t row = (int64_t)(J + w) * TS + lane;
+    fwdY[row] = row < d.nRed ? yb[128 + 64 * w + lane] : 0.0;
+  }
+  if (writer) {
+    if (two) store_block_tiles<8, 128>(Lscr + J * TS * TS, Lscr + (nT + J) * TS * TS, Lscr + (J + 1) * TS * TS, T, tid, 512);
+    else store_block_tiles<4, 128>(Lscr + J * TS * TS, nullptr, nullptr, T, tid, 512);
+    for (int i = tid; i < (two ? 2048 : 1024); i += 512) dinvAll[(int64_t)J * 1024 + i] = dinvS[i];
+  }
+  if (I < 0) return;
+  if (w >= 4) return;
+  double v = 0.0;
+  if (two) {
+    double4_t X[8];
+    trsm_lds<8, 128>(T, dinvS, a, X, lr, lq);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const int32_t t = k < 4 ? tI1 : tI2;
+      if (t >= 0) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) d.tiles[(int64_t)t * TS * TS + (16 * (k & 3) + lq + 4 * r) * TS + 16 * w + lr] = X[k][r];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) v += X[k][r] * yb[128 + 16 * k + lq + 4 * r];
+    }
+  } else {
+    double4_t a4[4], X[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) a4[k] = a[k];
+    trsm_lds<4, 128>(T, dinvS, a4, X, lr, lq);
+    store_rows(d.tiles + (int64_t)tI1 * TS * TS, X, w, lr, lq);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) v += X[k][r] * yb[128 + 16 * k + lq + 4 * r];
+  }
+  if (fwdB) {
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lq == 0) atomicAdd(fwdB + (int64_t)I * TS + 16 * w + lr, -v);
+  }
+}
+
 // The diagonal block of a supernode (items: tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1)):
 // L11 (potrf4_core), L21 = A21 L11^-T, A22 - L21 L21^T into LDS, L22; the 16 x 16 inverses of both
 // diagonal tiles; with the fused forward solve y_J, then b_{J+1} - L21 y_J (kept in LDS), then y_{J+1}.
@@ -1171,7 +1412,8 @@ __global__ void __launch_bounds__(256) snpotrf_kernel(Dev d, const int32_t* item
 // L_I2 = A_I2 L22^-T; with the fused forward solve b_I -= L_I1 y_J + L_I2 y_{J+1}
 __global__ void __launch_bounds__(256) sntrsm_kernel(Dev d, const int32_t* items, const double* dinvAll, const double* fwdY,
                                                      double* fwdB) {
-  const int32_t* it = items + 8 * (int64_t)blockIdx.x;
+  // consecutive items (the rows of one supernode) on one XCD: its L11 / L21 / L22 stay in that L2
+  const int32_t* it = items + 8 * xcd_block(blockIdx.x, gridDim.x);
   const int32_t tI1 = it[0], tI2 = it[1], J = it[2], J2 = it[3], I = it[4], t11 = it[5], t21 = it[6], t22 = it[7];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int lr = lane & 15, lq = lane >> 4;
@@ -1836,7 +2078,11 @@ void launch_potrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, 
 }
 void launch_snpotrf(const Dev& d, const int32_t* items, int n, double* dinv, hipStream_t st, const double* fwdB,
                     double* fwdY) {
-  if (n > 0) launchK(snpotrf_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdB, fwdY);
+  if (n > 0) launchK(snpotrf8_kernel, dim3(n), dim3(512), 0, st, d, items, dinv, fwdB, fwdY);
+}
+void launch_snpotrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr, double* dinv, hipStream_t st,
+                         double* fwdB, double* fwdY) {
+  if (n > 0) launchK(snpotrf_trsm8_kernel, dim3(n), dim3(512), 0, st, d, items, Lscr, dinv, fwdB, fwdY);
 }
 void launch_sntrsm(const Dev& d, const int32_t* items, int n, const double* dinv, hipStream_t st, const double* fwdY,
                    double* fwdB) {
