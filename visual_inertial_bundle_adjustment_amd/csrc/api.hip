@@ -273,7 +273,7 @@ struct Sched {
 
 // Two-column supernodes (VIBA_SUPERNODE, single handle): where column J + 1 is J's parent in the
 // elimination tree and J's other rows are rows of J + 1, the pair is factored as one 128-wide diagonal
-// block (snpotrf_kernel: L11, L21 = A21 L11^-T, A22 -= L21 L21^T, L22) and its rows by one kernel
+// block (snpotrf8_kernel: L11, L21 = A21 L11^-T, A22 -= L21 L21^T, L22) and its rows by one kernel
 // (sntrsm_kernel: L_I1 = A_I1 L11^-T, A_I2 -= L_I1 L21^T, L_I2 = A_I2 L22^-T), so the pair is ONE level
 // of the schedule: about half the levels (launches, dependency gaps, potrf latency chains) of the
 // column schedule.  The fan-in lists leave out the pair-internal contributions (J -> J + 1).
@@ -292,6 +292,7 @@ struct SnSched {
   std::vector<int64_t> lvF;
   int32_t *fusD = nullptr, *copyD = nullptr;
   int64_t nCopy = 0;
+
   hipGraphExec_t graph[2] = {nullptr, nullptr};
   bool built = false;
 };
@@ -404,7 +405,7 @@ struct vb_handle_s {
   double* hostRed = nullptr;  // pinned readback buffer: red[0, 17), then err[0, 2) as int32
   size_t profAtCost = 0;      // profiled event pairs recorded before evCost
   bool specReady = false;     // every speculative buffer, event and stream above exists (specPrepare)
-  SnSched sn;                 // two-column supernode schedule of the direct factorization
+  SnSched sn[2];              // two-column supernode schedules of sch[0] / sch[1] (direct factorization)
   bool useSn = true;          // VIBA_SUPERNODE=0 at creation: the column schedule
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
@@ -546,9 +547,13 @@ int readRedErr(vb_handle h, double* out, int n) {
   return errFromWords(h, ee);
 }
 
-// the two-column supernode schedule (SnSched) from the column patterns of the single-handle structure
-int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT, int64_t nTiles) {
-  SnSched& S = h->sn;
+// the two-column supernode schedule (SnSched) of a column schedule from the column patterns: colSel(J)
+// columns factored here, tgtSel(J) fan-in targets in column J, srcSel(K) contributions from column K
+// (the selectors of the column schedule's build(): all columns on a single handle; a rank's subtree plus
+// its ROOT targets, or the ROOT columns, in partition mode)
+int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx, int32_t nT, int64_t nTiles,
+                    const std::function<bool(int32_t)>& colSel, const std::function<bool(int32_t)>& tgtSel,
+                    const std::function<bool(int32_t)>& srcSel) {
   auto colRows = [&](int32_t J, int64_t& a, int64_t& b) { a = h->colStart[J], b = h->colStart[J + 1]; };
   // pair J with J + 1: J + 1 is J's first off-diagonal row (its parent) and every other row of J is a
   // row of J + 1 (so the pair's rows are J + 1's), both in one nested-dissection part
@@ -557,7 +562,9 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
     if (pr[J]) continue;
     int64_t a, b, a2, b2;
     colRows(J, a, b), colRows(J + 1, a2, b2);
-    if (b - a < 2 || h->colRowsH[a + 1] != J + 1 || h->colOwner[J] != h->colOwner[J + 1]) continue;
+    if (b - a < 2 || h->colRowsH[a + 1] != J + 1 || h->colOwner[J] != h->colOwner[J + 1] || !colSel(J) ||
+        !colSel(J + 1))
+      continue;
     bool sub = true;
     int64_t q = a2 + 1;
     for (int64_t c = a + 2; c < b && sub; c++) {
@@ -599,10 +606,12 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
     for (int32_t L = 0; L < nLev; L++)
       for (int32_t J0 : sup[L])
         for (int32_t K = J0; K <= J0 + (pr[J0] == 1 ? 1 : 0); K++) {
+          if (!srcSel(K)) continue;
           const int64_t c0 = h->colStart[K], n = h->colStart[K + 1] - c0;
           for (int64_t qi = 1; qi < n; qi++)
             for (int64_t qk = 1; qk <= qi; qk++) {
               if (pr[K] == 1 && qk == 1) continue;  // targets in column K + 1: inside the supernode
+              if (!tgtSel(h->colRowsH[c0 + qk])) continue;
               const int32_t t = tileIdx[(size_t)h->colRowsH[c0 + qi] * nT + h->colRowsH[c0 + qk]];
               if (t < 0) return fail(VB_E_STATE, "internal: symbolic fill incomplete");
               if (pass == 0) {
@@ -620,6 +629,7 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
   if (const char* e = getenv("VIBA_SN_FUSE")) fuseMax = atoll(e);
   std::vector<int32_t> fan, pot, rows, fus, copy;
   S.lvU.assign(nLev + 1, 0), S.lvS.assign(nLev + 1, 0), S.lvR.assign(nLev + 1, 0), S.lvF.assign(nLev + 1, 0);
+
   S.nTwo = 0;
   auto tile = [&](int32_t I, int32_t J) { return tileIdx[(size_t)I * nT + J]; };
   for (int32_t L = 0; L < nLev; L++) {
@@ -631,6 +641,7 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
     const size_t u0 = fan.size() / 4;
     int64_t nRowsL = 0;
     for (int32_t J0 : sup[L]) {
+      if (!colSel(J0)) continue;
       const int32_t Jl = pr[J0] == 1 ? J0 + 1 : J0;
       nRowsL += h->colStart[Jl + 1] - h->colStart[Jl] - 1;
     }
@@ -640,6 +651,7 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
       const int32_t J2 = two ? J0 + 1 : -1;
       for (int32_t J = J0; J <= (two ? J2 : J0); J++)
         for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
+          if (!tgtSel(J)) continue;
           const int32_t t = h->colTilesH[c];
           const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
           if (m == 0) continue;
@@ -649,6 +661,7 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
             fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
           }
         }
+      if (!colSel(J0)) continue;
       const int32_t t11 = tile(J0, J0), t21 = two ? tile(J2, J0) : -1, t22 = two ? tile(J2, J2) : -1;
       S.nTwo += two ? 1 : 0;
       // rows below the supernode: those of its last column (a pair's first column has no others)
@@ -688,7 +701,7 @@ int buildSupernodes(vb_handle h, const std::vector<int32_t>& tileIdx, int32_t nT
   }
   S.nLevels = nLev, S.nPairs = ccnt[nTiles];
   S.nSuper = 0;
-  for (int32_t J = 0; J < nT; J++) S.nSuper += pr[J] != 2 ? 1 : 0;
+  for (int32_t J = 0; J < nT; J++) S.nSuper += (pr[J] != 2 && colSel(J)) ? 1 : 0;
   S.nCopy = (int64_t)copy.size() / 2;
   if (upload(&S.updD, fan) || upload(&S.fanPairsD, pairs) || upload(&S.potD, pot) || upload(&S.rowD, rows) ||
       upload(&S.fusD, fus) || upload(&S.copyD, copy))
@@ -1736,8 +1749,19 @@ int doFinalize(vb_handle h) {
     }
     h->nLevels = nLev;
     h->nPairs = h->sch[0].nPairs + h->sch[1].nPairs;
-    if (W <= 1 && h->useSn)
-      if (int rc = buildSupernodes(h, tileIdx, nT, nTiles)) return rc;
+    if (h->useSn) {
+      if (W <= 1) {
+        auto any = [](int32_t) { return true; };
+        if (int rc = buildSupernodes(h, h->sn[0], tileIdx, nT, nTiles, any, any, any)) return rc;
+      } else {
+        auto own = [&](int32_t J) { return h->colOwner[J] == me; };
+        auto root = [&](int32_t J) { return h->colOwner[J] == W; };
+        auto ownOrRoot = [&](int32_t J) { return h->colOwner[J] == me || h->colOwner[J] == W; };
+        if (int rc = buildSupernodes(h, h->sn[0], tileIdx, nT, nTiles, own, ownOrRoot, own)) return rc;
+        if (me == 0)
+          if (int rc = buildSupernodes(h, h->sn[1], tileIdx, nT, nTiles, root, root, root)) return rc;
+      }
+    }
   }
   // ---------------- small factors (+ whitening square roots)
   for (int fk = 1; fk < 14; fk++) {
@@ -1970,10 +1994,10 @@ void factorSeq(vb_handle h, const Sched& S) {
 
 // the two-column supernode schedule (SnSched): per level the fan-in of its targets, the supernodes'
 // diagonal blocks, their rows; then the diagonal-tile inverses of the solves (every column)
-void factorSeqSn(vb_handle h) {
+void factorSeqSn(vb_handle h, int which) {
   Dev& d = h->d;
-  const SnSched& S = h->sn;
-  const bool fwd = fwdFused(h) && !h->factorOnly;
+  const SnSched& S = h->sn[which];
+  const bool fwd = fwdFused(h) && which == 0 && !h->factorOnly;
   double* fb = fwd ? h->rhsWork : nullptr;
   double* fy = fwd ? h->yvec : nullptr;
   for (int32_t L = 0; L < S.nLevels; L++) {
@@ -1991,16 +2015,16 @@ void factorSeqSn(vb_handle h) {
     profEnd(h, KF_TRSM);
   }
   if (S.nCopy) launch_copy_diag(d, S.copyD, (int)S.nCopy, h->lscrSn, h->st);
-  const Sched& C = h->sch[0];
+  const Sched& C = h->sch[which];
   launch_diag_inverse(d, C.potrfColD, C.lvP[C.nLevels], h->linv, h->st);
 }
 
 // launch sequences are fixed by the symbolic structure: capture them once into HIP graphs
 // (unless one of their kernel families is being profiled, which needs per-launch events)
-int captureGraph(vb_handle h, const Sched& S, hipGraphExec_t* out, bool sn = false) {
+int captureGraph(vb_handle h, const Sched& S, hipGraphExec_t* out, bool sn = false, int which = 0) {
   hipGraph_t g;
   HIPCHK(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
-  if (sn) factorSeqSn(h);
+  if (sn) factorSeqSn(h, which);
   else factorSeq(h, S);
   HIPCHK(hipStreamEndCapture(h->st, &g));
   HIPCHK(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
@@ -2015,15 +2039,15 @@ int factorReduced(vb_handle h, int which = 0) {
   const bool prof = h->profFamily == KF_POTRF || h->profFamily == KF_GEMM || h->profFamily == KF_TRSM;
   // (a profiled family runs launch by launch: its per-launch events, recorded as event nodes inside
   // a graph, cost as much as the graph saves -- measured)
-  const bool sn = which == 0 && h->sn.built;
+  const bool sn = h->sn[which].built;
   if (!h->useGraphs || prof || h->factorOnly) {
-    if (sn) factorSeqSn(h);
+    if (sn) factorSeqSn(h, which);
     else factorSeq(h, S);
     return 0;
   }
-  hipGraphExec_t& g = sn ? h->sn.graph[h->tileSet] : S.graph[h->tileSet];
+  hipGraphExec_t& g = sn ? h->sn[which].graph[h->tileSet] : S.graph[h->tileSet];
   if (!g)
-    if (int rc = captureGraph(h, S, &g, sn)) return rc;
+    if (int rc = captureGraph(h, S, &g, sn, which)) return rc;
   HIPCHK(hipGraphLaunch(g, h->st));
   return 0;
 }
@@ -2347,8 +2371,7 @@ int vb_destroy(vb_handle h) {
       if (e) hipEventDestroy(e);
   if (h->stR) hipStreamSynchronize(h->stR), hipStreamDestroy(h->stR);
   if (h->hostRed) hipHostFree(h->hostRed);
-  {
-    SnSched& N = h->sn;
+  for (SnSched& N : h->sn) {
     for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD, (void*)N.fusD, (void*)N.copyD})
       if (p) hipFree(p);
     for (hipGraphExec_t g : N.graph)
@@ -3215,8 +3238,9 @@ int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
 // two-column supernodes] (the column schedule: supernodes = columns, no two-column ones)
 int vb_factor_schedule_stats(vb_handle h, int64_t* out4) {
   if (!h || !h->finalized || !out4) return fail(VB_E_STATE, "not finalized");
-  if (h->sn.built) {
-    out4[0] = h->sn.nLevels, out4[1] = h->sn.nPairs, out4[2] = h->sn.nSuper, out4[3] = h->sn.nTwo;
+  if (h->sn[0].built) {
+    const SnSched& N = h->sn[0];
+    out4[0] = N.nLevels, out4[1] = N.nPairs, out4[2] = N.nSuper, out4[3] = N.nTwo;
   } else {
     out4[0] = h->nLevels, out4[1] = h->nPairs, out4[2] = h->d.nT, out4[3] = 0;
   }

@@ -1046,6 +1046,7 @@ __global__ void __launch_bounds__(256) potrf_trsm_kernel(Dev d, const int32_t* i
 // X = A L^-T for one tile row block per wave (trsm_kernel's body): acc holds A (D layout: lane (lr, lq),
 // register r = element (row 16 w + lr, column 16 k + lq + 4 r)); L the factored diagonal tile, dinv its
 // 16 x 16 block inverses.  Every operand is loaded before the substitution chain.
+template <int LD = TS>
 __device__ __forceinline__ void trsm_rows(const double* L, const double* dinv, double4_t (&acc)[4], double4_t (&Xt)[4],
                                           int lr, int lq) {
   double lv[6][4], dv[4][4];
@@ -1054,7 +1055,7 @@ __device__ __forceinline__ void trsm_rows(const double* L, const double* dinv, d
 #pragma unroll
     for (int k2 = 0; k2 < k; k2++)
 #pragma unroll
-      for (int s = 0; s < 4; s++) lv[k * (k - 1) / 2 + k2][s] = L[(16 * k2 + 4 * s + lq) * TS + 16 * k + lr];
+      for (int s = 0; s < 4; s++) lv[k * (k - 1) / 2 + k2][s] = L[(16 * k2 + 4 * s + lq) * LD + 16 * k + lr];
 #pragma unroll
   for (int k = 0; k < 4; k++)
 #pragma unroll
@@ -1074,6 +1075,7 @@ __device__ __forceinline__ void trsm_rows(const double* L, const double* dinv, d
 }
 // acc -= X M^T over all four column blocks of M (a full tile: the update of a supernode's second column by
 // its first), X in D layout, M column-major in memory (global or LDS)
+template <int LD = TS>
 __device__ __forceinline__ void gemm_nt_sub(const double* M, const double4_t (&Xt)[4], double4_t (&acc)[4], int lr, int lq,
                                             int kmax = 3) {
 #pragma unroll
@@ -1083,7 +1085,7 @@ __device__ __forceinline__ void gemm_nt_sub(const double* M, const double4_t (&X
 #pragma unroll
     for (int k2 = 0; k2 < 4; k2++)
 #pragma unroll
-      for (int s = 0; s < 4; s++) mv[k2][s] = M[(16 * k2 + 4 * s + lq) * TS + 16 * k + lr];
+      for (int s = 0; s < 4; s++) mv[k2][s] = M[(16 * k2 + 4 * s + lq) * LD + 16 * k + lr];
 #pragma unroll
     for (int k2 = 0; k2 < 4; k2++)
 #pragma unroll
@@ -1355,63 +1357,11 @@ __global__ void __launch_bounds__(512) snpotrf_trsm8_kernel(Dev d, const int32_t
   }
 }
 
-// The diagonal block of a supernode (items: tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1)):
-// L11 (potrf4_core), L21 = A21 L11^-T, A22 - L21 L21^T into LDS, L22; the 16 x 16 inverses of both
-// diagonal tiles; with the fused forward solve y_J, then b_{J+1} - L21 y_J (kept in LDS), then y_{J+1}.
-// A one-column supernode is potrf4_kernel.
-__global__ void __launch_bounds__(256) snpotrf_kernel(Dev d, const int32_t* items, double* dinvAll, const double* fwdB,
-                                                      double* fwdY) {
-  __shared__ double T[TS * TS];   // L11, then L22
-  __shared__ double U[TS * TS];   // A22 - L21 L21^T
-  __shared__ double M[TS * TS];   // L21
-  __shared__ double scratch[256];
-  __shared__ double dinvS[1024];
-  __shared__ double bS[TS];
-  const int32_t* it = items + 4 * (int64_t)blockIdx.x;
-  const int32_t t11 = it[0], J = it[1], t21 = it[2], t22 = it[3];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int lr = lane & 15, lq = lane >> 4;
-  double* A11 = d.tiles + (int64_t)t11 * TS * TS;
-  double4_t a21[4], a22[4];
-  if (t21 >= 0) {  // both operands of the second column in flight during the first factorization
-    load_rows(d.tiles + (int64_t)t21 * TS * TS, a21, w, lr, lq);
-    load_rows(d.tiles + (int64_t)t22 * TS * TS, a22, w, lr, lq);
-  }
-  potrf4_core(d, A11, T, scratch, dinvS, tid);
-  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, J, fwdB + (int64_t)J * TS, fwdY, lane);
-  __syncthreads();  // y_J (scratch[0, 64))
-  if (t21 < 0) {
-    lds_to_global(A11, T, TS * TS, tid, 256);
-    lds_to_global(dinvAll + (int64_t)J * 1024, dinvS, 1024, tid, 256);
-    return;
-  }
-  // L21 = A21 L11^-T: this wave's 16 rows, from T / dinvS in LDS
-  double4_t X[4];
-  trsm_rows(T, dinvS, a21, X, lr, lq);
-  store_rows(M, X, w, lr, lq);
-  if (fwdB) {  // b_{J+1} - L21 y_J for the second column's forward step
-    const double v = rows_dot(X, scratch, lq);
-    if (lq == 0) bS[16 * w + lr] = fwdB[(int64_t)(J + 1) * TS + 16 * w + lr] - v;
-  }
-  lds_to_global(A11, T, TS * TS, tid, 256);
-  lds_to_global(dinvAll + (int64_t)J * 1024, dinvS, 1024, tid, 256);
-  __syncthreads();  // M complete; T, dinvS, scratch free
-  // U = A22 - L21 L21^T: wave w its row block, column blocks <= w (the diagonal block whole)
-  gemm_nt_sub(M, X, a22, lr, lq, w);
-  store_rows(U, a22, w, lr, lq);
-  store_rows(d.tiles + (int64_t)t21 * TS * TS, X, w, lr, lq);
-  __syncthreads();
-  potrf4_core(d, U, T, scratch, dinvS, tid);
-  if (fwdB && w == 0) potrf_forward(d, T, dinvS, scratch, J + 1, bS, fwdY, lane);
-  lds_to_global(d.tiles + (int64_t)t22 * TS * TS, T, TS * TS, tid, 256);
-  lds_to_global(dinvAll + (int64_t)(J + 1) * 1024, dinvS, 1024, tid, 256);
-}
-
 // The rows of a supernode, one block per row I below it (items: tile (I, J) or -1, tile (I, J + 1) or -1,
 // J, J + 1 or -1, I, tiles (J, J), (J + 1, J), (J + 1, J + 1)): L_I1 = A_I1 L11^-T, A_I2 -= L_I1 L21^T,
 // L_I2 = A_I2 L22^-T; with the fused forward solve b_I -= L_I1 y_J + L_I2 y_{J+1}
-__global__ void __launch_bounds__(256) sntrsm_kernel(Dev d, const int32_t* items, const double* dinvAll, const double* fwdY,
-                                                     double* fwdB) {
+__device__ __forceinline__ void sntrsm_body(const Dev& d, const int32_t* items, const double* dinvAll, const double* fwdY,
+                                            double* fwdB) {
   // consecutive items (the rows of one supernode) on one XCD: its L11 / L21 / L22 stay in that L2
   const int32_t* it = items + 8 * xcd_block(blockIdx.x, gridDim.x);
   const int32_t tI1 = it[0], tI2 = it[1], J = it[2], J2 = it[3], I = it[4], t11 = it[5], t21 = it[6], t22 = it[7];
@@ -1436,6 +1386,15 @@ __global__ void __launch_bounds__(256) sntrsm_kernel(Dev d, const int32_t* items
     if (fwdB) v += rows_dot(X2, fwdY + (int64_t)J2 * TS, lq);
   }
   if (fwdB && lq == 0) atomicAdd(fwdB + (int64_t)I * TS + 16 * w + lr, -v);
+}
+__global__ void __launch_bounds__(256) sntrsm_kernel(Dev d, const int32_t* items, const double* dinvAll, const double* fwdY,
+                                                     double* fwdB) {
+  sntrsm_body(d, items, dinvAll, fwdY, fwdB);
+}
+// the same at four waves per SIMD (<= 128 VGPRs): more rows in flight per CU (VIBA_SN_TRSM_W4=1)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
+sntrsm_w4_kernel(Dev d, const int32_t* items, const double* dinvAll, const double* fwdY, double* fwdB) {
+  sntrsm_body(d, items, dinvAll, fwdY, fwdB);
 }
 
 // the diagonal tiles of the fused levels back from Lscr (pairs: diagonal tile, column)
@@ -2086,7 +2045,9 @@ void launch_snpotrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr
 }
 void launch_sntrsm(const Dev& d, const int32_t* items, int n, const double* dinv, hipStream_t st, const double* fwdY,
                    double* fwdB) {
-  if (n > 0) launchK(sntrsm_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdY, fwdB);
+  static const bool w4 = getenv("VIBA_SN_TRSM_W4") && atoi(getenv("VIBA_SN_TRSM_W4")) == 1;
+  if (n > 0 && w4) launchK(sntrsm_w4_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdY, fwdB);
+  else if (n > 0) launchK(sntrsm_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdY, fwdB);
 }
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(copy_diag_kernel, dim3(n), dim3(256), 0, st, d, pairs, Lscr);
