@@ -1394,6 +1394,23 @@ int doFinalize(vb_handle h) {
         }
       }
     for (TileWork& w : works) w.kind = itemsPerTile[w.tile] > 1 ? 1 : 0;
+    // VIBA_SCHUR_ORDER=1: items by the median landmark of their entries (landmarks are numbered by their
+    // earliest observing rig), so the items an XCD runs at one time share their landmarks' Y panels in
+    // its L2; default: tile-column order
+    if (const char* e = getenv("VIBA_SCHUR_ORDER"); e && atoi(e) == 1) {
+      std::vector<std::pair<int64_t, size_t>> key(works.size());
+      std::vector<uint32_t> lms;
+      for (size_t i = 0; i < works.size(); i++) {
+        lms.clear();
+        for (int32_t k = 0; k < works[i].count; k++) lms.push_back(ents[works[i].start + k].lm);
+        std::nth_element(lms.begin(), lms.begin() + lms.size() / 2, lms.end());
+        key[i] = {lms.empty() ? 0 : (int64_t)lms[lms.size() / 2], i};
+      }
+      std::stable_sort(key.begin(), key.end());
+      std::vector<TileWork> sorted(works.size());
+      for (size_t i = 0; i < works.size(); i++) sorted[i] = works[key[i].second];
+      works.swap(sorted);
+    }
     // a tile written by exactly one Schur item and by no direct term is stored whole by that item (kind
     // 2: no read of the tile) and left out of the clear in vb_linearize (single handle; shards and
     // partitions clear their tile ranges and add); the clear covers the rest, by tile list
