@@ -1480,7 +1480,7 @@ int doFinalize(vb_handle h) {
     }
     if (getenv("VIBA_SCHUR_STATS")) {  // diagnostics: compact widths, MFMA padding, runs, tasks
       int64_t hI[5] = {0}, hJ[5] = {0}, nRun = 0, nTask = 0, runLm = 0;
-      double useful = 0, issued = 0, issued4 = 0;
+      double useful = 0, issued = 0, issued4 = 0, gathered = 0, segBytes = 0;
       auto bin = [](int n) { return n <= 4 ? 0 : n <= 8 ? 1 : n <= 16 ? 2 : n <= 32 ? 3 : 4; };
       for (const TileWork& w : works) {
         const bool diag = w.I == w.J;
@@ -1502,14 +1502,27 @@ int doFinalize(vb_handle h) {
           issued4 += 2.0 * 4.0 * std::ceil(rows / 4.0) * 16.0 * ((nI + 3) / 4) * ((nJ + 3) / 4) * (diag ? 0.5 : 1.0);
         }
         nTask += w.wOff[4];
+        for (int t = 0; t < w.wOff[4]; t++) {  // gathered operand bytes: every k-step's NR + NBI 16-wide rows
+          const uint32_t code = tasksH[(size_t)w.taskFirst + t];
+          const int r = code & 255, nl = (code >> 16) & 63, a0 = (code >> 22) & 3;
+          const uint64_t mI = runsH[2 * ((size_t)w.runFirst + r)], mJ = runsH[2 * ((size_t)w.runFirst + r) + 1];
+          const int nbI = (__builtin_popcountll(mI) + 15) / 16, nbJ = (__builtin_popcountll(mJ) + 15) / 16;
+          const int nr = std::min(kSchurTR, nbJ - a0);
+          gathered += 4.0 * ((3 * nl + 3) / 4) * (nr + nbI) * 16 * sizeof(rec_t);
+        }
+        for (int e = 0; e < w.count; e++) {  // the entries' Y segments once per item
+          const TileEnt& a = ents[w.start + e];
+          segBytes += 3.0 * (__builtin_popcountll(a.maskI) + (diag ? 0 : __builtin_popcountll(a.maskJ))) * sizeof(rec_t);
+        }
       }
       fprintf(stderr,
               "[schur stats] items %zu runs %lld tasks %lld landmarks/run %.2f; nI <=4/8/16/32/64: %lld %lld %lld %lld "
-              "%lld; nJ: %lld %lld %lld %lld %lld; GFLOP useful %.2f issued(16x16) %.2f issued(4x4) %.2f\n",
+              "%lld; nJ: %lld %lld %lld %lld %lld; GFLOP useful %.2f issued(16x16) %.2f issued(4x4) %.2f; GB gathered %.2f, "
+              "entry segments %.2f\n",
               works.size(), (long long)nRun, (long long)nTask, (double)runLm / std::max<int64_t>(1, nRun),
               (long long)hI[0], (long long)hI[1], (long long)hI[2], (long long)hI[3], (long long)hI[4], (long long)hJ[0],
               (long long)hJ[1], (long long)hJ[2], (long long)hJ[3], (long long)hJ[4], useful * 1e-9, issued * 1e-9,
-              issued4 * 1e-9);
+              issued4 * 1e-9, gathered * 1e-9, segBytes * 1e-9);
     }
     if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH)) return VB_E_HIP;
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)

@@ -582,54 +582,14 @@ __device__ __forceinline__ int grp_col_row(const Dev& d, const int32_t* red, int
   return (int)(d.rvOff[X] + j);
 }
 
-__global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, int mode) {
-  __shared__ double red_[4][64][14];
-  const int64_t g = xcd_block(blockIdx.x, gridDim.x);
+// the end of a group: the 4 waves' accumulators reduced through LDS (`red`: 4 x 64 x 14 doubles, free on
+// entry), g into gRed / gRedNew (mode 1), H (diagonal damped by (1 + lambda)) scattered into the tiles
+__device__ __forceinline__ void group_finish(const Dev& d, double lambda, int mode, int row0, int row1, const hacc4_t& a00,
+                                             const hacc4_t& a10, const hacc4_t& a11, double g0, double g1, double* red) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l15 = lane & 15, l4 = lane >> 4;
-  const int32_t* rv = d.grpRed + 4 * g;
-  int p0, s0, p1, s1;
-  const int row0 = grp_col_row(d, rv, l15, p0, s0);
-  const int row1 = grp_col_row(d, rv, 16 + l15, p1, s1);
-  const int64_t o0 = d.grpStart[g], n = d.grpStart[g + 1] - o0;
-  const int r = l4 & 1;
-  const int64_t nks = (n + 1) / 2;
-  hacc4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
-  double g0 = 0.0, g1 = 0.0;
-  const rec_t* Jt = d.Jt;
-  // 4 k-steps per iteration (this wave's ks, ks + 4, ks + 8, ks + 12): their observation indices, then
-  // all their record loads, then the products, so the loads of one iteration are in flight together
-  constexpr int kU = 4;
-  for (int64_t ks0 = wave; ks0 < nks; ks0 += 4 * kU) {
-    int64_t oo[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const int64_t e = 2 * (ks0 + 4 * u) + (l4 >> 1);
-      oo[u] = e < n ? d.grpObs[o0 + e] : -1;
-    }
-    rec_t v0[kU], v1[kU], er[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      v0[u] = v1[u] = er[u] = 0;
-      const int64_t o = oo[u];
-      if (o >= 0) {
-        er[u] = Jt[o * kJA + kJe + r];
-        if (row0 >= 0) v0[u] = jt_plane(Jt, d.nObsPad, o, p0)[r * s0];
-        if (row1 >= 0) v1[u] = jt_plane(Jt, d.nObsPad, o, p1)[r * s1];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kU; u++) {
-      g0 += (double)v0[u] * er[u], g1 += (double)v1[u] * er[u];
-      if (mode == 0) {
-        a00 = mfma_h(v0[u], v0[u], a00);
-        a10 = mfma_h(v1[u], v0[u], a10);
-        a11 = mfma_h(v1[u], v1[u], a11);
-      }
-    }
-  }
   // reduce the 4 waves (and, for g, the 4 lane groups) through LDS
-  double* mine = red_[wave][lane];
+  double* mine = red + (wave * 64 + lane) * 14;
 #pragma unroll
   for (int k = 0; k < 4; k++) mine[k] = a00[k], mine[4 + k] = a10[k], mine[8 + k] = a11[k];
   mine[12] = g0, mine[13] = g1;
@@ -637,7 +597,7 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
   if (wave != 0) return;
   double t[14];
 #pragma unroll
-  for (int k = 0; k < 14; k++) t[k] = red_[0][lane][k] + red_[1][lane][k] + red_[2][lane][k] + red_[3][lane][k];
+  for (int k = 0; k < 14; k++) t[k] = red[lane * 14 + k] + red[(64 + lane) * 14 + k] + red[(128 + lane) * 14 + k] + red[(192 + lane) * 14 + k];
   // g: lanes l15 of the 4 lane groups hold partial sums of the same columns
   double gc0 = t[12], gc1 = t[13];
 #pragma unroll
@@ -653,7 +613,7 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
   if (mode != 0) return;
   // H (32 x 32, symmetric) into LDS over the reduction buffer (this wave has read it): D[m][n],
   // m = kAccL4 l4 + kAccR k (+16), n = l15 (+16); the cross block also mirrored
-  double* H = &red_[0][0][0];
+  double* H = red;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int m = kAccL4 * l4 + kAccR * k;
@@ -714,6 +674,110 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
     if (ti >= 0) atomicAdd(d.tiles + (int64_t)ti * TS * TS + (C % TS) * TS + (R % TS), v);
     else atomicOr(d.err, 4);
   }
+}
+
+// The group's records are streamed through LDS in chunks of kGrpChunk observations, each record copied
+// whole (both regions, 16 B per lane by global_load_lds: a handful of wide loads per thread per chunk,
+// where gathering the three operands of every k-step straight from HBM, behind an index load, ran
+// 1.05 ms against 0.86 alone on config C), double-buffered (chunk k + 1 in flight while chunk k feeds the
+// MFMAs).  Staged record c holds plane p at stage[c * kJPlanes + p].  The group's observation indices
+// come into LDS first, by windows of kGrpIdx.
+constexpr int kGrpChunk = 32;                                      // observations per staged chunk
+constexpr int kRecV = 16 / (int)sizeof(rec_t);                     // record elements per 16 B piece
+constexpr int kRecPieces = kJPlanes / kRecV;                       // 16 B pieces per record (36 / 18)
+constexpr int kGrpLoads = (kGrpChunk * kRecPieces + 255) / 256;    // global_load_lds per thread per chunk
+constexpr int kGrpStage = kGrpLoads * 256 * kRecV;                 // rec_t per buffer (tail pieces land past the chunk)
+constexpr int kGrpIdx = 1024;                                      // observation indices per window
+static_assert(kJA % kRecV == 0 && kJB % kRecV == 0, "record regions in whole 16 B pieces");
+constexpr int kGrpLds = 2 * kGrpStage * (int)sizeof(rec_t) > 4 * 64 * 14 * 8 ? 2 * kGrpStage * (int)sizeof(rec_t) : 4 * 64 * 14 * 8;
+
+// three LDS reads behind one wait, in inline asm: as plain loads the compiler put an s_waitcnt vmcnt(0)
+// before each (it cannot tell them from the global_load_lds stores in flight into the other buffer),
+// which drained the next chunk's loads before this chunk's products
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void lds_read3(const double* a, const double* b, const double* c, double& x, double& y, double& z) {
+  asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %4\n\tds_read_b64 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(x), "=&v"(y), "=&v"(z)
+               : "v"(lds_addr(a)), "v"(lds_addr(b)), "v"(lds_addr(c))
+               : "memory");
+}
+__device__ __forceinline__ void lds_read3(const float* a, const float* b, const float* c, float& x, float& y, float& z) {
+  asm volatile("ds_read_b32 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(x), "=&v"(y), "=&v"(z)
+               : "v"(lds_addr(a)), "v"(lds_addr(b)), "v"(lds_addr(c))
+               : "memory");
+}
+
+__device__ __forceinline__ void group_issue(const Dev& d, const int32_t* sIdx, int nv, rec_t* buf, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < kGrpLoads; j++) {
+    const int i = j * 256 + wave * 64 + lane;
+    int c = i / kRecPieces;
+    const int q = i - c * kRecPieces;
+    if (c >= nv) c = 0;  // past the chunk's observations: a valid record again, never read
+    const int64_t o = sIdx[c];
+    const rec_t* src = q < kJA / kRecV ? d.Jt + o * kJA + q * kRecV
+                                        : d.Jt + d.nObsPad * kJA + o * kJB + (q - kJA / kRecV) * kRecV;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(buf + (j * 256 + wave * 64) * kRecV), 16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, int mode) {
+  __shared__ __attribute__((aligned(16))) double smem[kGrpLds / 8];  // the two buffers, then the epilogue's
+  __shared__ int32_t sIdx[kGrpIdx];
+  rec_t* stg = reinterpret_cast<rec_t*>(smem);
+  const int64_t g = xcd_block(blockIdx.x, gridDim.x);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l15 = lane & 15, l4 = lane >> 4;
+  const int32_t* rv = d.grpRed + 4 * g;
+  int p0, s0, p1, s1;
+  const int row0 = grp_col_row(d, rv, l15, p0, s0);
+  const int row1 = grp_col_row(d, rv, 16 + l15, p1, s1);
+  const int64_t o0 = d.grpStart[g], n = d.grpStart[g + 1] - o0;
+  const int r = l4 & 1;
+  const int q0 = row0 >= 0 ? p0 + r * s0 : 0, q1 = row1 >= 0 ? p1 + r * s1 : 0;  // this lane's planes (K row parity r)
+  hacc4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
+  double g0 = 0.0, g1 = 0.0;
+  for (int64_t w0 = 0; w0 < n; w0 += kGrpIdx) {
+    const int nw = (int)min<int64_t>(n - w0, kGrpIdx);
+    for (int i = tid; i < nw; i += 256) sIdx[i] = d.grpObs[o0 + w0 + i];
+    __syncthreads();
+    const int nch = (nw + kGrpChunk - 1) / kGrpChunk;
+    group_issue(d, sIdx, min(nw, kGrpChunk), stg, wave, lane);
+    for (int k = 0; k < nch; k++) {
+      const int c0 = k * kGrpChunk, nv = min(nw - c0, kGrpChunk);
+      if (k + 1 < nch) {  // buffer (k + 1) & 1: its readers (chunk k - 1) passed the last barrier
+        group_issue(d, sIdx + c0 + kGrpChunk, min(nw - c0 - kGrpChunk, kGrpChunk), stg + ((k + 1) & 1) * kGrpStage, wave, lane);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGrpLoads) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();  // every wave's part of chunk k landed
+      __builtin_amdgcn_sched_barrier(0);
+      const rec_t* S = stg + (k & 1) * kGrpStage;
+      for (int ks = wave; 2 * ks < nv; ks += 4) {
+        const int c = 2 * ks + (l4 >> 1);
+        const rec_t* rc = S + min(c, nv - 1) * kJPlanes;  // branch-free: past the chunk / invalid columns masked
+        rec_t er, v0, v1;
+        lds_read3(rc + kJe + r, rc + q0, rc + q1, er, v0, v1);
+        if (c >= nv) er = v0 = v1 = 0;
+        if (row0 < 0) v0 = 0;
+        if (row1 < 0) v1 = 0;
+        g0 += (double)v0 * er, g1 += (double)v1 * er;
+        if (mode == 0) {
+          a00 = mfma_h(v0, v0, a00);
+          a10 = mfma_h(v1, v0, a10);
+          a11 = mfma_h(v1, v1, a11);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // chunk k's readers done before its buffer is refilled (or sIdx / the epilogue)
+    }
+  }
+  group_finish(d, lambda, mode, row0, row1, a00, a10, a11, g0, g1, smem);
 }
 
 // damping of the small-factor part of the diagonal (visual part: obs_group_kernel) and the
