@@ -191,7 +191,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-family", type=int, default=KF_GEMM)
+    ap.add_argument("--profile-family", type=int, default=KF_GEMM,
+                    help="kernel family whose launches a separate pass after the timed one event-times for the "
+                         "roofline (-1: none)")
+    ap.add_argument("--profile-steps", type=int, default=3, help="LM iterations of the profiled pass")
     ap.add_argument("--precision", choices=("fp64", "mixed"), default="fp64",
                     help="fp64 (the reference's arithmetic) or mixed (config E: fp32 Jacobian records and "
                          "Schur-complement products, fp64 Cholesky); mixed also reports its first-step "
@@ -267,19 +270,31 @@ def main():
     if args.warmup:
         s = e.optimize(settings(args.warmup))
         log(f"[bench] warmup {s.num_iterations} its, cost {s.initial_cost:.6g} -> {s.final_cost:.6g}")
-    e.profile_kernel(args.profile_family)
     e.synchronize()
     t0 = time.perf_counter()
     s = e.optimize(settings(args.steps))
     e.synchronize()
     elapsed = time.perf_counter() - t0
-    launches, kms = e.kernel_time()
-    e.profile_kernel(-1)
     iters = s.num_iterations
     ph = e.phase_times()
     log(f"[bench] timed {iters} its in {elapsed:.3f}s, cost {s.initial_cost:.6g} -> {s.final_cost:.6g}; "
         f"last it: lin {ph.linearize_ms:.2f} schur {ph.schur_ms:.2f} factor {ph.factor_ms:.2f} "
         f"solve {ph.solve_ms:.2f} step {ph.step_ms:.2f} cost {ph.cost_ms:.2f} rs-tables {ph.rs_update_ms:.3f} ms")
+    # the roofline's kernel timing: a separate pass of the same binary with the profiled family's launches
+    # event-timed one by one (the factorization's segments then run on one stream, so each fan-in launch
+    # has the chip to itself; the timed pass above ran the multi-stream schedule from the same kernels)
+    prof_iters = 0
+    launches, kms, busy_ms = 0, 0.0, 0.0
+    if args.profile_family >= 0 and args.profile_steps > 0:
+        e.profile_kernel(args.profile_family)
+        sp = e.optimize(settings(args.profile_steps))
+        e.synchronize()
+        launches, kms = e.kernel_time()
+        busy_ms = e.kernel_busy_time()
+        e.profile_kernel(-1)
+        prof_iters = sp.num_iterations
+        log(f"[bench] profiled pass: {prof_iters} its, {launches} launches of family {args.profile_family}, "
+            f"{kms:.3f} ms")
 
     # roofline of the profiled kernel family (average launch duration from HIP events on the engine
     # stream, algorithmic work from the symbolic structure)
@@ -292,12 +307,16 @@ def main():
         # LM iteration (the rescaled / sub-step attempts reuse it), and the launches are the fan-in
         # launches actually timed (levels without contributions launch none: 88 of the 89 levels at
         # config C), so flops per launch = contributions x iterations / launches
-        fan_per_factor = launches / max(1, iters)
+        fan_per_factor = launches / max(1, prof_iters)
         # the fan-in's own contributions (the two-column supernode schedule moves the pair-internal ones
         # into its trsm kernel; the column schedule's are st[6])
         fan_contrib = sched[1]
         per_launch = fan_contrib * 2.0 * 64 ** 3 / max(1e-9, fan_per_factor)
-        achieved = per_launch / (avg_ms * 1e-3) / 1e12
+        # the factorization's streams run fan-in launches side by side, so a launch's own duration counts
+        # time it shares with another: the duration per launch is the family's busy time (the union of
+        # its launches' intervals) over the launches -- the plain average when nothing overlaps
+        eff_ms = busy_ms / max(1, launches)
+        achieved = per_launch / (eff_ms * 1e-3) / 1e12
         # compulsory HBM bytes of one launch: within a level every contribution's L_IK is a distinct
         # tile (a column K has at most one ancestor column per level) and every L_JK is also the
         # I-side tile of the diagonal contribution (J, J, K), so the operands are pairs x 32 KB; each
@@ -310,7 +329,9 @@ def main():
                 "traffic_over_compulsory": traffic / compulsory if traffic else None,
                 "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
                           "v_mfma_f64_16x16x4_f64, operands via global_load_lds)",
-                "flops_per_launch": per_launch, "avg_launch_ms": avg_ms, "launches": launches,
+                "flops_per_launch": per_launch, "busy_ms_per_launch": eff_ms, "avg_launch_ms": avg_ms,
+                "launches": launches, "busy_ms_per_factorization": busy_ms / max(1, prof_iters),
+                "frac_per_launch_duration": per_launch / (avg_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TF,
                 "fanin_launches_per_factorization": fan_per_factor, "levels": int(sched[0]),
                 "fanin_contributions": int(fan_contrib), "supernodes": int(sched[2]),
                 "two_column_supernodes": int(sched[3]),
@@ -331,6 +352,9 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("visual_lin_kernel"),
                 "kernel": "visual_lin_kernel (Jacobian fill)", "bytes_per_launch": b, "avg_launch_ms": avg_ms,
                 "launches": launches}
+    if roof is not None:
+        roof["timing"] = (f"average launch duration from HIP events around each launch on its stream, in a separate "
+                          f"pass of {prof_iters} LM iterations after the timed ones ({launches} launches)")
     ms = elapsed * 1e3 / max(1, iters)
     if tolerance is not None:
         out_extra = {"precision": "mixed (fp32 Jacobian records + Schur products, fp64 Cholesky)",

@@ -488,6 +488,10 @@ void* vb_stream(vb_handle h);
  *  back-substitution, 8 visual cost, 9 small factors, 10 tile trsm; -1 disables); vb_kernel_time returns launches and summed device milliseconds since enabling */
 int vb_profile_kernel(vb_handle h, int family);
 int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms);
+/* The profiled family's busy time since enabling: the union of its launches' intervals (the factorization
+ * launches on several streams, so its launches can overlap and their summed durations count that time
+ * more than once).  Equal to vb_kernel_time's total when the launches do not overlap. */
+int vb_kernel_busy_time(vb_handle h, double* busy_ms);
 /* [nObs, nPoints, nReducedVars, reducedOrder, nTileCols, nTiles, nGemmPairs (per factorization),
  *  nSmallFactors, Schur landmark-pair entries, Schur observation-pair entries,
  *  elimination levels (one fan-in launch each, except a level without contributions), tiles of S

@@ -16,7 +16,8 @@ NAMES = {0: "potrf4 (one tile, scratch)", 1: "trsm (one tile, scratch)", 2: "fan
          10: "visual_lin (eval + record stores)", 12: "landmark elimination",
          13: "observation-group Gram blocks", 14: "Schur tile products", 15: "visual cost pass",
          16: "small factors' evaluation", 17: "small assembly, IMU kinds", 18: "small assembly, other kinds",
-         19: "reduced-system clear"}
+         19: "reduced-system clear", 20: "elimination beside tile products (timing probe)",
+         21: "elimination then tile products", 22: "elimination beside groups"}
 
 
 def main():

@@ -281,7 +281,11 @@ struct SnSched {
   int32_t nLevels = 0;
   int64_t nPairs = 0;                  // fan-in contributions (external to the supernodes)
   int64_t nSuper = 0, nTwo = 0;        // supernodes, of which two-column
-  std::vector<int64_t> lvU, lvS, lvR;  // per level: fan-in chunk, supernode and row-item ranges
+  std::vector<int64_t> lvU, lvS, lvR;  // per segment: fan-in chunk, supernode and row-item ranges
+  // segments: one level of one stream (nGroups > 1: independent subtrees and the separators above them),
+  // level-major; segL its level, segDep the bit mask of other streams it waits for
+  std::vector<int32_t> segG, segL, segDep;
+  int nGroups = 1;
   int32_t *updD = nullptr, *fanPairsD = nullptr;
   int32_t *potD = nullptr;  // per supernode: tile (J, J), J, tile (J + 1, J) or -1, tile (J + 1, J + 1) or -1
   int32_t *rowD = nullptr;  // per row item: tile (I, J) or -1, tile (I, J + 1) or -1, J, J + 1 or -1, I,
@@ -407,6 +411,12 @@ struct vb_handle_s {
   bool specReady = false;     // every speculative buffer, event and stream above exists (specPrepare)
   SnSched sn[2];              // two-column supernode schedules of sch[0] / sch[1] (direct factorization)
   bool useSn = true;          // VIBA_SUPERNODE=0 at creation: the column schedule
+  // streams of the single-handle supernode schedule (VIBA_SN_STREAMS, 1..4): 1, 2, 3 are st2, stZ, stF
+  // (idle during the factorization); fork and per-level events.  The forked schedule is launched eagerly:
+  // captured into a graph it ran 12% slower per iteration (r05k)
+  int snStreams = 2;
+  hipStream_t stF = nullptr;
+  hipEvent_t evSnFork = nullptr, evSnLvl[4] = {};
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
   bool deferred = false;
@@ -437,6 +447,7 @@ struct vb_handle_s {
   size_t profDone = 0;  // leading profEv entries known complete, harvested after the next enqueue
   int64_t profLaunches = 0;
   double profMs = 0.0;
+  double profBusyMs = 0.0;  // union of the profiled launches' intervals
 };
 
 namespace {
@@ -475,14 +486,30 @@ float profPairMs(hipEvent_t a, hipEvent_t b) {
   }
   return ms;
 }
+// the first n recorded pairs into the totals: the summed launch durations, and the family's busy time, the
+// union of the launches' intervals (launches on several streams overlap: the factorization's streams)
+void profAccumulate(vb_handle h, size_t n) {
+  std::vector<std::pair<double, double>> iv;
+  for (size_t i = 0; i < n; i += 2) {
+    const float ms = profPairMs(h->profEv[i], h->profEv[i + 1]);
+    h->profMs += ms;
+    h->profLaunches++;
+    float t0 = 0;
+    if (i > 0) (void)hipEventElapsedTime(&t0, h->profEv[0], h->profEv[i]);
+    iv.push_back({(double)t0, (double)t0 + ms});
+  }
+  std::sort(iv.begin(), iv.end());
+  double end = -1e300;
+  for (const auto& x : iv) {
+    if (x.first > end) h->profBusyMs += x.second - x.first, end = x.second;
+    else if (x.second > end) h->profBusyMs += x.second - end, end = x.second;
+  }
+}
 // harvest recorded pairs (call after a stream synchronisation)
 void profHarvest(vb_handle h) {
   if (h->profFamily < 0 || h->profUsed == 0) return;
   (void)hipStreamSynchronize(h->st);
-  for (size_t i = 0; i < h->profUsed; i += 2) {
-    h->profMs += profPairMs(h->profEv[i], h->profEv[i + 1]);
-    h->profLaunches++;
-  }
+  profAccumulate(h, h->profUsed);
   h->profUsed = 0, h->profDone = 0;
 }
 // harvest the first n entries (complete at the last stream sync) after the next iteration's work is
@@ -490,10 +517,7 @@ void profHarvest(vb_handle h) {
 // the entries still pending move to the front
 void profHarvestPrefix(vb_handle h, size_t n) {
   if (h->profFamily < 0 || n == 0 || n > h->profUsed) return;
-  for (size_t i = 0; i < n; i += 2) {
-    h->profMs += profPairMs(h->profEv[i], h->profEv[i + 1]);
-    h->profLaunches++;
-  }
+  profAccumulate(h, n);
   std::rotate(h->profEv.begin(), h->profEv.begin() + n, h->profEv.begin() + h->profUsed);
   h->profUsed -= n, h->profDone = 0;
 }
@@ -553,7 +577,7 @@ int readRedErr(vb_handle h, double* out, int n) {
 // its ROOT targets, or the ROOT columns, in partition mode)
 int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx, int32_t nT, int64_t nTiles,
                     const std::function<bool(int32_t)>& colSel, const std::function<bool(int32_t)>& tgtSel,
-                    const std::function<bool(int32_t)>& srcSel) {
+                    const std::function<bool(int32_t)>& srcSel, int nGroups = 1) {
   auto colRows = [&](int32_t J, int64_t& a, int64_t& b) { a = h->colStart[J], b = h->colStart[J + 1]; };
   // pair J with J + 1: J + 1 is J's first off-diagonal row (its parent) and every other row of J is a
   // row of J + 1 (so the pair's rows are J + 1's), both in one nested-dissection part
@@ -624,29 +648,122 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
         }
   }
   if (ccnt[nTiles] >= INT32_MAX) return fail(VB_E_STATE, "tile Cholesky too large (contribution count)");
-  const int64_t fanWgs = 3072;
+  // Streams (nGroups > 1): the supernodes' elimination tree (parent: the supernode of the first row below
+  // it) cut into independent subtrees on separate streams, so one subtree's diagonal blocks and rows
+  // (latency-bound, a few workgroups) run beside another's fan-in instead of behind a level barrier of the
+  // whole chip.  The tree is split from its roots down, heaviest subtree first, until none outweighs
+  // 1/nGroups of the frontier by more than 15%; the frontier's subtrees go to the streams longest first.
+  // Their ancestors (the separators above the cut) follow the stream of their heaviest child and wait for
+  // the others' (segDep), so sibling separators also run side by side.  Weights: the fan-in contributions
+  // into a supernode's columns.
+  std::vector<int32_t> grp(nT, 0);
+  std::vector<int32_t> snPar(nT, -1);
+  int G = std::max(1, nGroups);
+  if (G > 1) {
+    std::vector<int32_t> snOf(nT);
+    std::vector<int32_t>& par = snPar;
+    std::vector<double> W(nT, 0.0);
+    std::vector<std::vector<int32_t>> kids(nT);
+    for (int32_t J = 0; J < nT; J++) snOf[J] = pr[J] == 2 ? J - 1 : J;
+    for (int32_t J0 = 0; J0 < nT; J0++) {
+      if (pr[J0] == 2) continue;
+      const int32_t Jl = pr[J0] == 1 ? J0 + 1 : J0;
+      if (h->colStart[Jl + 1] - h->colStart[Jl] > 1) par[J0] = snOf[h->colRowsH[h->colStart[Jl] + 1]];
+      for (int32_t J = J0; J <= Jl; J++)
+        for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) W[J0] += (double)(ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]]);
+    }
+    std::vector<double> own(W);
+    for (int32_t J0 = 0; J0 < nT; J0++)  // parents come after their children in the elimination order
+      if (pr[J0] != 2 && par[J0] >= 0) W[par[J0]] += W[J0], kids[par[J0]].push_back(J0);
+    std::vector<int32_t> front;
+    for (int32_t J0 = 0; J0 < nT; J0++)
+      if (pr[J0] != 2 && par[J0] < 0) front.push_back(J0);
+    std::vector<int8_t> top(nT, 0);
+    for (int it = 0; it < 4 * nT && front.size() < 256; it++) {
+      double tot = 0.0;
+      size_t xi = 0;
+      for (size_t i = 0; i < front.size(); i++) {
+        tot += W[front[i]];
+        if (W[front[i]] > W[front[xi]]) xi = i;
+      }
+      const int32_t X = front[xi];
+      if (W[X] <= 1.15 * tot / G || kids[X].empty()) break;
+      top[X] = 1;
+      front.erase(front.begin() + (ptrdiff_t)xi);
+      front.insert(front.end(), kids[X].begin(), kids[X].end());
+    }
+    std::stable_sort(front.begin(), front.end(), [&](int32_t a, int32_t b) { return W[a] > W[b]; });
+    std::vector<double> load(G, 0.0);
+    std::vector<int32_t> rootG(nT, -1);
+    for (int32_t X : front) {
+      const int g = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+      load[g] += W[X], rootG[X] = g;
+    }
+    for (int32_t J0 = nT - 1; J0 >= 0; J0--)  // the frontier subtrees, parents first
+      if (pr[J0] != 2 && !top[J0]) grp[J0] = rootG[J0] >= 0 ? rootG[J0] : par[J0] >= 0 ? grp[par[J0]] : 0;
+    for (int32_t J0 = 0; J0 < nT; J0++)  // the separators above the cut, children first
+      if (pr[J0] != 2 && top[J0]) {
+        int32_t best = -1;
+        for (int32_t C : kids[J0])
+          if (best < 0 || W[C] > W[best]) best = C;
+        grp[J0] = best >= 0 ? grp[best] : 0;
+      }
+    for (int32_t J0 = 0; J0 < nT; J0++)
+      if (pr[J0] == 1) grp[J0 + 1] = grp[J0];
+    if (getenv("VIBA_FACTOR_STATS")) {
+      std::vector<double> gw(G, 0.0), gt(G, 0.0);
+      std::vector<int> gs(G, 0);
+      for (int32_t J0 = 0; J0 < nT; J0++)
+        if (pr[J0] != 2) gw[grp[J0]] += own[J0], gs[grp[J0]]++, gt[grp[J0]] += top[J0] ? own[J0] : 0.0;
+      for (int g = 0; g < G; g++)
+        fprintf(stderr, "[factor stats] stream %d: supernodes %d, contributions %.0f (%.0f above the cut)\n", g, gs[g], gw[g],
+                gt[g]);
+    }
+  }
+  // a stream's segment shares the chip with the other streams' segments of its level: the fan-in workgroup
+  // target and the fused-level threshold are divided by their number
+  std::vector<int> nAct(nLev, 0);
+  for (int32_t L = 0; L < nLev; L++) {
+    uint32_t m = 0;
+    for (int32_t J0 : sup[L]) m |= 1u << grp[J0];
+    nAct[L] = __builtin_popcount(m);
+  }
   int64_t fuseMax = 256;  // levels with at most this many row items run snpotrf_trsm8_kernel
   if (const char* e = getenv("VIBA_SN_FUSE")) fuseMax = atoll(e);
   std::vector<int32_t> fan, pot, rows, fus, copy;
-  S.lvU.assign(nLev + 1, 0), S.lvS.assign(nLev + 1, 0), S.lvR.assign(nLev + 1, 0), S.lvF.assign(nLev + 1, 0);
+  S.lvU.assign(1, 0), S.lvS.assign(1, 0), S.lvR.assign(1, 0), S.lvF.assign(1, 0);
+  S.segG.clear(), S.segL.clear(), S.segDep.clear();
 
   S.nTwo = 0;
   auto tile = [&](int32_t I, int32_t J) { return tileIdx[(size_t)I * nT + J]; };
-  for (int32_t L = 0; L < nLev; L++) {
-    int64_t total = 0;
+  // segments: (stream, level), level-major; segDep: the other streams whose earlier segments this one
+  // needs (streams of its supernodes' children)
+  for (int32_t L = 0; L < nLev; L++)
+  for (int g = 0; g < G; g++) {
+    std::vector<int32_t> supL;
+    uint32_t dep = 0;
     for (int32_t J0 : sup[L])
+      if (grp[J0] == g) supL.push_back(J0);
+    if (supL.empty()) continue;
+    if (G > 1)
+      for (int32_t J0 = 0; J0 < nT; J0++)
+        if (pr[J0] != 2 && snPar[J0] >= 0 && grp[snPar[J0]] == g && lev[snPar[J0]] == L && grp[J0] != g) dep |= 1u << grp[J0];
+    int64_t total = 0;
+    for (int32_t J0 : supL)
       for (int32_t J = J0; J <= J0 + (pr[J0] == 1 ? 1 : 0); J++)
         for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
+    const int share = std::max(1, nAct[L]);
+    const int64_t fanWgs = 3072 / share;
     const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
     const size_t u0 = fan.size() / 4;
     int64_t nRowsL = 0;
-    for (int32_t J0 : sup[L]) {
+    for (int32_t J0 : supL) {
       if (!colSel(J0)) continue;
       const int32_t Jl = pr[J0] == 1 ? J0 + 1 : J0;
       nRowsL += h->colStart[Jl + 1] - h->colStart[Jl] - 1;
     }
-    const bool fused = nRowsL <= fuseMax;
-    for (int32_t J0 : sup[L]) {
+    const bool fused = nRowsL <= fuseMax / share;
+    for (int32_t J0 : supL) {
       const bool two = pr[J0] == 1;
       const int32_t J2 = two ? J0 + 1 : -1;
       for (int32_t J = J0; J <= (two ? J2 : J0); J++)
@@ -696,9 +813,11 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
       for (size_t i = 0; i < q.size(); i++)
         for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
     }
-    S.lvU[L + 1] = (int64_t)fan.size() / 4, S.lvS[L + 1] = (int64_t)pot.size() / 4, S.lvR[L + 1] = (int64_t)rows.size() / 8;
-    S.lvF[L + 1] = (int64_t)fus.size() / 8;
+    S.lvU.push_back((int64_t)fan.size() / 4), S.lvS.push_back((int64_t)pot.size() / 4), S.lvR.push_back((int64_t)rows.size() / 8);
+    S.lvF.push_back((int64_t)fus.size() / 8);
+    S.segG.push_back(g), S.segL.push_back(L), S.segDep.push_back((int32_t)dep);
   }
+  S.nGroups = G;
   S.nLevels = nLev, S.nPairs = ccnt[nTiles];
   S.nSuper = 0;
   for (int32_t J = 0; J < nT; J++) S.nSuper += (pr[J] != 2 && colSel(J)) ? 1 : 0;
@@ -1782,7 +1901,7 @@ int doFinalize(vb_handle h) {
     if (h->useSn) {
       if (W <= 1) {
         auto any = [](int32_t) { return true; };
-        if (int rc = buildSupernodes(h, h->sn[0], tileIdx, nT, nTiles, any, any, any)) return rc;
+        if (int rc = buildSupernodes(h, h->sn[0], tileIdx, nT, nTiles, any, any, any, h->snStreams)) return rc;
       } else {
         auto own = [&](int32_t J) { return h->colOwner[J] == me; };
         auto root = [&](int32_t J) { return h->colOwner[J] == W; };
@@ -2022,28 +2141,63 @@ void factorSeq(vb_handle h, const Sched& S) {
   launch_diag_inverse(d, S.potrfColD, S.lvP[S.nLevels], h->linv, h->st);
 }
 
-// the two-column supernode schedule (SnSched): per level the fan-in of its targets, the supernodes'
-// diagonal blocks, their rows; then the diagonal-tile inverses of the solves (every column)
+// the two-column supernode schedule (SnSched): per segment (a level of one stream) the fan-in of its
+// targets, the supernodes' diagonal blocks, their rows; then the diagonal-tile inverses of the solves
+// (every column).  Streams (nGroups > 1): stream g on snStream(g), forked from the main stream and joined
+// back at the end; segments queued level by level, a segment after the streams it depends on (segDep)
+// record their progress (one event per stream and level: everything they have queued so far is of
+// earlier levels).  A profiled factor family runs the same schedule, eagerly (per-launch events).
 void factorSeqSn(vb_handle h, int which) {
   Dev& d = h->d;
   const SnSched& S = h->sn[which];
   const bool fwd = fwdFused(h) && which == 0 && !h->factorOnly;
   double* fb = fwd ? h->rhsWork : nullptr;
   double* fy = fwd ? h->yvec : nullptr;
-  for (int32_t L = 0; L < S.nLevels; L++) {
-    const int64_t u0 = S.lvU[L], s0 = S.lvS[L], r0 = S.lvR[L];
-    profBegin(h, KF_GEMM);
-    launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[L + 1] - u0), h->st);
-    profEnd(h, KF_GEMM);
-    profBegin(h, KF_POTRF);
-    if (S.lvF[L + 1] > S.lvF[L])
-      launch_snpotrf_trsm(d, S.fusD + 8 * S.lvF[L], (int)(S.lvF[L + 1] - S.lvF[L]), h->lscrSn, h->dinv, h->st, fb, fy);
-    launch_snpotrf(d, S.potD + 4 * s0, (int)(S.lvS[L + 1] - s0), h->dinv, h->st, fb, fy);
-    profEnd(h, KF_POTRF);
-    profBegin(h, KF_TRSM);
-    launch_sntrsm(d, S.rowD + 8 * r0, (int)(S.lvR[L + 1] - r0), h->dinv, h->st, fy, fb);
-    profEnd(h, KF_TRSM);
+  const bool forked = S.nGroups > 1;
+  const int G = forked ? S.nGroups : 1;
+  auto stOf = [&](int g) -> hipStream_t {
+    if (!forked) return h->st;
+    return g == 0 ? h->st : g == 1 ? h->st2 : g == 2 ? h->stZ : h->stF;
+  };
+  if (forked) {
+    (void)hipEventRecord(h->evSnFork, h->st);
+    for (int g = 1; g < G; g++) (void)hipStreamWaitEvent(stOf(g), h->evSnFork, 0);
   }
+  const int nSeg = (int)S.segG.size();
+  for (int i0 = 0; i0 < nSeg;) {
+    int i1 = i0;
+    while (i1 < nSeg && S.segL[i1] == S.segL[i0]) i1++;
+    if (forked) {  // the level's cross-stream dependencies, recorded before any of its launches
+      uint32_t need = 0;
+      for (int i = i0; i < i1; i++) need |= (uint32_t)S.segDep[i];
+      for (int q = 0; q < G; q++)
+        if (need >> q & 1) (void)hipEventRecord(h->evSnLvl[q], stOf(q));
+    }
+    for (int i = i0; i < i1; i++) {
+      hipStream_t st = stOf(S.segG[i]);
+      if (forked)
+        for (int q = 0; q < G; q++)
+          if ((uint32_t)S.segDep[i] >> q & 1) (void)hipStreamWaitEvent(st, h->evSnLvl[q], 0);
+      const int64_t u0 = S.lvU[i], s0 = S.lvS[i], r0 = S.lvR[i];
+      profBegin(h, KF_GEMM);
+      launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[i + 1] - u0), st);
+      profEnd(h, KF_GEMM);
+      profBegin(h, KF_POTRF);
+      if (S.lvF[i + 1] > S.lvF[i])
+        launch_snpotrf_trsm(d, S.fusD + 8 * S.lvF[i], (int)(S.lvF[i + 1] - S.lvF[i]), h->lscrSn, h->dinv, st, fb, fy);
+      launch_snpotrf(d, S.potD + 4 * s0, (int)(S.lvS[i + 1] - s0), h->dinv, st, fb, fy);
+      profEnd(h, KF_POTRF);
+      profBegin(h, KF_TRSM);
+      launch_sntrsm(d, S.rowD + 8 * r0, (int)(S.lvR[i + 1] - r0), h->dinv, st, fy, fb);
+      profEnd(h, KF_TRSM);
+    }
+    i0 = i1;
+  }
+  if (forked)
+    for (int q = 1; q < G; q++) {
+      (void)hipEventRecord(h->evSnLvl[q], stOf(q));
+      (void)hipStreamWaitEvent(h->st, h->evSnLvl[q], 0);
+    }
   if (S.nCopy) launch_copy_diag(d, S.copyD, (int)S.nCopy, h->lscrSn, h->st);
   const Sched& C = h->sch[which];
   launch_diag_inverse(d, C.potrfColD, C.lvP[C.nLevels], h->linv, h->st);
@@ -2070,7 +2224,7 @@ int factorReduced(vb_handle h, int which = 0) {
   // (a profiled family runs launch by launch: its per-launch events, recorded as event nodes inside
   // a graph, cost as much as the graph saves -- measured)
   const bool sn = h->sn[which].built;
-  if (!h->useGraphs || prof || h->factorOnly) {
+  if (!h->useGraphs || prof || h->factorOnly || (sn && h->sn[which].nGroups > 1)) {
     if (sn) factorSeqSn(h, which);
     else factorSeq(h, S);
     return 0;
@@ -2336,6 +2490,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   if (const char* e = getenv("VIBA_SPEC_EARLY")) h->specEarly = e[0] != '0';
   if (const char* e = getenv("VIBA_DEBUG_SPEC_FAIL")) h->specFailDebug = e[0] == '1';
   if (const char* e = getenv("VIBA_SUPERNODE")) h->useSn = e[0] == '1';
+  if (const char* e = getenv("VIBA_SN_STREAMS")) h->snStreams = std::max(1, std::min(4, atoi(e)));
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2350,6 +2505,9 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipEventCreateWithFlags(&h->evZero, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evSmallE, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evZJoin, hipEventDisableTiming));
+  HIPCHK(hipStreamCreateWithFlags(&h->stF, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&h->evSnFork, hipEventDisableTiming));
+  for (auto& e : h->evSnLvl) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   *out = h;
   return 0;
 }
@@ -2394,6 +2552,10 @@ int vb_destroy(vb_handle h) {
   if (h->evSmallE) hipEventDestroy(h->evSmallE);
   if (h->evZJoin) hipEventDestroy(h->evZJoin);
   if (h->stZ) hipStreamSynchronize(h->stZ), hipStreamDestroy(h->stZ);
+  if (h->stF) hipStreamSynchronize(h->stF), hipStreamDestroy(h->stF);
+  if (h->evSnFork) hipEventDestroy(h->evSnFork);
+  for (hipEvent_t e : h->evSnLvl)
+    if (e) hipEventDestroy(e);
   for (auto& e : h->profEv) hipEventDestroy(e);
   if (h->evCost) hipEventDestroy(h->evCost);
   for (auto& row : h->evS)
@@ -3236,7 +3398,7 @@ void* vb_stream(vb_handle h) { return h ? (void*)h->st : nullptr; }
 int vb_profile_kernel(vb_handle h, int family) {
   if (!h || family < -1 || family >= KF_COUNT) return fail(VB_E_ARG, "bad kernel family");
   profHarvest(h);
-  h->profFamily = family, h->profLaunches = 0, h->profMs = 0.0, h->profUsed = 0, h->profDone = 0;
+  h->profFamily = family, h->profLaunches = 0, h->profMs = 0.0, h->profBusyMs = 0.0, h->profUsed = 0, h->profDone = 0;
   return 0;
 }
 int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms) {
@@ -3244,6 +3406,12 @@ int vb_kernel_time(vb_handle h, int64_t* launches, double* total_ms) {
   profHarvest(h);
   if (launches) *launches = h->profLaunches;
   if (total_ms) *total_ms = h->profMs;
+  return 0;
+}
+int vb_kernel_busy_time(vb_handle h, double* busy_ms) {
+  if (!h || !busy_ms) return fail(VB_E_ARG, "null argument");
+  profHarvest(h);
+  *busy_ms = h->profBusyMs;
   return 0;
 }
 int vb_problem_stats(vb_handle h, int64_t* out) {  // 12 entries
@@ -3947,6 +4115,22 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
         case 18: launch_small_assemble(d, 0, d.gRed, h->st, 2); break;
         case 19:
           if (int rc = clearReduced(h, d, h->st)) return rc;
+          break;
+        // overlap probes (timing only: the products read the previous elimination's Y): landmark elimination
+        // and tile products side by side (20) or in sequence (21); 22: elimination + groups side by side
+        case 20:
+        case 22:
+          HIPCHK(hipEventRecord(h->evFork, h->st));
+          HIPCHK(hipStreamWaitEvent(h->st2, h->evFork, 0));
+          if (which == 20) launch_schur_products(d, 1e-5, h->st2);
+          else launch_groups(d, 1e-5, h->st2);
+          HIPCHK(hipEventRecord(h->evJoin, h->st2));
+          launch_landmark(d, 1e-5, 0, d.lmB, d.lmE, h->st);
+          HIPCHK(hipStreamWaitEvent(h->st, h->evJoin, 0));
+          break;
+        case 21:
+          launch_landmark(d, 1e-5, 0, d.lmB, d.lmE, h->st);
+          launch_schur_products(d, 1e-5, h->st);
           break;
         default: return fail(VB_E_ARG, "vb_bench_kernel: unknown kernel");
       }

@@ -524,6 +524,12 @@ class HipEngine(CEngineBase):
         self._check(self._fn("kernel_time", [C.POINTER(C.c_int64), _dp])(self.h, C.byref(n), C.byref(ms)))
         return n.value, ms.value
 
+    def kernel_busy_time(self):
+        """the profiled family's busy time (union of its launches' intervals), ms"""
+        ms = C.c_double()
+        self._check(self._fn("kernel_busy_time", [_dp])(self.h, C.byref(ms)))
+        return ms.value
+
     def problem_stats(self):
         out = (C.c_int64 * 12)()
         self._check(self._fn("problem_stats", [C.c_int64 * 12])(self.h, out))
