@@ -19,6 +19,8 @@ cd $R
 python scripts/pmc_summary.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG gpurun_out/pmc_summary_$TAG.json > /dev/null || exit $?
 f=$(ls gpurun_out/prof_$TAG/*kernel_stats.csv gpurun_out/prof_$TAG/*/*kernel_stats.csv 2>/dev/null | head -1)
 python scripts/prof_summary.py $(dirname $f) 12
+python scripts/busy_union.py $(dirname $f)/run_kernel_trace.csv fanin_kernel snpotrf sntrsm > gpurun_out/busy_union_$TAG.json || exit 1
+python scripts/factor_overlap.py $(dirname $f)/run_kernel_trace.csv > gpurun_out/factor_overlap_$TAG.txt || exit 1
 timeout -k 10 600 python bench.py --precision mixed --no-cpu-baseline > gpurun_out/bench_${TAG}_mixed.json 2> gpurun_out/bench_${TAG}_mixed.log || exit $?
 tail -1 gpurun_out/bench_${TAG}_mixed.json | cut -c1-300
 (cd /tmp && VIBA_NO_GRAPHS=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_${TAG}_mixed -o run -- python3 $R/bench.py --precision mixed --no-cpu-baseline --no-banded-count > $R/gpurun_out/bench_${TAG}_mixed_prof.json 2> $R/gpurun_out/bench_${TAG}_mixed_prof.log) || exit $?
