@@ -679,10 +679,13 @@ __device__ __forceinline__ void group_finish(const Dev& d, double lambda, int mo
 // The group's records are streamed through LDS in chunks of kGrpChunk observations, each record copied
 // whole (both regions, 16 B per lane by global_load_lds: a handful of wide loads per thread per chunk,
 // where gathering the three operands of every k-step straight from HBM, behind an index load, ran
-// 1.05 ms against 0.86 alone on config C), double-buffered (chunk k + 1 in flight while chunk k feeds the
+// 1.05 ms against 0.79 alone on config C), double-buffered (chunk k + 1 in flight while chunk k feeds the
 // MFMAs).  Staged record c holds plane p at stage[c * kJPlanes + p].  The group's observation indices
 // come into LDS first, by windows of kGrpIdx.
-constexpr int kGrpChunk = 32;                                      // observations per staged chunk
+// observations per staged chunk: swept at config C (r05u, the kernel alone): fp64 16 / 24 / 32 / 48 / 64 ->
+// 818 / 794 / 862 / 1045 / 1041 us (LDS per workgroup sets the occupancy); fp32 records 609 / 564 / 550 /
+// 543 / 632 us
+constexpr int kGrpChunk = VIBA_MIXED ? 32 : 24;
 constexpr int kRecV = 16 / (int)sizeof(rec_t);                     // record elements per 16 B piece
 constexpr int kRecPieces = kJPlanes / kRecV;                       // 16 B pieces per record (36 / 18)
 constexpr int kGrpLoads = (kGrpChunk * kRecPieces + 255) / 256;    // global_load_lds per thread per chunk
