@@ -353,8 +353,15 @@ def main():
                 "kernel": "visual_lin_kernel (Jacobian fill)", "bytes_per_launch": b, "avg_launch_ms": avg_ms,
                 "launches": launches}
     if roof is not None:
-        roof["timing"] = (f"average launch duration from HIP events around each launch on its stream, in a separate "
-                          f"pass of {prof_iters} LM iterations after the timed ones ({launches} launches)")
+        roof["timing"] = (f"HIP events around each launch on its own stream, in a separate pass of {prof_iters} LM "
+                          f"iterations after the timed ones ({launches} launches)")
+        if args.profile_family == KF_GEMM:
+            roof["divisor"] = ("busy time: the factorization runs its independent subtrees on two streams, so fan-in "
+                               "launches overlap and a launch's own duration (avg_launch_ms) includes time shared with "
+                               "the other stream's launch; achieved = flops per factorization / the union of the "
+                               "launches' intervals per factorization (busy_ms_per_launch = that union / launches, "
+                               "the plain average when nothing overlaps); frac_per_launch_duration divides by "
+                               "avg_launch_ms instead")
     ms = elapsed * 1e3 / max(1, iters)
     if tolerance is not None:
         out_extra = {"precision": "mixed (fp32 Jacobian records + Schur products, fp64 Cholesky)",
