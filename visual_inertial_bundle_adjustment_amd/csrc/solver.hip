@@ -1664,11 +1664,15 @@ __global__ void __launch_bounds__(kFanWaves * 64) fanin_kernel(Dev d, const int3
   fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
 }
 
-// Inverse of every factored diagonal tile (off the factorization's critical path, one wave per
-// tile, lane = column c of X = L^-1): X[i][c] = (delta_ic - sum_{k<i} L_ik X_kc) / L_ii.
+// Inverse of every factored diagonal tile (one wave per tile, lane = column c of X = L^-1, off the
+// factorization's critical path but before the backward solve): x_i = (delta_ic - sum_{k<i} L_ik x_k) / L_ii
+// with the 64 reciprocals formed first (one divide per lane) and each row's sum split over four partial
+// sums, so the dependent chain per row is a quarter of its FMAs and a multiply (one running sum and a
+// divide per row: ~105 us per factorization at config C).
 // linv[J] is column-major; the triangular solves apply it as a GEMV.
 __global__ void __launch_bounds__(64) diag_inverse_kernel(Dev d, const int32_t* cols, double* linv) {
   __shared__ double L[TS * TS];
+  __shared__ double rd[TS];
   const int J = cols ? cols[blockIdx.x] : (int)blockIdx.x, lane = threadIdx.x;
   const double* Ad = d.tiles + (int64_t)d.tileIdx[(int64_t)J * d.nT + J] * TS * TS;
   {
@@ -1679,13 +1683,20 @@ __global__ void __launch_bounds__(64) diag_inverse_kernel(Dev d, const int32_t* 
     for (int c = 0; c < TS; c++) L[c * TS + lane] = v[c];
   }
   __syncthreads();
+  rd[lane] = 1.0 / L[lane * TS + lane];
+  __syncthreads();
   double xi[TS];
 #pragma unroll
   for (int i = 0; i < TS; i++) {
-    double s = (i == lane) ? 1.0 : 0.0;
+    double s0 = (i == lane) ? 1.0 : 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
-    for (int k = 0; k < i; k++) s -= L[k * TS + i] * xi[k];
-    xi[i] = s / L[i * TS + i];
+    for (int k = 0; k + 3 < i; k += 4) {
+      s0 -= L[k * TS + i] * xi[k], s1 -= L[(k + 1) * TS + i] * xi[k + 1];
+      s2 -= L[(k + 2) * TS + i] * xi[k + 2], s3 -= L[(k + 3) * TS + i] * xi[k + 3];
+    }
+#pragma unroll
+    for (int k = i & ~3; k < i; k++) s0 -= L[k * TS + i] * xi[k];
+    xi[i] = ((s0 + s1) + (s2 + s3)) * rd[i];
   }
   double* out = linv + (int64_t)J * TS * TS + lane * TS;
 #pragma unroll
