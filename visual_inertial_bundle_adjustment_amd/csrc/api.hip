@@ -417,6 +417,7 @@ struct vb_handle_s {
   int snStreams = 2;
   hipStream_t stF = nullptr;
   hipEvent_t evSnFork = nullptr, evSnLvl[4] = {};
+  hipEvent_t evStep = nullptr, evRs = nullptr;  // vb_optimize: box-plus done; the speculative rebuild on stF done
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
   bool deferred = false;
@@ -2507,6 +2508,8 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipEventCreateWithFlags(&h->evZJoin, hipEventDisableTiming));
   HIPCHK(hipStreamCreateWithFlags(&h->stF, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->evSnFork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evStep, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evRs, hipEventDisableTiming));
   for (auto& e : h->evSnLvl) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   *out = h;
   return 0;
@@ -2554,6 +2557,8 @@ int vb_destroy(vb_handle h) {
   if (h->stZ) hipStreamSynchronize(h->stZ), hipStreamDestroy(h->stZ);
   if (h->stF) hipStreamSynchronize(h->stF), hipStreamDestroy(h->stF);
   if (h->evSnFork) hipEventDestroy(h->evSnFork);
+  if (h->evStep) hipEventDestroy(h->evStep);
+  if (h->evRs) hipEventDestroy(h->evRs);
   for (hipEvent_t e : h->evSnLvl)
     if (e) hipEventDestroy(e);
   for (auto& e : h->profEv) hipEventDestroy(e);
@@ -3504,15 +3509,21 @@ Dev specDev(vb_handle h) {
 // ark_vi_ba's preStepCallback (the rolling-shutter rebuild at the accepted variables) and the
 // linearization of the next iteration, queued behind this iteration's cost pass; event set p
 // With early set, specEarly queued the small factors' evaluation and the clear beside the cost pass.
-int specEnqueue(vb_handle h, int dontRetry, int p, bool early) {
+// rsDone: vb_optimize already cleared the speculative slots and queued the rebuild on stF (evRs), beside
+// the cost pass; the main stream only waits for it.
+int specEnqueue(vb_handle h, int dontRetry, int p, bool early, bool rsDone = false) {
   const Dev ds = specDev(h);
-  if (!early) {
+  if (!early && !rsDone) {
     HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
     HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
   }
-  HIPCHK(hipEventRecord(h->evS[p][0], h->st));
-  if (h->rsDevice) launch_rs_build(ds, h->st);
-  HIPCHK(hipEventRecord(h->evS[p][1], h->st));
+  if (rsDone) {
+    HIPCHK(hipStreamWaitEvent(h->st, h->evRs, 0));
+  } else {
+    HIPCHK(hipEventRecord(h->evS[p][0], h->st));
+    if (h->rsDevice) launch_rs_build(ds, h->st);
+    HIPCHK(hipEventRecord(h->evS[p][1], h->st));
+  }
   return linearizeBody(h, ds, 1, dontRetry, h->evS[p][2], h->evS[p][3], early);
 }
 // The part of the speculative linearization that needs only the stepped variables, queued on stZ after
@@ -3520,11 +3531,13 @@ int specEnqueue(vb_handle h, int dontRetry, int p, bool early) {
 // factors' evaluation into the staging slots and the clear of the spare tile store and gradient.  The
 // staging slots are free there (the iteration's assembly is joined, and vb_gradient_dot_step's
 // evaluation forks from the main stream after the speculative linearization's join).
-int specEarly(vb_handle h) {
+int specEarly(vb_handle h, bool cleared = false) {
   if (!smallHere(h, 0)) return 0;
   const Dev ds = specDev(h);
-  HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
-  HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
+  if (!cleared) {
+    HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
+    HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
+  }
   HIPCHK(hipEventRecord(h->evFork, h->st));
   HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
   launch_small_eval(ds, 0, ds.gRed, h->stZ);
@@ -3614,8 +3627,27 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     if ((rc = vb_backup(h))) return bail(rc);
     backedUp = true;
     if ((rc = applyStepEnqueue(h, 0, 10, 11))) return bail(rc);
-    const bool early = speculate && it + 1 < s.max_num_iterations && smallHere(h, 0) && h->specEarly;
-    if (early && (rc = specEarly(h))) return bail(rc);
+    const bool specNext = speculate && it + 1 < s.max_num_iterations;
+    const bool early = specNext && smallHere(h, 0) && h->specEarly;
+    // the next iteration's rolling-shutter rebuild (a few latency-bound waves) on stF beside the cost pass
+    // instead of after it on the main stream: the speculative slots are cleared first (the rebuild sets
+    // error bits), and the main stream waits for it (evRs) before the linearization -- and so before
+    // anything the host queues after its read, e.g. a restore of the variables the rebuild reads
+    bool rsSide = false;
+    if (specNext && h->rsDevice) {
+      const Dev ds = specDev(h);
+      const int p = specSet ^ 1;
+      if (hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st) != hipSuccess ||
+          hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st) != hipSuccess ||
+          hipEventRecord(h->evStep, h->st) != hipSuccess || hipStreamWaitEvent(h->stF, h->evStep, 0) != hipSuccess ||
+          hipEventRecord(h->evS[p][0], h->stF) != hipSuccess)
+        return bail(fail(VB_E_HIP, "speculative rebuild fork"));
+      launch_rs_build(ds, h->stF);
+      if (hipEventRecord(h->evS[p][1], h->stF) != hipSuccess || hipEventRecord(h->evRs, h->stF) != hipSuccess)
+        return bail(fail(VB_E_HIP, "speculative rebuild join"));
+      rsSide = true;
+    }
+    if (early && (rc = specEarly(h, rsSide))) return bail(rc);
     if ((rc = costEnqueue(h, 1, false))) return bail(rc);
     const bool wasSpec = specQueued;
     const int wasSet = specSet;
@@ -3627,7 +3659,7 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
       // after the last iteration: its work would only be discarded)
       if (it + 1 < s.max_num_iterations) {
         specSet ^= 1;
-        if ((rc = specEnqueue(h, dontRetry, specSet, early))) return bail(rc);
+        if ((rc = specEnqueue(h, dontRetry, specSet, early, rsSide))) return bail(rc);
         specQueued = true;
       }
     }
