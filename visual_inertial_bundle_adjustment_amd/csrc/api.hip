@@ -25,6 +25,7 @@ namespace viba {
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st);
 void launch_visual_cost(const Dev& d, int comparable, int64_t lo, int64_t hi, hipStream_t st);
 void launch_fold_red(const Dev& d, hipStream_t st);
+void launch_copy_vars(const Dev& d, bool backup, const int64_t* len, hipStream_t st);
 void launch_spec_commit(const Dev& d, hipStream_t st);
 void launch_small(const Dev& d, int mode, double* gOut, hipStream_t st);
 void launch_small_eval(const Dev& d, int mode, double* gOut, hipStream_t st);
@@ -3324,18 +3325,16 @@ int vb_cost(vb_handle h, int comparable, double* cost, vb_cost_stats* stats) {
 
 int vb_backup(vb_handle h) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
-  for (int k = 0; k < 9; k++)
-    if (!h->data[k].empty())
-      HIPCHK(hipMemcpyAsync(h->d.varBak[k], h->d.var[k], h->data[k].size() * sizeof(double), hipMemcpyDeviceToDevice,
-                            h->st));
+  int64_t len[9];
+  for (int k = 0; k < 9; k++) len[k] = (int64_t)h->data[k].size();
+  launch_copy_vars(h->d, true, len, h->st);
   return 0;
 }
 int vb_restore(vb_handle h) {
   if (!h || !h->finalized) return fail(VB_E_STATE, "not finalized");
-  for (int k = 0; k < 9; k++)
-    if (!h->data[k].empty())
-      HIPCHK(hipMemcpyAsync(h->d.var[k], h->d.varBak[k], h->data[k].size() * sizeof(double), hipMemcpyDeviceToDevice,
-                            h->st));
+  int64_t len[9];
+  for (int k = 0; k < 9; k++) len[k] = (int64_t)h->data[k].size();
+  launch_copy_vars(h->d, false, len, h->st);
   return 0;
 }
 

@@ -12,6 +12,7 @@
 //                         factor, scattered into the reduced tiles / gradient with fp64 atomics.
 #include "device_math.hpp"
 #include "engine.hpp"
+#include <algorithm>
 
 namespace viba {
 using namespace dev;
@@ -1221,6 +1222,31 @@ __global__ void fold_red_kernel(Dev d) {
   if (s != 0.0) atomicAdd(d.red + k, s);
 }
 void launch_fold_red(const Dev& d, hipStream_t st) { hipLaunchKernelGGL(fold_red_kernel, dim3(1), dim3(64), 0, st, d); }
+// vb_backup / vb_restore: the nine variable arrays in one launch (nine D2D copies cost ~55 us of
+// back-to-back copy kernels at the end of every LM iteration)
+struct VarCopy {
+  const double* src[9];
+  double* dst[9];
+  int64_t off[10];  // prefix sums of the arrays' lengths (doubles)
+};
+__global__ void __launch_bounds__(256) copy_vars_kernel(VarCopy c) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < c.off[9]; i += (int64_t)gridDim.x * 256) {
+    int k = 0;
+    while (i >= c.off[k + 1]) k++;
+    c.dst[k][i - c.off[k]] = c.src[k][i - c.off[k]];
+  }
+}
+void launch_copy_vars(const Dev& d, bool backup, const int64_t* len, hipStream_t st) {
+  VarCopy c{};
+  c.off[0] = 0;
+  for (int k = 0; k < 9; k++) {
+    c.src[k] = backup ? d.var[k] : d.varBak[k];
+    c.dst[k] = backup ? d.varBak[k] : d.var[k];
+    c.off[k + 1] = c.off[k] + len[k];
+  }
+  if (c.off[9] > 0)
+    hipLaunchKernelGGL(copy_vars_kernel, dim3((unsigned)std::min<int64_t>(1024, (c.off[9] + 255) / 256)), dim3(256), 0, st, c);
+}
 // vb_optimize's speculative linearization accepted: its cost (red[48]) and error words (err[4, 6)) become
 // the iteration's (red[0], err[0, 2))
 __global__ void spec_commit_kernel(Dev d) {
