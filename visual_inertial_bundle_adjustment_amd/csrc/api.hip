@@ -395,6 +395,16 @@ struct vb_handle_s {
   // (VIBA_NO_GRAPHS=1: eager)
   bool useGraphs = true;
   bool specEarly = true;  // specEarly beside the cost pass (VIBA_SPEC_EARLY=0: inside the speculative linearization)
+  // vb_optimize folds the cost pass of the global-shutter observations into the speculative
+  // linearization (VIBA_COST_FUSE=0: the whole cost pass first); costRsB: where the rolling-shutter
+  // observations of [obB, obE) and [fB, fE) start in obCostOrder (each range global shutter first)
+  bool costFuse = true;
+  // vb_optimize: the clear of the spare tile store for the next iteration's speculative linearization
+  // queued on stZ from inside the factorization, at the top separators' chain (one stream, a few
+  // latency-bound launches per level, HBM idle) instead of beside the cost pass (VIBA_CLEAR_IN_FACTOR=0);
+  // clearWanted: factorSeqSn queues it (then sets clearQueued)
+  bool clearInFactor = true, clearWanted = false, clearQueued = false;
+  int64_t costRsB[2] = {0, 0};
   // vb_optimize's speculative linearization (specEnqueue): the next iteration's rolling-shutter rebuild
   // and linearization are queued behind this iteration's cost pass, before the host reads its scalars,
   // into a second tile store, ResultCache, gradient and rolling-shutter table set (and reduction /
@@ -417,7 +427,7 @@ struct vb_handle_s {
   // captured into a graph it ran 12% slower per iteration (r05k)
   int snStreams = 2;
   hipStream_t stF = nullptr;
-  hipEvent_t evSnFork = nullptr, evSnLvl[4] = {};
+  hipEvent_t evSnFork = nullptr, evSnLvl[4] = {}, evClr = nullptr;
   hipEvent_t evStep = nullptr, evRs = nullptr;  // vb_optimize: box-plus done; the speculative rebuild on stF done
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
@@ -1994,6 +2004,14 @@ int doFinalize(vb_handle h) {
   }
   if (upload(&d.obCostOrder, costOrder)) return VB_E_HIP;
   {
+    auto rsStart = [&](int64_t b, int64_t e) {
+      int64_t n = 0;
+      for (int64_t i = b; i < e; i++) n += obRS[i] < 0;
+      return b + n;
+    };
+    h->costRsB[0] = rsStart(d.obB, d.obE), h->costRsB[1] = rsStart(d.fB, d.fE);
+  }
+  {
     std::vector<int32_t> pack((size_t)nObs * 8);
     std::vector<double> cp((size_t)nObs * 6);
     for (int64_t i = 0; i < nObs; i++) {
@@ -2074,7 +2092,7 @@ int doFinalize(vb_handle h) {
         upload(&d.rsN, cnt))
       return VB_E_HIP;
   }
-  if (alloc0(&d.red, 64) || alloc0(&d.redS, 64 * 8) || alloc0(&d.err, 8)) return VB_E_HIP;
+  if (alloc0(&d.red, 64) || alloc0(&d.redS, 2 * 64 * 8) || alloc0(&d.err, 8)) return VB_E_HIP;
   d.cacheW = d.cache;
   h->finalized = true;
   return 0;
@@ -2149,6 +2167,12 @@ void factorSeq(vb_handle h, const Sched& S) {
 // back at the end; segments queued level by level, a segment after the streams it depends on (segDep)
 // record their progress (one event per stream and level: everything they have queued so far is of
 // earlier levels).  A profiled factor family runs the same schedule, eagerly (per-launch events).
+}  // namespace
+extern "C" {  // (defined in the C ABI block below)
+int clearReduced(vb_handle h, const Dev& d, hipStream_t zs);
+Dev specDev(vb_handle h);
+}
+namespace {
 void factorSeqSn(vb_handle h, int which) {
   Dev& d = h->d;
   const SnSched& S = h->sn[which];
@@ -2166,9 +2190,20 @@ void factorSeqSn(vb_handle h, int which) {
     for (int g = 1; g < G; g++) (void)hipStreamWaitEvent(stOf(g), h->evSnFork, 0);
   }
   const int nSeg = (int)S.segG.size();
+  // the top separators' chain: the trailing run of levels with one segment each
+  int chain0 = 0;
+  for (int i = 1; i < nSeg; i++)
+    if (S.segL[i] == S.segL[i - 1]) chain0 = i + 1;
+  const bool clearHere = h->clearWanted && which == 0 && S.nGroups == 2 && !h->factorOnly;
   for (int i0 = 0; i0 < nSeg;) {
     int i1 = i0;
     while (i1 < nSeg && S.segL[i1] == S.segL[i0]) i1++;
+    if (clearHere && i0 == chain0) {  // vb_optimize's clear of the spare tile store (stZ: not a factor stream at G = 2)
+      (void)hipEventRecord(h->evClr, stOf(S.segG[i0]));
+      (void)hipStreamWaitEvent(h->stZ, h->evClr, 0);
+      if (clearReduced(h, specDev(h), h->stZ) == 0) h->clearQueued = true;
+      h->clearWanted = false;
+    }
     if (forked) {  // the level's cross-stream dependencies, recorded before any of its launches
       uint32_t need = 0;
       for (int i = i0; i < i1; i++) need |= (uint32_t)S.segDep[i];
@@ -2490,6 +2525,8 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   h->cfg = c;
   if (const char* e = getenv("VIBA_NO_GRAPHS")) h->useGraphs = e[0] != '1';
   if (const char* e = getenv("VIBA_SPEC_EARLY")) h->specEarly = e[0] != '0';
+  if (const char* e = getenv("VIBA_COST_FUSE")) h->costFuse = e[0] != '0';
+  if (const char* e = getenv("VIBA_CLEAR_IN_FACTOR")) h->clearInFactor = e[0] != '0';
   if (const char* e = getenv("VIBA_DEBUG_SPEC_FAIL")) h->specFailDebug = e[0] == '1';
   if (const char* e = getenv("VIBA_SUPERNODE")) h->useSn = e[0] == '1';
   if (const char* e = getenv("VIBA_SN_STREAMS")) h->snStreams = std::max(1, std::min(4, atoi(e)));
@@ -2509,6 +2546,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipEventCreateWithFlags(&h->evZJoin, hipEventDisableTiming));
   HIPCHK(hipStreamCreateWithFlags(&h->stF, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->evSnFork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evClr, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evStep, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evRs, hipEventDisableTiming));
   for (auto& e : h->evSnLvl) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2558,6 +2596,7 @@ int vb_destroy(vb_handle h) {
   if (h->stZ) hipStreamSynchronize(h->stZ), hipStreamDestroy(h->stZ);
   if (h->stF) hipStreamSynchronize(h->stF), hipStreamDestroy(h->stF);
   if (h->evSnFork) hipEventDestroy(h->evSnFork);
+  if (h->evClr) hipEventDestroy(h->evClr);
   if (h->evStep) hipEventDestroy(h->evStep);
   if (h->evRs) hipEventDestroy(h->evRs);
   for (hipEvent_t e : h->evSnLvl)
@@ -2855,6 +2894,7 @@ int clearReduced(vb_handle h, const Dev& d, hipStream_t zs) {
 // evaluation and the clear were queued on stZ already (specEarly)
 int linearizeBody(vb_handle h, const Dev& d, int update_cache, int dont_retry_failed, hipEvent_t evA, hipEvent_t evB,
                   bool early = false) {
+  const bool fuseCost = d.costS != nullptr;
   HIPCHK(hipEventRecord(evA, h->st));
   // the reduced system is cleared and the small factors assembled on the side stream while the visual
   // factors linearize on the main stream (they write only their records and the cost)
@@ -2889,6 +2929,12 @@ int linearizeBody(vb_handle h, const Dev& d, int update_cache, int dont_retry_fa
     HIPCHK(hipEventRecord(h->evZJoin, h->stZ));
   }
   visualLinShard(h, d, update_cache, dont_retry_failed);
+  if (fuseCost) {  // the rest of vb_optimize's cost pass (costFusedEnqueue): its sums into red[1..4]
+    launch_fold_red(h->d, h->st);
+    HIPCHK(hipEventRecord(h->ev[7], h->st));
+    HIPCHK(hipEventRecord(h->evCost, h->st));
+    h->profAtCost = h->profUsed;
+  }
   joinSmall(h);
   if (side) HIPCHK(hipStreamWaitEvent(h->st, h->evZJoin, 0));
   HIPCHK(hipEventRecord(evB, h->st));
@@ -3300,6 +3346,22 @@ int costEnqueue(vb_handle h, int comparable, bool clearErr) {
   HIPCHK(hipEventRecord(h->ev[7], h->st));
   return 0;
 }
+// vb_optimize's cost pass with the global-shutter observations folded into the speculative
+// linearization queued next (specEnqueue with fuseCost: visual_lin_kernel<true>, then the fold and
+// ev[7] / evCost): here only the small factors and the rolling-shutter observations, evaluated with the
+// iteration's tables while the rebuild for the next one runs on stF
+int costFusedEnqueue(vb_handle h) {
+  Dev& d = h->d;
+  HIPCHK(hipEventRecord(h->ev[6], h->st));
+  HIPCHK(hipMemsetAsync(d.red + 1, 0, 4 * sizeof(double), h->st));
+  forkSmall(h, 2, nullptr);
+  profBegin(h, KF_VISUAL_COST);
+  launch_visual_cost(d, 1, h->costRsB[0], d.obE, h->st);
+  launch_visual_cost(d, 1, h->costRsB[1], d.fE, h->st);
+  profEnd(h, KF_VISUAL_COST);
+  joinSmall(h);
+  return 0;
+}
 void costStats(vb_handle h, const double* r, double* cost, vb_cost_stats* stats) {
   int64_t nSmall = 0;
   if (h->isRoot)
@@ -3502,6 +3564,7 @@ Dev specDev(vb_handle h) {
   Dev ds = h->d;
   ds.tiles = h->tilesAlt, ds.cacheW = h->cacheAlt, ds.gRed = h->gRedAlt;
   ds.red = h->d.red + 48, ds.err = h->d.err + 4;
+  ds.redS = h->d.redS + 64 * 8;  // own stripes: the fused cost pass adds into the handle's (costS)
   if (h->rsDevice) ds.rsS = h->rsSAlt, ds.rsI = h->rsIAlt, ds.rsG = h->rsGAlt, ds.rsN = h->rsNAlt;
   return ds;
 }
@@ -3510,8 +3573,9 @@ Dev specDev(vb_handle h) {
 // With early set, specEarly queued the small factors' evaluation and the clear beside the cost pass.
 // rsDone: vb_optimize already cleared the speculative slots and queued the rebuild on stF (evRs), beside
 // the cost pass; the main stream only waits for it.
-int specEnqueue(vb_handle h, int dontRetry, int p, bool early, bool rsDone = false) {
-  const Dev ds = specDev(h);
+int specEnqueue(vb_handle h, int dontRetry, int p, bool early, bool rsDone = false, bool fuseCost = false) {
+  Dev ds = specDev(h);
+  if (fuseCost) ds.costS = h->d.redS;
   if (!early && !rsDone) {
     HIPCHK(hipMemsetAsync(ds.red, 0, 16 * sizeof(double), h->st));
     HIPCHK(hipMemsetAsync(ds.err, 0, 2 * sizeof(int32_t), h->st));
@@ -3530,7 +3594,7 @@ int specEnqueue(vb_handle h, int dontRetry, int p, bool early, bool rsDone = fal
 // factors' evaluation into the staging slots and the clear of the spare tile store and gradient.  The
 // staging slots are free there (the iteration's assembly is joined, and vb_gradient_dot_step's
 // evaluation forks from the main stream after the speculative linearization's join).
-int specEarly(vb_handle h, bool cleared = false) {
+int specEarly(vb_handle h, bool cleared = false, bool storeCleared = false) {
   if (!smallHere(h, 0)) return 0;
   const Dev ds = specDev(h);
   if (!cleared) {
@@ -3540,7 +3604,8 @@ int specEarly(vb_handle h, bool cleared = false) {
   HIPCHK(hipEventRecord(h->evFork, h->st));
   HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
   launch_small_eval(ds, 0, ds.gRed, h->stZ);
-  return clearReduced(h, ds, h->stZ);
+  // (storeCleared: the factorization queued the clear on stZ already, factorSeqSn)
+  return storeCleared ? 0 : clearReduced(h, ds, h->stZ);
 }
 // the step was accepted at full size: the speculative buffers become the handle's
 void specCommit(vb_handle h) {
@@ -3622,12 +3687,16 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
     // pass: none of them changes what the queued work does
     double prevCost, modelRed, ratios[3], newCost;
     vb_cost_stats st;
-    if ((rc = dampFactorSolveEnqueue(h, damping, false))) return bail(rc);
+    const bool specNext = speculate && it + 1 < s.max_num_iterations;
+    const bool early = specNext && smallHere(h, 0) && h->specEarly;
+    h->clearWanted = early && h->clearInFactor, h->clearQueued = false;
+    rc = dampFactorSolveEnqueue(h, damping, false);
+    const bool storeCleared = h->clearQueued;
+    h->clearWanted = h->clearQueued = false;
+    if (rc) return bail(rc);
     if ((rc = vb_backup(h))) return bail(rc);
     backedUp = true;
     if ((rc = applyStepEnqueue(h, 0, 10, 11))) return bail(rc);
-    const bool specNext = speculate && it + 1 < s.max_num_iterations;
-    const bool early = specNext && smallHere(h, 0) && h->specEarly;
     // the next iteration's rolling-shutter rebuild (a few latency-bound waves) on stF beside the cost pass
     // instead of after it on the main stream: the speculative slots are cleared first (the rebuild sets
     // error bits), and the main stream waits for it (evRs) before the linearization -- and so before
@@ -3646,19 +3715,24 @@ int vb_optimize(vb_handle h, const vb_settings* sp, vb_log_cb log, vb_prestep_cb
         return bail(fail(VB_E_HIP, "speculative rebuild join"));
       rsSide = true;
     }
-    if (early && (rc = specEarly(h, rsSide))) return bail(rc);
-    if ((rc = costEnqueue(h, 1, false))) return bail(rc);
+    if (early && (rc = specEarly(h, rsSide, storeCleared))) return bail(rc);
+    // the global-shutter part of the cost pass inside the speculative linearization (every observation
+    // evaluated there: not under dontRetry)
+    const bool fuseCost = specNext && h->costFuse && !dontRetry;
+    if ((rc = fuseCost ? costFusedEnqueue(h) : costEnqueue(h, 1, false))) return bail(rc);
     const bool wasSpec = specQueued;
     const int wasSet = specSet;
     specQueued = false;
     if (speculate) {
-      if (hipEventRecord(h->evCost, h->st) != hipSuccess) return bail(fail(VB_E_HIP, "hipEventRecord"));
-      h->profAtCost = h->profUsed;
+      if (!fuseCost) {  // (fused: recorded after the speculative visual linearization)
+        if (hipEventRecord(h->evCost, h->st) != hipSuccess) return bail(fail(VB_E_HIP, "hipEventRecord"));
+        h->profAtCost = h->profUsed;
+      }
       // the next iteration's rebuild + linearization, assuming this step is accepted at full size (not
       // after the last iteration: its work would only be discarded)
       if (it + 1 < s.max_num_iterations) {
         specSet ^= 1;
-        if ((rc = specEnqueue(h, dontRetry, specSet, early, rsSide))) return bail(rc);
+        if ((rc = specEnqueue(h, dontRetry, specSet, early, rsSide, fuseCost))) return bail(rc);
         specQueued = true;
       }
     }

@@ -231,6 +231,10 @@ struct Dev {
   // the visual kernels' cost sums striped over 64 slots of 8 (slot blockIdx & 63): one atomic target
   // per cost word serialised ~90k atomics in L2; fold_red_kernel adds them into red[0..8) and clears them
   double* redS = nullptr;
+  // vb_optimize's speculative linearization with the cost pass's global-shutter part folded in: the
+  // CostStats of those observations (comparable) go to these stripes (the handle's own redS, columns
+  // 1..4 as visual_cost_kernel); nullptr otherwise
+  double* costS = nullptr;
   int32_t* err = nullptr;  // error flags
   // landmark shard of this handle (multi-GPU; the whole problem on a single GPU): landmarks
   // [lmB, lmE), their observations [obB, obE), constant-point observations [fB, fE) (all of

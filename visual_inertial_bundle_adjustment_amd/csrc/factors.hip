@@ -211,6 +211,12 @@ __device__ __forceinline__ void store_planes(double* p, double a, double b) { *(
 __device__ __forceinline__ void store_planes(float* p, double a, double b) { *(float2_t*)p = float2_t{(float)a, (float)b}; }
 constexpr int kVisBlock = 128;  // two waves, 2 x 20 KB of staging
 
+// Cost: also the cost pass's sums (visual_cost_kernel, comparable) of the global-shutter observations
+// into d.costS -- the linearization point of a speculative linearization is the stepped variables the
+// cost pass evaluates; the rolling-shutter ones are not folded in (the cost pass evaluates them with
+// the tables of the iteration's linearization, the speculative linearization with rebuilt ones).
+// Only with dontRetry = 0: every observation is evaluated.
+template <bool Cost>
 __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int updateCache, int dontRetry, int64_t lo,
                                                                int64_t hi) {
   __shared__ double stage[kVisBlock / 64][64 * kJB];
@@ -224,6 +230,7 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
   const int32_t o = pa.x;
   double* S = stage[wave];
   double acc[1] = {0.0};
+  double cst[4] = {0.0, 0.0, 0.0, 0.0};  // Cost: cost, numTotal, numInvalid, numPrevInvalid
   VisOut v;
   v.Jintr = S + lane * kJB;  // region-B position of the record (intrinsics are planes 32..65)
   bool ok = false;
@@ -262,6 +269,13 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
       w = sqrt(drho);
       acc[0] = 0.5 * rho;
       if (updateCache) d.cacheW[o] = 0.5 * rho;
+    }
+    if (Cost && pb.y < 0) {  // visual_cost_kernel's sums, comparable
+      const bool prevInvalid = c0 < 0.0;
+      cst[1] = 1.0;
+      cst[2] = ok ? 0.0 : 1.0;
+      cst[3] = prevInvalid ? 1.0 : 0.0;
+      cst[0] = prevInvalid ? 0.0 : (ok ? acc[0] : c0);
     }
   }
   // region B (intrinsics already in place from the evaluation): scale by w, velocity, copy out
@@ -316,6 +330,15 @@ __global__ void __launch_bounds__(kVisBlock) visual_lin_kernel(Dev d, int update
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
   if (lane == 0 && x != 0.0) atomicAdd(d.redS + (blockIdx.x & 63) * 8 + 0, x);
+  if (Cost) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      double y = cst[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) y += __shfl_down(y, off, 64);
+      if (lane == 0 && y != 0.0) atomicAdd(d.costS + (blockIdx.x & 63) * 8 + 1 + k, y);
+    }
+  }
 }
 
 // cost pass: red[1] += cost, red[2..4] += stats (numTotal, numInvalid, numPrevInvalid)
@@ -1209,8 +1232,12 @@ void launch_refine_points(const Dev& d, const int64_t* gStart, const int32_t* gO
 void launch_visual_lin(const Dev& d, int updateCache, int dontRetry, int64_t lo, int64_t hi, hipStream_t st) {
   if (hi <= lo) return;
   const int64_t n = hi - lo;
-  launchK(visual_lin_kernel, dim3((unsigned)((n + kVisBlock - 1) / kVisBlock)), dim3(kVisBlock), 0, st, d, updateCache,
-          dontRetry, lo, hi);
+  if (d.costS)
+    launchK(visual_lin_kernel<true>, dim3((unsigned)((n + kVisBlock - 1) / kVisBlock)), dim3(kVisBlock), 0, st, d,
+            updateCache, dontRetry, lo, hi);
+  else
+    launchK(visual_lin_kernel<false>, dim3((unsigned)((n + kVisBlock - 1) / kVisBlock)), dim3(kVisBlock), 0, st, d,
+            updateCache, dontRetry, lo, hi);
 }
 // red[k] += sum of the 64 stripes of redS[., k] (atomically: the small factors add into red beside), and
 // the stripes cleared for the next launch
