@@ -403,7 +403,7 @@ struct vb_handle_s {
   // queued on stZ from inside the factorization, at the top separators' chain (one stream, a few
   // latency-bound launches per level, HBM idle) instead of beside the cost pass (VIBA_CLEAR_IN_FACTOR=0);
   // clearWanted: factorSeqSn queues it (then sets clearQueued)
-  bool clearInFactor = true, clearWanted = false, clearQueued = false;
+  bool clearInFactor = true, clearWanted = false, clearQueued = false, clearOnF = false;
   int64_t costRsB[2] = {0, 0};
   // vb_optimize's speculative linearization (specEnqueue): the next iteration's rolling-shutter rebuild
   // and linearization are queued behind this iteration's cost pass, before the host reads its scalars,
@@ -427,7 +427,7 @@ struct vb_handle_s {
   // captured into a graph it ran 12% slower per iteration (r05k)
   int snStreams = 2;
   hipStream_t stF = nullptr;
-  hipEvent_t evSnFork = nullptr, evSnLvl[4] = {}, evClr = nullptr;
+  hipEvent_t evSnFork = nullptr, evSnLvl[4] = {}, evClr = nullptr, evClrDone = nullptr;
   hipEvent_t evStep = nullptr, evRs = nullptr;  // vb_optimize: box-plus done; the speculative rebuild on stF done
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
@@ -2194,14 +2194,19 @@ void factorSeqSn(vb_handle h, int which) {
   int chain0 = 0;
   for (int i = 1; i < nSeg; i++)
     if (S.segL[i] == S.segL[i - 1]) chain0 = i + 1;
-  const bool clearHere = h->clearWanted && which == 0 && S.nGroups == 2 && !h->factorOnly;
+  // (on a stream the schedule leaves free: stZ at G = 2, stF at G = 3; stZ then waits for it, evClrDone)
+  const bool clearHere = h->clearWanted && which == 0 && (S.nGroups == 2 || S.nGroups == 3) && !h->factorOnly;
+  hipStream_t cs = S.nGroups == 2 ? h->stZ : h->stF;
   for (int i0 = 0; i0 < nSeg;) {
     int i1 = i0;
     while (i1 < nSeg && S.segL[i1] == S.segL[i0]) i1++;
-    if (clearHere && i0 == chain0) {  // vb_optimize's clear of the spare tile store (stZ: not a factor stream at G = 2)
+    if (clearHere && i0 == chain0) {  // vb_optimize's clear of the spare tile store
       (void)hipEventRecord(h->evClr, stOf(S.segG[i0]));
-      (void)hipStreamWaitEvent(h->stZ, h->evClr, 0);
-      if (clearReduced(h, specDev(h), h->stZ) == 0) h->clearQueued = true;
+      (void)hipStreamWaitEvent(cs, h->evClr, 0);
+      if (clearReduced(h, specDev(h), cs) == 0) h->clearQueued = true;
+      // (stF: specEarly makes stZ wait for it -- not here, where stZ is a factor stream the join waits for)
+      h->clearOnF = cs != h->stZ;
+      if (h->clearOnF) (void)hipEventRecord(h->evClrDone, cs);
       h->clearWanted = false;
     }
     if (forked) {  // the level's cross-stream dependencies, recorded before any of its launches
@@ -2547,6 +2552,7 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipStreamCreateWithFlags(&h->stF, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->evSnFork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evClr, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evClrDone, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evStep, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evRs, hipEventDisableTiming));
   for (auto& e : h->evSnLvl) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -2597,6 +2603,7 @@ int vb_destroy(vb_handle h) {
   if (h->stF) hipStreamSynchronize(h->stF), hipStreamDestroy(h->stF);
   if (h->evSnFork) hipEventDestroy(h->evSnFork);
   if (h->evClr) hipEventDestroy(h->evClr);
+  if (h->evClrDone) hipEventDestroy(h->evClrDone);
   if (h->evStep) hipEventDestroy(h->evStep);
   if (h->evRs) hipEventDestroy(h->evRs);
   for (hipEvent_t e : h->evSnLvl)
@@ -3603,6 +3610,7 @@ int specEarly(vb_handle h, bool cleared = false, bool storeCleared = false) {
   }
   HIPCHK(hipEventRecord(h->evFork, h->st));
   HIPCHK(hipStreamWaitEvent(h->stZ, h->evFork, 0));
+  if (storeCleared && h->clearOnF) HIPCHK(hipStreamWaitEvent(h->stZ, h->evClrDone, 0));
   launch_small_eval(ds, 0, ds.gRed, h->stZ);
   // (storeCleared: the factorization queued the clear on stZ already, factorSeqSn)
   return storeCleared ? 0 : clearReduced(h, ds, h->stZ);
