@@ -98,22 +98,3 @@ def test_supernode_streams_match_one_stream(streams):
     sg, sc = g2.optimize(s), c2.optimize(s)
     assert sg.num_iterations == sc.num_iterations and sg.num_rescaled == sc.num_rescaled
     assert abs(sg.final_cost - sc.final_cost) <= 1e-10 * sc.final_cost
-
-
-def test_supernode_fanin_target_pairs_match_single_targets():
-    """the fan-in by target pairs (VIBA_FAN_PAIRS=1, solver.hip fanin_kernel2: L_IK staged once for the two
-    targets (I, J), (I, J + 1) of a two-column supernode) forms the same factor as the single-target
-    fan-in: the step of one LM iteration on config B to round-off, and against the oracle"""
-    from test_parity_gpu import assert_step_parity
-    p = synth.generate(synth.config("B"))
-    with pytest.MonkeyPatch.context() as mp:
-        mp.setenv("VIBA_FAN_PAIRS", "1")
-        g = _hip(p, True)
-    c = _hip(p, True)
-    og, oc = one_step(g), one_step(c)
-    for k in range(NUM_VAR_KINDS - 1):
-        if oc["step"][k].size:
-            assert rel(og["step"][k], oc["step"][k]) < 1e-9, VAR_NAMES[k]
-    r = RefEngine(imu_calib_options=p.imu_calib_options)
-    synth.load_into(r, p)
-    assert_step_parity(og, one_step(r))

@@ -12,7 +12,6 @@
 #include <functional>
 #include <climits>
 #include <numeric>
-#include <unordered_map>
 #include <string>
 #include <unordered_map>
 #include <map>
@@ -58,7 +57,6 @@ void launch_snpotrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr
 void launch_sntrsm(const Dev& d, const int32_t* items, int n, const double* dinv, hipStream_t st, const double* fwdY,
                    double* fwdB);
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st);
-void launch_fanin2(const Dev& d, const int32_t* work, const int32_t* pairs, const int32_t* trips, int n, hipStream_t st);
 void launch_tile_symv(const double* tiles, const int32_t* tileList, const int32_t* tileRC, int64_t n, const double* x,
                       double* y, const double* stop, hipStream_t st);
 void launch_jacobi_init(const Dev& d, double* jac, hipStream_t st);
@@ -299,11 +297,6 @@ struct SnSched {
   std::vector<int64_t> lvF;
   int32_t *fusD = nullptr, *copyD = nullptr;
   int64_t nCopy = 0;
-  // pairT: fan-in work items of 8 (fanin_kernel2: single targets with pairs in fanPairsD, the two target
-  // tiles (I, J), (I, J + 1) of a two-column supernode with triples in tripsD); else items of 4 (fanin_kernel)
-  bool pairT = false;
-  int32_t* tripsD = nullptr;
-  int64_t nTriples = 0;
 
   hipGraphExec_t graph[2] = {nullptr, nullptr};
   bool built = false;
@@ -433,8 +426,6 @@ struct vb_handle_s {
   // (idle during the factorization); fork and per-level events.  The forked schedule is launched eagerly:
   // captured into a graph it ran 12% slower per iteration (r05k)
   int snStreams = 2;
-  // the supernode schedule's fan-in by target pairs (VIBA_FAN_PAIRS=1; measured slower)
-  bool fanPairT = false;
   hipStream_t stF = nullptr;
   hipEvent_t evSnFork = nullptr, evSnLvl[4] = {}, evClr = nullptr, evClrDone = nullptr;
   hipEvent_t evStep = nullptr, evRs = nullptr;  // vb_optimize: box-plus done; the speculative rebuild on stF done
@@ -598,7 +589,7 @@ int readRedErr(vb_handle h, double* out, int n) {
 // its ROOT targets, or the ROOT columns, in partition mode)
 int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx, int32_t nT, int64_t nTiles,
                     const std::function<bool(int32_t)>& colSel, const std::function<bool(int32_t)>& tgtSel,
-                    const std::function<bool(int32_t)>& srcSel, int nGroups = 1, bool pairT = false) {
+                    const std::function<bool(int32_t)>& srcSel, int nGroups = 1) {
   auto colRows = [&](int32_t J, int64_t& a, int64_t& b) { a = h->colStart[J], b = h->colStart[J + 1]; };
   // pair J with J + 1: J + 1 is J's first off-diagonal row (its parent) and every other row of J is a
   // row of J + 1 (so the pair's rows are J + 1's), both in one nested-dissection part
@@ -752,8 +743,6 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
   int64_t fuseMax = 256;  // levels with at most this many row items run snpotrf_trsm8_kernel
   if (const char* e = getenv("VIBA_SN_FUSE")) fuseMax = atoll(e);
   std::vector<int32_t> fan, pot, rows, fus, copy;
-  std::vector<int32_t> pairsOut, trips;  // pairT: the single targets' pairs in item order, the triples
-  const int FS = pairT ? 8 : 4;           // ints per fan-in work item
   S.lvU.assign(1, 0), S.lvS.assign(1, 0), S.lvR.assign(1, 0), S.lvF.assign(1, 0);
   S.segG.clear(), S.segL.clear(), S.segDep.clear();
 
@@ -778,7 +767,7 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
     const int share = std::max(1, nAct[L]);
     const int64_t fanWgs = 3072 / share;
     const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
-    const size_t u0 = fan.size() / FS;
+    const size_t u0 = fan.size() / 4;
     int64_t nRowsL = 0;
     for (int32_t J0 : supL) {
       if (!colSel(J0)) continue;
@@ -786,83 +775,21 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
       nRowsL += h->colStart[Jl + 1] - h->colStart[Jl] - 1;
     }
     const bool fused = nRowsL <= fuseMax / share;
-    // pairT: a target's single contributions copied to pairsOut, chunked into items
-    auto singles = [&](int32_t t, const std::vector<int32_t>& pl) {
-      const int64_t m = (int64_t)pl.size() / 2;
-      if (m == 0) return;
-      const int64_t b = (int64_t)pairsOut.size() / 2;
-      pairsOut.insert(pairsOut.end(), pl.begin(), pl.end());
-      const int64_t nch = (m + cs - 1) / cs;
-      for (int64_t k = 0; k < nch; k++) {
-        const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
-        fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), 0, -1, 0, 0, 0});
-      }
-    };
     for (int32_t J0 : supL) {
       const bool two = pr[J0] == 1;
       const int32_t J2 = two ? J0 + 1 : -1;
-      if (pairT && two && tgtSel(J0) && tgtSel(J2)) {
-        // (J0, J0) alone; every row I of J2 (J2 itself first) with its partner (I, J0) where J0 has that row
-        // (J0's rows below the pair are a subset of J2's): the contributions
-        // of one source column K to both become a triple (matched by their tile L_IK), the rest singles
-        auto plist = [&](int32_t t) {
-          return std::vector<int32_t>(pairs.begin() + 2 * ccnt[t], pairs.begin() + 2 * ccnt[t + 1]);
-        };
-        singles(tile(J0, J0), plist(tile(J0, J0)));
-        const int64_t cs3 = std::max<int64_t>(2, cs / 2);
-        for (int64_t c = h->colStart[J2]; c < h->colStart[J2 + 1]; c++) {
-          const int32_t I = h->colRowsH[c], t2 = h->colTilesH[c], t1 = tile(I, J0);
-          if (t1 < 0) {  // (a row of J2 only: J0's rows below the pair are a subset of J2's)
-            singles(t2, plist(t2));
-            continue;
+      for (int32_t J = J0; J <= (two ? J2 : J0); J++)
+        for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
+          if (!tgtSel(J)) continue;
+          const int32_t t = h->colTilesH[c];
+          const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
+          if (m == 0) continue;
+          const int64_t nch = (m + cs - 1) / cs;
+          for (int64_t k = 0; k < nch; k++) {
+            const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
+            fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
           }
-          const std::vector<int32_t> l1 = plist(t1), l2 = plist(t2);
-          std::unordered_map<int32_t, int64_t> at2;
-          for (size_t k = 0; k < l2.size(); k += 2) at2[l2[k]] = (int64_t)k;
-          std::vector<int8_t> used2(l2.size() / 2, 0);
-          std::vector<int32_t> r1, tr;
-          for (size_t k = 0; k < l1.size(); k += 2) {
-            auto it = at2.find(l1[k]);
-            if (it != at2.end() && !used2[it->second / 2]) {
-              used2[it->second / 2] = 1;
-              tr.insert(tr.end(), {l1[k], l1[k + 1], l2[it->second + 1]});
-            } else {
-              r1.insert(r1.end(), {l1[k], l1[k + 1]});
-            }
-          }
-          std::vector<int32_t> r2;
-          for (size_t k = 0; k < l2.size(); k += 2)
-            if (!used2[k / 2]) r2.insert(r2.end(), {l2[k], l2[k + 1]});
-          const int64_t m = (int64_t)tr.size() / 3;
-          if (m > 0) {
-            const int64_t b = (int64_t)trips.size() / 3;
-            trips.insert(trips.end(), tr.begin(), tr.end());
-            const int64_t nch = (m + cs3 - 1) / cs3;
-            for (int64_t k = 0; k < nch; k++) {
-              const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
-              fan.insert(fan.end(), {t1, (int32_t)s0, (int32_t)(s1 - s0), 0, t2, 0, 0, 0});
-            }
-          }
-          singles(t1, r1), singles(t2, r2);
         }
-      } else {
-        for (int32_t J = J0; J <= (two ? J2 : J0); J++)
-          for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) {
-            if (!tgtSel(J)) continue;
-            const int32_t t = h->colTilesH[c];
-            if (pairT) {
-              singles(t, std::vector<int32_t>(pairs.begin() + 2 * ccnt[t], pairs.begin() + 2 * ccnt[t + 1]));
-              continue;
-            }
-            const int64_t b = ccnt[t], m = ccnt[t + 1] - b;
-            if (m == 0) continue;
-            const int64_t nch = (m + cs - 1) / cs;
-            for (int64_t k = 0; k < nch; k++) {
-              const int64_t s0 = b + m * k / nch, s1 = b + m * (k + 1) / nch;
-              fan.insert(fan.end(), {t, (int32_t)s0, (int32_t)(s1 - s0), nch > 1 ? 1 : 0});
-            }
-          }
-      }
       if (!colSel(J0)) continue;
       const int32_t t11 = tile(J0, J0), t21 = two ? tile(J2, J0) : -1, t22 = two ? tile(J2, J2) : -1;
       S.nTwo += two ? 1 : 0;
@@ -885,30 +812,20 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
         rows.insert(rows.end(), {two ? tile(I, J0) : h->colTilesH[c], two ? h->colTilesH[c] : -1, J0, J2, I, t11, t21, t22});
       }
     }
-    if (pairT) {  // a target written by more than one item of the launch takes atomic adds
-      std::unordered_map<int32_t, int> writers;
-      for (size_t i = u0; i < fan.size() / 8; i++) {
-        writers[fan[8 * i]]++;
-        if (fan[8 * i + 4] >= 0) writers[fan[8 * i + 4]]++;
-      }
-      for (size_t i = u0; i < fan.size() / 8; i++)
-        fan[8 * i + 3] = (writers[fan[8 * i]] > 1 || (fan[8 * i + 4] >= 0 && writers[fan[8 * i + 4]] > 1)) ? 1 : 0;
-    }
-    {  // longest chunks first within each XCD's range (as the column schedule); a triple is two contributions
-      std::vector<std::array<int32_t, 8>> q((fan.size() / FS) - u0);
+    {  // longest chunks first within each XCD's range (as the column schedule)
+      std::vector<std::array<int32_t, 4>> q((fan.size() / 4) - u0);
       for (size_t i = 0; i < q.size(); i++)
-        for (int k = 0; k < FS; k++) q[i][k] = fan[FS * (u0 + i) + k];
-      auto work = [&](const std::array<int32_t, 8>& a) { return (int64_t)a[2] * (FS == 8 && a[4] >= 0 ? 2 : 1); };
+        for (int k = 0; k < 4; k++) q[i][k] = fan[4 * (u0 + i) + k];
       const size_t nq = q.size(), qq = nq / 8, rr = nq % 8;
       for (size_t x = 0, b0 = 0; x < 8; x++) {
         const size_t len = qq + (x < rr ? 1 : 0);
-        std::stable_sort(q.begin() + b0, q.begin() + b0 + len, [&](const auto& a, const auto& b) { return work(a) > work(b); });
+        std::stable_sort(q.begin() + b0, q.begin() + b0 + len, [](const auto& a, const auto& b) { return a[2] > b[2]; });
         b0 += len;
       }
       for (size_t i = 0; i < q.size(); i++)
-        for (int k = 0; k < FS; k++) fan[FS * (u0 + i) + k] = q[i][k];
+        for (int k = 0; k < 4; k++) fan[4 * (u0 + i) + k] = q[i][k];
     }
-    S.lvU.push_back((int64_t)fan.size() / FS), S.lvS.push_back((int64_t)pot.size() / 4), S.lvR.push_back((int64_t)rows.size() / 8);
+    S.lvU.push_back((int64_t)fan.size() / 4), S.lvS.push_back((int64_t)pot.size() / 4), S.lvR.push_back((int64_t)rows.size() / 8);
     S.lvF.push_back((int64_t)fus.size() / 8);
     S.segG.push_back(g), S.segL.push_back(L), S.segDep.push_back((int32_t)dep);
   }
@@ -917,15 +834,9 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
   S.nSuper = 0;
   for (int32_t J = 0; J < nT; J++) S.nSuper += (pr[J] != 2 && colSel(J)) ? 1 : 0;
   S.nCopy = (int64_t)copy.size() / 2;
-  S.pairT = pairT;
-  S.nTriples = (int64_t)trips.size() / 3;
-  if (trips.empty()) trips.assign(3, 0);
-  if (upload(&S.updD, fan) || upload(&S.fanPairsD, pairT ? pairsOut : pairs) || upload(&S.potD, pot) ||
-      upload(&S.rowD, rows) || upload(&S.fusD, fus) || upload(&S.copyD, copy) || upload(&S.tripsD, trips))
+  if (upload(&S.updD, fan) || upload(&S.fanPairsD, pairs) || upload(&S.potD, pot) || upload(&S.rowD, rows) ||
+      upload(&S.fusD, fus) || upload(&S.copyD, copy))
     return VB_E_HIP;
-  if (getenv("VIBA_FACTOR_STATS"))
-    fprintf(stderr, "[factor stats] fan-in items %zu, triples %lld (contributions %lld)\n", fan.size() / FS,
-            (long long)S.nTriples, (long long)ccnt[nTiles]);
   if (S.nCopy && !h->lscrSn && alloc0(&h->lscrSn, 2 * (size_t)nT * TS * TS)) return VB_E_HIP;
   S.built = true;
   return 0;
@@ -2002,7 +1913,7 @@ int doFinalize(vb_handle h) {
     if (h->useSn) {
       if (W <= 1) {
         auto any = [](int32_t) { return true; };
-        if (int rc = buildSupernodes(h, h->sn[0], tileIdx, nT, nTiles, any, any, any, h->snStreams, h->fanPairT)) return rc;
+        if (int rc = buildSupernodes(h, h->sn[0], tileIdx, nT, nTiles, any, any, any, h->snStreams)) return rc;
       } else {
         auto own = [&](int32_t J) { return h->colOwner[J] == me; };
         auto root = [&](int32_t J) { return h->colOwner[J] == W; };
@@ -2311,8 +2222,7 @@ void factorSeqSn(vb_handle h, int which) {
           if ((uint32_t)S.segDep[i] >> q & 1) (void)hipStreamWaitEvent(st, h->evSnLvl[q], 0);
       const int64_t u0 = S.lvU[i], s0 = S.lvS[i], r0 = S.lvR[i];
       profBegin(h, KF_GEMM);
-      if (S.pairT) launch_fanin2(d, S.updD + 8 * u0, S.fanPairsD, S.tripsD, (int)(S.lvU[i + 1] - u0), st);
-      else launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[i + 1] - u0), st);
+      launch_fanin(d, S.updD + 4 * u0, S.fanPairsD, (int)(S.lvU[i + 1] - u0), st);
       profEnd(h, KF_GEMM);
       profBegin(h, KF_POTRF);
       if (S.lvF[i + 1] > S.lvF[i])
@@ -2625,7 +2535,6 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   if (const char* e = getenv("VIBA_DEBUG_SPEC_FAIL")) h->specFailDebug = e[0] == '1';
   if (const char* e = getenv("VIBA_SUPERNODE")) h->useSn = e[0] == '1';
   if (const char* e = getenv("VIBA_SN_STREAMS")) h->snStreams = std::max(1, std::min(4, atoi(e)));
-  if (const char* e = getenv("VIBA_FAN_PAIRS")) h->fanPairT = e[0] != '0';
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -2707,8 +2616,7 @@ int vb_destroy(vb_handle h) {
   if (h->stR) hipStreamSynchronize(h->stR), hipStreamDestroy(h->stR);
   if (h->hostRed) hipHostFree(h->hostRed);
   for (SnSched& N : h->sn) {
-    for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD, (void*)N.fusD, (void*)N.copyD,
-                    (void*)N.tripsD})
+    for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD, (void*)N.fusD, (void*)N.copyD})
       if (p) hipFree(p);
     for (hipGraphExec_t g : N.graph)
       if (g) hipGraphExecDestroy(g);

@@ -1664,121 +1664,6 @@ __global__ void __launch_bounds__(kFanWaves * 64) fanin_kernel(Dev d, const int3
   fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
 }
 
-// Target pairs of a two-column supernode (J, J + 1): [A_IJ A_I,J+1] -= sum_K L_IK [L_JK L_J+1,K]^T, so
-// L_IK is staged once for both targets (three half-tile slabs per stage instead of four for two
-// single-target contributions).  Triples (L_IK, L_JK, L_J+1,K); wave w takes 32 columns of the
-// 128: waves 0, 1 of tile (I, J), waves 2, 3 of tile (I, J + 1), all 64 rows (eight 16 x 16 blocks).
-constexpr int kStage3 = 3 * kFanK * TS;             // doubles per stage: [L_JK, L_J+1,K, L_IK][kFanK][64]
-constexpr int kGlds3 = kStage3 / 128 / kFanWaves;   // 6 global_load_lds per wave per stage
-#ifndef VIBA_FAN3_RING
-#define VIBA_FAN3_RING 3
-#endif
-constexpr int kFanRing3 = VIBA_FAN3_RING;            // stages in the target-pair ring
-
-__device__ __forceinline__ void fanin3_issue(const Dev& d, const int32_t* trip, int32_t start, int s, double* buf,
-                                             int wave, int lane) {
-  const int64_t c = start + s / (TS / kFanK);
-  const int k0 = (s % (TS / kFanK)) * kFanK;
-  const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)trip;
-  const int64_t ti = pc[3 * c], tj = pc[3 * c + 1], tj2 = pc[3 * c + 2];
-  const int hi = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < kGlds3; j++) {
-    const int i = wave * kGlds3 + j, tile = i / (kFanK / 2), cp = i % (kFanK / 2);
-    const int row = (2 * (lane & 31) - fan_rot(2 * cp + hi)) & 63;
-    const int64_t t = tile == 0 ? tj : tile == 1 ? tj2 : ti;
-    const double* src = d.tiles + t * TS * TS + (int64_t)(k0 + 2 * cp + hi) * TS + row;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(buf + tile * kFanK * TS + cp * 2 * TS),
-                                     16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ void fanin3_accum(const Dev& d, const int32_t* trip, int32_t start, int32_t count,
-                                             double* stg, int wave, int lane, double4_t (&acc)[2][4]) {
-  static_assert(kGlds3 * (kFanRing3 - 1) <= 63, "vmcnt range");
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int slab = wave >> 1, jr = (wave & 1) * 32;
-  const int32_t nst = (TS / kFanK) * count;
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 4; b++) acc[a][b] = double4_t{0, 0, 0, 0};
-  constexpr int kAhead = kFanRing3 - 1;
-  for (int s = 0; s < kAhead && s < nst; s++) fanin3_issue(d, trip, start, s, stg + s * kStage3, wave, lane);
-  for (int s = 0; s < nst; s++) {
-    if (s + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGlds3) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + kAhead < nst) fanin3_issue(d, trip, start, s + kAhead, stg + ((s + kAhead) % kFanRing3) * kStage3, wave, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    const double* bs = stg + (s % kFanRing3) * kStage3;
-    const double* bj = bs + slab * kFanK * TS;
-    const double* bi = bs + 2 * kFanK * TS;
-#pragma unroll
-    for (int t0 = 0; t0 < kFanK; t0 += 4) {
-      const int t = t0 + l4, rot = (t & 1) * 16;
-      double av[2], bv[4];
-#pragma unroll
-      for (int a = 0; a < 2; a++) av[a] = bj[t * TS + ((jr + a * 16 + l15 + rot) & 63)];
-#pragma unroll
-      for (int b = 0; b < 4; b++) bv[b] = bi[t * TS + ((b * 16 + l15 + rot) & 63)];
-#pragma unroll
-      for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) acc[a][b] = mfma64(av[a], bv[b], acc[a][b]);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-__device__ __forceinline__ void fanin3_store(double* C, bool atomic, int jr, int lane, const double4_t (&acc)[2][4]) {
-  const int l15 = lane & 15, l4 = lane >> 4;
-  double* Cw = C + (jr + l4) * TS + l15;
-  if (atomic) {
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) atomicAdd(Cw + (a * 16 + 4 * r) * TS + b * 16, -acc[a][b][r]);
-  } else {
-    double v[2][4][4];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) v[a][b][r] = Cw[(a * 16 + 4 * r) * TS + b * 16];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) Cw[(a * 16 + 4 * r) * TS + b * 16] = v[a][b][r] - acc[a][b][r];
-  }
-}
-
-// One launch per level segment with both item kinds: work items of 8 (target tile, start, count, split
-// (atomic stores), second target tile or -1, 0, 0, 0); a single target's contributions are pairs (L_IK,
-// L_JK) in `pairs`, a target pair's are triples in `trips`
-__global__ void __launch_bounds__(kFanWaves * 64) fanin_kernel2(Dev d, const int32_t* work, const int32_t* pairs,
-                                                               const int32_t* trips) {
-  __shared__ double stg[kFanRing3 * kStage3 > kFanRing * kStage ? kFanRing3 * kStage3 : kFanRing * kStage];
-  const int32_t* wk = work + 8 * xcd_block(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (wk[4] < 0) {
-    double4_t acc[2][2];
-    fanin_accum(d, pairs, wk[1], wk[2], stg, wave, lane, acc);
-    fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
-  } else {
-    double4_t acc[2][4];
-    fanin3_accum(d, trips, wk[1], wk[2], stg, wave, lane, acc);
-    fanin3_store(d.tiles + (int64_t)wk[(wave >> 1) ? 4 : 0] * TS * TS, wk[3] != 0, (wave & 1) * 32, lane, acc);
-  }
-}
-
 // Inverse of every factored diagonal tile (one wave per tile, lane = column c of X = L^-1, off the
 // factorization's critical path but before the backward solve): x_i = (delta_ic - sum_{k<i} L_ik x_k) / L_ii
 // with the 64 reciprocals formed first (one divide per lane) and each row's sum split over four partial
@@ -2274,10 +2159,6 @@ void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, cons
 
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
   if (n > 0) launchK(fanin_kernel, dim3(n), dim3(kFanWaves * 64), 0, st, d, work, pairs);
-}
-// the supernode schedule's form: single targets and target pairs (fanin_kernel2)
-void launch_fanin2(const Dev& d, const int32_t* work, const int32_t* pairs, const int32_t* trips, int n, hipStream_t st) {
-  if (n > 0) launchK(fanin_kernel2, dim3(n), dim3(kFanWaves * 64), 0, st, d, work, pairs, trips);
 }
 // inverses of the diagonal factor tiles of the listed columns (all columns if cols == nullptr)
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st) {
