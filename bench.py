@@ -281,8 +281,9 @@ def main():
         f"last it: lin {ph.linearize_ms:.2f} schur {ph.schur_ms:.2f} factor {ph.factor_ms:.2f} "
         f"solve {ph.solve_ms:.2f} step {ph.step_ms:.2f} cost {ph.cost_ms:.2f} rs-tables {ph.rs_update_ms:.3f} ms")
     # the roofline's kernel timing: a separate pass of the same binary with the profiled family's launches
-    # event-timed one by one (the factorization's segments then run on one stream, so each fan-in launch
-    # has the chip to itself; the timed pass above ran the multi-stream schedule from the same kernels)
+    # event-timed one by one, on the same multi-stream schedule as the timed pass: a launch can share the
+    # chip with the other stream's, so the roofline divides by the family's busy time (the union of its
+    # launch intervals, vb_kernel_busy_time), not by the sum of launch durations
     prof_iters = 0
     launches, kms, busy_ms = 0, 0.0, 0.0
     if args.profile_family >= 0 and args.profile_steps > 0:
