@@ -742,6 +742,8 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
   }
   int64_t fuseMax = 256;  // levels with at most this many row items run snpotrf_trsm8_kernel
   if (const char* e = getenv("VIBA_SN_FUSE")) fuseMax = atoll(e);
+  int64_t fanTarget = 3072;  // fan-in workgroups per level launch, divided among the level's active streams
+  if (const char* e = getenv("VIBA_SN_FANWGS")) fanTarget = std::max<int64_t>(256, atoll(e));
   std::vector<int32_t> fan, pot, rows, fus, copy;
   S.lvU.assign(1, 0), S.lvS.assign(1, 0), S.lvR.assign(1, 0), S.lvF.assign(1, 0);
   S.segG.clear(), S.segL.clear(), S.segDep.clear();
@@ -765,7 +767,7 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
       for (int32_t J = J0; J <= J0 + (pr[J0] == 1 ? 1 : 0); J++)
         for (int64_t c = h->colStart[J]; c < h->colStart[J + 1]; c++) total += ccnt[h->colTilesH[c] + 1] - ccnt[h->colTilesH[c]];
     const int share = std::max(1, nAct[L]);
-    const int64_t fanWgs = 3072 / share;
+    const int64_t fanWgs = fanTarget / share;
     const int64_t cs = std::min<int64_t>(32, std::max<int64_t>(4, (total + fanWgs - 1) / fanWgs));
     const size_t u0 = fan.size() / 4;
     int64_t nRowsL = 0;
