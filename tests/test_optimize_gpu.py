@@ -4,7 +4,9 @@ path, and the rescaling count, against the oracle's Optimizer::optimize (Optimiz
 vb_optimize queues the next iteration's rolling-shutter rebuild and linearization behind the cost pass,
 into second buffers, before the host has read the iteration's scalars; they are used only when the step
 is accepted at full size.  Its small factors and the clear start right after the box-plus, beside the
-cost pass (VIBA_SPEC_EARLY=0 at handle creation keeps them inside the speculative linearization).  A
+cost pass (VIBA_SPEC_EARLY=0 at handle creation keeps them inside the speculative linearization); the
+cost pass's global-shutter part runs inside the speculative linearization (VIBA_COST_FUSE) and the spare
+tile store is cleared during the factorization (VIBA_CLEAR_IN_FACTOR), both also tested off.  A
 prestep callback turns speculation off (the callback must run before the linearization), so the same
 problem with and without a callback runs both controller paths.
 """
@@ -45,9 +47,15 @@ def test_speculative_and_plain_controller_match_oracle(which):
     iterations, troubled sequences, rescaled steps, final cost, variables."""
     p = synth.generate(synth.config(which))
     runs = []
-    for cb, early in ((None, "1"), (None, "0"), (lambda it: None, "1")):
+    # (placements: the speculative side work beside the cost pass or inside the linearization; the cost
+    # pass's global-shutter part fused into the speculative linearization or not; the spare tile store
+    # cleared inside the factorization or beside the cost pass)
+    for cb, early, fuse, clear in ((None, "1", "1", "1"), (None, "0", "1", "1"), (None, "1", "0", "0"),
+                                   (lambda it: None, "1", "1", "1")):
         with pytest.MonkeyPatch.context() as mp:
             mp.setenv("VIBA_SPEC_EARLY", early)  # read when the handle is created
+            mp.setenv("VIBA_COST_FUSE", fuse)
+            mp.setenv("VIBA_CLEAR_IN_FACTOR", clear)
             e = hip()(imu_calib_options=p.imu_calib_options)
         synth.load_into(e, p, rs_device=True)
         runs.append((e, e.optimize(_settings(max_num_iterations=12), prestep=cb)))
