@@ -263,6 +263,72 @@ __global__ void __launch_bounds__(512) k_potrf8(Dev d, const double* A11, const 
   if (threadIdx.x == 0) cyc[b ? 1 : 0] = t1 - t0;
 }
 
+// diag16's parts timed one by one (a copy of its body with clock64() between the parts; the inverse is
+// stored to LDS and summed into a global sink after the loop, so nothing is dead): staging S through
+// LDS into row registers, the Chol16 pivot chain, L_ii into scratch + T with the wave barrier, the
+// inverse, its stores into dinvS
+__global__ void __launch_bounds__(64) k_diag16_parts(const double* A, int iters, long long* cyc, double* sink) {
+  __shared__ double T[64 * 64];
+  __shared__ double scratch[256];
+  __shared__ double dinvS[4 * 256];
+  const int lane = threadIdx.x, lr = lane & 15, lq = lane >> 4;
+  double4_t S;
+  for (int r = 0; r < 4; r++) S[r] = A[(lq + 4 * r) * 128 + lr];
+  bool bad = false;
+  long long part[5] = {0, 0, 0, 0, 0};
+  __syncthreads();
+  for (int it = 0; it < iters; it++) {
+    const int i = it & 3;
+    long long t0 = clock64();
+#pragma unroll
+    for (int r = 0; r < 4; r++) scratch[(lq + 4 * r) * 16 + lr] = S[r] + it * 1e-300;
+    __builtin_amdgcn_wave_barrier();
+    double s[16], invd[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) s[c] = scratch[lr * 16 + c];
+    long long t1 = clock64();
+    Chol16<0>::run(s, invd, lane, bad);
+    long long t2 = clock64();
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 16) {
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const double v = (c <= lane) ? s[c] : 0.0;
+        scratch[lane * 16 + c] = v;
+        T[(16 * i + c) * 64 + 16 * i + lane] = v;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    long long t3 = clock64();
+    double acc[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = (r == lr) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      acc[k] *= invd[k];
+#pragma unroll
+      for (int r = k + 1; r < 16; r++) acc[r] -= scratch[r * 16 + k] * acc[k];
+    }
+    long long t4 = clock64();
+    if (lane < 16) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) dinvS[i * 256 + lane * 16 + r] = acc[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+    long long t5 = clock64();
+    part[0] += t1 - t0, part[1] += t2 - t1, part[2] += t3 - t2, part[3] += t4 - t3, part[4] += t5 - t4;
+  }
+  __syncthreads();
+  double v = 0.0;
+  for (int j = lane; j < 1024; j += 64) v += dinvS[j];
+  for (int j = lane; j < 4096; j += 64) v += T[j];
+  sink[lane] = v + (bad ? 1.0 : 0.0);
+  if (lane == 0)
+    for (int p = 0; p < 5; p++) cyc[p] = part[p] / iters;
+}
+
 int main() {
   const int n = 128;
   std::mt19937_64 rng(7);
@@ -304,6 +370,10 @@ int main() {
     hipLaunchKernelGGL(k_chol16, dim3(1), dim3(64), 0, 0, dA, 64, cyc, sink);
     hipMemcpy(h, cyc, 8, hipMemcpyDeviceToHost);
     printf("Chol16 (pivot chain + row loads): %lld cycles per call\n", h[0]);
+    hipLaunchKernelGGL(k_diag16_parts, dim3(1), dim3(64), 0, 0, dA, 64, cyc, sink);
+    hipMemcpy(h, cyc, 5 * 8, hipMemcpyDeviceToHost);
+    printf("diag16 parts (cycles per call): staging %lld, Chol16 %lld, L stores + barrier %lld, inverse %lld, "
+           "inverse stores %lld\n", h[0], h[1], h[2], h[3], h[4]);
     hipLaunchKernelGGL(k_potrf8, dim3(1), dim3(512), 0, 0, d, d11, d21, d22, (const double*)nullptr, cyc);
     hipLaunchKernelGGL(k_potrf8, dim3(1), dim3(512), 0, 0, d, d11, d21, d22, (const double*)db, cyc);
     hipMemcpy(h, cyc, 16, hipMemcpyDeviceToHost);
