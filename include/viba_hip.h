@@ -458,7 +458,7 @@ int vb_set_deferred(vb_handle h, int on);
 /* device pointers: red[0] linearization cost, [1] cost-pass cost, [2..4] CostStats (numTotal of the
  * visual factors, numInvalid, numPrevInvalid), [8] max step ratio, [9] sum of squared step ratios,
  * [10] sum of step ratios, [16] twice the model cost reduction -- this handle's partials; err[0..2)
- * error bit words (max / bitwise-or reducible) */
+ * error bit words (bitwise-or reducible) */
 int vb_scalar_slots(vb_handle h, double** red, int32_t** err);
 /* what numTotal adds for this handle's non-visual factors in the cost pass (the root's, else 0) */
 int vb_small_factor_count(vb_handle h, int64_t* n);
@@ -468,6 +468,13 @@ int vb_mark_scalars(vb_handle h);
 /* copy red[0, n) (n <= 24) to the host after the mark (or after all queued work) and return the error
  * the error words encode (0 if none) */
 int vb_read_scalars(vb_handle h, double* out, int n);
+/* the two error bit words behind the last error check of this handle (vb_read_scalars, or any
+ * synchronous call); a multi-process controller ORs them over the ranks */
+int vb_error_words(vb_handle h, int32_t* out2);
+/* the code (and vb_last_error text) two error bit words encode, checked in causal order as every
+ * synchronous call does: after the words are ORed over the ranks, each rank raises the same error with
+ * the same message (the reference's XR_CHECK / throw sites, Optimizer.cpp:200-231, RollingShutterData.cpp) */
+int vb_error_from_words(vb_handle h, const int32_t* words2);
 /* vb_optimize's speculative next-iteration linearization for an external controller: *ok = 1 when its
  * spare buffers (a second tile store, ResultCache, gradient, rolling-shutter tables) are allocated */
 int vb_spec_prepare(vb_handle h, int* ok);
@@ -477,6 +484,10 @@ int vb_spec_linearize(vb_handle h, int dont_retry_failed);
 /* use = 1 (the step stayed applied at full size): the spare buffers become the handle's and the handle
  * is linearized (cost partial in red[0]); use = 0: dropped */
 int vb_spec_commit(vb_handle h, int use);
+/* out2 = [rolling-shutter rebuild ms, linearization ms] of the speculative linearization last committed
+ * (its device events; complete once the iteration that used it has read its scalars): an external
+ * controller's phase clock attributes them to that iteration, as vb_optimize's vb_phase_times does */
+int vb_spec_phase_ms(vb_handle h, double* out2);
 
 /* the HIP stream of the handle (hipStream_t), for interop with torch / RCCL */
 void* vb_stream(vb_handle h);

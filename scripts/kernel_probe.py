@@ -17,7 +17,8 @@ NAMES = {0: "potrf4 (one tile, scratch)", 1: "trsm (one tile, scratch)", 2: "fan
          13: "observation-group Gram blocks", 14: "Schur tile products", 15: "visual cost pass",
          16: "small factors' evaluation", 17: "small assembly, IMU kinds", 18: "small assembly, other kinds",
          19: "reduced-system clear", 20: "elimination beside tile products (timing probe)",
-         21: "elimination then tile products", 22: "elimination beside groups"}
+         21: "elimination then tile products", 22: "elimination beside groups",
+         23: "factorization (its streams)", 24: "factorization beside tile products (timing probe)"}
 
 
 def main():

@@ -132,3 +132,30 @@ def test_partitioned_controller_matches_single_process(world, tmp_path):
             ref = e.get_vars(kind)
             if len(ref):
                 assert rel(r[k][f"v{kind}"], ref) < 1e-7, kind
+
+
+def _words_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from visual_inertial_bundle_adjustment_amd.distributed import bits_word, word_bits
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 0: RS lookup out of range (err[0] bit 0) and a preintegration gap (err[1] bit 3); rank 1: reduced
+    # Cholesky breakdown (err[0] bit 3) and the cost pass's RS range (bit 5)
+    words = [np.array([1, 8], np.int32), np.array([8 | 32, 0], np.int32)][rank]
+    t = torch.tensor(word_bits(words), dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    np.save(os.path.join(out_dir, f"w{rank}.npy"), bits_word(t.tolist()))
+    dist.destroy_process_group()
+
+
+def test_error_words_ored_over_ranks(tmp_path):
+    """The multi-process controllers combine the ranks' error bit words by a MAX over one 0/1 per bit, i.e. a
+    bitwise OR (distributed.word_bits / bits_word): a MAX of the words themselves would keep only the
+    larger (bit 8 over bit 1), and the causal-order decode (vb_error_from_words) would then report the
+    reduced-system breakdown instead of the rolling-shutter range error a single process reports."""
+    world = 2
+    mp.spawn(_words_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        assert np.load(tmp_path / f"w{r}.npy").tolist() == [1 | 8 | 32, 8]

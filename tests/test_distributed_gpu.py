@@ -23,7 +23,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, which, its, out_dir, mode="shard", precision="fp64"):
+def _worker(rank, world, port, which, its, out_dir, mode="shard", precision="fp64", backend="gloo"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "tests")]
@@ -37,7 +37,11 @@ def _worker(rank, world, port, which, its, out_dir, mode="shard", precision="fp6
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if mode == "partition" and which == "miniB":
         os.environ["VIBA_ND_LEAF"] = "128"  # miniB is small: finer dissection so 4 ranks get subtrees
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":  # RCCL: one GPU per rank, so world 1 on this box
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     p = synth.generate(synth.config(which))
     lb, le = shard_bounds(p, world)[rank]
     e = HipEngine(imu_calib_options=p.imu_calib_options, device=0, precision=precision)
@@ -51,7 +55,9 @@ def _worker(rank, world, port, which, its, out_dir, mode="shard", precision="fp6
     opt = cls(e, ShardComm(rank, world, torch.device("cuda", 0)))
     s = opt.optimize(Settings.default(max_num_iterations=its))
     res = {"iters": s.num_iterations, "initial": s.initial_cost, "final": s.final_cost,
-           "reads": np.array(opt.reads_per_iteration), "spec": opt.spec_used}
+           "reads": np.array(opt.reads_per_iteration), "spec": opt.spec_used, "nccl": opt.c.nccl,
+           "phases": np.array([opt.phases.ms.get(k, 0.0) for k in ("rs_update_ms", "linearize_ms", "schur_ms",
+                                                                   "factor_ms", "solve_ms")])}
     if mode == "partition":
         res["part"] = np.array(e.part_info())
     for k in range(1, 8):
@@ -119,6 +125,28 @@ def _check_against_single(tmp_path, world, which, its, precision="fp64"):
                 if len(ref[f"v{kind}"]):
                     d = rel(r[k][f"v{kind}"], ref[f"v{kind}"])
                     assert d < var_tol, (engine, kind, d)
+
+
+@pytest.mark.parametrize("mode", ["partition", "shard"])
+def test_rccl_world_one(mode, tmp_path):
+    """Both multi-process controllers through the nccl backend (RCCL) with one rank, the most this one-GPU
+    box allows (RCCL refuses two ranks on one device): device tensors on the wire, the in-place all-reduce
+    of the scalar slots on the engine stream, the bitwise OR of the error words, and (partitioned, world 1:
+    rank 0 factors both subtrees below the top separator and that separator as the ROOT) the ROOT tile /
+    row reduce, the ROOT x broadcast and the x all-reduce.  Against vb_optimize and the oracle on miniB;
+    the phase clock reports the speculatively queued linearization (Optimizer.cpp:200-206's elimination
+    split into the protocol's steps)."""
+    world, which, its = 1, "miniB", 8
+    mp.spawn(_worker, args=(world, _free_port(), which, its, str(tmp_path), mode, "fp64", "nccl"), nprocs=world,
+             join=True)
+    _check_against_single(tmp_path, world, which, its)
+    r = np.load(tmp_path / "rank0.npz")
+    assert bool(r["nccl"])
+    rs_ms, lin_ms, schur_ms, factor_ms, solve_ms = r["phases"]
+    assert lin_ms > 0 and schur_ms > 0 and factor_ms > 0 and solve_ms > 0, r["phases"]
+    if mode == "partition":
+        own, root_cols, pairs_local, pairs_root, root_tiles = r["part"]
+        assert own > 0 and root_cols > 0 and pairs_root > 0 and root_tiles > 0, r["part"]
 
 
 @pytest.mark.parametrize("which,its", [("miniB", 8)])

@@ -15,7 +15,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.environ.get("VIBA_LIB_DIR", os.path.join(HERE, "lib"))
-HIP_SOURCES = ["factors.hip", "solver.hip", "rs.hip", "preint.hip", "pcg.hip", "selinv.hip", "lowprec.hip", "api.hip"]
+HIP_SOURCES = ["factors.hip", "schur.hip", "solver.hip", "rs.hip", "preint.hip", "pcg.hip", "selinv.hip", "lowprec.hip", "api.hip",
+               "finalize.hip", "covariances.hip", "multi.hip", "tools.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("VIBA_OFFLOAD_ARCH", "gfx950")
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",

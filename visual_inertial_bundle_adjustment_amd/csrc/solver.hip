@@ -1,825 +1,16 @@
-// Sparse direct solve of the damped Gauss-Newton system (gfx950), replacing BaSpaCho's sparse
-// elimination of the point range + supernodal Cholesky (Optimizer.cpp:200-231).
-//
-//   landmark_obs_kernel   one wave per landmark: V = sum Jp^T Jp (damped, Optimizer.cpp:136-146), g_p, the
-//   (_wg, landmark_kernel) W panel in LDS, 3x3 Cholesky, z = L^-1 g_p, Y = L^-1 W
-//   obs_group_kernel      direct visual terms J~^T J~ per (rig, camera) group on fp64 MFMA
-//   schur_run4_kernel     S_IJ -= sum_l Y_lI^T Y_lJ by target tile, compact runs, register operands
+// Sparse direct solve of the damped, Schur-reduced system (gfx950), replacing BaSpaCho's supernodal
+// Cholesky (Optimizer.cpp:200-231):
 //   fanin_kernel          level-scheduled tile Cholesky: A_IJ -= sum_K L_IK L_JK^T (v_mfma_f64_16x16x4)
 //   potrf4_kernel,        64x64 diagonal factor (+ 16x16 block inverses), off-diagonal L_IJ = A_IJ L_JJ^-T;
 //   trsm_kernel,          the forward solve rides these launches
-//   potrf_trsm_kernel
+//   potrf_trsm_kernel, snpotrf8 / snpotrf_trsm8 / sntrsm (two-column supernodes)
 //   fwd/bwd_fanout_kernel persistent fan-out triangular solves; backsub_kernel x_p = L^-T (z - Y x_c)
-#include "device_math.hpp"
-#include "engine.hpp"
+//   boxplus_*             applyStep
+#include "kernel_common.hpp"
 #include <algorithm>
 #include <string>
 
 namespace viba {
-using namespace dev;
-
-constexpr int TS = 64;  // tile size (rows/cols of a dense reduced-system tile)
-typedef double double4_t __attribute__((ext_vector_type(4)));
-typedef float float4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ double4_t mfma64(double a, double b, double4_t c) {
-  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-}
-// Hessian products of the Schur complement (observation-group Gram blocks, landmark tile products) in
-// the record precision: fp64 MFMA, or v_mfma_f32_16x16x4_f32 in the VIBA_MIXED build.  The two differ
-// in their C/D map: f64 D row = (lane >> 4) + 4 r, f32 D row = 4 (lane >> 4) + r (column lane & 15 in
-// both; A/B maps identical), so accumulator register r of lane l sits at D row kAccL4 (l >> 4) + kAccR r.
-#if VIBA_MIXED
-typedef float4_t hacc4_t;
-__device__ __forceinline__ hacc4_t mfma_h(float a, float b, hacc4_t c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-constexpr int kAccL4 = 4, kAccR = 1;
-#else
-typedef double4_t hacc4_t;
-__device__ __forceinline__ hacc4_t mfma_h(double a, double b, hacc4_t c) { return mfma64(a, b, c); }
-constexpr int kAccL4 = 1, kAccR = 4;
-#endif
-
-__device__ inline int rv_dim(const Dev& d, int r) { return d.rvDim[r]; }
-
-// ------------------------------------------------------------------ landmark elimination
-// One wave per landmark (Optimizer.cpp:136-146 restricted to the point block, then the point part
-// of the sparse elimination, Optimizer.cpp:200-231):
-//   lanes over the landmark's observations: V = sum Jp^T Jp, g = sum Jp^T e (record planes 0..7,
-//   64 B of each 576 B record), wave reduction; every lane then holds the damped 3 x 3 Cholesky L
-//   mode 0: lanes over the Y panel columns: W(:, c) = sum over the observation slots of the column's
-//   block of Jp^T J_x(:, j), Y(:, c) = L^-1 W(:, c) (no atomics: each column has one owner)
-//   mode 1: gradient only into gpNew
-// all-lane sum: within each 16-lane row by DPP (quad swaps, then row rotations by 4 and 8), the four
-// row sums by v_readlane -- VALU-local, no LDS-crossbar ds_bpermute round trips
-template <int kCtrl>
-__device__ __forceinline__ double dpp_f64(double x) {
-  const int2 w = __builtin_bit_cast(int2, x);
-  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_update_dpp(0, w.x, kCtrl, 0xf, 0xf, false),
-                                              __builtin_amdgcn_update_dpp(0, w.y, kCtrl, 0xf, 0xf, false)));
-}
-__device__ __forceinline__ double lane_f64(double x, int l) {
-  const int2 w = __builtin_bit_cast(int2, x);
-  return __builtin_bit_cast(double, make_int2(__builtin_amdgcn_readlane(w.x, l), __builtin_amdgcn_readlane(w.y, l)));
-}
-__device__ __forceinline__ double wave_sum(double x) {
-  x += dpp_f64<0xB1>(x);   // quad_perm [1, 0, 3, 2]
-  x += dpp_f64<0x4E>(x);   // quad_perm [2, 3, 0, 1]
-  x += dpp_f64<0x124>(x);  // row_ror:4
-  x += dpp_f64<0x128>(x);  // row_ror:8
-  return (lane_f64(x, 0) + lane_f64(x, 16)) + (lane_f64(x, 32) + lane_f64(x, 48));
-}
-
-__device__ __forceinline__ void landmark_eliminate(const Dev& d, double lambda, int mode, int64_t l) {
-  const int lane = threadIdx.x & 63;
-  const rec_t* Jt = d.Jt;
-  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
-  double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  for (int64_t o = o0 + lane; o < o1; o += 64) {
-    const rec_t* r = Jt + o * kJA;  // planes 0..7 live in region A
-    const double e0 = r[kJe], e1 = r[kJe + 1];
-    const double a0 = r[kJpt + 0], a1 = r[kJpt + 1], a2 = r[kJpt + 2];
-    const double b0 = r[kJpt + 3], b1 = r[kJpt + 4], b2 = r[kJpt + 5];
-    g0 += a0 * e0 + b0 * e1, g1 += a1 * e0 + b1 * e1, g2 += a2 * e0 + b2 * e1;
-    if (mode == 0) {
-      v00 += a0 * a0 + b0 * b0, v10 += a1 * a0 + b1 * b0, v20 += a2 * a0 + b2 * b0;
-      v11 += a1 * a1 + b1 * b1, v21 += a2 * a1 + b2 * b1, v22 += a2 * a2 + b2 * b2;
-    }
-  }
-  g0 = wave_sum(g0), g1 = wave_sum(g1), g2 = wave_sum(g2);
-  if (mode == 1) {
-    if (lane == 0) d.gpNew[l * 3] = g0, d.gpNew[l * 3 + 1] = g1, d.gpNew[l * 3 + 2] = g2;
-    return;
-  }
-  v00 = wave_sum(v00), v10 = wave_sum(v10), v20 = wave_sum(v20);
-  v11 = wave_sum(v11), v21 = wave_sum(v21), v22 = wave_sum(v22);
-  v00 = v00 * (1.0 + lambda) + lambda;
-  v11 = v11 * (1.0 + lambda) + lambda;
-  v22 = v22 * (1.0 + lambda) + lambda;
-  const double l00 = sqrt(v00);
-  const double l10 = v10 / l00, l20 = v20 / l00;
-  const double d11 = v11 - l10 * l10;
-  const double l11 = sqrt(d11);
-  const double l21 = (v21 - l20 * l10) / l11;
-  const double d22 = v22 - l20 * l20 - l21 * l21;
-  const double l22 = sqrt(d22);
-  if (lane == 0) {
-    if (!(v00 > 0) || !(d11 > 0) || !(d22 > 0)) atomicOr(d.err, 2);
-    double* L = d.Vchol + l * 6;
-    L[0] = l00, L[1] = l10, L[2] = l20, L[3] = l11, L[4] = l21, L[5] = l22;
-    const double z0 = g0 / l00, z1 = (g1 - l10 * z0) / l11, z2 = (g2 - l20 * z0 - l21 * z1) / l22;
-    d.z[l * 3] = z0, d.z[l * 3 + 1] = z1, d.z[l * 3 + 2] = z2;
-    d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
-  }
-  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
-  const int64_t yq = d.nYcol;
-  for (int64_t c = lane; c < ncol; c += 64) {
-    const int32_t b = d.pcBlk[cb + c];
-    const int j = (int)(c - d.blkCol[b]);
-    double w0 = 0, w1 = 0, w2 = 0;
-    for (int64_t e = d.bxStart[b]; e < d.bxStart[b + 1]; e++) {
-      const int32_t ent = d.bxEnt[e];
-      const int s = ent & 3;
-      const int64_t o = ent >> 2;
-      const rec_t* r = Jt + o * kJA;
-      const rec_t* x = jt_plane(Jt, d.nObsPad, o, slotPlane(s) + j);
-      const double x0 = x[0], x1 = x[slotStride(s)];
-      w0 += r[kJpt + 0] * x0 + r[kJpt + 3] * x1;
-      w1 += r[kJpt + 1] * x0 + r[kJpt + 4] * x1;
-      w2 += r[kJpt + 2] * x0 + r[kJpt + 5] * x1;
-    }
-    const double y0 = w0 / l00;
-    const double y1 = (w1 - l10 * y0) / l11;
-    const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
-    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
-  }
-}
-__global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int mode, int64_t lo, int64_t hi) {
-  const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (l >= hi) return;
-  landmark_eliminate(d, lambda, mode, l);
-}
-
-// Landmark elimination by observation (mode 0, default).  One wave per landmark; each half-wave takes
-// one of the landmark's observations at a time and its 32 lanes the observation's 32 slot columns
-// [pose 6 | extr 6 | intr 17 | vel 3] (record planes 8..71, read once and coalesced, with the point
-// Jacobian and residual of planes 0..7): the column's contribution Jp^T J_x(:, j) goes into the
-// landmark's W panel in LDS at panel column obCol + j with LDS atomics (both halves may hit a shared
-// calibration block), and lane 0 of the half accumulates V and g.  Then the damped 3 x 3 Cholesky,
-// z, and Y = L^-1 W over the panel columns.  No per-block observation lists: every record is read
-// once.  Two launches by panel width (api.hip lmList): landmarks with up to kLmSmallCols columns one
-// per wave with a 24 KB workgroup (6 per CU); the wider ones (long tracks) one per workgroup,
-// landmark_obs_wg_kernel, whose panel is per workgroup.  Measured on config C: 1.04 + 0.72 ms against
-// 2.63 for the per-column landmark_kernel; one 48 KB per-wave class for all ran at 2.9 ms and the
-// per-workgroup kernel for all at 2.1 (occupancy vs. barriers).
-// one observation's share of a half-wave (lane jj = slot column j of slot s): the point Jacobian
-// (broadcast), the lane's two slot-column planes, the packed panel column / block width of the slot, and
-// (lane jj == 0) the residual; observations past o1 load observation o0 and add nothing
-struct ObsCols {
-  double a[6], x0, x1, e0, e1;
-  int32_t pc;
-};
-__device__ __forceinline__ void obs_cols_load(const Dev& d, const rec_t* Jt, int64_t o, int64_t o1, int64_t o0, int pl,
-                                              int st, int s, int jj, ObsCols& q) {
-  const bool valid = o < o1;
-  if (!valid) o = o0;
-  const rec_t* r = Jt + o * kJA;
-#pragma unroll
-  for (int k = 0; k < 6; k++) q.a[k] = r[kJpt + k];
-  const rec_t* x = jt_plane(Jt, d.nObsPad, o, pl);
-  q.x0 = x[0], q.x1 = x[st];
-  q.pc = valid ? d.obCol[o * 4 + s] : -1;
-  q.e0 = jj == 0 ? (double)r[kJe] : 0.0, q.e1 = jj == 0 ? (double)r[kJe + 1] : 0.0;
-}
-// W(:, column) += Jp^T J_x(:, j) for the lane's slot column (LDS atomics: both half-waves may hit a shared
-// calibration block)
-__device__ __forceinline__ void obs_cols_add(const ObsCols& q, int j, double* W) {
-  if (q.pc >= 0 && j < (q.pc & 31)) {
-    const int c = (q.pc >> 5) + j;
-    atomicAdd(&W[3 * c + 0], q.a[0] * q.x0 + q.a[3] * q.x1);
-    atomicAdd(&W[3 * c + 1], q.a[1] * q.x0 + q.a[4] * q.x1);
-    atomicAdd(&W[3 * c + 2], q.a[2] * q.x0 + q.a[5] * q.x1);
-  }
-}
-
-constexpr int kLmBigCols = 2048;  // 3 x 2048 doubles = 48 KB of dynamic LDS per workgroup; wider: per-column path
-
-__global__ void __launch_bounds__(256) landmark_obs_kernel(Dev d, double lambda, int64_t first, int64_t n, int cap) {
-  extern __shared__ double Wl[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t li = (int64_t)blockIdx.x * 4 + wave;
-  if (li >= n) return;
-  const int64_t l = d.lmList[first + li];
-  const rec_t* Jt = d.Jt;
-  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
-  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  double* W = Wl + wave * 3 * cap;  // cap: panel columns per wave of this launch
-  for (int i = lane; i < 3 * ncol; i += 64) W[i] = 0.0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int h = lane >> 5, jj = lane & 31;
-  const int s = jj < 6 ? 0 : jj < 12 ? 1 : jj < 29 ? 2 : 3;
-  const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
-  const int pl = slotPlane(s) + j, st = slotStride(s);
-  double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  // software-pipelined by one observation: the next observation's record reads are in flight while
-  // this one's products go into the panel
-  ObsCols q, qn;
-  obs_cols_load(d, Jt, o0 + h, o1, o0, pl, st, s, jj, q);
-  for (int64_t o = o0 + h; o < o1; o += 2) {
-    obs_cols_load(d, Jt, o + 2, o1, o0, pl, st, s, jj, qn);
-    if (jj == 0) {
-      g0 += q.a[0] * q.e0 + q.a[3] * q.e1, g1 += q.a[1] * q.e0 + q.a[4] * q.e1, g2 += q.a[2] * q.e0 + q.a[5] * q.e1;
-      v00 += q.a[0] * q.a[0] + q.a[3] * q.a[3], v10 += q.a[1] * q.a[0] + q.a[4] * q.a[3];
-      v20 += q.a[2] * q.a[0] + q.a[5] * q.a[3], v11 += q.a[1] * q.a[1] + q.a[4] * q.a[4];
-      v21 += q.a[2] * q.a[1] + q.a[5] * q.a[4], v22 += q.a[2] * q.a[2] + q.a[5] * q.a[5];
-    }
-    obs_cols_add(q, j, W);
-    q = qn;
-  }
-  g0 = wave_sum(g0), g1 = wave_sum(g1), g2 = wave_sum(g2);
-  v00 = wave_sum(v00), v10 = wave_sum(v10), v20 = wave_sum(v20);
-  v11 = wave_sum(v11), v21 = wave_sum(v21), v22 = wave_sum(v22);
-  v00 = v00 * (1.0 + lambda) + lambda;
-  v11 = v11 * (1.0 + lambda) + lambda;
-  v22 = v22 * (1.0 + lambda) + lambda;
-  const double l00 = sqrt(v00);
-  const double l10 = v10 / l00, l20 = v20 / l00;
-  const double d11 = v11 - l10 * l10;
-  const double l11 = sqrt(d11);
-  const double l21 = (v21 - l20 * l10) / l11;
-  const double d22 = v22 - l20 * l20 - l21 * l21;
-  const double l22 = sqrt(d22);
-  if (lane == 0) {
-    if (!(v00 > 0) || !(d11 > 0) || !(d22 > 0)) atomicOr(d.err, 2);
-    double* L = d.Vchol + l * 6;
-    L[0] = l00, L[1] = l10, L[2] = l20, L[3] = l11, L[4] = l21, L[5] = l22;
-    const double z0 = g0 / l00, z1 = (g1 - l10 * z0) / l11, z2 = (g2 - l20 * z0 - l21 * z1) / l22;
-    d.z[l * 3] = z0, d.z[l * 3 + 1] = z1, d.z[l * 3 + 2] = z2;
-    d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
-  const int64_t yq = d.nYcol;
-  for (int64_t c = lane; c < ncol; c += 64) {
-    const double y0 = W[3 * c] / l00;
-    const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
-    const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
-    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
-  }
-}
-
-// the same with one workgroup per landmark (its 8 half-waves share the observations, the W panel is
-// one per workgroup): for the wide class, whose per-wave panels would cap the occupancy
-__global__ void __launch_bounds__(256) landmark_obs_wg_kernel(Dev d, double lambda, int64_t first, int cap) {
-  extern __shared__ double W[];
-  __shared__ double part[4][9];
-  __shared__ double Ls[6];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t l = d.lmList[first + blockIdx.x];
-  const rec_t* Jt = d.Jt;
-  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
-  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  for (int i = tid; i < 3 * ncol; i += 256) W[i] = 0.0;
-  __syncthreads();
-  const int h = tid >> 5, jj = lane & 31;
-  const int s = jj < 6 ? 0 : jj < 12 ? 1 : jj < 29 ? 2 : 3;
-  const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
-  const int pl = slotPlane(s) + j, st = slotStride(s);
-  double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // v00 v10 v20 v11 v21 v22 g0 g1 g2
-  ObsCols q, qn;
-  obs_cols_load(d, Jt, o0 + h, o1, o0, pl, st, s, jj, q);
-  for (int64_t o = o0 + h; o < o1; o += 8) {
-    obs_cols_load(d, Jt, o + 8, o1, o0, pl, st, s, jj, qn);
-    if (jj == 0) {
-      v[6] += q.a[0] * q.e0 + q.a[3] * q.e1, v[7] += q.a[1] * q.e0 + q.a[4] * q.e1, v[8] += q.a[2] * q.e0 + q.a[5] * q.e1;
-      v[0] += q.a[0] * q.a[0] + q.a[3] * q.a[3], v[1] += q.a[1] * q.a[0] + q.a[4] * q.a[3];
-      v[2] += q.a[2] * q.a[0] + q.a[5] * q.a[3], v[3] += q.a[1] * q.a[1] + q.a[4] * q.a[4];
-      v[4] += q.a[2] * q.a[1] + q.a[5] * q.a[4], v[5] += q.a[2] * q.a[2] + q.a[5] * q.a[5];
-    }
-    obs_cols_add(q, j, W);
-    q = qn;
-  }
-#pragma unroll
-  for (int k = 0; k < 9; k++) v[k] = wave_sum(v[k]);
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < 9; k++) part[wave][k] = v[k];
-  __syncthreads();
-  if (tid == 0) {
-#pragma unroll
-    for (int k = 0; k < 9; k++) v[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
-    const double v00 = v[0] * (1.0 + lambda) + lambda, v11 = v[3] * (1.0 + lambda) + lambda;
-    const double v22 = v[5] * (1.0 + lambda) + lambda;
-    const double l00 = sqrt(v00);
-    const double l10 = v[1] / l00, l20 = v[2] / l00;
-    const double d11 = v11 - l10 * l10;
-    const double l11 = sqrt(d11);
-    const double l21 = (v[4] - l20 * l10) / l11;
-    const double d22 = v22 - l20 * l20 - l21 * l21;
-    const double l22 = sqrt(d22);
-    if (!(v00 > 0) || !(d11 > 0) || !(d22 > 0)) atomicOr(d.err, 2);
-    double* L = d.Vchol + l * 6;
-    L[0] = Ls[0] = l00, L[1] = Ls[1] = l10, L[2] = Ls[2] = l20, L[3] = Ls[3] = l11, L[4] = Ls[4] = l21;
-    L[5] = Ls[5] = l22;
-    const double z0 = v[6] / l00, z1 = (v[7] - l10 * z0) / l11, z2 = (v[8] - l20 * z0 - l21 * z1) / l22;
-    d.z[l * 3] = z0, d.z[l * 3 + 1] = z1, d.z[l * 3 + 2] = z2;
-    d.gp[l * 3] = v[6], d.gp[l * 3 + 1] = v[7], d.gp[l * 3 + 2] = v[8];
-  }
-  __syncthreads();
-  const double l00 = Ls[0], l10 = Ls[1], l20 = Ls[2], l11 = Ls[3], l21 = Ls[4], l22 = Ls[5];
-  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
-  const int64_t yq = d.nYcol;
-  for (int64_t c = tid; c < ncol; c += 256) {
-    const double y0 = W[3 * c] / l00;
-    const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
-    const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
-    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
-  }
-}
-
-// the wide class when its panels exceed kLmBigCols: landmark_kernel's per-column path
-__global__ void __launch_bounds__(256) landmark_list_kernel(Dev d, double lambda, int64_t first, int64_t n) {
-  const int64_t li = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (li >= n) return;
-  landmark_eliminate(d, lambda, 0, d.lmList[first + li]);
-}
-
-// mode 2: zNew = L^-1 gpNew, one thread per landmark
-__global__ void __launch_bounds__(256) landmark_z_kernel(Dev d, int64_t lo, int64_t hi) {
-  const int64_t l = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= hi) return;
-  const double* L = d.Vchol + l * 6;
-  const double* g = d.gpNew + l * 3;
-  const double z0 = g[0] / L[0];
-  const double z1 = (g[1] - L[1] * z0) / L[3];
-  const double z2 = (g[2] - L[2] * z0 - L[4] * z1) / L[5];
-  d.zNew[l * 3] = z0, d.zNew[l * 3 + 1] = z1, d.zNew[l * 3 + 2] = z2;
-}
-
-// ------------------------------------------------------------------ Schur column assembly
-
-__device__ inline double* tile_ptr(const Dev& d, int64_t r, int64_t c) {
-  const int32_t ti = d.tileIdx[(r / TS) * d.nT + (c / TS)];
-  if (ti < 0) return nullptr;
-  return d.tiles + (int64_t)ti * TS * TS + (c % TS) * TS + (r % TS);
-}
-
-// XCD-aware block id: blocks b and b + 8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch), so
-// hand each XCD a contiguous range of work (bijective for any grid size)
-__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nb) {
-  const int64_t q = nb / 8, r = nb % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// Schur assembly by target tile (api.hip builds the work list; engine.hpp TileWork / TileEnt), in
-// compact runs with register operands.  api.hip sorts every tile's landmark entries by their (row mask
-// in tile I, row mask in tile J): a work item is a sequence of RUNS of landmarks touching exactly the
-// same tile rows.  Within a run the c-th panel column of a landmark inside tile I is compact column c
-// (its rows ascend with its columns), K is dense (3 rows per landmark), and the compact nJ x nI product
-// needs only ceil(nJ / 16) x ceil(nI / 16) blocks of v_mfma_f64_16x16x4_f64 per 4 K rows: 34M MFMAs
-// on config C against 70M for the tile-coordinate form (16-row masks, one padded k-step per landmark;
-// that form and the LDS-image forms are in the history).  No images and no barriers: a task is (run, chunk of <= kCh landmarks, compact
-// block row a of the J side); a wave takes every fourth task of its item and accumulates the nI-wide
-// block row over the chunk's dense K (3 rows per landmark), its operands gathered straight from the Y
-// panel (lane l: compact column 16 a + (l & 15) / 16 b + (l & 15), K row 4 ks + (l >> 4)), the next
-// k-step's loads issued before the current MFMAs.  At the end of the task the block row is added into
-// the item's LDS tile accumulator with LDS atomics (tasks of different waves overlap), through
-// wave-private compact -> tile row maps.
-constexpr int kCh = kSchurCh;  // landmarks per task
-constexpr int kTR = kSchurTR;  // compact block rows per task (1 or 2)
-
-// C -= acc of one task through the run's compact -> tile row maps: every map entry of the task read up
-// front (one LDS wait), the adds predicated
-template <int NBI, int NR, bool DIAG>
-__device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], int a0, int l4, int l15,
-                                               const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
-  int colT[NBI];
-  int rowT[NR][4];
-#pragma unroll
-  for (int b = 0; b < NBI; b++) colT[b] = posI[min(16 * b + l15, TS - 1)];
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) rowT[i][q] = posJ[min(16 * (a0 + i) + kAccL4 * l4 + kAccR * q, TS - 1)];
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const bool mv = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q < nJ;
-#pragma unroll
-      for (int b = 0; b < NBI; b++)
-        if ((!DIAG || a0 + i <= b) && mv && 16 * b + l15 < nI) atomicAdd(C + rowT[i][q] * TS + colT[b], -(double)acc[i][b][q]);
-    }
-}
-
-// rhs -= Y^T z over a chunk's landmarks (diagonal tiles), lanes over the run's compact I columns, four
-// landmarks' loads in flight per step
-__device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2], const TileEnt* ents, int c0, int nl,
-                                          int lane, const uint8_t* posI, double* rq) {
-  const int64_t pq = d.nYcol;
-  double racc = 0.0;
-  int e = c0;
-  for (; e + 4 <= c0 + nl; e += 4) {
-    double y[4][3], z[4][3];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const rec_t* yp = d.Y + (int64_t)ecol[e + u][0] + lane;
-      const double* zz = d.z + 3 * (int64_t)ents[e + u].lm;
-#pragma unroll
-      for (int q = 0; q < 3; q++) y[u][q] = (double)yp[q * pq], z[u][q] = zz[q];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) racc += y[u][0] * z[u][0] + y[u][1] * z[u][1] + y[u][2] * z[u][2];
-  }
-  for (; e < c0 + nl; e++) {
-    const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
-    const double* zz = d.z + 3 * (int64_t)ents[e].lm;
-    racc += (double)y[0] * zz[0] + (double)y[pq] * zz[1] + (double)y[2 * pq] * zz[2];
-  }
-  atomicAdd(&rq[posI[lane]], -racc);
-}
-
-// One task's K loop: acc[i][b] += A_i^T B_b over the dense K rows (3 per landmark) of landmarks
-// c0 .. c0 + rows / 3, A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block
-// b < NBI.  Lane (l4, l15) at k-step ks takes K row kr = 4 ks + l4, i.e. plane q = kr % 3 of landmark
-// c0 + kr / 3 (advanced incrementally), and gathers its NR + NBI operands at fixed offsets 16 i / 16 b
-// from the landmark's first panel column in tile J / I.  Columns past nJ / nI load neighbouring
-// panel data into accumulator rows / columns that are never stored; K rows past `rows` read the zero
-// pad.  The next step's gathers are issued before the current step's MFMAs.
-template <int NBI, int NR, bool DIAG>
-__device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0, int rows, int a0, int l4, int l15,
-                                           const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
-  hacc4_t acc[NR][NBI];
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int b = 0; b < NBI; b++) acc[i][b] = hacc4_t{0, 0, 0, 0};
-  const int nks = (rows + 3) >> 2;
-  const int64_t pq = d.nYcol;
-  const rec_t* Y = d.Y;
-  const rec_t* zp = d.yZero + l15;
-  int kr = l4, e = c0 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
-  auto ld = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
-    const bool kv = kr < rows;
-    const uint2 c = ec[kv ? e : c0];
-    const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
-    const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
-    const rec_t* pI = kv ? base + c.x : zp;
-#pragma unroll
-    for (int i = 0; i < NR; i++) av[i] = pJ[16 * i];
-#pragma unroll
-    for (int b = 0; b < NBI; b++) bv[b] = pI[16 * b];
-    kr += 4, e += 1, q += 1;
-    if (q == 3) q = 0, e += 1;
-  };
-  auto mm = [&](const rec_t (&av)[NR], const rec_t (&bv)[NBI]) {
-#pragma unroll
-    for (int i = 0; i < NR; i++)
-#pragma unroll
-      for (int b = 0; b < NBI; b++)
-        if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
-  };
-  rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
-  ld(a0v, b0v);
-  for (int ks = 0; ks < nks; ks += 2) {
-    if (ks + 1 < nks) ld(a1v, b1v);
-    mm(a0v, b0v);
-    if (ks + 2 < nks) ld(a0v, b0v);
-    if (ks + 1 < nks) mm(a1v, b1v);
-  }
-  // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
-  schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
-}
-
-// Schur tile products, one workgroup per work item (TileWork: a target tile and <= 256 of its landmark
-// entries).  The item's runs (masks) and its tasks come precomputed from finalize (api.hip), the
-// tasks dealt to the waves longest-first (TileWork::wOff), so the kernel has no run scan and the waves
-// are balanced at the final barrier.  Four waves per SIMD (the k-loops are bound by gather latency).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run4_kernel(Dev d, double lambda) {
-  __shared__ double C[TS * TS];
-  __shared__ uint32_t ecol[256][2];
-  __shared__ uint64_t rmask[256][2];
-  __shared__ uint8_t posW[4][2][TS];
-  __shared__ double rq[TS];
-  const int64_t w = xcd_block(blockIdx.x, gridDim.x);
-  const TileWork* wp = d.tileWorks + w;  // fields read in place (a by-value copy went to scratch:
-  const TileWork wk = *wp;                 // wOff is indexed by the wave)
-  const bool diag = wk.I == wk.J;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int cnt = wk.count;
-  const TileEnt* ents = d.tileEnts + wk.start;
-  if (tid < cnt) ecol[tid][0] = ents[tid].colI, ecol[tid][1] = ents[tid].colJ;
-  if (tid < wk.nRuns) {
-    const uint64_t* rm = d.schurRuns + 2 * ((int64_t)wk.runFirst + tid);
-    rmask[tid][0] = rm[0], rmask[tid][1] = rm[1];
-  }
-  for (int i = tid; i < TS * TS; i += 256) C[i] = 0.0;
-  if (tid < TS) rq[tid] = 0.0;
-  __syncthreads();
-  uint8_t* posI = posW[wave][0];
-  uint8_t* posJ = posW[wave][1];
-  const uint2* ec2 = reinterpret_cast<const uint2*>(&ecol[0][0]);
-  const uint32_t* tasks = d.schurTasks + wk.taskFirst;
-  const int tBeg = wp->wOff[wave], tEnd = wp->wOff[wave + 1];
-  int cur = -1;
-  for (int t = tBeg; t < tEnd; t++) {
-    const uint32_t code = __builtin_amdgcn_readfirstlane(tasks[t]);
-    const int r = code & 255, c0 = (code >> 8) & 255, nl = (code >> 16) & 63, a0 = (code >> 22) & 3;
-    const uint64_t mI = uniform64(rmask[r][0]), mJ = uniform64(rmask[r][1]);
-    const int nI = __popcll(mI), nJ = __popcll(mJ);
-    const int nbI = (nI + 15) >> 4, nbJ = (nJ + 15) >> 4;
-    if (r != cur) {  // the run's compact -> tile row maps (wave-private)
-      __builtin_amdgcn_wave_barrier();  // the previous run's readers are done
-      if ((mI >> lane) & 1) posI[__popcll(mI & ((1ull << lane) - 1))] = (uint8_t)lane;
-      if ((mJ >> lane) & 1) posJ[__popcll(mJ & ((1ull << lane) - 1))] = (uint8_t)lane;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      cur = r;
-    }
-    const int rows = 3 * nl;
-    const int nr = min(kTR, nbJ - a0);
-    const int sel = ((nbI - 1) * 2 + (nr - 1)) * 2 + (diag ? 1 : 0);
-    // one specialised task (k-loop + epilogue) per (I-side blocks, J-side rows of this task, diagonal
-    // tile): no per-MFMA predicates, gathers at immediate offsets from per-step base pointers
-    switch (sel) {
-#define VIBA_SCHUR_CASE(NBI, NR)                                                                      \
-  case ((NBI - 1) * 2 + (NR - 1)) * 2:                                                                \
-    schur_task<NBI, NR, false>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                 \
-    break;                                                                                            \
-  case ((NBI - 1) * 2 + (NR - 1)) * 2 + 1:                                                            \
-    schur_task<NBI, NR, true>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                  \
-    break;
-      VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(2, 2)
-      VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 1) VIBA_SCHUR_CASE(4, 2)
-#undef VIBA_SCHUR_CASE
-      default: break;
-    }
-    if (diag && a0 == 0 && lane < nI) schur_rhs(d, ecol, ents, c0, nl, lane, posI, rq);
-  }
-  __syncthreads();
-  double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-  if (wk.kind == 1) {
-    for (int i = tid; i < TS * TS; i += 256)
-      if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
-  } else if (wk.kind == 2) {  // the only writer of the tile (left out of the clear)
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] = C[i];
-  } else {
-    for (int i = tid; i < TS * TS; i += 256) Ct[i] += C[i];
-  }
-  if (diag && tid < TS) {
-    const int64_t row = (int64_t)wk.I * TS + tid;
-    if (row < d.nRed && rq[tid] != 0.0) atomicAdd(d.rhs + row, rq[tid]);
-  }
-}
-
-// Direct visual terms by observation group (observations sharing their reduced blocks: one rig, one
-// camera).  Per group: H = sum_o J~_o^T J~_o over the 32 columns [pose 6 | extr 6 | intr <= 17 |
-// vel 3] and g = sum_o J~_o^T e~_o, on v_mfma_f64_16x16x4_f64 (K = the group's residual rows, 4 per
-// k-step = 2 observations; the 4 waves split K and reduce through LDS).  Lane l owns the columns
-// l & 15 and 16 + (l & 15); an accumulator D[m][n] (lane: n = l & 15, rows m = (l >> 4) + 4 r) is the
-// Gram block directly.  mode 0: H (diagonal damped by (1 + lambda)) into the tiles, g into gRed;
-// mode 1: g only into gRedNew (gradient pass of the bad-step path).
-constexpr int kGrpBase[4] = {0, 6, 12, 29};
-
-__device__ __forceinline__ int grp_col_row(const Dev& d, const int32_t* red, int c, int& plane, int& stride) {
-  const int s = c < 6 ? 0 : c < 12 ? 1 : c < 29 ? 2 : 3;
-  const int j = c - kGrpBase[s];
-  const int32_t X = red[s];
-  plane = slotPlane(s) + j, stride = slotStride(s);
-  if (X < 0 || j >= d.rvDim[X]) return -1;
-  return (int)(d.rvOff[X] + j);
-}
-
-// the end of a group: the 4 waves' accumulators reduced through LDS (`red`: 4 x 64 x 14 doubles, free on
-// entry), g into gRed / gRedNew (mode 1), H (diagonal damped by (1 + lambda)) scattered into the tiles
-__device__ __forceinline__ void group_finish(const Dev& d, double lambda, int mode, int row0, int row1, const hacc4_t& a00,
-                                             const hacc4_t& a10, const hacc4_t& a11, double g0, double g1, double* red) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l15 = lane & 15, l4 = lane >> 4;
-  // reduce the 4 waves (and, for g, the 4 lane groups) through LDS
-  double* mine = red + (wave * 64 + lane) * 14;
-#pragma unroll
-  for (int k = 0; k < 4; k++) mine[k] = a00[k], mine[4 + k] = a10[k], mine[8 + k] = a11[k];
-  mine[12] = g0, mine[13] = g1;
-  __syncthreads();
-  if (wave != 0) return;
-  double t[14];
-#pragma unroll
-  for (int k = 0; k < 14; k++) t[k] = red[lane * 14 + k] + red[(64 + lane) * 14 + k] + red[(128 + lane) * 14 + k] + red[(192 + lane) * 14 + k];
-  // g: lanes l15 of the 4 lane groups hold partial sums of the same columns
-  double gc0 = t[12], gc1 = t[13];
-#pragma unroll
-  for (int off = 16; off < 64; off += 16) {
-    gc0 += __shfl(t[12], (lane + off) & 63, 64);
-    gc1 += __shfl(t[13], (lane + off) & 63, 64);
-  }
-  double* gOut = mode == 0 ? d.gRed : d.gRedNew;
-  if (l4 == 0) {
-    if (row0 >= 0 && gc0 != 0.0) atomicAdd(gOut + row0, gc0);
-    if (row1 >= 0 && gc1 != 0.0) atomicAdd(gOut + row1, gc1);
-  }
-  if (mode != 0) return;
-  // H (32 x 32, symmetric) into LDS over the reduction buffer (this wave has read it): D[m][n],
-  // m = kAccL4 l4 + kAccR k (+16), n = l15 (+16); the cross block also mirrored
-  double* H = red;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int m = kAccL4 * l4 + kAccR * k;
-    H[m * 32 + l15] = t[k];
-    H[(16 + m) * 32 + 16 + l15] = t[8 + k];
-    H[(16 + m) * 32 + l15] = t[4 + k], H[l15 * 32 + 16 + m] = t[4 + k];
-  }
-  // the valid columns ordered by reduced row (lane c < 32: column c), their distinct tile rows
-  int32_t* ord = reinterpret_cast<int32_t*>(H + 32 * 32);  // [32] column at sorted position
-  int32_t* crow = ord + 32;                                // [32] column's reduced row
-  int32_t* cu = crow + 32;                                 // [32] column's tile-row slot
-  int32_t* trow = cu + 32;                                 // [8] distinct tile rows
-  int32_t* tpair = trow + 8;                               // [64] tileIdx of (tile row u, v)
-  const int rowc = lane < 32 ? (lane < 16 ? row0 : row1) : -1;  // lane c < 32: column c
-  const bool val = rowc >= 0;
-  int rank = 0;
-  for (int c = 0; c < 32; c++) {
-    const int rc = __builtin_amdgcn_readlane(rowc, c);
-    if (rc >= 0 && rc < rowc) rank++;
-  }
-  const int nc = __popcll(__ballot(val));
-  if (val) ord[rank] = lane;
-  const int tr = rowc / TS;
-  uint64_t left = __ballot(val);
-  int nu = 0, u = -1;
-  while (left) {
-    const int tl = __builtin_amdgcn_readlane(tr, __builtin_ctzll(left));
-    const bool hit = val && tr == tl;
-    left &= ~__ballot(hit);
-    if (hit) u = nu;
-    if (lane == 0) trow[nu] = tl;
-    nu++;  // <= 8: four variables, a tile row boundary inside each at most
-  }
-  if (lane < 32) crow[lane] = rowc, cu[lane] = u;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  for (int q = lane; q < nu * nu; q += 64) {
-    const int tu = trow[q / nu], tv = trow[q % nu];
-    tpair[q] = tu >= tv ? d.tileIdx[(int64_t)tu * d.nT + tv] : -1;
-  }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  // lower-triangle entries column by column over the ordered columns (consecutive lanes on consecutive
-  // rows of one tile column); diagonal damped by (1 + lambda)
-  const int P = nc * (nc + 1) / 2;
-  for (int p = lane; p < P; p += 64) {
-    const int q = P - 1 - p;
-    int i = (int)((sqrtf(8.0f * q + 1.0f) - 1.0f) * 0.5f);
-    while (i * (i + 1) / 2 > q) i--;
-    while ((i + 1) * (i + 2) / 2 <= q) i++;
-    const int b = nc - 1 - i, a = nc - 1 - (q - i * (i + 1) / 2);
-    const int ca = ord[a], cb = ord[b];
-    double v = H[ca * 32 + cb];
-    if (v == 0.0) continue;
-    const int R = crow[ca], C = crow[cb];
-    if (a == b) v *= 1.0 + lambda;
-    const int32_t ti = tpair[cu[ca] * nu + cu[cb]];
-    if (ti >= 0) atomicAdd(d.tiles + (int64_t)ti * TS * TS + (C % TS) * TS + (R % TS), v);
-    else atomicOr(d.err, 4);
-  }
-}
-
-// The group's records are streamed through LDS in chunks of kGrpChunk observations, each record copied
-// whole (both regions, 16 B per lane by global_load_lds: a handful of wide loads per thread per chunk,
-// where gathering the three operands of every k-step straight from HBM, behind an index load, ran
-// 1.05 ms against 0.79 alone on config C), double-buffered (chunk k + 1 in flight while chunk k feeds the
-// MFMAs).  Staged record c holds plane p at stage[c * kJPlanes + p].  The group's observation indices
-// come into LDS first, by windows of kGrpIdx.
-// observations per staged chunk: swept at config C (r05u, the kernel alone): fp64 16 / 24 / 32 / 48 / 64 ->
-// 818 / 794 / 862 / 1045 / 1041 us (LDS per workgroup sets the occupancy); fp32 records 609 / 564 / 550 /
-// 543 / 632 us
-constexpr int kGrpChunk = VIBA_MIXED ? 32 : 24;
-constexpr int kRecV = 16 / (int)sizeof(rec_t);                     // record elements per 16 B piece
-constexpr int kRecPieces = kJPlanes / kRecV;                       // 16 B pieces per record (36 / 18)
-constexpr int kGrpLoads = (kGrpChunk * kRecPieces + 255) / 256;    // global_load_lds per thread per chunk
-constexpr int kGrpStage = kGrpLoads * 256 * kRecV;                 // rec_t per buffer (tail pieces land past the chunk)
-constexpr int kGrpIdx = 1024;                                      // observation indices per window
-static_assert(kJA % kRecV == 0 && kJB % kRecV == 0, "record regions in whole 16 B pieces");
-constexpr int kGrpLds = 2 * kGrpStage * (int)sizeof(rec_t) > 4 * 64 * 14 * 8 ? 2 * kGrpStage * (int)sizeof(rec_t) : 4 * 64 * 14 * 8;
-
-// three LDS reads behind one wait, in inline asm: as plain loads the compiler put an s_waitcnt vmcnt(0)
-// before each (it cannot tell them from the global_load_lds stores in flight into the other buffer),
-// which drained the next chunk's loads before this chunk's products
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-__device__ __forceinline__ void lds_read3(const double* a, const double* b, const double* c, double& x, double& y, double& z) {
-  asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %4\n\tds_read_b64 %2, %5\n\ts_waitcnt lgkmcnt(0)"
-               : "=&v"(x), "=&v"(y), "=&v"(z)
-               : "v"(lds_addr(a)), "v"(lds_addr(b)), "v"(lds_addr(c))
-               : "memory");
-}
-__device__ __forceinline__ void lds_read3(const float* a, const float* b, const float* c, float& x, float& y, float& z) {
-  asm volatile("ds_read_b32 %0, %3\n\tds_read_b32 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
-               : "=&v"(x), "=&v"(y), "=&v"(z)
-               : "v"(lds_addr(a)), "v"(lds_addr(b)), "v"(lds_addr(c))
-               : "memory");
-}
-
-__device__ __forceinline__ void group_issue(const Dev& d, const int32_t* sIdx, int nv, rec_t* buf, int wave, int lane) {
-#pragma unroll
-  for (int j = 0; j < kGrpLoads; j++) {
-    const int i = j * 256 + wave * 64 + lane;
-    int c = i / kRecPieces;
-    const int q = i - c * kRecPieces;
-    if (c >= nv) c = 0;  // past the chunk's observations: a valid record again, never read
-    const int64_t o = sIdx[c];
-    const rec_t* src = q < kJA / kRecV ? d.Jt + o * kJA + q * kRecV
-                                        : d.Jt + d.nObsPad * kJA + o * kJB + (q - kJA / kRecV) * kRecV;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(buf + (j * 256 + wave * 64) * kRecV), 16, 0, 0);
-  }
-}
-
-__global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, int mode) {
-  __shared__ __attribute__((aligned(16))) double smem[kGrpLds / 8];  // the two buffers, then the epilogue's
-  __shared__ int32_t sIdx[kGrpIdx];
-  rec_t* stg = reinterpret_cast<rec_t*>(smem);
-  const int64_t g = xcd_block(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int32_t* rv = d.grpRed + 4 * g;
-  int p0, s0, p1, s1;
-  const int row0 = grp_col_row(d, rv, l15, p0, s0);
-  const int row1 = grp_col_row(d, rv, 16 + l15, p1, s1);
-  const int64_t o0 = d.grpStart[g], n = d.grpStart[g + 1] - o0;
-  const int r = l4 & 1;
-  const int q0 = row0 >= 0 ? p0 + r * s0 : 0, q1 = row1 >= 0 ? p1 + r * s1 : 0;  // this lane's planes (K row parity r)
-  hacc4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
-  double g0 = 0.0, g1 = 0.0;
-  for (int64_t w0 = 0; w0 < n; w0 += kGrpIdx) {
-    const int nw = (int)min<int64_t>(n - w0, kGrpIdx);
-    for (int i = tid; i < nw; i += 256) sIdx[i] = d.grpObs[o0 + w0 + i];
-    __syncthreads();
-    const int nch = (nw + kGrpChunk - 1) / kGrpChunk;
-    group_issue(d, sIdx, min(nw, kGrpChunk), stg, wave, lane);
-    for (int k = 0; k < nch; k++) {
-      const int c0 = k * kGrpChunk, nv = min(nw - c0, kGrpChunk);
-      if (k + 1 < nch) {  // buffer (k + 1) & 1: its readers (chunk k - 1) passed the last barrier
-        group_issue(d, sIdx + c0 + kGrpChunk, min(nw - c0 - kGrpChunk, kGrpChunk), stg + ((k + 1) & 1) * kGrpStage, wave, lane);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGrpLoads) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();  // every wave's part of chunk k landed
-      __builtin_amdgcn_sched_barrier(0);
-      const rec_t* S = stg + (k & 1) * kGrpStage;
-      for (int ks = wave; 2 * ks < nv; ks += 4) {
-        const int c = 2 * ks + (l4 >> 1);
-        const rec_t* rc = S + min(c, nv - 1) * kJPlanes;  // branch-free: past the chunk / invalid columns masked
-        rec_t er, v0, v1;
-        lds_read3(rc + kJe + r, rc + q0, rc + q1, er, v0, v1);
-        if (c >= nv) er = v0 = v1 = 0;
-        if (row0 < 0) v0 = 0;
-        if (row1 < 0) v1 = 0;
-        g0 += (double)v0 * er, g1 += (double)v1 * er;
-        if (mode == 0) {
-          a00 = mfma_h(v0, v0, a00);
-          a10 = mfma_h(v1, v0, a10);
-          a11 = mfma_h(v1, v1, a11);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();  // chunk k's readers done before its buffer is refilled (or sIdx / the epilogue)
-    }
-  }
-  group_finish(d, lambda, mode, row0, row1, a00, a10, a11, g0, g1, smem);
-}
-
-// damping of the small-factor part of the diagonal (visual part: obs_group_kernel) and the
-// identity term (Optimizer.cpp:136-146 addDamping: H_ii += lambda * H_ii + lambda)
-__global__ void damp_small_kernel(Dev d, double lambda, int addIdentity) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= d.nRed || !owns_col(d, r / TS)) return;
-  double* p = tile_ptr(d, r, r);
-  *p = *p * (1.0 + lambda) + (addIdentity ? lambda : 0.0);
-}
-
-// new reduced RHS (vb_solve_with_new_gradient / vb_assemble_new_rhs): rhs = gRedNew - sum Y^T zNew over this
-// shard's landmarks; rhs starts as a copy of gRedNew, one block per chunk of <= 1024 landmarks of one
-// reduced variable X (the calibration variables see every landmark: one block each took 2.6 ms)
-__global__ void __launch_bounds__(256) reduced_rhs_kernel(Dev d) {
-  __shared__ double g[4][32];
-  const int64_t* ch = d.lxChunk + 3 * (int64_t)blockIdx.x;
-  const int X1 = (int)ch[0];
-  const int d1 = d.rvDim[X1];
-  const int64_t off1 = d.rvOff[X1];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // lanes = (landmark slot, column j): P = d1 rounded up to a power of two lanes per landmark, so a
-  // wave reads 64 / P landmarks' panel rows at once (runs of d1 doubles per plane) instead of one
-  // landmark's 3 d1 values per lane
-  const int P = d1 <= 4 ? 4 : d1 <= 8 ? 8 : d1 <= 16 ? 16 : 32;
-  const int S = 64 / P, slot = lane / P, j = lane % P;
-  const int64_t yq = d.nYcol;
-  double acc = 0.0;
-  for (int64_t idx = ch[1] + wave * S + slot; idx < ch[2]; idx += 4 * S) {
-    const int64_t l = d.lxLm[idx];
-    if (j >= d1 || l < d.lmB || l >= d.lmE) continue;
-    const rec_t* y1 = d.Y + d.lmY[l] / 3 + d.lxCol[idx] + j;
-    acc += (double)y1[0] * d.zNew[l * 3] + (double)y1[yq] * d.zNew[l * 3 + 1] + (double)y1[2 * yq] * d.zNew[l * 3 + 2];
-  }
-  for (int o = P; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);  // over the landmark slots
-  if (lane < P && lane < d1) g[wave][lane] = acc;
-  __syncthreads();
-  if (tid < d1) atomicAdd(&d.rhs[off1 + tid], -(g[0][tid] + g[1][tid] + g[2][tid] + g[3][tid]));
-}
 
 // ------------------------------------------------------------------ tile Cholesky
 // Level-scheduled tile Cholesky (factorSeq in api.hip), per elimination level of the nested-dissection
@@ -1458,11 +649,7 @@ __global__ void __launch_bounds__(256) sntrsm_kernel(Dev d, const int32_t* items
                                                      double* fwdB) {
   sntrsm_body(d, items, dinvAll, fwdY, fwdB);
 }
-// the same at four waves per SIMD (<= 128 VGPRs): more rows in flight per CU (VIBA_SN_TRSM_W4=1)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4)))
-sntrsm_w4_kernel(Dev d, const int32_t* items, const double* dinvAll, const double* fwdY, double* fwdB) {
-  sntrsm_body(d, items, dinvAll, fwdY, fwdB);
-}
+// (a four-waves-per-SIMD build of the same body spilled 10 VGPRs: 52.3 against 52.9 it/s, r05)
 
 // the diagonal tiles of the fused levels back from Lscr (pairs: diagonal tile, column)
 __global__ void __launch_bounds__(256) copy_diag_kernel(Dev d, const int32_t* pairs, const double* Lscr) {
@@ -2054,55 +1241,8 @@ __global__ void __launch_bounds__(256) boxplus_reduced_kernel(Dev d, const doubl
 }
 
 // ------------------------------------------------------------------ launch wrappers
-static inline unsigned blocks(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 void launch_axpby(double* y, const double* x, double a, double b, int64_t n, hipStream_t st);
 
-void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t hi, hipStream_t st) {
-  if (hi <= lo) return;
-  if (mode == 2) {
-    launchK(landmark_z_kernel, dim3(blocks(hi - lo, 256)), dim3(256), 0, st, d, lo, hi);
-  } else if (mode == 0 && lo == d.lmB && hi == d.lmE) {
-    if (d.nLmSmall)
-      launchK(landmark_obs_kernel, dim3(blocks(d.nLmSmall, 4)), dim3(256),
-              (uint32_t)(4 * 3 * kLmSmallCols * sizeof(double)), st, d, lambda, (int64_t)0, d.nLmSmall, kLmSmallCols);
-    if (d.nLmBig && d.lmBigCols <= kLmBigCols)
-      hipLaunchKernelGGL(landmark_obs_wg_kernel, dim3((unsigned)d.nLmBig), dim3(256),
-                         (uint32_t)(3 * d.lmBigCols * sizeof(double)), st, d, lambda, d.nLmSmall, (int)d.lmBigCols);
-    else if (d.nLmBig)
-      hipLaunchKernelGGL(landmark_list_kernel, dim3(blocks(d.nLmBig, 4)), dim3(256), 0, st, d, lambda, d.nLmSmall,
-                         d.nLmBig);
-  } else {
-    launchK(landmark_kernel, dim3(blocks(hi - lo, 4)), dim3(256), 0, st, d, lambda, mode, lo, hi);
-  }
-}
-// S(tiles) += damping + direct - Schur; rhs = gRed(+visual) - sum Y^T z  (rhs must be zero on entry), in
-// three parts: the damping of the assembled direct terms (a read-modify-write of the diagonal, so it
-// precedes the observation-group atomics), the observation-group Gram blocks (independent of the
-// landmark elimination: vb_damp_factor_solve runs them on the side stream beside it), the tile products
-void launch_damp(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
-  if (d.nRed) hipLaunchKernelGGL(damp_small_kernel, dim3(blocks(d.nRed, 256)), dim3(256), 0, st, d, lambda, addIdentity);
-}
-void launch_groups(const Dev& d, double lambda, hipStream_t st) {
-  if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, lambda, 0);
-}
-void launch_schur_products(const Dev& d, double lambda, hipStream_t st);
-void launch_schur(const Dev& d, double lambda, int addIdentity, hipStream_t st) {
-  launch_damp(d, lambda, addIdentity, st);
-  launch_groups(d, lambda, st);
-  launch_schur_products(d, lambda, st);
-}
-void launch_schur_products(const Dev& d, double lambda, hipStream_t st) {
-  if (d.nTileWorks) launchK(schur_run4_kernel, dim3((unsigned)d.nTileWorks), dim3(256), 0, st, d, lambda);
-  launch_axpby(d.rhs, d.gRed, 1.0, 1.0, d.nRed, st);
-}
-void launch_reduced_grad(const Dev& d, int mode, hipStream_t st) {
-  if (mode == 0) {  // visual gradient of this shard's observations, by observation group
-    if (d.nGroups) hipLaunchKernelGGL(obs_group_kernel, dim3((unsigned)d.nGroups), dim3(256), 0, st, d, 0.0, 1);
-    return;
-  }
-  (void)hipMemcpyAsync(d.rhs, d.gRedNew, (size_t)d.nT * TS * sizeof(double), hipMemcpyDeviceToDevice, st);
-  if (d.nLxChunk) hipLaunchKernelGGL(reduced_rhs_kernel, dim3((unsigned)d.nLxChunk), dim3(256), 0, st, d);
-}
 // fwdB / fwdY (may be null): the forward solve fused into the factorization (potrf: y_J from b_J;
 // trsm: b_I -= L_IJ y_J for its tile, rows[] = the tile's row I)
 void launch_potrf(const Dev& d, const int32_t* tiles, const int32_t* cols, int n, double* dinv, hipStream_t st,
@@ -2123,9 +1263,7 @@ void launch_snpotrf_trsm(const Dev& d, const int32_t* items, int n, double* Lscr
 }
 void launch_sntrsm(const Dev& d, const int32_t* items, int n, const double* dinv, hipStream_t st, const double* fwdY,
                    double* fwdB) {
-  static const bool w4 = getenv("VIBA_SN_TRSM_W4") && atoi(getenv("VIBA_SN_TRSM_W4")) == 1;
-  if (n > 0 && w4) launchK(sntrsm_w4_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdY, fwdB);
-  else if (n > 0) launchK(sntrsm_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdY, fwdB);
+  if (n > 0) launchK(sntrsm_kernel, dim3(n), dim3(256), 0, st, d, items, dinv, fwdY, fwdB);
 }
 void launch_copy_diag(const Dev& d, const int32_t* pairs, int n, const double* Lscr, hipStream_t st) {
   if (n > 0) hipLaunchKernelGGL(copy_diag_kernel, dim3(n), dim3(256), 0, st, d, pairs, Lscr);
@@ -2195,5 +1333,6 @@ void launch_boxplus(const Dev& d, const double* stepRed, const double* stepPt, h
 }
 
 }  // namespace viba
+
 
 

@@ -173,6 +173,18 @@ class ShardComm:
 
 
 # ------------------------------------------------------------------ one scalar read per iteration
+def word_bits(words):
+    """two error bit words (int32, bits 0..30) -> 62 floats 0/1 (bit k of word i at 31 i + k): a MAX
+    reduction of these over the ranks is the bitwise OR of the words (collectives have no bitwise-or)"""
+    return [float((int(w) >> k) & 1) for w in words for k in range(31)]
+
+
+def bits_word(bits):
+    """inverse of word_bits (over MAX-reduced floats)"""
+    return np.array([sum(int(round(float(bits[31 * i + k]))) << k for k in range(31)) for i in range(2)],
+                    dtype=np.int32)
+
+
 class _IterScalars:
     """The LM scalars of one iteration (vb_scalar_slots layout: [0] linearization cost, [1] cost pass
     cost, [2..4] CostStats, [8] max step ratio, [9] sum of squared ratios, [10] sum of ratios, [16] twice
@@ -180,10 +192,11 @@ class _IterScalars:
 
     HIP engine (deferred mode, vb_set_deferred): the phase functions leave their partials in the
     engine's device slots.  With RCCL they are all-reduced in place on the engine stream (sum; the max
-    ratio and the error words by max), the scalar point is marked (vb_mark_scalars) so work queued after
-    it -- the next iteration's speculative linearization -- does not delay the read, and the host reads
-    them once (vb_read_scalars).  With gloo (host-staged) the host reads the partials once and the
-    reduction runs on host tensors.  Host engines (the oracle): the phase functions return their
+    ratio by max, the error words bitwise-ORed), the scalar point is marked (vb_mark_scalars) so work
+    queued after it -- the next iteration's speculative linearization -- does not delay the read, and the
+    host reads them once (vb_read_scalars).  With gloo (host-staged) the host reads the partials and the
+    error words once and the reduction runs on host tensors; either way every rank decodes the same ORed
+    words (vb_error_from_words), so all raise the same code and message.  Host engines (the oracle): the phase functions return their
     partials, collected here, reduced over gloo."""
 
     SUM = [0, 1, 2, 3, 4, 9, 10, 16]
@@ -199,6 +212,7 @@ class _IterScalars:
             self.err = _tensor(ep, 2, comm.device, int32=True)
             small = engine.small_factor_count()
             self.spec = engine.spec_prepare()
+            self.shifts = torch.arange(31, dtype=torch.int64, device=comm.device)
         else:
             self.host = np.zeros(17)
             small = 0  # the host engine's CostStats count every factor it evaluates
@@ -219,39 +233,51 @@ class _IterScalars:
         dist = c.dist
         if self.device and c.nccl:
             red, err = self.red, self.err
-            mx = torch.cat([red[8:9], err.to(torch.float64)])
+            # the error words are bit flags: ORed over the ranks as one 0/1 per bit reduced by MAX (RCCL
+            # has no bitwise-or), in the same collective as the max step ratio
+            bits = ((err.to(torch.int64).unsqueeze(1) >> self.shifts) & 1).to(torch.float64).flatten()
+            mx = torch.cat([red[8:9], bits])
             dist.all_reduce(mx, op=dist.ReduceOp.MAX)
             red[5:9].zero_()
             red[11:16].zero_()
             dist.all_reduce(red[0:17])
             red[8:9].copy_(mx[0:1])
-            err.copy_(mx[1:3].to(torch.int32))
+            err.copy_((mx[1:].view(2, 31).to(torch.int64) << self.shifts).sum(1).to(torch.int32))
             if self.spec:
                 self.e.mark_scalars()
             if queue_after:
                 queue_after()
+            # the code (and the engine's last_error text) of the ORed words: the same on every rank
             rc, v = self.e.read_scalars(17, check=False)
         else:
+            words = None
             if self.device:
                 if self.spec:
                     self.e.mark_scalars()
                 if queue_after:
                     queue_after()
                 rc, v = self.e.read_scalars(17, check=False)
+                words = self.e.error_words()
             else:
                 rc, v = 0, self.host.copy()
             t = torch.tensor([v[i] for i in self.SUM], dtype=torch.float64)
-            m = torch.tensor([v[8], -float(rc)], dtype=torch.float64)
+            bits = [] if words is None else word_bits(words)
+            m = torch.tensor([v[8], -float(rc)] + bits, dtype=torch.float64)
             dist.all_reduce(t)
             dist.all_reduce(m, op=dist.ReduceOp.MAX)
             v = np.zeros(17)
             v[self.SUM] = t.numpy()
-            v[8], rc = float(m[0]), -int(round(float(m[1])))
+            v[8] = float(m[0])
+            if words is None:  # host engines raise inside their calls; only a code travels
+                rc = -int(round(float(m[1])))
+            else:  # the ORed words, decoded as the RCCL path decodes them
+                ored = bits_word(m[2:].tolist())
+                rc = self.e.error_from_words(ored) if ored.any() else 0
         c.host_reads += 1
-        if rc:  # every rank raises the same code (the error words are reduced over the ranks)
+        if rc:  # every rank raises the same code with the same message (the error words ORed over the ranks)
             from .engine import VbError
-            raise VbError(rc, f"LM iteration failed (error words over {c.world} ranks; this rank's last error: "
-                              f"{self.e.last_error()})")
+            msg = self.e.last_error() if hasattr(self.e, "last_error") else ""
+            raise VbError(rc, f"LM iteration failed (error words ORed over {c.world} ranks): {msg}")
         v = np.array(v, dtype=np.float64)
         v[2] += self.n_small
         return v
@@ -391,6 +417,7 @@ class ShardedOptimizer:
                 # cost pass; their scalars reduced over the ranks and read once (vb_optimize's pattern)
                 if deferred:
                     e.set_deferred(True)
+                used_spec = spec_pending
                 if spec_pending:
                     e.spec_commit(True)  # the step stayed applied at full size: its linearization is ready
                     spec_pending = False
@@ -419,6 +446,12 @@ class ShardedOptimizer:
                     self.phases.mark(None)
                 v = sc.read(queue_spec if speculate else None)
                 spec_pending = speculate
+                if used_spec and hasattr(e, "spec_phase_ms"):
+                    # this iteration's rebuild + linearization ran in the previous iteration's queue: their
+                    # own device events (complete: they precede the cost pass just read), as vb_optimize
+                    rs_ms, lin_ms = e.spec_phase_ms()
+                    self.phases.add("rs_update_ms", rs_ms)
+                    self.phases.add("linearize_ms", lin_ms)
                 if deferred:
                     e.set_deferred(False)
                 self.phases.close_iteration()
@@ -515,8 +548,10 @@ class _PhaseClock:
     on the engine's stream at the phase boundaries, without extra synchronisation: an iteration's marks are
     evaluated at the next iteration's close (or the final one), when the device has passed them.  A phase's
     time includes its collectives and any stream idle while the host stages them (gloo).  An iteration whose
-    linearization was queued speculatively by the previous one has no rs_update / linearize marks; the
-    previous iteration's spec_linearize_ms is that work.  Host engines: nothing is recorded."""
+    linearization was queued speculatively by the previous one has no rs_update / linearize marks: the
+    controller adds that work's own device times (vb_spec_phase_ms) to it instead, so rs_update_ms and
+    linearize_ms are this iteration's as in vb_phase_times, while spec_linearize_ms is the span the previous
+    iteration's queue spent on it.  Host engines: nothing is recorded."""
 
     NAMES = ("rs_update_ms", "linearize_ms", "schur_ms", "factor_ms", "solve_ms", "step_ms", "cost_ms",
              "spec_linearize_ms")
@@ -526,6 +561,7 @@ class _PhaseClock:
         self.ms = {k: 0.0 for k in self.NAMES}
         self.marks = []    # the iteration being queued
         self.pending = []  # the last closed iteration, evaluated at the next close
+        self.extra, self.pending_extra = {}, {}  # phase times measured elsewhere (add())
 
     def mark(self, name):
         """The phase `name` starts here (None: nothing is timed from here)."""
@@ -536,12 +572,19 @@ class _PhaseClock:
         ev.record(self.ext)
         self.marks.append((name, ev))
 
-    def _evaluate(self, marks):
+    def add(self, name, ms):
+        """device time of a phase of the iteration being queued, measured by the engine's own events"""
+        if self.ext is not None:
+            self.extra[name] = self.extra.get(name, 0.0) + ms
+
+    def _evaluate(self, marks, extra):
         marks[-1][1].synchronize()
         ms = {k: 0.0 for k in self.NAMES}
         for (name, a), (_, b) in zip(marks, marks[1:]):
             if name is not None:
                 ms[name] += a.elapsed_time(b)
+        for name, v in extra.items():
+            ms[name] += v
         ms["total_ms"] = marks[0][1].elapsed_time(marks[-1][1])
         self.ms = ms
 
@@ -549,11 +592,12 @@ class _PhaseClock:
         if self.ext is None:
             return
         if self.pending:
-            self._evaluate(self.pending)
+            self._evaluate(self.pending, self.pending_extra)
         self.pending, self.marks = self.marks, []
+        self.pending_extra, self.extra = self.extra, {}
         if final and self.pending:
-            self._evaluate(self.pending)
-            self.pending = []
+            self._evaluate(self.pending, self.pending_extra)
+            self.pending, self.pending_extra = [], {}
 
 
 class PartitionedOptimizer(ShardedOptimizer):

@@ -590,6 +590,17 @@ class HipEngine(CEngineBase):
             return out
         return rc, out
 
+    def error_words(self):
+        """the two error bit words behind the last check (vb_error_words)"""
+        w = np.zeros(2, np.int32)
+        self._check(self._fn("error_words", [C.POINTER(C.c_int32)])(self.h, w.ctypes.data_as(C.POINTER(C.c_int32))))
+        return w
+
+    def error_from_words(self, words) -> int:
+        """the code two (rank-ORed) error words encode; sets last_error() to its message (vb_error_from_words)"""
+        w = np.ascontiguousarray(words, dtype=np.int32)
+        return int(self._fn("error_from_words", [C.POINTER(C.c_int32)])(self.h, w.ctypes.data_as(C.POINTER(C.c_int32))))
+
 
     def spec_prepare(self) -> bool:
         ok = C.c_int()
@@ -601,6 +612,13 @@ class HipEngine(CEngineBase):
 
     def spec_commit(self, use: bool):
         self._check(self._fn("spec_commit", [C.c_int])(self.h, int(use)))
+
+    def spec_phase_ms(self):
+        """(rolling-shutter rebuild ms, linearization ms) of the speculative linearization last committed
+        (vb_spec_phase_ms)"""
+        out = np.zeros(2)
+        self._check(self._fn("spec_phase_ms", [_dp])(self.h, out.ctypes.data_as(_dp)))
+        return float(out[0]), float(out[1])
 
     # partitioned factorization (HIP engine only; include/viba_hip.h vb_set_partition)
     def bench_kernel(self, which: int, iters: int = 200) -> float:
