@@ -51,16 +51,32 @@ def visual_bytes_per_launch(p, nobs: int) -> float:
     return nobs * per_obs + shared
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this round
-    (profiles/pmc_summary.json, written by scripts/pmc_summary.py from separate FETCH_SIZE /
-    WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def pmc_traffic(kernel: str, path: str | None = None):
+    """(HBM bytes per launch of `kernel`, provenance) from the committed rocprofv3 PMC summary
+    (profiles/pmc_summary.json, written by scripts/pmc_summary.py from separate FETCH_SIZE / WRITE_SIZE
+    passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).  The bytes are None unless the summary was
+    measured on exactly the HIP sources this tree builds (sources digest, build.sources_digest): a summary of
+    other code is reported as stale, never as this binary's traffic."""
+    from visual_inertial_bundle_adjustment_amd.build import sources_digest
+    path = path or os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            return json.load(f)[kernel]["hbm_bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
-        return None
+            summ = json.load(f)
+    except (OSError, ValueError):
+        return None, {"status": "missing"}
+    meta = summ.get("_meta", {})
+    here = sources_digest()
+    prov = {"measured_at_commit": meta.get("commit"), "sources_sha256": meta.get("sources_sha256"),
+            "tree_sources_sha256": here}
+    if meta.get("sources_sha256") != here:
+        prov["status"] = "stale: measured on other HIP sources than this tree's"
+        return None, prov
+    prov["status"] = "measured on this tree's HIP sources"
+    try:
+        return summ[kernel]["hbm_bytes_per_launch"], prov
+    except KeyError:
+        prov["status"] = f"no {kernel} entry"
+        return None, prov
 
 
 def host_threads() -> tuple[int, int]:
@@ -171,13 +187,11 @@ def spawn_ranks(n: int) -> int:
     """`bench.py --gpus N` without a launcher: run this script under torch.distributed.run with N ranks
     (one per GPU, RCCL) as a child process, before anything here touches a GPU, and return its exit code
     (the driver's own N > 1 form sets WORLD_SIZE and never comes here)."""
-    import socket
     import subprocess
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    # a standalone c10d rendezvous: its store binds a free port itself (no probe-then-bind port race), and
+    # the workers reach it at 127.0.0.1 (the container hostname may not resolve)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--standalone",
+           "--local-addr", "127.0.0.1", os.path.abspath(__file__), *sys.argv[1:]]
     log(f"[bench] launching {n} ranks: {' '.join(cmd[1:])}")
     return subprocess.call(cmd)
 
@@ -323,9 +337,9 @@ def main():
         # I-side tile of the diagonal contribution (J, J, K), so the operands are pairs x 32 KB; each
         # target tile is read and written once (st[5] tiles over the launches bounds the targets)
         compulsory = (fan_contrib * 64 * 64 * 8 + st[5] * 2 * 64 * 64 * 8) / max(1e-9, fan_per_factor)
-        traffic = pmc_traffic("fanin_kernel")
+        traffic, tprov = pmc_traffic("fanin_kernel")
         roof = {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": traffic,
+                "frac": achieved / FP64_MFMA_PEAK_TF, "traffic": traffic, "traffic_provenance": tprov,
                 "compulsory_bytes_per_launch": compulsory,
                 "traffic_over_compulsory": traffic / compulsory if traffic else None,
                 "kernel": "fanin_kernel (level-batched fan-in tile update A_IJ -= sum_K L_IK L_JK^T on "
@@ -343,14 +357,14 @@ def main():
         b = st[11] * (64 * 64 * 8 + 2 * 64 * 8)
         achieved = b / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("tile_symv_kernel"),
+                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("tile_symv_kernel")[0],
                 "kernel": "tile_symv_kernel (PCG product y += S x over the lower tiles of S, fill skipped)",
                 "bytes_per_launch": b, "avg_launch_ms": avg_ms, "launches": launches}
     else:
         b = visual_bytes_per_launch(p, st[0])
         achieved = b / (avg_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("visual_lin_kernel"),
+                "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic("visual_lin_kernel")[0],
                 "kernel": "visual_lin_kernel (Jacobian fill)", "bytes_per_launch": b, "avg_launch_ms": avg_ms,
                 "launches": launches}
     if roof is not None:

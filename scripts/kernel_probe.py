@@ -18,7 +18,8 @@ NAMES = {0: "potrf4 (one tile, scratch)", 1: "trsm (one tile, scratch)", 2: "fan
          16: "small factors' evaluation", 17: "small assembly, IMU kinds", 18: "small assembly, other kinds",
          19: "reduced-system clear", 20: "elimination beside tile products (timing probe)",
          21: "elimination then tile products", 22: "elimination beside groups",
-         23: "factorization (its streams)", 24: "factorization beside tile products (timing probe)"}
+         23: "factorization (its streams)", 24: "factorization beside tile products (timing probe)",
+         25: "factorization beside tile products on stZ (timing probe)"}
 
 
 def main():

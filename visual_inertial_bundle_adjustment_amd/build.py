@@ -27,6 +27,19 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-f
              *os.environ.get("VIBA_EXTRA_HIPFLAGS", "").split()]
 
 
+def sources_digest() -> str:
+    """sha256 over the HIP library's sources and headers (csrc/*.hip, *.hpp, include/viba_hip.h): ties a
+    measurement (profiles/pmc_summary.json) to the code it measured -- bench.py reports the PMC traffic
+    only when the running tree's digest equals the recorded one."""
+    import hashlib
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".h")))
+    h = hashlib.sha256()
+    for f in names + ["../../include/viba_hip.h"]:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
 def _newer(target: str, deps: list[str]) -> bool:
     return os.path.exists(target) and all(os.path.getmtime(target) >= os.path.getmtime(d) for d in deps)
 

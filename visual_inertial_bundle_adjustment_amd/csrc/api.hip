@@ -52,8 +52,9 @@ void profAccumulate(vb_handle h, size_t n) {
     const float ms = profPairMs(h->profEv[i], h->profEv[i + 1]);
     h->profMs += ms;
     h->profLaunches++;
-    float t0 = 0;
-    if (i > 0) (void)hipEventElapsedTime(&t0, h->profEv[0], h->profEv[i]);
+    // the launch's start against the first one's, with the same not-ready retry as its duration (a
+    // not-ready pair read as 0 would place the launch at the origin and shrink the busy union)
+    const float t0 = i > 0 ? profPairMs(h->profEv[0], h->profEv[i]) : 0.0f;
     iv.push_back({(double)t0, (double)t0 + ms});
   }
   std::sort(iv.begin(), iv.end());

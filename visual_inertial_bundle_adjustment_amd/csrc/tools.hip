@@ -141,13 +141,16 @@ extern "C" int vb_bench_kernel(vb_handle h, int which, int iters, double* avg_us
           if (int rc = factorReduced(h, 0)) return rc;
           break;
         case 24:
+        case 25: {  // 25: the products on stZ instead
+          hipStream_t ps = which == 24 ? h->stF : h->stZ;
           HIPCHK(hipEventRecord(h->evFork, h->st));
-          HIPCHK(hipStreamWaitEvent(h->stF, h->evFork, 0));
-          launch_schur_products(d, 1e-5, h->stF);
-          HIPCHK(hipEventRecord(evP, h->stF));
+          HIPCHK(hipStreamWaitEvent(ps, h->evFork, 0));
+          launch_schur_products(d, 1e-5, ps);
+          HIPCHK(hipEventRecord(evP, ps));
           if (int rc = factorReduced(h, 0)) return rc;
           HIPCHK(hipStreamWaitEvent(h->st, evP, 0));
           break;
+        }
         default: return fail(VB_E_ARG, "vb_bench_kernel: unknown kernel");
       }
       HIPCHK(hipEventRecord(e1, h->st));
