@@ -381,10 +381,25 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
   int kr = l4, e = c0 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
   auto ld = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
     const bool kv = kr < rows;
+#if VIBA_SCHUR_L2PROBE == 1  // diagnostic build (timing only, S is garbage): gathers confined to 4096 columns
+    const uint2 c = make_uint2(ec[kv ? e : c0].x & 4095u, ec[kv ? e : c0].y & 4095u);
+#elif VIBA_SCHUR_L2PROBE == 6  // diagnostic (timing only): every 16-column gather row on one 128 B line
+    const uint2 c = make_uint2(ec[kv ? e : c0].x & ~15u, ec[kv ? e : c0].y & ~15u);
+#else
     const uint2 c = ec[kv ? e : c0];
+#endif
+#if VIBA_SCHUR_L2PROBE == 6
+    const rec_t* base = Y + ((q == 0 ? 0 : q == 1 ? pq : 2 * pq) & ~(int64_t)15) + l15;
+#else
     const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
+#endif
+#if VIBA_SCHUR_L2PROBE == 5  // diagnostic (timing only): every gather reads the zero pad (one L1 line)
+    const rec_t* pJ = zp;
+    const rec_t* pI = zp + (kv ? 0 : 0);
+#else
     const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
     const rec_t* pI = kv ? base + c.x : zp;
+#endif
 #pragma unroll
     for (int i = 0; i < NR; i++) av[i] = pJ[16 * i];
 #pragma unroll
@@ -397,7 +412,11 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     for (int i = 0; i < NR; i++)
 #pragma unroll
       for (int b = 0; b < NBI; b++)
+#if VIBA_SCHUR_L2PROBE == 2  // diagnostic build (timing only): the operands consumed without the MFMAs
+        if (!DIAG || a0 + i <= b) acc[i][b][0] += (double)av[i] * (double)bv[b];
+#else
         if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
+#endif
   };
   rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
   ld(a0v, b0v);
@@ -408,7 +427,18 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     if (ks + 1 < nks) mm(a1v, b1v);
   }
   // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
+#if VIBA_SCHUR_L2PROBE == 3  // diagnostic (timing only): no epilogue (one LDS add keeps the k-loop live)
+  double sum = 0.0;
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+#pragma unroll
+    for (int b = 0; b < NBI; b++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) sum += (double)acc[i][b][q];
+  asm volatile("" ::"v"(sum));  // consumed: the k-loop cannot be sunk or dropped
+#else
   schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
+#endif
 }
 
 // Schur tile products, one workgroup per work item (TileWork: a target tile and <= 256 of its landmark
@@ -480,6 +510,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
   }
   __syncthreads();
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
+#if VIBA_SCHUR_L2PROBE == 4  // diagnostic (timing only): no tile write-back
+  if (C[tid] == 12345.0) Ct[tid] = 0.0;
+  return;
+#endif
   if (wk.kind == 1) {
     for (int i = tid; i < TS * TS; i += 256)
       if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
