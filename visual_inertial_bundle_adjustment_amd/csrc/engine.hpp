@@ -33,7 +33,7 @@ typedef float rec_t;
 typedef double rec_t;
 #endif
 
-constexpr int kLmSmallCols = 256;  // landmark_obs_kernel's narrow class (Y panel columns)
+constexpr int kLmSmallCols = 256;  // landmark_stage_kernel's narrow class (Y panel columns)
 
 // planes of the whitened visual Jacobian record
 constexpr int kJe = 0;      // e0, e1
@@ -241,7 +241,7 @@ struct Dev {
   // [obFree, nObs) on the root unless partitioned); the root also owns the reduced-variable step
   // ratios and, unless partitioned, every small factor
   int64_t lmB = 0, lmE = 0, obB = 0, obE = 0, obFree = 0, fB = 0, fE = 0;
-  // this handle's landmarks by Y panel width for landmark_obs_kernel: lmList[0, nLmSmall) have at
+  // this handle's landmarks by Y panel width for landmark_stage_kernel: lmList[0, nLmSmall) have at
   // most kLmSmallCols panel columns, lmList[nLmSmall, nLmSmall + nLmBig) at most lmBigCols
   int32_t* lmList = nullptr;
   int64_t nLmSmall = 0, nLmBig = 0;

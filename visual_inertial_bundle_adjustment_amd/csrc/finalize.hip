@@ -742,7 +742,7 @@ int doFinalize(vb_handle h) {
   if (h->lmEnd < 0) h->lmBegin = 0, h->lmEnd = nPts;
   if (h->lmBegin < 0 || h->lmEnd > nPts || h->lmBegin > h->lmEnd) return fail(VB_E_ARG, "bad landmark shard range");
   d.lmB = h->lmBegin, d.lmE = h->lmEnd, d.root = h->isRoot ? 1 : 0;
-  {  // landmark lists by panel width (solver.hip landmark_obs_kernel)
+  {  // landmark lists by panel width (schur.hip landmark_stage_kernel)
     std::vector<int32_t> small, big;
     int64_t bigCols = 0;
     for (int64_t l = h->lmBegin; l < h->lmEnd; l++) {

@@ -1,6 +1,6 @@
 // Schur complement of the landmark block (replacing BaSpaCho's elimination of the point range,
 // Optimizer.cpp:200-206, and addDamping, Optimizer.cpp:136-146), gfx950:
-//   landmark_obs_kernel   one wave per landmark: V = sum Jp^T Jp (damped), g_p, the W panel in LDS,
+//   landmark_stage_kernel one wave per landmark: V = sum Jp^T Jp (damped), g_p, the W panel in LDS,
 //   (_wg, landmark_kernel) 3x3 Cholesky, z = L^-1 g_p, Y = L^-1 W
 //   obs_group_kernel      direct visual terms J~^T J~ per (rig, camera) group on fp64 MFMA
 //   schur_run4_kernel     S_IJ -= sum_l Y_lI^T Y_lJ by target tile, compact runs, register operands
@@ -95,11 +95,11 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
 // landmark's W panel in LDS at panel column obCol + j with LDS atomics (both halves may hit a shared
 // calibration block), and lane 0 of the half accumulates V and g.  Then the damped 3 x 3 Cholesky,
 // z, and Y = L^-1 W over the panel columns.  No per-block observation lists: every record is read
-// once.  Two launches by panel width (api.hip lmList): landmarks with up to kLmSmallCols columns one
-// per wave with a 24 KB workgroup (6 per CU); the wider ones (long tracks) one per workgroup,
-// landmark_obs_wg_kernel, whose panel is per workgroup.  Measured on config C: 1.04 + 0.72 ms against
-// 2.63 for the per-column landmark_kernel; one 48 KB per-wave class for all ran at 2.9 ms and the
-// per-workgroup kernel for all at 2.1 (occupancy vs. barriers).
+// once.  Two launches by panel width (finalize.hip lmList): landmarks with up to kLmSmallCols columns one
+// per wave, their records staged in LDS (landmark_stage_kernel, below); the wider ones (long tracks) one
+// per workgroup, landmark_obs_wg_kernel, whose panel is per workgroup.  Measured on config C (r01-r04):
+// 1.04 + 0.72 ms against 2.63 for the per-column landmark_kernel; one 48 KB per-wave class for all ran at
+// 2.9 ms and the per-workgroup kernel for all at 2.1 (occupancy vs. barriers).
 // one observation's share of a half-wave (lane jj = slot column j of slot s): the point Jacobian
 // (broadcast), the lane's two slot-column planes, the packed panel column / block width of the slot, and
 // (lane jj == 0) the residual; observations past o1 load observation o0 and add nothing
@@ -132,40 +132,137 @@ __device__ __forceinline__ void obs_cols_add(const ObsCols& q, int j, double* W)
 
 constexpr int kLmBigCols = 2048;  // 3 x 2048 doubles = 48 KB of dynamic LDS per workgroup; wider: per-column path
 
-__global__ void __launch_bounds__(256) landmark_obs_kernel(Dev d, double lambda, int64_t first, int64_t n, int cap) {
-  extern __shared__ double Wl[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t li = (int64_t)blockIdx.x * 4 + wave;
-  if (li >= n) return;
-  const int64_t l = d.lmList[first + li];
-  const rec_t* Jt = d.Jt;
-  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
+// The narrow class with the landmark's records streamed through LDS (round 6): a landmark's observations
+// are consecutive, so its records are one contiguous span of each record region; the wave copies them in
+// chunks of kLmCh observations with 16 B global_load_lds (a handful of wide loads per chunk instead of
+// ~10 narrow loads per observation and half-wave), double-buffered (chunk k + 1 in flight while chunk k
+// is consumed), wave-private: one wave per workgroup, no barriers.  The half-waves then read their
+// observation's point Jacobian, residual and slot-column planes from LDS (inline-asm ds_reads behind one
+// wait: plain LDS loads would make the compiler drain the DMA in flight first, as in obs_group_kernel).
+constexpr int kRecV = 16 / (int)sizeof(rec_t);          // record elements per 16 B piece
+// observations per staged chunk: swept at config C (r06n, the elimination alone): fp64 2 / 3 / 4 / 6 / 8 / 16
+// -> 1265 / 1249 / 1239 / 1299 / 1331 / 1555 us (the LDS per wave sets the occupancy), fp32 records 2 / 3 / 4 /
+// 6 -> 1154 / 1161 / 1084 / 1070 us; the per-lane load form it replaces: 1339 / 1106 us
+constexpr int kLmCh = VIBA_MIXED ? 6 : 4;
+constexpr int kLmInA = (kLmCh * kJA / kRecV + 63) / 64;  // global_load_lds per chunk, region A
+constexpr int kLmInB = (kLmCh * kJB / kRecV + 63) / 64;  // region B (the tail lanes land in padding)
+constexpr int kLmBOff = kLmInA * 64 * kRecV;             // staged region B (rec_t offset in a buffer)
+constexpr int kLmCOff = (kLmInA + kLmInB) * 64 * kRecV;  // staged obCol words of the chunk (64 int32 slots)
+constexpr int kLmBuf = kLmCOff + 256 / (int)sizeof(rec_t);  // rec_t per buffer
+static_assert(kLmCh * kJA <= kLmBOff, "region A of a chunk fits its DMA slots");
+
+__device__ __forceinline__ void lm_issue(const Dev& d, int64_t oa, int nv, rec_t* buf, int lane) {
+  const rec_t* gA = d.Jt + oa * kJA;
+  const rec_t* gB = d.Jt + d.nObsPad * kJA + oa * kJB;
+  const int vA = nv * (kJA / kRecV), vB = nv * (kJB / kRecV);  // the chunk's pieces; others re-read piece 0
+#pragma unroll
+  for (int j = 0; j < kLmInA; j++) {
+    const int p = j * 64 + lane;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gA + (p < vA ? p : 0) * kRecV),
+                                     (__attribute__((address_space(3))) void*)(buf + j * 64 * kRecV), 16, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < kLmInB; j++) {
+    const int p = j * 64 + lane;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gB + (p < vB ? p : 0) * kRecV),
+                                     (__attribute__((address_space(3))) void*)(buf + kLmBOff + j * 64 * kRecV), 16, 0, 0);
+  }
+  // the packed panel column / width words of the chunk's observation slots (4 per observation)
+  const int32_t* gC = d.obCol + oa * 4;
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(gC + (lane < 4 * nv ? lane : 0)),
+                                   (__attribute__((address_space(3))) void*)(buf + kLmCOff), 4, 0, 0);
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+// one observation's share of a half-wave from the staged record: e (2), point Jacobian (6) at ra, the lane's
+// two slot-column planes at rx and rx1
+__device__ __forceinline__ void lm_read(const rec_t* ra, const rec_t* rx, const rec_t* rx1, const int32_t* rc,
+                                        double (&a)[6], double& e0, double& e1, double& x0, double& x1, int32_t& pc) {
+#if VIBA_MIXED
+  float v[10];
+  asm volatile(
+      "ds_read_b32 %0, %11\n\tds_read_b32 %1, %11 offset:4\n\tds_read_b32 %2, %11 offset:8\n\t"
+      "ds_read_b32 %3, %11 offset:12\n\tds_read_b32 %4, %11 offset:16\n\tds_read_b32 %5, %11 offset:20\n\t"
+      "ds_read_b32 %6, %11 offset:24\n\tds_read_b32 %7, %11 offset:28\n\tds_read_b32 %8, %12\n\t"
+      "ds_read_b32 %9, %13\n\tds_read_b32 %10, %14\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
+        "=&v"(v[8]), "=&v"(v[9]), "=&v"(pc)
+      : "v"(lds_u32(ra)), "v"(lds_u32(rx)), "v"(lds_u32(rx1)), "v"(lds_u32(rc))
+      : "memory");
+#else
+  double v[10];
+  asm volatile(
+      "ds_read_b64 %0, %11\n\tds_read_b64 %1, %11 offset:8\n\tds_read_b64 %2, %11 offset:16\n\t"
+      "ds_read_b64 %3, %11 offset:24\n\tds_read_b64 %4, %11 offset:32\n\tds_read_b64 %5, %11 offset:40\n\t"
+      "ds_read_b64 %6, %11 offset:48\n\tds_read_b64 %7, %11 offset:56\n\tds_read_b64 %8, %12\n\t"
+      "ds_read_b64 %9, %13\n\tds_read_b32 %10, %14\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
+        "=&v"(v[8]), "=&v"(v[9]), "=&v"(pc)
+      : "v"(lds_u32(ra)), "v"(lds_u32(rx)), "v"(lds_u32(rx1)), "v"(lds_u32(rc))
+      : "memory");
+#endif
+  static_assert(kJe == 0 && kJpt == 2, "record planes 0..7: e, point Jacobian");
+  e0 = v[0], e1 = v[1];
+#pragma unroll
+  for (int k = 0; k < 6; k++) a[k] = v[2 + k];
+  x0 = v[8], x1 = v[9];
+}
+
+__global__ void __launch_bounds__(64) landmark_stage_kernel(Dev d, double lambda, int64_t first, int cap) {
+  extern __shared__ __attribute__((aligned(16))) double lsm[];
+  rec_t* stg = reinterpret_cast<rec_t*>(lsm);  // two chunk buffers, then the W panel
+  double* W = lsm + (2 * kLmBuf * (int)sizeof(rec_t) + 7) / 8;
+  const int lane = threadIdx.x;
+  const int64_t l = d.lmList[first + xcd_block(blockIdx.x, gridDim.x)];
+  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1], n = o1 - o0;
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  double* W = Wl + wave * 3 * cap;  // cap: panel columns per wave of this launch
+  const int nch = (int)((n + kLmCh - 1) / kLmCh);
   for (int i = lane; i < 3 * ncol; i += 64) W[i] = 0.0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the clear landed before the asm atomics below
+  if (nch > 0) lm_issue(d, o0, (int)min<int64_t>(n, kLmCh), stg, lane);
   const int h = lane >> 5, jj = lane & 31;
   const int s = jj < 6 ? 0 : jj < 12 ? 1 : jj < 29 ? 2 : 3;
   const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
   const int pl = slotPlane(s) + j, st = slotStride(s);
+  // the lane's planes inside a staged record (a slot's planes never straddle the regions)
+  const int xo = pl < kJA ? pl : kLmBOff + (pl - kJA), xstep = pl < kJA ? kJA : kJB;
   double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  // software-pipelined by one observation: the next observation's record reads are in flight while
-  // this one's products go into the panel
-  ObsCols q, qn;
-  obs_cols_load(d, Jt, o0 + h, o1, o0, pl, st, s, jj, q);
-  for (int64_t o = o0 + h; o < o1; o += 2) {
-    obs_cols_load(d, Jt, o + 2, o1, o0, pl, st, s, jj, qn);
-    if (jj == 0) {
-      g0 += q.a[0] * q.e0 + q.a[3] * q.e1, g1 += q.a[1] * q.e0 + q.a[4] * q.e1, g2 += q.a[2] * q.e0 + q.a[5] * q.e1;
-      v00 += q.a[0] * q.a[0] + q.a[3] * q.a[3], v10 += q.a[1] * q.a[0] + q.a[4] * q.a[3];
-      v20 += q.a[2] * q.a[0] + q.a[5] * q.a[3], v11 += q.a[1] * q.a[1] + q.a[4] * q.a[4];
-      v21 += q.a[2] * q.a[1] + q.a[5] * q.a[4], v22 += q.a[2] * q.a[2] + q.a[5] * q.a[5];
+  for (int k = 0; k < nch; k++) {
+    const int64_t ob = o0 + (int64_t)k * kLmCh;
+    const int nv = (int)min<int64_t>(n - (int64_t)k * kLmCh, kLmCh);
+    if (k + 1 < nch) {  // buffer (k + 1) & 1: its reads (chunk k - 1) completed in program order
+      lm_issue(d, ob + kLmCh, (int)min<int64_t>(n - (int64_t)(k + 1) * kLmCh, kLmCh), stg + ((k + 1) & 1) * kLmBuf, lane);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLmInA + kLmInB + 1) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    obs_cols_add(q, j, W);
-    q = qn;
+    const rec_t* S = stg + (k & 1) * kLmBuf;
+    for (int c = h; c < nv + (nv & 1); c += 2) {  // both halves run the same trip count (odd tail: one idles)
+      const int cc = min(c, nv - 1);
+      double a[6], e0, e1, x0, x1;
+      int32_t pc;
+      lm_read(S + cc * kJA, S + xo + cc * xstep, S + xo + cc * xstep + st,
+              reinterpret_cast<const int32_t*>(S + kLmCOff) + 4 * cc + s, a, e0, e1, x0, x1, pc);
+      const bool valid = c < nv;
+      if (valid && jj == 0) {
+        g0 += a[0] * e0 + a[3] * e1, g1 += a[1] * e0 + a[4] * e1, g2 += a[2] * e0 + a[5] * e1;
+        v00 += a[0] * a[0] + a[3] * a[3], v10 += a[1] * a[0] + a[4] * a[3];
+        v20 += a[2] * a[0] + a[5] * a[3], v11 += a[1] * a[1] + a[4] * a[4];
+        v21 += a[2] * a[1] + a[5] * a[4], v22 += a[2] * a[2] + a[5] * a[5];
+      }
+      if (valid && pc >= 0 && j < (pc & 31)) {
+        // LDS atomics in inline asm: as atomicAdd the compiler put an s_waitcnt vmcnt(0) before them (it
+        // cannot tell W from the DMA target), draining the next chunk's loads at every observation
+        const int col = (pc >> 5) + j;
+        const double w0 = a[0] * x0 + a[3] * x1, w1 = a[1] * x0 + a[4] * x1, w2 = a[2] * x0 + a[5] * x1;
+        asm volatile("ds_add_f64 %0, %1\n\tds_add_f64 %0, %2 offset:8\n\tds_add_f64 %0, %3 offset:16"
+                     ::"v"(lds_u32(W + 3 * col)), "v"(w0), "v"(w1), "v"(w2)
+                     : "memory");
+      }
+    }
   }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // every atomic into W landed
   g0 = wave_sum(g0), g1 = wave_sum(g1), g2 = wave_sum(g2);
   v00 = wave_sum(v00), v10 = wave_sum(v10), v20 = wave_sum(v20);
   v11 = wave_sum(v11), v21 = wave_sum(v21), v22 = wave_sum(v22);
@@ -650,7 +747,6 @@ __device__ __forceinline__ void group_finish(const Dev& d, double lambda, int mo
 // 818 / 794 / 862 / 1045 / 1041 us (LDS per workgroup sets the occupancy); fp32 records 609 / 564 / 550 /
 // 543 / 632 us
 constexpr int kGrpChunk = VIBA_MIXED ? 32 : 24;
-constexpr int kRecV = 16 / (int)sizeof(rec_t);                     // record elements per 16 B piece
 constexpr int kRecPieces = kJPlanes / kRecV;                       // 16 B pieces per record (36 / 18)
 constexpr int kGrpLoads = (kGrpChunk * kRecPieces + 255) / 256;    // global_load_lds per thread per chunk
 constexpr int kGrpStage = kGrpLoads * 256 * kRecV;                 // rec_t per buffer (tail pieces land past the chunk)
@@ -794,8 +890,9 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
     launchK(landmark_z_kernel, dim3(blocks(hi - lo, 256)), dim3(256), 0, st, d, lo, hi);
   } else if (mode == 0 && lo == d.lmB && hi == d.lmE) {
     if (d.nLmSmall)
-      launchK(landmark_obs_kernel, dim3(blocks(d.nLmSmall, 4)), dim3(256),
-              (uint32_t)(4 * 3 * kLmSmallCols * sizeof(double)), st, d, lambda, (int64_t)0, d.nLmSmall, kLmSmallCols);
+      launchK(landmark_stage_kernel, dim3((unsigned)d.nLmSmall), dim3(64),
+              (uint32_t)((2 * kLmBuf * sizeof(rec_t) + 7) / 8 * 8 + 3 * kLmSmallCols * sizeof(double)), st, d, lambda,
+              (int64_t)0, kLmSmallCols);
     if (d.nLmBig && d.lmBigCols <= kLmBigCols)
       hipLaunchKernelGGL(landmark_obs_wg_kernel, dim3((unsigned)d.nLmBig), dim3(256),
                          (uint32_t)(3 * d.lmBigCols * sizeof(double)), st, d, lambda, d.nLmSmall, (int)d.lmBigCols);
