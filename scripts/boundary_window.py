@@ -9,5 +9,5 @@ i=vl[int(sys.argv[2])]
 t0=ks[i][0]
 j=i
 while not ks[j][2].startswith('boxplus_points'): j-=1
-while not ks[j][2].startswith('landmark_obs'):
+while not ks[j][2].startswith('landmark_'):
     s,e,n,q,g=ks[j]; print(f"{(s-t0)/1e3:8.1f} {(e-t0)/1e3:8.1f} {(e-s)/1e3:7.1f} q{q} g{g:6d} {n}"); j+=1

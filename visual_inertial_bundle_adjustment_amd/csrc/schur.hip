@@ -100,36 +100,6 @@ __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int
 // per workgroup, landmark_obs_wg_kernel, whose panel is per workgroup.  Measured on config C (r01-r04):
 // 1.04 + 0.72 ms against 2.63 for the per-column landmark_kernel; one 48 KB per-wave class for all ran at
 // 2.9 ms and the per-workgroup kernel for all at 2.1 (occupancy vs. barriers).
-// one observation's share of a half-wave (lane jj = slot column j of slot s): the point Jacobian
-// (broadcast), the lane's two slot-column planes, the packed panel column / block width of the slot, and
-// (lane jj == 0) the residual; observations past o1 load observation o0 and add nothing
-struct ObsCols {
-  double a[6], x0, x1, e0, e1;
-  int32_t pc;
-};
-__device__ __forceinline__ void obs_cols_load(const Dev& d, const rec_t* Jt, int64_t o, int64_t o1, int64_t o0, int pl,
-                                              int st, int s, int jj, ObsCols& q) {
-  const bool valid = o < o1;
-  if (!valid) o = o0;
-  const rec_t* r = Jt + o * kJA;
-#pragma unroll
-  for (int k = 0; k < 6; k++) q.a[k] = r[kJpt + k];
-  const rec_t* x = jt_plane(Jt, d.nObsPad, o, pl);
-  q.x0 = x[0], q.x1 = x[st];
-  q.pc = valid ? d.obCol[o * 4 + s] : -1;
-  q.e0 = jj == 0 ? (double)r[kJe] : 0.0, q.e1 = jj == 0 ? (double)r[kJe + 1] : 0.0;
-}
-// W(:, column) += Jp^T J_x(:, j) for the lane's slot column (LDS atomics: both half-waves may hit a shared
-// calibration block)
-__device__ __forceinline__ void obs_cols_add(const ObsCols& q, int j, double* W) {
-  if (q.pc >= 0 && j < (q.pc & 31)) {
-    const int c = (q.pc >> 5) + j;
-    atomicAdd(&W[3 * c + 0], q.a[0] * q.x0 + q.a[3] * q.x1);
-    atomicAdd(&W[3 * c + 1], q.a[1] * q.x0 + q.a[4] * q.x1);
-    atomicAdd(&W[3 * c + 2], q.a[2] * q.x0 + q.a[5] * q.x1);
-  }
-}
-
 constexpr int kLmBigCols = 2048;  // 3 x 2048 doubles = 48 KB of dynamic LDS per workgroup; wider: per-column path
 
 // The narrow class with the landmark's records streamed through LDS (round 6): a landmark's observations
@@ -209,35 +179,30 @@ __device__ __forceinline__ void lm_read(const rec_t* ra, const rec_t* rx, const 
   x0 = v[8], x1 = v[9];
 }
 
-__global__ void __launch_bounds__(64) landmark_stage_kernel(Dev d, double lambda, int64_t first, int cap) {
-  extern __shared__ __attribute__((aligned(16))) double lsm[];
-  rec_t* stg = reinterpret_cast<rec_t*>(lsm);  // two chunk buffers, then the W panel
-  double* W = lsm + (2 * kLmBuf * (int)sizeof(rec_t) + 7) / 8;
-  const int lane = threadIdx.x;
-  const int64_t l = d.lmList[first + xcd_block(blockIdx.x, gridDim.x)];
-  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1], n = o1 - o0;
-  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
+// one wave's share of a landmark's observations, from LDS: the chunks k = wave, wave + nwaves, ... of
+// kLmCh observations each (double-buffered in the wave's own two buffers at stg), W panel atomics in LDS;
+// v[0..8] = the lane's partial V (v00 v10 v20 v11 v21 v22) and g (lanes jj == 0 of each half only)
+__device__ __forceinline__ void lm_stage_loop(const Dev& d, int64_t o0, int64_t n, rec_t* stg, double* W, int wave,
+                                              int nwaves, int lane, double (&v)[9]) {
   const int nch = (int)((n + kLmCh - 1) / kLmCh);
-  for (int i = lane; i < 3 * ncol; i += 64) W[i] = 0.0;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the clear landed before the asm atomics below
-  if (nch > 0) lm_issue(d, o0, (int)min<int64_t>(n, kLmCh), stg, lane);
   const int h = lane >> 5, jj = lane & 31;
   const int s = jj < 6 ? 0 : jj < 12 ? 1 : jj < 29 ? 2 : 3;
   const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
   const int pl = slotPlane(s) + j, st = slotStride(s);
   // the lane's planes inside a staged record (a slot's planes never straddle the regions)
   const int xo = pl < kJA ? pl : kLmBOff + (pl - kJA), xstep = pl < kJA ? kJA : kJB;
-  double v00 = 0, v10 = 0, v20 = 0, v11 = 0, v21 = 0, v22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  for (int k = 0; k < nch; k++) {
+  auto nvOf = [&](int k) { return (int)min<int64_t>(n - (int64_t)k * kLmCh, kLmCh); };
+  if (wave < nch) lm_issue(d, o0 + (int64_t)wave * kLmCh, nvOf(wave), stg, lane);
+  for (int k = wave, b = 0; k < nch; k += nwaves, b ^= 1) {
     const int64_t ob = o0 + (int64_t)k * kLmCh;
-    const int nv = (int)min<int64_t>(n - (int64_t)k * kLmCh, kLmCh);
-    if (k + 1 < nch) {  // buffer (k + 1) & 1: its reads (chunk k - 1) completed in program order
-      lm_issue(d, ob + kLmCh, (int)min<int64_t>(n - (int64_t)(k + 1) * kLmCh, kLmCh), stg + ((k + 1) & 1) * kLmBuf, lane);
+    const int nv = nvOf(k);
+    if (k + nwaves < nch) {  // the other buffer: its reads (the wave's previous chunk) completed in program order
+      lm_issue(d, ob + (int64_t)nwaves * kLmCh, nvOf(k + nwaves), stg + (b ^ 1) * kLmBuf, lane);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLmInA + kLmInB + 1) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    const rec_t* S = stg + (k & 1) * kLmBuf;
+    const rec_t* S = stg + b * kLmBuf;
     for (int c = h; c < nv + (nv & 1); c += 2) {  // both halves run the same trip count (odd tail: one idles)
       const int cc = min(c, nv - 1);
       double a[6], e0, e1, x0, x1;
@@ -246,10 +211,10 @@ __global__ void __launch_bounds__(64) landmark_stage_kernel(Dev d, double lambda
               reinterpret_cast<const int32_t*>(S + kLmCOff) + 4 * cc + s, a, e0, e1, x0, x1, pc);
       const bool valid = c < nv;
       if (valid && jj == 0) {
-        g0 += a[0] * e0 + a[3] * e1, g1 += a[1] * e0 + a[4] * e1, g2 += a[2] * e0 + a[5] * e1;
-        v00 += a[0] * a[0] + a[3] * a[3], v10 += a[1] * a[0] + a[4] * a[3];
-        v20 += a[2] * a[0] + a[5] * a[3], v11 += a[1] * a[1] + a[4] * a[4];
-        v21 += a[2] * a[1] + a[5] * a[4], v22 += a[2] * a[2] + a[5] * a[5];
+        v[6] += a[0] * e0 + a[3] * e1, v[7] += a[1] * e0 + a[4] * e1, v[8] += a[2] * e0 + a[5] * e1;
+        v[0] += a[0] * a[0] + a[3] * a[3], v[1] += a[1] * a[0] + a[4] * a[3];
+        v[2] += a[2] * a[0] + a[5] * a[3], v[3] += a[1] * a[1] + a[4] * a[4];
+        v[4] += a[2] * a[1] + a[5] * a[4], v[5] += a[2] * a[2] + a[5] * a[5];
       }
       if (valid && pc >= 0 && j < (pc & 31)) {
         // LDS atomics in inline asm: as atomicAdd the compiler put an s_waitcnt vmcnt(0) before them (it
@@ -263,6 +228,21 @@ __global__ void __launch_bounds__(64) landmark_stage_kernel(Dev d, double lambda
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // every atomic into W landed
+}
+
+__global__ void __launch_bounds__(64) landmark_stage_kernel(Dev d, double lambda, int64_t first, int cap) {
+  extern __shared__ __attribute__((aligned(16))) double lsm[];
+  rec_t* stg = reinterpret_cast<rec_t*>(lsm);  // two chunk buffers, then the W panel
+  double* W = lsm + (2 * kLmBuf * (int)sizeof(rec_t) + 7) / 8;
+  const int lane = threadIdx.x;
+  const int64_t l = d.lmList[first + xcd_block(blockIdx.x, gridDim.x)];
+  const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1], n = o1 - o0;
+  const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
+  for (int i = lane; i < 3 * ncol; i += 64) W[i] = 0.0;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the clear landed before the asm atomics below
+  double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  lm_stage_loop(d, o0, n, stg, W, 0, 1, lane, v);
+  double v00 = v[0], v10 = v[1], v20 = v[2], v11 = v[3], v21 = v[4], v22 = v[5], g0 = v[6], g1 = v[7], g2 = v[8];
   g0 = wave_sum(g0), g1 = wave_sum(g1), g2 = wave_sum(g2);
   v00 = wave_sum(v00), v10 = wave_sum(v10), v20 = wave_sum(v20);
   v11 = wave_sum(v11), v21 = wave_sum(v21), v22 = wave_sum(v22);
@@ -300,34 +280,20 @@ __global__ void __launch_bounds__(64) landmark_stage_kernel(Dev d, double lambda
 // the same with one workgroup per landmark (its 8 half-waves share the observations, the W panel is
 // one per workgroup): for the wide class, whose per-wave panels would cap the occupancy
 __global__ void __launch_bounds__(256) landmark_obs_wg_kernel(Dev d, double lambda, int64_t first, int cap) {
-  extern __shared__ double W[];
+  // the four waves' staging buffers (lm_stage_loop: wave w takes chunks w, w + 4, ...), then the W panel
+  extern __shared__ __attribute__((aligned(16))) double lsm[];
   __shared__ double part[4][9];
   __shared__ double Ls[6];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  rec_t* stg = reinterpret_cast<rec_t*>(lsm) + wave * 2 * kLmBuf;
+  double* W = lsm + (8 * kLmBuf * (int)sizeof(rec_t) + 7) / 8;
   const int64_t l = d.lmList[first + blockIdx.x];
-  const rec_t* Jt = d.Jt;
   const int64_t o0 = d.lmObs[l], o1 = d.lmObs[l + 1];
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
   for (int i = tid; i < 3 * ncol; i += 256) W[i] = 0.0;
   __syncthreads();
-  const int h = tid >> 5, jj = lane & 31;
-  const int s = jj < 6 ? 0 : jj < 12 ? 1 : jj < 29 ? 2 : 3;
-  const int j = jj - (s == 0 ? 0 : s == 1 ? 6 : s == 2 ? 12 : 29);
-  const int pl = slotPlane(s) + j, st = slotStride(s);
   double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // v00 v10 v20 v11 v21 v22 g0 g1 g2
-  ObsCols q, qn;
-  obs_cols_load(d, Jt, o0 + h, o1, o0, pl, st, s, jj, q);
-  for (int64_t o = o0 + h; o < o1; o += 8) {
-    obs_cols_load(d, Jt, o + 8, o1, o0, pl, st, s, jj, qn);
-    if (jj == 0) {
-      v[6] += q.a[0] * q.e0 + q.a[3] * q.e1, v[7] += q.a[1] * q.e0 + q.a[4] * q.e1, v[8] += q.a[2] * q.e0 + q.a[5] * q.e1;
-      v[0] += q.a[0] * q.a[0] + q.a[3] * q.a[3], v[1] += q.a[1] * q.a[0] + q.a[4] * q.a[3];
-      v[2] += q.a[2] * q.a[0] + q.a[5] * q.a[3], v[3] += q.a[1] * q.a[1] + q.a[4] * q.a[4];
-      v[4] += q.a[2] * q.a[1] + q.a[5] * q.a[4], v[5] += q.a[2] * q.a[2] + q.a[5] * q.a[5];
-    }
-    obs_cols_add(q, j, W);
-    q = qn;
-  }
+  lm_stage_loop(d, o0, o1 - o0, stg, W, wave, 4, lane, v);
 #pragma unroll
   for (int k = 0; k < 9; k++) v[k] = wave_sum(v[k]);
   if (lane == 0)
@@ -895,7 +861,8 @@ void launch_landmark(const Dev& d, double lambda, int mode, int64_t lo, int64_t 
               (int64_t)0, kLmSmallCols);
     if (d.nLmBig && d.lmBigCols <= kLmBigCols)
       hipLaunchKernelGGL(landmark_obs_wg_kernel, dim3((unsigned)d.nLmBig), dim3(256),
-                         (uint32_t)(3 * d.lmBigCols * sizeof(double)), st, d, lambda, d.nLmSmall, (int)d.lmBigCols);
+                         (uint32_t)((8 * kLmBuf * sizeof(rec_t) + 7) / 8 * 8 + 3 * d.lmBigCols * sizeof(double)), st, d,
+                         lambda, d.nLmSmall, (int)d.lmBigCols);
     else if (d.nLmBig)
       hipLaunchKernelGGL(landmark_list_kernel, dim3(blocks(d.nLmBig, 4)), dim3(256), 0, st, d, lambda, d.nLmSmall,
                          d.nLmBig);
