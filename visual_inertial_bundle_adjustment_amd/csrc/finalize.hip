@@ -1026,6 +1026,7 @@ int doFinalize(vb_handle h) {
     if (getenv("VIBA_STATS")) {  // diagnostics: compact widths, MFMA padding, runs, tasks
       int64_t hI[5] = {0}, hJ[5] = {0}, nRun = 0, nTask = 0, runLm = 0;
       double useful = 0, issued = 0, issued4 = 0, gathered = 0, segBytes = 0;
+      double nlHist[17] = {0}, kDense = 0, kGroup = 0, gDense = 0, gGroup = 0;
       auto bin = [](int n) { return n <= 4 ? 0 : n <= 8 ? 1 : n <= 16 ? 2 : n <= 32 ? 3 : 4; };
       for (const TileWork& w : works) {
         const bool diag = w.I == w.J;
@@ -1054,6 +1055,14 @@ int doFinalize(vb_handle h) {
           const int nbI = (__builtin_popcountll(mI) + 15) / 16, nbJ = (__builtin_popcountll(mJ) + 15) / 16;
           const int nr = std::min(kSchurTR, nbJ - a0);
           gathered += 4.0 * ((3 * nl + 3) / 4) * (nr + nbI) * 16 * sizeof(rec_t);
+          // k-steps and gather instructions of the dense K mapping (3 rows per landmark, 4 per k-step) against a
+          // plane-grouped one (each lane group one landmark's 3 planes over 3 k-steps, the remainder dense)
+          int mf = 0;
+          for (int i = 0; i < nr; i++)
+            for (int b = 0; b < nbI; b++) mf += (!diag || a0 + i <= b) ? 1 : 0;
+          const int ksD = (3 * nl + 3) / 4, ksG = 3 * (nl / 4) + (3 * (nl % 4) + 3) / 4;
+          nlHist[std::min(nl, 16)] += 1.0, kDense += (double)ksD * mf, kGroup += (double)ksG * mf;
+          gDense += (double)ksD * (nr + nbI), gGroup += (double)((nl / 4) * 2 + (3 * (nl % 4) + 3) / 4) * (nr + nbI);
         }
         for (int e = 0; e < w.count; e++) {  // the entries' Y segments once per item
           const TileEnt& a = ents[w.start + e];
@@ -1068,6 +1077,10 @@ int doFinalize(vb_handle h) {
               (long long)hI[0], (long long)hI[1], (long long)hI[2], (long long)hI[3], (long long)hI[4], (long long)hJ[0],
               (long long)hJ[1], (long long)hJ[2], (long long)hJ[3], (long long)hJ[4], useful * 1e-9, issued * 1e-9,
               issued4 * 1e-9, gathered * 1e-9, segBytes * 1e-9);
+      fprintf(stderr, "[schur stats] tasks by landmarks:");
+      for (int k = 1; k <= 16; k++) fprintf(stderr, " %d:%.0f", k, nlHist[k]);
+      fprintf(stderr, "; MFMAs dense K %.3g, plane-grouped K %.3g; gather instructions dense %.3g, plane-grouped %.3g\n",
+              kDense, kGroup, gDense, gGroup);
     }
     if (upload(&d.schurRuns, runsH) || upload(&d.schurTasks, tasksH)) return VB_E_HIP;
     // longest-first is unnecessary: chunks are bounded; keep column order (locality of Y / records)
