@@ -370,8 +370,11 @@ constexpr int kTR = kSchurTR;  // compact block rows per task (1 or 2)
 
 // C -= acc of one task through the run's compact -> tile row maps: every map entry of the task read up
 // front (one LDS wait), the adds predicated
+// the plane groups' loads one group ahead (fp64: the operands of two groups and the accumulators need three
+// waves per SIMD; at four the kernel spilled 164 VGPRs and ran 2x slower) or not (fp32 records: four waves per
+// SIMD with no spill, the other waves cover the latency: 2026 -> 1726 us alone at config C, r06r)
 #ifndef VIBA_SCHUR_PF
-#define VIBA_SCHUR_PF 1
+#define VIBA_SCHUR_PF (VIBA_MIXED ? 0 : 1)
 #endif
 // one panel column's three planes of the plane-interleaved Y: a 16 B and an 8 B load (fp64), one 12 B load (fp32)
 __device__ __forceinline__ void load3(const double* p, double (&v)[3]) {
@@ -502,10 +505,12 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     }
   }
 #else
+#pragma unroll 1
   for (int m = 0; m < nfull; m++) {  // (the other waves of the SIMD cover the loads' latency)
     rec_t a3[NR][3], b3[NBI][3];
     ld3(m, a3, b3);
     mm3(a3, b3);
+    __builtin_amdgcn_sched_barrier(0);  // no hoisting of the next group's loads (register pressure)
   }
 #endif
   // the remaining nl % 4 landmarks, dense: K row kr = 4 ks + l4 is plane kr % 3 of landmark kr / 3 (advanced
