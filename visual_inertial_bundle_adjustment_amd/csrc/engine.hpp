@@ -168,8 +168,8 @@ struct Dev {
   int64_t* bxStart = nullptr; // per landmark block: its observation slots bxEnt[bxStart[b] ..)
   int32_t* bxEnt = nullptr;   // (obs << 2) | slot
   double *Vchol = nullptr, *gp = nullptr, *z = nullptr, *xp = nullptr;
-  rec_t* yZero = nullptr;  // 128 zeros: the gathers of K rows past a Schur task's landmarks
-  rec_t* Y = nullptr;  // landmark panels Y = L^-1 W, q-planar: row q of global panel column c at Y[q * nYcol + c] (fp32 in the VIBA_MIXED build)
+  rec_t* yZero = nullptr;  // 256 zeros: the gathers of K rows past a Schur task's landmarks
+  rec_t* Y = nullptr;  // landmark panels Y = L^-1 W, plane-interleaved: row q of global panel column c at Y[3 c + q] (fp32 in the VIBA_MIXED build)
   double *gpNew = nullptr, *zNew = nullptr;
   int32_t* ptRed = nullptr;  // point param registered? (1/0) per point var handle
   int32_t* ptLm = nullptr;   // point var handle -> landmark index (-1)

@@ -1460,7 +1460,7 @@ int doFinalize(vb_handle h) {
       upload(&d.bxStart, bxStart) || upload(&d.bxEnt, bxEnt))
     return VB_E_HIP;
   if (alloc0(&d.Vchol, nPts * 6) || alloc0(&d.gp, nPts * 3) || alloc0(&d.z, nPts * 3) || alloc0(&d.xp, nPts * 3) ||
-      alloc0(&d.Y, lmY[nPts] + 128) || alloc0(&d.yZero, 128) ||  // + the over-read of the Schur gathers
+      alloc0(&d.Y, lmY[nPts] + 128) || alloc0(&d.yZero, 256) ||  // + the over-read of the Schur gathers
       alloc0(&d.gpNew, nPts * 3) || alloc0(&d.zNew, nPts * 3))
     return VB_E_HIP;
   std::vector<int64_t> lxChunk;

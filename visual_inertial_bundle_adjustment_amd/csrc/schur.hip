@@ -59,8 +59,7 @@ __device__ __forceinline__ void landmark_eliminate(const Dev& d, double lambda, 
     d.gp[l * 3] = g0, d.gp[l * 3 + 1] = g1, d.gp[l * 3 + 2] = g2;
   }
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
-  const int64_t yq = d.nYcol;
+  rec_t* Y = d.Y + d.lmY[l];  // plane-interleaved: plane q of panel column c at Y[3 c + q]
   for (int64_t c = lane; c < ncol; c += 64) {
     const int32_t b = d.pcBlk[cb + c];
     const int j = (int)(c - d.blkCol[b]);
@@ -79,7 +78,7 @@ __device__ __forceinline__ void landmark_eliminate(const Dev& d, double lambda, 
     const double y0 = w0 / l00;
     const double y1 = (w1 - l10 * y0) / l11;
     const double y2 = (w2 - l20 * y0 - l21 * y1) / l22;
-    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
+    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
   }
 }
 __global__ void __launch_bounds__(256) landmark_kernel(Dev d, double lambda, int mode, int64_t lo, int64_t hi) {
@@ -267,13 +266,12 @@ __global__ void __launch_bounds__(64) landmark_stage_kernel(Dev d, double lambda
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
-  const int64_t yq = d.nYcol;
+  rec_t* Y = d.Y + d.lmY[l];  // plane-interleaved: plane q of panel column c at Y[3 c + q]
   for (int64_t c = lane; c < ncol; c += 64) {
     const double y0 = W[3 * c] / l00;
     const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
     const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
-    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
+    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
   }
 }
 
@@ -322,13 +320,12 @@ __global__ void __launch_bounds__(256) landmark_obs_wg_kernel(Dev d, double lamb
   }
   __syncthreads();
   const double l00 = Ls[0], l10 = Ls[1], l20 = Ls[2], l11 = Ls[3], l21 = Ls[4], l22 = Ls[5];
-  rec_t* Y = d.Y + d.lmY[l] / 3;  // q-planar: plane q at Y + q * nYcol
-  const int64_t yq = d.nYcol;
+  rec_t* Y = d.Y + d.lmY[l];  // plane-interleaved: plane q of panel column c at Y[3 c + q]
   for (int64_t c = tid; c < ncol; c += 256) {
     const double y0 = W[3 * c] / l00;
     const double y1 = (W[3 * c + 1] - l10 * y0) / l11;
     const double y2 = (W[3 * c + 2] - l20 * y0 - l21 * y1) / l22;
-    Y[c] = y0, Y[yq + c] = y1, Y[2 * yq + c] = y2;
+    Y[3 * c] = y0, Y[3 * c + 1] = y1, Y[3 * c + 2] = y2;
   }
 }
 
@@ -373,6 +370,24 @@ constexpr int kTR = kSchurTR;  // compact block rows per task (1 or 2)
 
 // C -= acc of one task through the run's compact -> tile row maps: every map entry of the task read up
 // front (one LDS wait), the adds predicated
+// the plane groups' loads one group ahead (fp64: the operands of two groups and the accumulators need three
+// waves per SIMD; at four the kernel spilled 164 VGPRs and ran 2x slower) or not (fp32 records: four waves per
+// SIMD with no spill, the other waves cover the latency: 2026 -> 1726 us alone at config C, r06r)
+#ifndef VIBA_SCHUR_PF
+#define VIBA_SCHUR_PF (VIBA_MIXED ? 0 : 1)
+#endif
+// one panel column's three planes of the plane-interleaved Y: a 16 B and an 8 B load (fp64), one 12 B load (fp32)
+__device__ __forceinline__ void load3(const double* p, double (&v)[3]) {
+  typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
+  const d2u x = *reinterpret_cast<const d2u*>(p);
+  v[0] = x.x, v[1] = x.y, v[2] = p[2];
+}
+__device__ __forceinline__ void load3(const float* p, float (&v)[3]) {
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  const f3u x = *reinterpret_cast<const f3u*>(p);
+  v[0] = x.x, v[1] = x.y, v[2] = x.z;
+}
+
 template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], int a0, int l4, int l15,
                                                const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
@@ -399,25 +414,24 @@ __device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], in
 // landmarks' loads in flight per step
 __device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2], const TileEnt* ents, int c0, int nl,
                                           int lane, const uint8_t* posI, double* rq) {
-  const int64_t pq = d.nYcol;
   double racc = 0.0;
   int e = c0;
   for (; e + 4 <= c0 + nl; e += 4) {
     double y[4][3], z[4][3];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const rec_t* yp = d.Y + (int64_t)ecol[e + u][0] + lane;
+      const rec_t* yp = d.Y + 3 * ((int64_t)ecol[e + u][0] + lane);
       const double* zz = d.z + 3 * (int64_t)ents[e + u].lm;
 #pragma unroll
-      for (int q = 0; q < 3; q++) y[u][q] = (double)yp[q * pq], z[u][q] = zz[q];
+      for (int q = 0; q < 3; q++) y[u][q] = (double)yp[q], z[u][q] = zz[q];
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) racc += y[u][0] * z[u][0] + y[u][1] * z[u][1] + y[u][2] * z[u][2];
   }
   for (; e < c0 + nl; e++) {
-    const rec_t* y = d.Y + (int64_t)ecol[e][0] + lane;
+    const rec_t* y = d.Y + 3 * ((int64_t)ecol[e][0] + lane);
     const double* zz = d.z + 3 * (int64_t)ents[e].lm;
-    racc += (double)y[0] * zz[0] + (double)y[pq] * zz[1] + (double)y[2 * pq] * zz[2];
+    racc += (double)y[0] * zz[0] + (double)y[1] * zz[1] + (double)y[2] * zz[2];
   }
   atomicAdd(&rq[posI[lane]], -racc);
 }
@@ -437,57 +451,89 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
   for (int i = 0; i < NR; i++)
 #pragma unroll
     for (int b = 0; b < NBI; b++) acc[i][b] = hacc4_t{0, 0, 0, 0};
-  const int nks = (rows + 3) >> 2;
-  const int64_t pq = d.nYcol;
-  const rec_t* Y = d.Y;
-  const rec_t* zp = d.yZero + l15;
-  int kr = l4, e = c0 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
-  auto ld = [&](rec_t (&av)[NR], rec_t (&bv)[NBI]) {
-    const bool kv = kr < rows;
-#if VIBA_SCHUR_L2PROBE == 1  // diagnostic build (timing only, S is garbage): gathers confined to 4096 columns
-    const uint2 c = make_uint2(ec[kv ? e : c0].x & 4095u, ec[kv ? e : c0].y & 4095u);
-#elif VIBA_SCHUR_L2PROBE == 6  // diagnostic (timing only): every 16-column gather row on one 128 B line
-    const uint2 c = make_uint2(ec[kv ? e : c0].x & ~15u, ec[kv ? e : c0].y & ~15u);
-#else
-    const uint2 c = ec[kv ? e : c0];
-#endif
-#if VIBA_SCHUR_L2PROBE == 6
-    const rec_t* base = Y + ((q == 0 ? 0 : q == 1 ? pq : 2 * pq) & ~(int64_t)15) + l15;
-#else
-    const rec_t* base = Y + (q == 0 ? 0 : q == 1 ? pq : 2 * pq) + l15;
-#endif
-#if VIBA_SCHUR_L2PROBE == 5  // diagnostic (timing only): every gather reads the zero pad (one L1 line)
-    const rec_t* pJ = zp;
-    const rec_t* pI = zp + (kv ? 0 : 0);
-#else
-    const rec_t* pJ = kv ? base + c.y + 16 * a0 : zp;
-    const rec_t* pI = kv ? base + c.x : zp;
-#endif
-#pragma unroll
-    for (int i = 0; i < NR; i++) av[i] = pJ[16 * i];
-#pragma unroll
-    for (int b = 0; b < NBI; b++) bv[b] = pI[16 * b];
-    kr += 4, e += 1, q += 1;
-    if (q == 3) q = 0, e += 1;
-  };
+  const rec_t* Y = d.Y;  // plane-interleaved: plane q of global panel column c at Y[3 c + q]
   auto mm = [&](const rec_t (&av)[NR], const rec_t (&bv)[NBI]) {
 #pragma unroll
     for (int i = 0; i < NR; i++)
 #pragma unroll
       for (int b = 0; b < NBI; b++)
-#if VIBA_SCHUR_L2PROBE == 2  // diagnostic build (timing only): the operands consumed without the MFMAs
-        if (!DIAG || a0 + i <= b) acc[i][b][0] += (double)av[i] * (double)bv[b];
-#else
         if (!DIAG || a0 + i <= b) acc[i][b] = mfma_h(av[i], bv[b], acc[i][b]);
-#endif
   };
-  rec_t a0v[NR], b0v[NBI], a1v[NR], b1v[NBI];
-  ld(a0v, b0v);
-  for (int ks = 0; ks < nks; ks += 2) {
-    if (ks + 1 < nks) ld(a1v, b1v);
-    mm(a0v, b0v);
-    if (ks + 2 < nks) ld(a0v, b0v);
-    if (ks + 1 < nks) mm(a1v, b1v);
+  // groups of four landmarks: lane group l4 takes landmark c0 + 4 m + l4 and its three planes over three
+  // consecutive k-steps, so its operands of those k-steps are one column's three consecutive values (one 16 B
+  // and one 8 B load per operand block instead of three 8 B gathers); the next group's loads are issued
+  // before this group's MFMAs
+  const int nl = rows / 3, nfull = nl >> 2;
+  auto ld3 = [&](int m, rec_t (&a3)[NR][3], rec_t (&b3)[NBI][3]) {
+    const uint2 c = ec[c0 + 4 * m + l4];
+    const rec_t* pJ = Y + 3 * ((int64_t)c.y + 16 * a0 + l15);
+    const rec_t* pI = Y + 3 * ((int64_t)c.x + l15);
+#pragma unroll
+    for (int i = 0; i < NR; i++) load3(pJ + 48 * i, a3[i]);
+#pragma unroll
+    for (int b = 0; b < NBI; b++) load3(pI + 48 * b, b3[b]);
+  };
+  auto mm3 = [&](const rec_t (&a3)[NR][3], const rec_t (&b3)[NBI][3]) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      rec_t av[NR], bv[NBI];
+#pragma unroll
+      for (int i = 0; i < NR; i++) av[i] = a3[i][q];
+#pragma unroll
+      for (int b = 0; b < NBI; b++) bv[b] = b3[b][q];
+      mm(av, bv);
+    }
+  };
+#if VIBA_SCHUR_PF
+  if (nfull > 0) {
+    rec_t a3[NR][3], b3[NBI][3];
+    ld3(0, a3, b3);
+    for (int m = 0; m < nfull; m++) {
+      rec_t a3n[NR][3], b3n[NBI][3];
+      if (m + 1 < nfull) ld3(m + 1, a3n, b3n);
+      mm3(a3, b3);
+      if (m + 1 < nfull) {
+#pragma unroll
+        for (int i = 0; i < NR; i++)
+#pragma unroll
+          for (int q = 0; q < 3; q++) a3[i][q] = a3n[i][q];
+#pragma unroll
+        for (int b = 0; b < NBI; b++)
+#pragma unroll
+          for (int q = 0; q < 3; q++) b3[b][q] = b3n[b][q];
+      }
+    }
+  }
+#else
+#pragma unroll 1
+  for (int m = 0; m < nfull; m++) {  // (the other waves of the SIMD cover the loads' latency)
+    rec_t a3[NR][3], b3[NBI][3];
+    ld3(m, a3, b3);
+    mm3(a3, b3);
+    __builtin_amdgcn_sched_barrier(0);  // no hoisting of the next group's loads (register pressure)
+  }
+#endif
+  // the remaining nl % 4 landmarks, dense: K row kr = 4 ks + l4 is plane kr % 3 of landmark kr / 3 (advanced
+  // incrementally); K rows past them read the zero pad
+  const int c1 = c0 + 4 * nfull, rrows = 3 * (nl - 4 * nfull);
+  if (rrows > 0) {
+    const int nks = (rrows + 3) >> 2;
+    const rec_t* zp = d.yZero + 3 * l15;
+    int kr = l4, e = c1 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
+    for (int ks = 0; ks < nks; ks++) {
+      const bool kv = kr < rrows;
+      const uint2 c = ec[kv ? e : c1];
+      const rec_t* pJ = kv ? Y + 3 * ((int64_t)c.y + 16 * a0 + l15) + q : zp;
+      const rec_t* pI = kv ? Y + 3 * ((int64_t)c.x + l15) + q : zp;
+      rec_t av[NR], bv[NBI];
+#pragma unroll
+      for (int i = 0; i < NR; i++) av[i] = pJ[48 * i];
+#pragma unroll
+      for (int b = 0; b < NBI; b++) bv[b] = pI[48 * b];
+      mm(av, bv);
+      kr += 4, e += 1, q += 1;
+      if (q == 3) q = 0, e += 1;
+    }
   }
   // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
 #if VIBA_SCHUR_L2PROBE == 3  // diagnostic (timing only): no epilogue (one LDS add keeps the k-loop live)
@@ -508,7 +554,7 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
 // entries).  The item's runs (masks) and its tasks come precomputed from finalize (api.hip), the
 // tasks dealt to the waves longest-first (TileWork::wOff), so the kernel has no run scan and the waves
 // are balanced at the final barrier.  Four waves per SIMD (the k-loops are bound by gather latency).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) schur_run4_kernel(Dev d, double lambda) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_SCHUR_PF ? 3 : 4, VIBA_SCHUR_PF ? 3 : 4))) schur_run4_kernel(Dev d, double lambda) {
   __shared__ double C[TS * TS];
   __shared__ uint32_t ecol[256][2];
   __shared__ uint64_t rmask[256][2];
@@ -833,13 +879,12 @@ __global__ void __launch_bounds__(256) reduced_rhs_kernel(Dev d) {
   // landmark's 3 d1 values per lane
   const int P = d1 <= 4 ? 4 : d1 <= 8 ? 8 : d1 <= 16 ? 16 : 32;
   const int S = 64 / P, slot = lane / P, j = lane % P;
-  const int64_t yq = d.nYcol;
   double acc = 0.0;
   for (int64_t idx = ch[1] + wave * S + slot; idx < ch[2]; idx += 4 * S) {
     const int64_t l = d.lxLm[idx];
     if (j >= d1 || l < d.lmB || l >= d.lmE) continue;
-    const rec_t* y1 = d.Y + d.lmY[l] / 3 + d.lxCol[idx] + j;
-    acc += (double)y1[0] * d.zNew[l * 3] + (double)y1[yq] * d.zNew[l * 3 + 1] + (double)y1[2 * yq] * d.zNew[l * 3 + 2];
+    const rec_t* y1 = d.Y + d.lmY[l] + 3 * (d.lxCol[idx] + j);
+    acc += (double)y1[0] * d.zNew[l * 3] + (double)y1[1] * d.zNew[l * 3 + 1] + (double)y1[2] * d.zNew[l * 3 + 2];
   }
   for (int o = P; o < 64; o <<= 1) acc += __shfl_xor(acc, o, 64);  // over the landmark slots
   if (lane < P && lane < d1) g[wave][lane] = acc;

@@ -1082,16 +1082,15 @@ __global__ void __launch_bounds__(256) backsub_kernel(Dev d, int mode, int64_t l
   const int64_t l = lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (l >= hi) return;
   const int64_t cb = d.lmY[l] / 3, ncol = d.lmY[l + 1] / 3 - cb;
-  const rec_t* Y = d.Y + cb;
-  const int64_t yq = d.nYcol;
+  const rec_t* Y = d.Y + 3 * cb;  // plane-interleaved: plane q of column c at Y[3 c + q]
   double t0 = 0, t1 = 0, t2 = 0;
   // two columns per lane and step: both row-index loads, then both gathers of x, in flight together
   for (int64_t c = lane; c < ncol; c += 128) {
     const bool two = c + 64 < ncol;
     const int32_t ra = d.pcRow[cb + c], rb = two ? d.pcRow[cb + c + 64] : ra;
-    const double ya0 = Y[c], ya1 = Y[yq + c], ya2 = Y[2 * yq + c];
-    const double yb0 = two ? (double)Y[c + 64] : 0.0, yb1 = two ? (double)Y[yq + c + 64] : 0.0;
-    const double yb2 = two ? (double)Y[2 * yq + c + 64] : 0.0;
+    const double ya0 = Y[3 * c], ya1 = Y[3 * c + 1], ya2 = Y[3 * c + 2];
+    const double yb0 = two ? (double)Y[3 * (c + 64)] : 0.0, yb1 = two ? (double)Y[3 * (c + 64) + 1] : 0.0;
+    const double yb2 = two ? (double)Y[3 * (c + 64) + 2] : 0.0;
     const double va = xr[ra], vb = xr[rb];
     t0 += ya0 * va + yb0 * vb, t1 += ya1 * va + yb1 * vb, t2 += ya2 * va + yb2 * vb;
   }
