@@ -351,8 +351,8 @@ __global__ void __launch_bounds__(256) landmark_z_kernel(Dev d, int64_t lo, int6
 // ------------------------------------------------------------------ Schur column assembly
 
 
-// Schur assembly by target tile (api.hip builds the work list; engine.hpp TileWork / TileEnt), in
-// compact runs with register operands.  api.hip sorts every tile's landmark entries by their (row mask
+// Schur assembly by target tile (finalize.hip builds the work list; engine.hpp TileWork / TileEnt), in
+// compact runs with register operands.  finalize.hip sorts every tile's landmark entries by their (row mask
 // in tile I, row mask in tile J): a work item is a sequence of RUNS of landmarks touching exactly the
 // same tile rows.  Within a run the c-th panel column of a landmark inside tile I is compact column c
 // (its rows ascend with its columns), K is dense (3 rows per landmark), and the compact nJ x nI product
@@ -360,9 +360,8 @@ __global__ void __launch_bounds__(256) landmark_z_kernel(Dev d, int64_t lo, int6
 // on config C against 70M for the tile-coordinate form (16-row masks, one padded k-step per landmark;
 // that form and the LDS-image forms are in the history).  No images and no barriers: a task is (run, chunk of <= kCh landmarks, compact
 // block row a of the J side); a wave takes every fourth task of its item and accumulates the nI-wide
-// block row over the chunk's dense K (3 rows per landmark), its operands gathered straight from the Y
-// panel (lane l: compact column 16 a + (l & 15) / 16 b + (l & 15), K row 4 ks + (l >> 4)), the next
-// k-step's loads issued before the current MFMAs.  At the end of the task the block row is added into
+// block row over the chunk's K (3 rows per landmark), its operands loaded straight from the Y panel (lane l:
+// compact column 16 a + (l & 15) / 16 b + (l & 15); K rows by plane groups, schur_task).  At the end of the task the block row is added into
 // the item's LDS tile accumulator with LDS atomics (tasks of different waves overlap), through
 // wave-private compact -> tile row maps.
 constexpr int kCh = kSchurCh;  // landmarks per task
@@ -436,13 +435,15 @@ __device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2
   atomicAdd(&rq[posI[lane]], -racc);
 }
 
-// One task's K loop: acc[i][b] += A_i^T B_b over the dense K rows (3 per landmark) of landmarks
-// c0 .. c0 + rows / 3, A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block
-// b < NBI.  Lane (l4, l15) at k-step ks takes K row kr = 4 ks + l4, i.e. plane q = kr % 3 of landmark
-// c0 + kr / 3 (advanced incrementally), and gathers its NR + NBI operands at fixed offsets 16 i / 16 b
-// from the landmark's first panel column in tile J / I.  Columns past nJ / nI load neighbouring
-// panel data into accumulator rows / columns that are never stored; K rows past `rows` read the zero
-// pad.  The next step's gathers are issued before the current step's MFMAs.
+// One task's K loop: acc[i][b] += A_i^T B_b over the K rows (3 per landmark) of landmarks c0 .. c0 + rows / 3,
+// A_i = compact J-side block row a0 + i (NR of them), B_b = compact I-side block b < NBI.  Round 6: Y is
+// plane-interleaved (plane q of panel column c at Y[3 c + q]) and the K rows are taken in plane groups: per
+// group of four landmarks, lane group l4 takes landmark c0 + 4 m + l4 and its three planes over three
+// consecutive k-steps, so a lane loads one column's three planes at once (a 16 B and an 8 B load, or one 12 B
+// load for fp32 records) instead of three 8 B gathers for three k-steps (the gathers cost as instructions:
+// DESIGN.md §4).  The task's last nl % 4 landmarks keep the dense mapping (K row kr = 4 ks + l4 is plane
+// kr % 3 of landmark kr / 3).  Columns past nJ / nI load neighbouring panel data into accumulator rows /
+// columns that are never stored; K rows past `rows` read the zero pad.
 template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0, int rows, int a0, int l4, int l15,
                                            const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
@@ -536,18 +537,7 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     }
   }
   // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
-#if VIBA_SCHUR_L2PROBE == 3  // diagnostic (timing only): no epilogue (one LDS add keeps the k-loop live)
-  double sum = 0.0;
-#pragma unroll
-  for (int i = 0; i < NR; i++)
-#pragma unroll
-    for (int b = 0; b < NBI; b++)
-#pragma unroll
-      for (int q = 0; q < 4; q++) sum += (double)acc[i][b][q];
-  asm volatile("" ::"v"(sum));  // consumed: the k-loop cannot be sunk or dropped
-#else
   schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
-#endif
 }
 
 // Schur tile products, one workgroup per work item (TileWork: a target tile and <= 256 of its landmark
@@ -619,10 +609,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
   }
   __syncthreads();
   double* Ct = d.tiles + (int64_t)wk.tile * TS * TS;
-#if VIBA_SCHUR_L2PROBE == 4  // diagnostic (timing only): no tile write-back
-  if (C[tid] == 12345.0) Ct[tid] = 0.0;
-  return;
-#endif
   if (wk.kind == 1) {
     for (int i = tid; i < TS * TS; i += 256)
       if (C[i] != 0.0) atomicAdd(Ct + i, C[i]);
