@@ -9,10 +9,8 @@ TAG=${1:-r01}
 COMMIT=${2:-unknown}  # the commit of the measured sources (the box has no .git): stamped into the PMC summary
 timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.log || exit $?
 cd /tmp
-# rocprofv3 kernel tracing crashes (host SIGSEGV) on replays of the captured hipGraphs; the profiled
-# kernel family runs eagerly in bench.py anyway, so the profiled runs turn graphs off
-export VIBA_NO_GRAPHS=1
+# (rocprofv3 traces the graph replays too since ROCm 7.2; the two-stream factorization launches eagerly)
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --no-cpu-baseline --no-banded-count > $R/gpurun_out/bench_${TAG}_prof.json 2> $R/gpurun_out/bench_${TAG}_prof.log || exit $?
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "fanin_kernel|visual_lin_kernel|schur_run[0-9]_kernel|landmark_obs|obs_group_kernel|trsm_kernel|potrf|small_assemble|zero_tiles" --output-format csv -d $R/gpurun_out/pmc_fetch_$TAG -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-banded-count > /dev/null 2> $R/gpurun_out/pmc_fetch_$TAG.log || exit $?
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "fanin_kernel|visual_lin_kernel|schur_run[0-9]_kernel|landmark_obs|obs_group_kernel|trsm_kernel|potrf|small_assemble|zero_tiles" --output-format csv -d $R/gpurun_out/pmc_write_$TAG -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-banded-count > /dev/null 2> $R/gpurun_out/pmc_write_$TAG.log || exit $?
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "fanin_kernel|visual_lin_kernel|schur_run[0-9]_kernel|landmark_|obs_group_kernel|trsm_kernel|potrf|small_assemble|zero_tiles" --output-format csv -d $R/gpurun_out/pmc_fetch_$TAG -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-banded-count > /dev/null 2> $R/gpurun_out/pmc_fetch_$TAG.log || exit $?
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "fanin_kernel|visual_lin_kernel|schur_run[0-9]_kernel|landmark_|obs_group_kernel|trsm_kernel|potrf|small_assemble|zero_tiles" --output-format csv -d $R/gpurun_out/pmc_write_$TAG -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-banded-count > /dev/null 2> $R/gpurun_out/pmc_write_$TAG.log || exit $?
 cd $R && python scripts/pmc_summary.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG gpurun_out/pmc_summary_$TAG.json $COMMIT > /dev/null
