@@ -167,11 +167,13 @@ def mixed_vs_fp64(p, device, rs_device):
 
 
 def banded_contributions(p, device, rs_device, precision):
-    """Tile-pair contributions of the reduced system's Cholesky in the time order (VIBA_ND_OFF: the
-    symbolic analysis without the nested dissection), from a second handle that is only finalized."""
+    """Tile-pair contributions of the reduced system's Cholesky in the time order (a nested-dissection
+    leaf larger than the whole system: one part, in time order), from a second handle that is only
+    finalized."""
     from visual_inertial_bundle_adjustment_amd import synth
     from visual_inertial_bundle_adjustment_amd.engine import HipEngine
-    os.environ["VIBA_ND_OFF"] = "1"
+    prev = os.environ.get("VIBA_ND_LEAF")
+    os.environ["VIBA_ND_LEAF"] = str(1 << 62)
     try:
         eb = HipEngine(imu_calib_options=p.imu_calib_options, device=device, precision=precision)
         try:
@@ -180,7 +182,10 @@ def banded_contributions(p, device, rs_device, precision):
         finally:
             eb.close()
     finally:
-        del os.environ["VIBA_ND_OFF"]
+        if prev is None:
+            del os.environ["VIBA_ND_LEAF"]
+        else:
+            os.environ["VIBA_ND_LEAF"] = prev
 
 
 def spawn_ranks(n: int) -> int:

@@ -56,3 +56,14 @@ def test_stats_knob_prints_and_changes_nothing(capfd):
     assert tuple(st0) == tuple(st1) and abs(mr0 - mr1) <= 1e-11 * abs(mr0)
     for a, b in zip(s0, s1):
         assert rel(np.asarray(a), np.asarray(b)) < 1e-10
+
+
+def test_time_order_leaf_same_step_more_contributions():
+    """A leaf larger than the system (VIBA_ND_LEAF, what bench.py's banded count sets): one part in time
+    order, the band the reference's solver sees. Same step; the dissection needs fewer contributions."""
+    st_nd, mr_nd, s_nd = _run({})
+    st_tm, mr_tm, s_tm = _run({"VIBA_ND_LEAF": str(1 << 62)})
+    assert st_tm[6] > st_nd[6], (st_tm[6], st_nd[6])
+    assert abs(mr_tm - mr_nd) <= 1e-9 * abs(mr_nd)
+    for a, b in zip(s_tm, s_nd):
+        assert rel(np.asarray(a), np.asarray(b)) < 1e-8
