@@ -58,7 +58,7 @@ def test_stats_knob_prints_and_changes_nothing(capfd):
         assert rel(np.asarray(a), np.asarray(b)) < 1e-10
 
 
-def test_time_order_leaf_same_step_more_contributions():
+def test_time_order_leaf_same_step_fewer_contributions_more_levels():
     """A leaf larger than the system (VIBA_ND_LEAF, what bench.py's banded count sets): one part in time
     order, the band the reference's solver sees. Same step. The band needs fewer tile contributions (config B:
     69k against the dissection's 132k) but is one long chain of dependent columns: the dissection buys its
