@@ -370,8 +370,9 @@ constexpr int kTR = kSchurTR;  // compact block rows per task (1 or 2)
 // C -= acc of one task through the run's compact -> tile row maps: every map entry of the task read up
 // front (one LDS wait), the adds predicated
 // the plane groups' loads one group ahead (fp64: the operands of two groups and the accumulators need three
-// waves per SIMD; at four the kernel spilled 164 VGPRs and ran 2x slower) or not (fp32 records: four waves per
-// SIMD with no spill, the other waves cover the latency: 2026 -> 1726 us alone at config C, r06r)
+// waves per SIMD; without the look-ahead at four waves, 128 VGPRs unspilled, it runs the same: 2558 against
+// 2557 us, r06w) or not (fp32 records: four waves per SIMD, the other waves cover the latency: 2026 -> 1726 us
+// alone at config C, r06r)
 #ifndef VIBA_SCHUR_PF
 #define VIBA_SCHUR_PF (VIBA_MIXED ? 0 : 1)
 #endif
@@ -441,9 +442,10 @@ __device__ __forceinline__ void schur_rhs(const Dev& d, const uint32_t (*ecol)[2
 // group of four landmarks, lane group l4 takes landmark c0 + 4 m + l4 and its three planes over three
 // consecutive k-steps, so a lane loads one column's three planes at once (a 16 B and an 8 B load, or one 12 B
 // load for fp32 records) instead of three 8 B gathers for three k-steps (the gathers cost as instructions:
-// DESIGN.md §4).  The task's last nl % 4 landmarks keep the dense mapping (K row kr = 4 ks + l4 is plane
-// kr % 3 of landmark kr / 3).  Columns past nJ / nI load neighbouring panel data into accumulator rows /
-// columns that are never stored; K rows past `rows` read the zero pad.
+// DESIGN.md §4).  The last group's lanes past the task's landmarks read the zero pad (a dense remainder loop
+// for the last nl % 4 landmarks held the accumulators across two loop bodies: fp64 spilled at four waves per
+// SIMD; r06w: 2609 -> 2557 us alone at config C).  Columns past nJ / nI load neighbouring panel data into
+// accumulator rows / columns that are never stored.
 template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0, int rows, int a0, int l4, int l15,
                                            const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
@@ -464,11 +466,13 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
   // consecutive k-steps, so its operands of those k-steps are one column's three consecutive values (one 16 B
   // and one 8 B load per operand block instead of three 8 B gathers); the next group's loads are issued
   // before this group's MFMAs
-  const int nl = rows / 3, nfull = nl >> 2;
+  const int nl = rows / 3, nfull = (nl + 3) >> 2;
+  const rec_t* zp = d.yZero + 3 * l15;
   auto ld3 = [&](int m, rec_t (&a3)[NR][3], rec_t (&b3)[NBI][3]) {
-    const uint2 c = ec[c0 + 4 * m + l4];
-    const rec_t* pJ = Y + 3 * ((int64_t)c.y + 16 * a0 + l15);
-    const rec_t* pI = Y + 3 * ((int64_t)c.x + l15);
+    const bool lv = 4 * m + l4 < nl;  // lanes past the task's landmarks read the zero pad
+    const uint2 c = ec[lv ? c0 + 4 * m + l4 : c0];
+    const rec_t* pJ = lv ? Y + 3 * ((int64_t)c.y + 16 * a0 + l15) : zp;
+    const rec_t* pI = lv ? Y + 3 * ((int64_t)c.x + l15) : zp;
 #pragma unroll
     for (int i = 0; i < NR; i++) load3(pJ + 48 * i, a3[i]);
 #pragma unroll
@@ -514,28 +518,6 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
     __builtin_amdgcn_sched_barrier(0);  // no hoisting of the next group's loads (register pressure)
   }
 #endif
-  // the remaining nl % 4 landmarks, dense: K row kr = 4 ks + l4 is plane kr % 3 of landmark kr / 3 (advanced
-  // incrementally); K rows past them read the zero pad
-  const int c1 = c0 + 4 * nfull, rrows = 3 * (nl - 4 * nfull);
-  if (rrows > 0) {
-    const int nks = (rrows + 3) >> 2;
-    const rec_t* zp = d.yZero + 3 * l15;
-    int kr = l4, e = c1 + (l4 == 3 ? 1 : 0), q = l4 == 3 ? 0 : l4;
-    for (int ks = 0; ks < nks; ks++) {
-      const bool kv = kr < rrows;
-      const uint2 c = ec[kv ? e : c1];
-      const rec_t* pJ = kv ? Y + 3 * ((int64_t)c.y + 16 * a0 + l15) + q : zp;
-      const rec_t* pI = kv ? Y + 3 * ((int64_t)c.x + l15) + q : zp;
-      rec_t av[NR], bv[NBI];
-#pragma unroll
-      for (int i = 0; i < NR; i++) av[i] = pJ[48 * i];
-#pragma unroll
-      for (int b = 0; b < NBI; b++) bv[b] = pI[48 * b];
-      mm(av, bv);
-      kr += 4, e += 1, q += 1;
-      if (q == 3) q = 0, e += 1;
-    }
-  }
   // C -= acc through the run's compact -> tile maps (LDS atomics: tasks of other waves overlap)
   schur_epilogue<NBI, NR, DIAG>(acc, a0, l4, l15, posI, posJ, nI, nJ, C);
 }
