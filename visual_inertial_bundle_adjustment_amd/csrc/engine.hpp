@@ -122,7 +122,8 @@ struct TileWork {
 };
 // one task of schur_run4_kernel (32 bits): run (8) | first entry of its landmark chunk (8) | landmarks
 // (6) | first compact block row (2); built at finalize with kSchurCh landmarks x kSchurTR block rows
-constexpr int kSchurCh = 16, kSchurTR = 2;
+// (landmarks per task: 16 / 24 / 32 -> 2546 / 2536 / 2550 us alone at config C with plane groups, r06x)
+constexpr int kSchurCh = 24, kSchurTR = 2;
 
 struct Dev {
   // variables

@@ -998,11 +998,12 @@ int doFinalize(vb_handle h) {
         for (int c0 = rs[r]; c0 < rs[r + 1]; c0 += kSchurCh)
           for (int a0 = 0; a0 < nbJ; a0 += kSchurTR) {
             const int nl = std::min(kSchurCh, rs[r + 1] - c0), nr = std::min(kSchurTR, nbJ - a0);
-            const int nks = (3 * nl + 3) / 4;
+            // plane groups of four landmarks (schur_task): three k-steps and two loads per operand block each
+            const int ng = (nl + 3) / 4;
             int mf = 0;
             for (int i = 0; i < nr; i++)
               for (int b = 0; b < nbI; b++) mf += (!diag || a0 + i <= b) ? 1 : 0;
-            const double cost = nks * (16.0 * mf + 3.0 * (nr + nbI)) + 6.0 * mf + 24.0 + (diag && a0 == 0 ? 6.0 * nl : 0.0);
+            const double cost = ng * (48.0 * mf + 6.0 * (nr + nbI)) + 6.0 * mf + 24.0 + (diag && a0 == 0 ? 6.0 * nl : 0.0);
             tl.push_back({(uint32_t)r | ((uint32_t)c0 << 8) | ((uint32_t)nl << 16) | ((uint32_t)a0 << 22), cost});
           }
       }
