@@ -387,26 +387,51 @@ __device__ __forceinline__ void load3(const float* p, float (&v)[3]) {
   const f3u x = *reinterpret_cast<const f3u*>(p);
   v[0] = x.x, v[1] = x.y, v[2] = x.z;
 }
+// two adjacent panel columns' planes (fp64: three 16 B loads for six values, where two load3 take four)
+__device__ __forceinline__ void load6(const double* p, double (&v0)[3], double (&v1)[3]) {
+  typedef double d2u __attribute__((ext_vector_type(2), aligned(8)));
+  const d2u x = *reinterpret_cast<const d2u*>(p), y = *reinterpret_cast<const d2u*>(p + 2),
+            z = *reinterpret_cast<const d2u*>(p + 4);
+  v0[0] = x.x, v0[1] = x.y, v0[2] = y.x, v1[0] = y.y, v1[1] = z.x, v1[2] = z.y;
+}
+
+__device__ __forceinline__ void load6(const float* p, float (&v0)[3], float (&v1)[3]) { load3(p, v0), load3(p + 3, v1); }
+
+// Compact column of operand block b, lane l15 (I side), and compact row r of J-side block i.  Off-diagonal
+// fp64 tasks pair the blocks: blocks 2p and 2p + 1 take the even and the odd compact columns of
+// [32 p, 32 p + 32), so a lane's two columns are adjacent in the panel (load6); an unpaired block (the last of
+// an odd count, a one-row task, diagonal tiles, fp32 records) takes 16 consecutive columns.  The diagonal
+// tiles keep the consecutive map: their block triangle must be the element triangle.
+template <int NB, bool PAIR>
+__device__ __forceinline__ int schur_col(int b, int l15) {
+  return (PAIR && b < 2 * (NB / 2)) ? 32 * (b >> 1) + 2 * l15 + (b & 1) : 16 * b + l15;
+}
+template <int NR, bool PAIR>
+__device__ __forceinline__ int schur_row(int a0, int i, int r) {
+  return (PAIR && NR == 2) ? 32 * (a0 >> 1) + 2 * r + i : 16 * (a0 + i) + r;
+}
 
 template <int NBI, int NR, bool DIAG>
 __device__ __forceinline__ void schur_epilogue(const hacc4_t (&acc)[NR][NBI], int a0, int l4, int l15,
                                                const uint8_t* posI, const uint8_t* posJ, int nI, int nJ, double* C) {
+  constexpr bool PAIR = !DIAG && !VIBA_MIXED;
   int colT[NBI];
   int rowT[NR][4];
 #pragma unroll
-  for (int b = 0; b < NBI; b++) colT[b] = posI[min(16 * b + l15, TS - 1)];
+  for (int b = 0; b < NBI; b++) colT[b] = posI[min(schur_col<NBI, PAIR>(b, l15), TS - 1)];
 #pragma unroll
   for (int i = 0; i < NR; i++)
 #pragma unroll
-    for (int q = 0; q < 4; q++) rowT[i][q] = posJ[min(16 * (a0 + i) + kAccL4 * l4 + kAccR * q, TS - 1)];
+    for (int q = 0; q < 4; q++) rowT[i][q] = posJ[min(schur_row<NR, PAIR>(a0, i, kAccL4 * l4 + kAccR * q), TS - 1)];
 #pragma unroll
   for (int i = 0; i < NR; i++)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const bool mv = 16 * (a0 + i) + kAccL4 * l4 + kAccR * q < nJ;
+      const bool mv = schur_row<NR, PAIR>(a0, i, kAccL4 * l4 + kAccR * q) < nJ;
 #pragma unroll
       for (int b = 0; b < NBI; b++)
-        if ((!DIAG || a0 + i <= b) && mv && 16 * b + l15 < nI) atomicAdd(C + rowT[i][q] * TS + colT[b], -(double)acc[i][b][q]);
+        if ((!DIAG || a0 + i <= b) && mv && schur_col<NBI, PAIR>(b, l15) < nI)
+          atomicAdd(C + rowT[i][q] * TS + colT[b], -(double)acc[i][b][q]);
     }
 }
 
@@ -467,16 +492,28 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
   // and one 8 B load per operand block instead of three 8 B gathers); the next group's loads are issued
   // before this group's MFMAs
   const int nl = rows / 3, nfull = (nl + 3) >> 2;
-  const rec_t* zp = d.yZero + 3 * l15;
+  constexpr bool PAIR = !DIAG && !VIBA_MIXED;
   auto ld3 = [&](int m, rec_t (&a3)[NR][3], rec_t (&b3)[NBI][3]) {
-    const bool lv = 4 * m + l4 < nl;  // lanes past the task's landmarks read the zero pad
-    const uint2 c = ec[lv ? c0 + 4 * m + l4 : c0];
-    const rec_t* pJ = lv ? Y + 3 * ((int64_t)c.y + 16 * a0 + l15) : zp;
-    const rec_t* pI = lv ? Y + 3 * ((int64_t)c.x + l15) : zp;
+    // lanes past the task's landmarks read the zero pad (panel column 0 of yZero: every offset below < 192)
+    const bool lv = 4 * m + l4 < nl;
+    const uint2 c = lv ? ec[c0 + 4 * m + l4] : make_uint2(0u, 0u);
+    const rec_t* base = lv ? Y : d.yZero;
+    const rec_t* pJ = base + 3 * (int64_t)c.y;
+    const rec_t* pI = base + 3 * (int64_t)c.x;
+    if constexpr (PAIR && NR == 2) {
+      load6(pJ + 3 * schur_row<NR, PAIR>(a0, 0, l15), a3[0], a3[1]);
+    } else {
 #pragma unroll
-    for (int i = 0; i < NR; i++) load3(pJ + 48 * i, a3[i]);
+      for (int i = 0; i < NR; i++) load3(pJ + 3 * schur_row<NR, PAIR>(a0, i, l15), a3[i]);
+    }
 #pragma unroll
-    for (int b = 0; b < NBI; b++) load3(pI + 48 * b, b3[b]);
+    for (int b = 0; b < NBI; b++) {
+      if (PAIR && b < 2 * (NBI / 2)) {
+        if ((b & 1) == 0) load6(pI + 3 * schur_col<NBI, PAIR>(b, l15), b3[b], b3[b + 1]);
+      } else {
+        load3(pI + 3 * schur_col<NBI, PAIR>(b, l15), b3[b]);
+      }
+    }
   };
   auto mm3 = [&](const rec_t (&a3)[NR][3], const rec_t (&b3)[NBI][3]) {
 #pragma unroll
