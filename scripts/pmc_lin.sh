@@ -10,9 +10,12 @@ mkdir -p $R/gpurun_out/$TAG
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/$TAG/trace -o run -- python3 $R/scripts/kernel_probe.py C 3 fp64 $KS > $R/gpurun_out/$TAG/probe.json || exit $?
 i=0
-for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY" \
-           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS TCC_HIT_sum TCC_MISS_sum" \
-           "FETCH_SIZE" "WRITE_SIZE"; do
+# PMC_SETS="set1;set2;..." replaces the default counter sets (each within one pass's block limits)
+if [ -n "$PMC_SETS" ]; then IFS=';' read -ra SETS <<< "$PMC_SETS"; else
+SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY"
+      "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS TCC_HIT_sum TCC_MISS_sum"
+      "FETCH_SIZE" "WRITE_SIZE"); fi
+for set in "${SETS[@]}"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d $R/gpurun_out/$TAG/p$i -o run -- python3 $R/scripts/kernel_probe.py C 3 fp64 $KS > /dev/null || exit $?
 done
