@@ -123,7 +123,12 @@ struct TileWork {
 // one task of schur_run4_kernel (32 bits): run (8) | first entry of its landmark chunk (8) | landmarks
 // (6) | first compact block row (2); built at finalize with kSchurCh landmarks x kSchurTR block rows
 // (landmarks per task: 16 / 24 / 32 -> 2546 / 2536 / 2550 us alone at config C with plane groups, r06x)
-constexpr int kSchurCh = 24, kSchurTR = 2;
+// compact block rows per task: fp64 one (its accumulators and operands then fit four waves per SIMD without
+// the look-ahead: 2522 -> 2458 us alone at config C), fp32 records two (one: 1693 -> 1860 us), r06aa
+#ifndef VIBA_SCHUR_TR
+#define VIBA_SCHUR_TR (VIBA_MIXED ? 2 : 1)
+#endif
+constexpr int kSchurCh = 24, kSchurTR = VIBA_SCHUR_TR;
 
 struct Dev {
   // variables

@@ -369,12 +369,15 @@ constexpr int kTR = kSchurTR;  // compact block rows per task (1 or 2)
 
 // C -= acc of one task through the run's compact -> tile row maps: every map entry of the task read up
 // front (one LDS wait), the adds predicated
-// the plane groups' loads one group ahead (fp64: the operands of two groups and the accumulators need three
-// waves per SIMD; without the look-ahead at four waves, 128 VGPRs unspilled, it runs the same: 2558 against
-// 2557 us, r06w) or not (fp32 records: four waves per SIMD, the other waves cover the latency: 2026 -> 1726 us
-// alone at config C, r06r)
+// the plane groups' loads one group ahead (VIBA_SCHUR_PF=1: with two-row fp64 tasks the operands of two groups
+// and the accumulators need three waves per SIMD, and ran as fast as four waves without it, 2558 / 2557 us, r06w)
+// or not (default: four waves per SIMD, the other waves cover the latency; fp32 records 2026 -> 1726 us alone
+// at config C, r06r; fp64 with one-row tasks 2522 -> 2458 us, r06aa)
 #ifndef VIBA_SCHUR_PF
-#define VIBA_SCHUR_PF (VIBA_MIXED ? 0 : 1)
+#define VIBA_SCHUR_PF 0
+#endif
+#ifndef VIBA_SCHUR_WAVES
+#define VIBA_SCHUR_WAVES (VIBA_SCHUR_PF ? 3 : 4)
 #endif
 // one panel column's three planes of the plane-interleaved Y: a 16 B and an 8 B load (fp64), one 12 B load (fp32)
 __device__ __forceinline__ void load3(const double* p, double (&v)[3]) {
@@ -563,7 +566,7 @@ __device__ __forceinline__ void schur_task(const Dev& d, const uint2* ec, int c0
 // entries).  The item's runs (masks) and its tasks come precomputed from finalize (api.hip), the
 // tasks dealt to the waves longest-first (TileWork::wOff), so the kernel has no run scan and the waves
 // are balanced at the final barrier.  Four waves per SIMD (the k-loops are bound by gather latency).
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_SCHUR_PF ? 3 : 4, VIBA_SCHUR_PF ? 3 : 4))) schur_run4_kernel(Dev d, double lambda) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_SCHUR_WAVES, VIBA_SCHUR_WAVES))) schur_run4_kernel(Dev d, double lambda) {
   __shared__ double C[TS * TS];
   __shared__ uint32_t ecol[256][2];
   __shared__ uint64_t rmask[256][2];
@@ -619,8 +622,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(VIBA_S
   case ((NBI - 1) * 2 + (NR - 1)) * 2 + 1:                                                            \
     schur_task<NBI, NR, true>(d, ec2, c0, rows, a0, l4, l15, posI, posJ, nI, nJ, C);                  \
     break;
-      VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(2, 2)
-      VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 1) VIBA_SCHUR_CASE(4, 2)
+      VIBA_SCHUR_CASE(1, 1) VIBA_SCHUR_CASE(2, 1) VIBA_SCHUR_CASE(3, 1) VIBA_SCHUR_CASE(4, 1)
+#if VIBA_SCHUR_TR == 2
+      VIBA_SCHUR_CASE(1, 2) VIBA_SCHUR_CASE(2, 2) VIBA_SCHUR_CASE(3, 2) VIBA_SCHUR_CASE(4, 2)
+#endif
 #undef VIBA_SCHUR_CASE
       default: break;
     }
