@@ -763,14 +763,21 @@ __device__ __forceinline__ void group_finish(const Dev& d, double lambda, int mo
 // whole (both regions, 16 B per lane by global_load_lds: a handful of wide loads per thread per chunk,
 // where gathering the three operands of every k-step straight from HBM, behind an index load, ran
 // 1.05 ms against 0.79 alone on config C), double-buffered (chunk k + 1 in flight while chunk k feeds the
-// MFMAs).  Staged record c holds plane p at stage[c * kJPlanes + p].  The group's observation indices
+// MFMAs).  Staged record c holds plane p at stage[c * kGrpPlanes + p] (p < 2) / [.. + p - kGrpShift] (p >= 8).  The group's observation indices
 // come into LDS first, by windows of kGrpIdx.
 // observations per staged chunk: swept at config C (r05u, the kernel alone): fp64 16 / 24 / 32 / 48 / 64 ->
 // 818 / 794 / 862 / 1045 / 1041 us (LDS per workgroup sets the occupancy); fp32 records 609 / 564 / 550 /
 // 543 / 632 us
-constexpr int kGrpChunk = VIBA_MIXED ? 32 : 24;
+// Round 6 (r06ad): the point Jacobian's pieces (planes 2..7, never read here) are not staged, and the chunk
+// takes as many records as the same loads and buffer hold: fp64 33 pieces x 31 records in 4 loads per thread
+// (24 x 36 before), fp32 records 17 x 45 in 3 (32 x 18).
 constexpr int kRecPieces = kJPlanes / kRecV;                       // 16 B pieces per record (36 / 18)
-constexpr int kGrpLoads = (kGrpChunk * kRecPieces + 255) / 256;    // global_load_lds per thread per chunk
+constexpr int kGrpSkip = 8 / kRecV - 1;                            // pieces after the first holding planes < 8 only
+constexpr int kGrpPieces = kRecPieces - kGrpSkip;                  // staged pieces per record (33 / 17)
+constexpr int kGrpPlanes = kGrpPieces * kRecV;                     // staged planes per record
+constexpr int kGrpShift = kGrpSkip * kRecV;                        // record plane p >= 8 is staged plane p - kGrpShift
+constexpr int kGrpLoads = VIBA_MIXED ? 3 : 4;                      // global_load_lds per thread per chunk
+constexpr int kGrpChunk = kGrpLoads * 256 / kGrpPieces;            // records per chunk (31 / 45)
 constexpr int kGrpStage = kGrpLoads * 256 * kRecV;                 // rec_t per buffer (tail pieces land past the chunk)
 constexpr int kGrpIdx = 1024;                                      // observation indices per window
 static_assert(kJA % kRecV == 0 && kJB % kRecV == 0, "record regions in whole 16 B pieces");
@@ -799,8 +806,9 @@ __device__ __forceinline__ void group_issue(const Dev& d, const int32_t* sIdx, i
 #pragma unroll
   for (int j = 0; j < kGrpLoads; j++) {
     const int i = j * 256 + wave * 64 + lane;
-    int c = i / kRecPieces;
-    const int q = i - c * kRecPieces;
+    int c = i / kGrpPieces;
+    const int qs = i - c * kGrpPieces;
+    const int q = qs == 0 ? 0 : qs + kGrpSkip;  // the record's piece (the point Jacobian's are skipped)
     if (c >= nv) c = 0;  // past the chunk's observations: a valid record again, never read
     const int64_t o = sIdx[c];
     const rec_t* src = q < kJA / kRecV ? d.Jt + o * kJA + q * kRecV
@@ -823,7 +831,8 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
   const int row1 = grp_col_row(d, rv, 16 + l15, p1, s1);
   const int64_t o0 = d.grpStart[g], n = d.grpStart[g + 1] - o0;
   const int r = l4 & 1;
-  const int q0 = row0 >= 0 ? p0 + r * s0 : 0, q1 = row1 >= 0 ? p1 + r * s1 : 0;  // this lane's planes (K row parity r)
+  // this lane's staged planes (K row parity r)
+  const int q0 = row0 >= 0 ? p0 + r * s0 - kGrpShift : 0, q1 = row1 >= 0 ? p1 + r * s1 - kGrpShift : 0;
   hacc4_t a00 = {0, 0, 0, 0}, a10 = {0, 0, 0, 0}, a11 = {0, 0, 0, 0};
   double g0 = 0.0, g1 = 0.0;
   for (int64_t w0 = 0; w0 < n; w0 += kGrpIdx) {
@@ -845,7 +854,7 @@ __global__ void __launch_bounds__(256) obs_group_kernel(Dev d, double lambda, in
       const rec_t* S = stg + (k & 1) * kGrpStage;
       for (int ks = wave; 2 * ks < nv; ks += 4) {
         const int c = 2 * ks + (l4 >> 1);
-        const rec_t* rc = S + min(c, nv - 1) * kJPlanes;  // branch-free: past the chunk / invalid columns masked
+        const rec_t* rc = S + min(c, nv - 1) * kGrpPlanes;  // branch-free: past the chunk / invalid columns masked
         rec_t er, v0, v1;
         lds_read3(rc + kJe + r, rc + q0, rc + q1, er, v0, v1);
         if (c >= nv) er = v0 = v1 = 0;
