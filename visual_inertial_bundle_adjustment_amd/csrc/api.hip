@@ -228,9 +228,22 @@ void factorSeqSn(vb_handle h, int which) {
   // (on a stream the schedule leaves free: stZ at G = 2, stF at G = 3; stZ then waits for it, evClrDone)
   const bool clearHere = h->clearWanted && which == 0 && (S.nGroups == 2 || S.nGroups == 3) && !h->factorOnly;
   hipStream_t cs = S.nGroups == 2 ? h->stZ : h->stF;
+  // the diagonal-tile inverses of the columns factored before the chain, on the same free stream while the
+  // chain runs (a few latency-bound waves per level: the chip has room), instead of after the join
+  const bool invEarly = which == 0 && (S.nGroups == 2 || S.nGroups == 3) && S.nInvEarly > 0 && chain0 > 0;
+  bool invQueued = false;
   for (int i0 = 0; i0 < nSeg;) {
     int i1 = i0;
     while (i1 < nSeg && S.segL[i1] == S.segL[i0]) i1++;
+    if (invEarly && i0 == chain0) {  // every stream's levels so far are done: the tiles before the chain are final
+      for (int q = 0; q < G; q++) {
+        (void)hipEventRecord(h->evInvAt[q], stOf(q));
+        (void)hipStreamWaitEvent(cs, h->evInvAt[q], 0);
+      }
+      launch_diag_inverse(d, S.invEarlyD, S.nInvEarly, h->linv, cs);
+      (void)hipEventRecord(h->evInvDone, cs);
+      invQueued = true;
+    }
     if (clearHere && i0 == chain0) {  // vb_optimize's clear of the spare tile store
       (void)hipEventRecord(h->evClr, stOf(S.segG[i0]));
       (void)hipStreamWaitEvent(cs, h->evClr, 0);
@@ -272,6 +285,11 @@ void factorSeqSn(vb_handle h, int which) {
       (void)hipStreamWaitEvent(h->st, h->evSnLvl[q], 0);
     }
   if (S.nCopy) launch_copy_diag(d, S.copyD, (int)S.nCopy, h->lscrSn, h->st);
+  if (invQueued) {
+    launch_diag_inverse(d, S.invLateD, S.nInvLate, h->linv, h->st);
+    (void)hipStreamWaitEvent(h->st, h->evInvDone, 0);
+    return;
+  }
   const Sched& C = h->sch[which];
   launch_diag_inverse(d, C.potrfColD, C.lvP[C.nLevels], h->linv, h->st);
 }
@@ -583,6 +601,8 @@ int vb_create(const vb_config* cfg, vb_handle* out) {
   HIPCHK(hipEventCreateWithFlags(&h->evSnFork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evClr, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evClrDone, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->evInvDone, hipEventDisableTiming));
+  for (auto& e : h->evInvAt) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evStep, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->evRs, hipEventDisableTiming));
   for (auto& e : h->evSnLvl) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -634,6 +654,9 @@ int vb_destroy(vb_handle h) {
   if (h->evSnFork) hipEventDestroy(h->evSnFork);
   if (h->evClr) hipEventDestroy(h->evClr);
   if (h->evClrDone) hipEventDestroy(h->evClrDone);
+  if (h->evInvDone) hipEventDestroy(h->evInvDone);
+  for (auto& e : h->evInvAt)
+    if (e) hipEventDestroy(e);
   if (h->evStep) hipEventDestroy(h->evStep);
   if (h->evRs) hipEventDestroy(h->evRs);
   for (hipEvent_t e : h->evSnLvl)
@@ -646,7 +669,8 @@ int vb_destroy(vb_handle h) {
   if (h->stR) hipStreamSynchronize(h->stR), hipStreamDestroy(h->stR);
   if (h->hostRed) hipHostFree(h->hostRed);
   for (SnSched& N : h->sn) {
-    for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD, (void*)N.fusD, (void*)N.copyD})
+    for (void* p : {(void*)N.updD, (void*)N.fanPairsD, (void*)N.potD, (void*)N.rowD, (void*)N.fusD, (void*)N.copyD,
+                    (void*)N.invEarlyD, (void*)N.invLateD})
       if (p) hipFree(p);
     for (hipGraphExec_t g : N.graph)
       if (g) hipGraphExecDestroy(g);

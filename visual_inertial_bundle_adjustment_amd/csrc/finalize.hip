@@ -260,8 +260,28 @@ int buildSupernodes(vb_handle h, SnSched& S, const std::vector<int32_t>& tileIdx
   S.nSuper = 0;
   for (int32_t J = 0; J < nT; J++) S.nSuper += (pr[J] != 2 && colSel(J)) ? 1 : 0;
   S.nCopy = (int64_t)copy.size() / 2;
+  // diagonal-tile inverses (factorSeqSn): the columns of in-place (not fused) supernodes before the top
+  // separators' chain, and the rest; the same rule for the chain as factorSeqSn's
+  std::vector<int32_t> invE, invL;
+  {
+    const int nSeg = (int)S.segG.size();
+    int chain0 = 0;
+    for (int i = 1; i < nSeg; i++)
+      if (S.segL[i] == S.segL[i - 1]) chain0 = i + 1;
+    std::vector<uint8_t> early(nT, 0);
+    for (int i = 0; i < chain0; i++)
+      for (int64_t k = S.lvS[i]; k < S.lvS[i + 1]; k++) {
+        early[pot[4 * k + 1]] = 1;
+        if (pot[4 * k + 2] >= 0) early[pot[4 * k + 1] + 1] = 1;
+      }
+    for (int32_t J = 0; J < nT; J++) {
+      if (!colSel(J)) continue;
+      (early[J] ? invE : invL).push_back(J);
+    }
+  }
+  S.nInvEarly = (int64_t)invE.size(), S.nInvLate = (int64_t)invL.size();
   if (upload(&S.updD, fan) || upload(&S.fanPairsD, pairs) || upload(&S.potD, pot) || upload(&S.rowD, rows) ||
-      upload(&S.fusD, fus) || upload(&S.copyD, copy))
+      upload(&S.fusD, fus) || upload(&S.copyD, copy) || upload(&S.invEarlyD, invE) || upload(&S.invLateD, invL))
     return VB_E_HIP;
   if (S.nCopy && !h->lscrSn && alloc0(&h->lscrSn, 2 * (size_t)nT * TS * TS)) return VB_E_HIP;
   S.built = true;

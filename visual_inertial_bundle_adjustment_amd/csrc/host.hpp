@@ -296,6 +296,10 @@ struct SnSched {
   std::vector<int64_t> lvF;
   int32_t *fusD = nullptr, *copyD = nullptr;
   int64_t nCopy = 0;
+  // the solves' diagonal-tile inverses: of the columns factored in place before the top separators' chain
+  // (invEarlyD, queued on a free stream when the chain starts) and of the rest (invLateD, after the join)
+  int32_t *invEarlyD = nullptr, *invLateD = nullptr;
+  int64_t nInvEarly = 0, nInvLate = 0;
 
   hipGraphExec_t graph[2] = {nullptr, nullptr};
   bool built = false;
@@ -428,7 +432,7 @@ struct vb_handle_s {
   // captured into a graph it ran 12% slower per iteration (r05k)
   int snStreams = 2;
   hipStream_t stF = nullptr;
-  hipEvent_t evSnFork = nullptr, evSnLvl[4] = {}, evClr = nullptr, evClrDone = nullptr;
+  hipEvent_t evSnFork = nullptr, evSnLvl[4] = {}, evClr = nullptr, evClrDone = nullptr, evInvAt[4] = {}, evInvDone = nullptr;
   hipEvent_t evStep = nullptr, evRs = nullptr;  // vb_optimize: box-plus done; the speculative rebuild on stF done
   // vb_set_deferred: the phase functions of the multi-process controllers queue their work and return
   // without a host wait or scalar read; their scalars stay in red[0, 17) / err for one vb_read_scalars
