@@ -851,157 +851,6 @@ __global__ void __launch_bounds__(kFanWaves * 64) fanin_kernel(Dev d, const int3
   fanin_store(d.tiles + (int64_t)wk[0] * TS * TS, wk[3] != 0, wave, lane, acc);
 }
 
-// The same update with the operands loaded straight into registers (no LDS ring, no barriers): lane (l15, l4)
-// of wave (pb, qb) takes, per k-step of four columns t0 + l4, the two adjacent J rows pb + 2 l15, + 1 of L_JK
-// and I rows qb + 2 l15, + 1 of L_IK in one 16 B load each, so MFMA block a / b holds the even / odd rows
-// (D row m <-> J row pb + 2 m + a, column n <-> I row qb + 2 n + b); a group of four k-steps (8 loads) is in
-// flight while the previous one feeds the MFMAs.  The two waves of a WG sharing a half-tile read it within
-// a few cycles of each other (L1).  (VIBA_FAN_DIRECT, r06ai A/B)
-typedef double fan_d2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void fanin_direct_issue(const Dev& d, const int32_t* pairs, int32_t start, int g, int pb, int qb,
-                                                   int l15, int l4, fan_d2 (&a)[4], fan_d2 (&b)[4]) {
-  const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
-  const int64_t c = start + (g >> 2);
-  const int64_t tk = pc[2 * c + 1], ti = pc[2 * c];
-  const int col = 16 * (g & 3) + l4;
-  const double* pa = d.tiles + tk * TS * TS + (int64_t)col * TS + pb + 2 * l15;
-  const double* pi = d.tiles + ti * TS * TS + (int64_t)col * TS + qb + 2 * l15;
-#pragma unroll
-  for (int k = 0; k < 4; k++) a[k] = *reinterpret_cast<const fan_d2*>(pa + 4 * k * TS), b[k] = *reinterpret_cast<const fan_d2*>(pi + 4 * k * TS);
-}
-__global__ void __launch_bounds__(kFanWaves * 64) fanin_direct_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
-  const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l15 = lane & 15, l4 = lane >> 4;
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  const int32_t start = wk[1], ng = 4 * wk[2];  // groups of four k-steps (16 columns), four per contribution
-  double4_t acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; a++)
-#pragma unroll
-    for (int b = 0; b < 2; b++) acc[a][b] = double4_t{0, 0, 0, 0};
-  // two operand sets, no copies and no conditional loads (ng is even; the last iteration reloads the last
-  // group into the idle set), so the compiler's waits leave the other set's eight loads in flight
-  fan_d2 a0[4], b0[4], a1[4], b1[4];
-  auto mm = [&](const fan_d2 (&ca)[4], const fan_d2 (&cb)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      acc[0][0] = mfma64(ca[k].x, cb[k].x, acc[0][0]);
-      acc[0][1] = mfma64(ca[k].x, cb[k].y, acc[0][1]);
-      acc[1][0] = mfma64(ca[k].y, cb[k].x, acc[1][0]);
-      acc[1][1] = mfma64(ca[k].y, cb[k].y, acc[1][1]);
-    }
-  };
-  fanin_direct_issue(d, pairs, start, 0, pb, qb, l15, l4, a0, b0);
-  for (int g = 0; g < ng; g += 2) {
-    fanin_direct_issue(d, pairs, start, g + 1, pb, qb, l15, l4, a1, b1);
-    mm(a0, b0);
-    fanin_direct_issue(d, pairs, start, min(g + 2, ng - 1), pb, qb, l15, l4, a0, b0);
-    mm(a1, b1);
-  }
-  // C -= acc: element (J row pb + 2 (l4 + 4 r) + a, I row qb + 2 l15 + b); the two b of a lane are adjacent
-  double* C = d.tiles + (int64_t)wk[0] * TS * TS;
-  if (wk[3] != 0) {
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        double* p = C + (pb + 2 * (l4 + 4 * r) + a) * TS + qb + 2 * l15;
-        atomicAdd(p, -acc[a][0][r]);
-        atomicAdd(p + 1, -acc[a][1][r]);
-      }
-  } else {
-    fan_d2 v[2][4];
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) v[a][r] = *reinterpret_cast<const fan_d2*>(C + (pb + 2 * (l4 + 4 * r) + a) * TS + qb + 2 * l15);
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-      for (int r = 0; r < 4; r++)
-        *reinterpret_cast<fan_d2*>(C + (pb + 2 * (l4 + 4 * r) + a) * TS + qb + 2 * l15) =
-            fan_d2{v[a][r].x - acc[a][0][r], v[a][r].y - acc[a][1][r]};
-  }
-}
-
-// The same update on v_mfma_f64_4x4x4_4b, operands straight into registers.  The instruction computes four
-// 4 x 4 x 4 products, block q = (lane >> 2) & 3: lane 16 k + 4 q + x holds A_q[x][k] and B_q[k][x], and
-// D_q[i][j] sits in lane 16 i + 4 q + j (profiles/r02_mfma4_layout.txt).  Wave (pb, qb) covers its 32 x 32
-// quadrant as 64 pieces: block q takes J rows pb + 16 (q >> 1) + 4 x + u_a and I rows qb + 16 (q & 1) + 4 x +
-// u_b, so one register per u_a (A) and per u_b (B) feeds 16 instructions (u_a, u_b) per k-step, and a lane's
-// four rows of each operand are contiguous (two 16 B loads).  16 accumulators per lane; a lane's four u_b
-// results are four adjacent I rows of one J row.  (VIBA_FAN_DIRECT=2, r06aj A/B)
-__device__ __forceinline__ void fanin_d4_issue(const Dev& d, const int32_t* pairs, int32_t start, int g, int ra, int rb, int kk,
-                                               fan_d2 (&a)[2][2], fan_d2 (&b)[2][2]) {
-  const __attribute__((address_space(4))) int32_t* pc = (const __attribute__((address_space(4))) int32_t*)pairs;
-  const int64_t c = start + (g >> 3);
-  const int64_t tk = pc[2 * c + 1], ti = pc[2 * c];
-  const int col = 8 * (g & 7) + kk;  // k-steps 2 (g & 7) and + 1: columns col and col + 4
-  const double* pa = d.tiles + tk * TS * TS + (int64_t)col * TS + ra;
-  const double* pi = d.tiles + ti * TS * TS + (int64_t)col * TS + rb;
-#pragma unroll
-  for (int s = 0; s < 2; s++)
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-      a[s][h] = *reinterpret_cast<const fan_d2*>(pa + 4 * s * TS + 2 * h),
-      b[s][h] = *reinterpret_cast<const fan_d2*>(pi + 4 * s * TS + 2 * h);
-}
-__global__ void __launch_bounds__(kFanWaves * 64) fanin_d4_kernel(Dev d, const int32_t* work, const int32_t* pairs) {
-  const int32_t* wk = work + 4 * xcd_block(blockIdx.x, gridDim.x);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kk = lane >> 4, q = (lane >> 2) & 3, x = lane & 3;
-  const int pb = (wave >> 1) * 32, qb = (wave & 1) * 32;
-  const int ra = pb + 16 * (q >> 1) + 4 * x, rb = qb + 16 * (q & 1) + 4 * x;
-  const int32_t start = wk[1], ng = 8 * wk[2];  // groups of two k-steps (8 columns), eight per contribution
-  double acc[16];
-#pragma unroll
-  for (int u = 0; u < 16; u++) acc[u] = 0.0;
-  fan_d2 a0[2][2], b0[2][2], a1[2][2], b1[2][2];  // two operand sets (as fanin_direct_kernel)
-  auto mm = [&](const fan_d2 (&ca)[2][2], const fan_d2 (&cb)[2][2]) {
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const double av[4] = {ca[s][0].x, ca[s][0].y, ca[s][1].x, ca[s][1].y};
-      const double bv[4] = {cb[s][0].x, cb[s][0].y, cb[s][1].x, cb[s][1].y};
-#pragma unroll
-      for (int ua = 0; ua < 4; ua++)
-#pragma unroll
-        for (int ub = 0; ub < 4; ub++)
-          acc[4 * ua + ub] = __builtin_amdgcn_mfma_f64_4x4x4f64(av[ua], bv[ub], acc[4 * ua + ub], 0, 0, 0);
-    }
-  };
-  fanin_d4_issue(d, pairs, start, 0, ra, rb, kk, a0, b0);
-  for (int g = 0; g < ng; g += 2) {
-    fanin_d4_issue(d, pairs, start, g + 1, ra, rb, kk, a1, b1);
-    mm(a0, b0);
-    fanin_d4_issue(d, pairs, start, min(g + 2, ng - 1), ra, rb, kk, a0, b0);
-    mm(a1, b1);
-  }
-  // C -= acc: lane (i, q, j) holds, for u_a, the J row pb + 16 (q >> 1) + 4 i + u_a at I rows qb + 16 (q & 1) +
-  // 4 j + u_b, u_b = 0..3 (adjacent)
-  double* C = d.tiles + (int64_t)wk[0] * TS * TS;
-  const int i = lane >> 4, j = lane & 3;
-  double* Cw = C + (pb + 16 * (q >> 1) + 4 * i) * TS + qb + 16 * (q & 1) + 4 * j;
-  if (wk[3] != 0) {
-#pragma unroll
-    for (int ua = 0; ua < 4; ua++)
-#pragma unroll
-      for (int ub = 0; ub < 4; ub++) atomicAdd(Cw + ua * TS + ub, -acc[4 * ua + ub]);
-  } else {
-    fan_d2 v[4][2];
-#pragma unroll
-    for (int ua = 0; ua < 4; ua++)
-#pragma unroll
-      for (int h = 0; h < 2; h++) v[ua][h] = *reinterpret_cast<const fan_d2*>(Cw + ua * TS + 2 * h);
-#pragma unroll
-    for (int ua = 0; ua < 4; ua++)
-#pragma unroll
-      for (int h = 0; h < 2; h++)
-        *reinterpret_cast<fan_d2*>(Cw + ua * TS + 2 * h) =
-            fan_d2{v[ua][h].x - acc[4 * ua + 2 * h], v[ua][h].y - acc[4 * ua + 2 * h + 1]};
-  }
-}
-
 // Inverse of every factored diagonal tile (one wave per tile, lane = column c of X = L^-1, off the
 // factorization's critical path but before the backward solve): x_i = (delta_ic - sum_{k<i} L_ik x_k) / L_ii
 // with the 64 reciprocals formed first (one divide per lane) and each row's sum split over four partial
@@ -1445,13 +1294,8 @@ void launch_tile_scatter_add(const Dev& d, const int32_t* tiles, int64_t n, cons
   launch_chunk_copy(d.tiles, tiles, n, TS * TS, const_cast<double*>(in), 2, st);
 }
 
-#ifndef VIBA_FAN_DIRECT
-#define VIBA_FAN_DIRECT 0
-#endif
 void launch_fanin(const Dev& d, const int32_t* work, const int32_t* pairs, int n, hipStream_t st) {
-  if (n > 0)
-    launchK(VIBA_FAN_DIRECT == 2 ? fanin_d4_kernel : VIBA_FAN_DIRECT ? fanin_direct_kernel : fanin_kernel, dim3(n),
-            dim3(kFanWaves * 64), 0, st, d, work, pairs);
+  if (n > 0) launchK(fanin_kernel, dim3(n), dim3(kFanWaves * 64), 0, st, d, work, pairs);
 }
 // inverses of the diagonal factor tiles of the listed columns (all columns if cols == nullptr)
 void launch_diag_inverse(const Dev& d, const int32_t* cols, int64_t n, double* linv, hipStream_t st) {
